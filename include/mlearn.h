@@ -1,0 +1,278 @@
+/*
+ * mlearn.h — C ABI of the MI355X-native batched-PPO hot path.
+ *
+ * This is the drop-in boundary beneath the Python plugin surface that
+ * madrona-learn exposes for its PPO iteration (rollout collection -> GAE ->
+ * minibatch PPO update).  The reference has no native ABI: every entry point
+ * below names the reference function (file:line, relative to the
+ * shacklettbp/madrona-learn source tree, src/madrona_learn/) whose arithmetic
+ * it replaces.  The Python host package (madrona-learn_amd/madrona_learn)
+ * calls these through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers to device memory (HBM) + sizes; no torch/framework types.
+ *  - The caller owns every buffer.  No entry point allocates or synchronises,
+ *    so every call is safe inside HIP-graph capture.  Scratch comes from a
+ *    caller-supplied workspace whose size is queried up front.
+ *  - Every call takes an explicit hipStream_t (as mlearn_stream_t) and returns
+ *    an int status: MLEARN_OK (0), MLEARN_EINVAL (<0: bad argument, nothing
+ *    launched) or MLEARN_EHIP (launch failure).  mlearn_last_error() returns a
+ *    thread-local message for the last failing call.
+ *  - Layouts are row-major.  Rollout arrays are [T][N] (time-major, env-minor)
+ *    which is exactly the reference's pre-finalize store [C][T/C][P][B]
+ *    (rollouts.py:460-478) viewed flat.
+ */
+#ifndef MLEARN_H
+#define MLEARN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MLEARN_ABI_VERSION 1
+
+#define MLEARN_OK 0
+#define MLEARN_EINVAL (-1)
+#define MLEARN_EHIP (-2)
+
+#define MLEARN_DTYPE_F32 0
+#define MLEARN_DTYPE_BF16 1
+
+#define MLEARN_MAX_LAYERS 4
+#define MLEARN_MAX_GROUPS 16
+#define MLEARN_HEAD_COLS 32 /* actor logits + 1 critic output, padded */
+
+typedef void* mlearn_stream_t; /* hipStream_t */
+
+const char* mlearn_last_error(void);
+int mlearn_abi_version(void);
+
+/* ---------------------------------------------------------------------- */
+/* RNG: Philox4x32-10 (replaces jax.random threefry; see DESIGN.md "RNG")  */
+/* ---------------------------------------------------------------------- */
+/* out[i] = philox4x32(ctr[i], {k0,k1}); ctr/out are [n][4] uint32 in HBM. */
+int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,
+                      int64_t n, mlearn_stream_t stream);
+
+/* Counters.  Every RNG-consuming entry point takes (const uint64_t* ctr,
+ * uint64_t add): the effective counter is (ctr ? *ctr : 0) + add, read on the
+ * device, so a captured HIP graph replays with fresh randomness once the
+ * counters are advanced on the stream with mlearn_counters_add. */
+int mlearn_counters_add(uint64_t* ctr, int32_t n, const uint64_t* deltas /* host, n <= 8 */,
+                        mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Returns / advantages                                                    */
+/* ---------------------------------------------------------------------- */
+/* Reverse-time GAE scan over [T][N] (algo_common.py:84-130) fused with
+ * returns = advantages + values (rollouts.py:761-769).  dones are bytes
+ * (bool, rollouts.py:454-455,933).  bootstrap is [N]. */
+int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
+                   const float* bootstrap, float* advantages, float* returns, int32_t T,
+                   int64_t N, float gamma, float gae_lambda, mlearn_stream_t stream);
+
+/* Discounted returns without advantages (algo_common.py:45-81), used when
+ * TrainConfig.compute_advantages is False. */
+int mlearn_returns_f32(const float* rewards, const uint8_t* dones, const float* bootstrap,
+                       float* returns, int32_t T, int64_t N, float gamma,
+                       mlearn_stream_t stream);
+
+/* Whole-array z-score (algo_common.py:133-140): out = (x-mean)*rsqrt(max(var,1e-5)).
+ * workspace >= mlearn_zscore_workspace_bytes(n). */
+int64_t mlearn_zscore_workspace_bytes(int64_t n);
+int mlearn_zscore_f32(const float* x, int64_t n, float* out, void* workspace,
+                      mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Discrete action distributions (dists.py:12-77)                          */
+/* ---------------------------------------------------------------------- */
+typedef struct mlearn_action_layout {
+    int32_t num_groups;                        /* K sub-actions */
+    int32_t num_logits;                        /* sum of buckets (<= 31) */
+    int32_t offsets[MLEARN_MAX_GROUPS + 1];    /* group k = logits[offsets[k], offsets[k+1]) */
+} mlearn_action_layout;
+
+/* DiscreteActionDistributions.sample (dists.py:26-44): Gumbel-max per group
+ * with noise from Philox(ctr={env_offset+n, j>>2, step}, key={k0,k1}); the
+ * log-prob is logit[a] - logsumexp(group); step = *step_ctr + step.
+ * sample == 0 gives best()
+ * (dists.py:46-52, first-index argmax) and log_probs may be NULL. */
+int mlearn_discrete_sample_f32(const float* logits, int64_t ld, mlearn_action_layout layout,
+                               int64_t N, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
+                               uint64_t step, uint32_t env_offset, int32_t sample,
+                               int32_t* actions, float* log_probs, mlearn_stream_t stream);
+
+/* DiscreteActionDistributions.action_stats (dists.py:54-77). */
+int mlearn_action_stats_f32(const float* logits, int64_t ld, mlearn_action_layout layout,
+                            int64_t N, const int32_t* actions, float* log_probs,
+                            float* entropies, mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* MLP actor-critic (actor_critic.py:38-128 with BackboneShared 202-244,   */
+/* BackboneEncoder 131-153, models.py MLP 99-119, LayerNorm 46-56,          */
+/* DenseLayerDiscreteActor 122-139, DenseLayerCritic 142-154).             */
+/* ---------------------------------------------------------------------- */
+typedef struct mlearn_mlp_policy {
+    int32_t dtype;       /* compute dtype: MLEARN_DTYPE_F32 / MLEARN_DTYPE_BF16 */
+    int32_t obs_dim;     /* multiple of 16, <= 256 */
+    int32_t hidden;      /* 64, 128 or 256 */
+    int32_t num_layers;  /* 1..MLEARN_MAX_LAYERS */
+    mlearn_action_layout actions;
+    const void* w_t[MLEARN_MAX_LAYERS];    /* [hidden][in_l] compute dtype (Dense kernel^T) */
+    const void* w[MLEARN_MAX_LAYERS];      /* [in_l][hidden] compute dtype (Dense kernel) */
+    const float* ln_scale[MLEARN_MAX_LAYERS];  /* [hidden] f32 */
+    const float* ln_bias[MLEARN_MAX_LAYERS];   /* [hidden] f32 */
+    const void* head_t;      /* [32][hidden] compute dtype; rows 0..A-1 actor, row A critic */
+    const void* head;        /* [hidden][32] compute dtype */
+    const float* head_bias;  /* [32] f32 */
+} mlearn_mlp_policy;
+
+/* One rollout step of ActorCritic.rollout (actor_critic.py:74-96) fused with
+ * the post-inference store (rollouts.py:637-668): preprocess (cast to the
+ * compute dtype) -> MLP trunk -> actor logits + critic -> sample -> write
+ * obs_store[N][obs_dim] (may be NULL), actions[N][K] i32, log_probs[N][K] f32,
+ * values[N] f32.  actions == NULL computes only the critic
+ * (ActorCritic.critic_only, actor_critic.py:65-72, used for the bootstrap
+ * values, rollouts.py:607-635). */
+int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const float* obs, int64_t N,
+                               void* obs_store, int32_t* actions, float* log_probs,
+                               float* values, uint32_t k0, uint32_t k1,
+                               const uint64_t* step_ctr, uint64_t step, uint32_t env_offset,
+                               int32_t sample, mlearn_stream_t stream);
+
+/* Post-step bookkeeping of rollout_loop (rollouts.py:933-973, _post_step_cb
+ * 682-714): store rewards/dones at step t, env_returns = r + gamma*env_returns,
+ * trace it (for the 'Env Returns' metric), then zero it where done. */
+int mlearn_rollout_post_step(const float* rewards, const uint8_t* dones, int64_t N,
+                             float* store_rewards, uint8_t* store_dones, float* env_returns,
+                             float* env_returns_trace, float gamma, mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Metrics (metrics.py:31-48 Metric.init_from_data): mean, m2, min, max,   */
+/* count of up to 16 float arrays in one launch.                           */
+/* ---------------------------------------------------------------------- */
+typedef struct mlearn_metric_job {
+    const float* x;
+    int64_t n;
+    int32_t abs_value;  /* 1: metric of |x| (ppo.py:358 'Value Errors') */
+    int32_t pad;
+} mlearn_metric_job;
+
+int64_t mlearn_metrics_workspace_bytes(int32_t num_jobs);
+/* out[j*5 + {0..4}] = {mean, m2, min, max, count} */
+int mlearn_metrics_f32(const mlearn_metric_job* jobs, int32_t num_jobs, float* out,
+                       void* workspace, mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* PPO update (ppo.py:109-488)                                             */
+/* ---------------------------------------------------------------------- */
+/* Epoch permutation of n sequence ids (ppo.py:445-458, random.permutation):
+ * perm = argsort of Philox keys (ctr={i, rank, epoch lo, epoch hi}), ties
+ * broken by index.  n <= 16384 per call. */
+int mlearn_minibatch_perm(uint32_t k0, uint32_t k1, const uint64_t* epoch_ctr, uint64_t epoch,
+                          uint32_t rank, int32_t n, int32_t* perm, mlearn_stream_t stream);
+
+typedef struct mlearn_rollout_view {
+    const void* obs;          /* [T][N][obs_dim] compute dtype */
+    const int32_t* actions;   /* [T][N][K] */
+    const float* log_probs;   /* [T][N][K] */
+    const float* advantages;  /* [T][N] */
+    const float* returns;     /* [T][N] */
+    const float* values;      /* [T][N] */
+    int32_t T;                /* steps per update */
+    int32_t bptt_len;         /* T / num_bptt_chunks */
+    int64_t N;                /* envs (P*B) on this rank */
+} mlearn_rollout_view;
+
+/* Per-minibatch advantage statistics for zscore_data (algo_common.py:133-140,
+ * ppo.py:134-143): for minibatch m of the epoch, double partials of
+ * (sum x, sum x^2) over its mb_size sequences x bptt_len steps.  Output
+ * partials[m][2] (to be all-reduced across ranks under data parallelism),
+ * finished by mlearn_adv_stats_finish into stats[m] = {mean, rsqrt(max(var,1e-5))}.
+ * `partials` must hold num_mb * 66 doubles; the first num_mb * 2 are the
+ * per-minibatch sums (the rest is scratch). */
+int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
+                     int32_t mb_size, double* partials, mlearn_stream_t stream);
+int mlearn_adv_stats_finish(const double* partials, int32_t num_mb, double count,
+                            float* stats, mlearn_stream_t stream);
+
+typedef struct mlearn_ppo_hparams {
+    float clip_coef;
+    float value_loss_coef;
+    float entropy_coef[MLEARN_MAX_GROUPS]; /* per sub-action (ppo.py:231-239) */
+    int32_t normalize_advantages;          /* TrainConfig.normalize_advantages */
+    int32_t clip_value_loss;               /* PPOConfig.clip_value_loss */
+    int32_t huber_value_loss;              /* PPOConfig.huber_value_loss */
+    float loss_scale;                      /* 1/world_size under DP (mean of means) */
+} mlearn_ppo_hparams;
+
+/* Size of the minibatch workspace (activations + gradient slabs). */
+int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows);
+
+/* One PPO minibatch step up to the flat gradient: forward (ActorCritic.update,
+ * actor_critic.py:98-128), loss (ppo.py:129-262), backward (jax.value_and_grad,
+ * ppo.py:276-281) and the reduction of all per-row-tile partials into
+ * grad[param_count] (flat f32, layout of mlearn_param_offsets).
+ * mb_seq = the mb_size sequence ids of this minibatch (a slice of perm).
+ * adv_stats = {mean, rstd} of this minibatch.  loss_out (may be NULL) receives
+ * 5 x {mean, m2, min, max, count}: 'Loss' {loss,0,loss,loss,1}, 'Action Obj',
+ * 'Value Loss', 'Value Errors', 'Entropy' (ppo.py:95-106, 351-362). */
+int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                              const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                              const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
+                              void* workspace, mlearn_stream_t stream);
+
+/* Parameter layout of the flat f32 buffers (params, grads, Adam m/v):
+ * per layer l: W_l [in_l][hidden], ln_scale_l [hidden], ln_bias_l [hidden];
+ * then head W [hidden][A+1] (logits then critic), head bias [A+1]. */
+int64_t mlearn_param_count(const mlearn_mlp_policy* policy);
+
+typedef struct mlearn_optim_state {
+    float* params;        /* flat f32 master weights */
+    const float* grads;   /* flat f32 (already all-reduced / averaged) */
+    float* adam_m;
+    float* adam_v;
+    const float* init_norms;   /* [num_layers] Frobenius norms of W_l at init */
+    int32_t* step;        /* device int32 Adam step counter (optax count) */
+    float lr, b1, b2, eps, max_grad_norm;
+    int32_t normalize_params;      /* ppo.py:303-310 */
+    int32_t normalize_layernorms;  /* ppo.py:312-338 */
+} mlearn_optim_state;
+
+int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy);
+/* optax.chain(clip_by_global_norm, adam) (ppo.py:84-90, 283-286), then the
+ * weight-norm re-projection and LayerNorm renorm (ppo.py:303-338), then the
+ * compute-dtype weight copies referenced by `policy` are refreshed. */
+int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state* st,
+                      void* workspace, mlearn_stream_t stream);
+
+/* Refresh the compute-dtype copies (w_t, w, head_t, head, head_bias) of
+ * `policy` from flat f32 params (used at init and after checkpoint loads). */
+int mlearn_policy_sync_weights(const mlearn_mlp_policy* policy, const float* params,
+                               mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Synthetic dummy vec-env (test/bench sim plugin, not part of the         */
+/* reference: stands in for the Madrona sim_fns['step'] custom call,       */
+/* rollouts.py:905-936).                                                   */
+/* ---------------------------------------------------------------------- */
+/* state is [N][4] int32 per env: {episode step, env step lo, env step hi, 0}.
+ * Episode length of env g = env_offset + n is 16 + (g*7 mod 33) (staggered,
+ * deterministic dones).  obs[n][f] = Irwin-Hall(4) approximation of N(0,1)
+ * from Philox(ctr={g, f, env step}, key={k0, k1^0x5eed}); reward =
+ * U[-1,1) + 0.01*action[n][0].  dones are bytes.  Reset puts every env at
+ * episode step g mod L_g and env step 0. */
+int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int64_t N,
+                          int32_t obs_dim, uint32_t k0, uint32_t k1, uint32_t env_offset,
+                          float* obs, float* rewards, uint8_t* dones, mlearn_stream_t stream);
+int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t k0,
+                           uint32_t k1, uint32_t env_offset, float* obs,
+                           mlearn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MLEARN_H */

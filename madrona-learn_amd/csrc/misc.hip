@@ -1,0 +1,722 @@
+// Streaming / reduction kernels of the PPO iteration:
+//   GAE + returns, discounted returns, z-score, discrete sampling and
+//   action stats, metrics, epoch permutation, advantage statistics,
+//   rollout post-step bookkeeping, and the synthetic dummy environment.
+// All are HBM/latency-bound integer or fp32 streaming work: coalesced
+// [T][N] rows, 16-B loads where the layout allows, wave-shuffle reductions,
+// deterministic partial slabs instead of float atomics.
+
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+#include "dists.h"
+
+namespace ml {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return MLEARN_EHIP;
+    }
+    return MLEARN_OK;
+}
+
+static inline int grid_for(int64_t n, int block, int cap = 1 << 20) {
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// ---------------------------------------------------------------------------
+// Philox
+// ---------------------------------------------------------------------------
+__global__ void philox_kernel(const uint4* __restrict__ ctr, uint32_t k0, uint32_t k1,
+                              uint4* __restrict__ out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        uint4 c = ctr[i];
+        u32x4 r = philox4x32(u32x4{c.x, c.y, c.z, c.w}, k0, k1);
+        out[i] = make_uint4(r.x, r.y, r.z, r.w);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GAE (algo_common.py:84-130) + returns = adv + values (rollouts.py:761-769).
+// One lane per env column, VEC envs per lane (16-B loads of rewards/values).
+// The reverse recurrence per column:
+//   nv = d_t ? 0 : nv ;  na = d_t ? 0 : na
+//   A_t = (r_t + g*nv - v_t) + g*l*na ;  nv = v_t ;  na = A_t
+// Operation order mirrors the reference expression tree; contraction is off
+// so the fp32 result is reproducible against the oracle's fp32 mode.
+// ---------------------------------------------------------------------------
+template <int VEC>
+__global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewards,
+                                                  const float* __restrict__ values,
+                                                  const uint8_t* __restrict__ dones,
+                                                  const float* __restrict__ boot,
+                                                  float* __restrict__ adv, float* __restrict__ ret,
+                                                  int T, int64_t N, float gamma, float gl) {
+#pragma clang fp contract(off)
+    int64_t n0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * VEC;
+    if (n0 >= N) return;
+    float nv[VEC], na[VEC];
+    if (VEC == 4) {
+        float4 b = *(const float4*)(boot + n0);
+        nv[0] = b.x; nv[1] = b.y; nv[2] = b.z; nv[3] = b.w;
+    } else {
+        for (int j = 0; j < VEC; ++j) nv[j] = boot[n0 + j];
+    }
+    for (int j = 0; j < VEC; ++j) na[j] = 0.f;
+
+    for (int t = T - 1; t >= 0; --t) {
+        int64_t o = (int64_t)t * N + n0;
+        float r[VEC], v[VEC];
+        uint32_t d[VEC];
+        if (VEC == 4) {
+            float4 r4 = *(const float4*)(rewards + o);
+            float4 v4 = *(const float4*)(values + o);
+            uint32_t d4 = *(const uint32_t*)(dones + o);
+            r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
+            v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+            for (int j = 0; j < 4; ++j) d[j] = (d4 >> (8 * j)) & 0xffu;
+        } else {
+            for (int j = 0; j < VEC; ++j) {
+                r[j] = rewards[o + j];
+                v[j] = values[o + j];
+                d[j] = dones[o + j];
+            }
+        }
+        float a[VEC], rt[VEC];
+        for (int j = 0; j < VEC; ++j) {
+            float nvj = d[j] ? 0.f : nv[j];
+            float naj = d[j] ? 0.f : na[j];
+            float td = (r[j] + gamma * nvj) - v[j];
+            a[j] = td + gl * naj;
+            rt[j] = a[j] + v[j];
+            nv[j] = v[j];
+            na[j] = a[j];
+        }
+        if (VEC == 4) {
+            *(float4*)(adv + o) = make_float4(a[0], a[1], a[2], a[3]);
+            *(float4*)(ret + o) = make_float4(rt[0], rt[1], rt[2], rt[3]);
+        } else {
+            for (int j = 0; j < VEC; ++j) {
+                adv[o + j] = a[j];
+                ret[o + j] = rt[j];
+            }
+        }
+    }
+}
+
+// compute_returns (algo_common.py:45-81)
+__global__ __launch_bounds__(256) void returns_kernel(const float* __restrict__ rewards,
+                                                      const uint8_t* __restrict__ dones,
+                                                      const float* __restrict__ boot,
+                                                      float* __restrict__ ret, int T, int64_t N,
+                                                      float gamma) {
+#pragma clang fp contract(off)
+    int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float nr = boot[n];
+    for (int t = T - 1; t >= 0; --t) {
+        int64_t o = (int64_t)t * N + n;
+        nr = dones[o] ? 0.f : nr;
+        nr = rewards[o] + gamma * nr;
+        ret[o] = nr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Block-level double reductions with a fixed order (deterministic).
+// ---------------------------------------------------------------------------
+template <int BLOCK>
+__device__ inline double block_sum_d(double v, double* sh) {
+    v = wave_sum64d(v);
+    int w = threadIdx.x / 64, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double s = 0;
+    for (int i = 0; i < BLOCK / 64; ++i) s += sh[i];
+    return s;
+}
+
+__device__ inline float wave_min(float v) {
+    for (int o = 1; o < 64; o <<= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ inline float wave_max(float v) {
+    for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Metrics: Metric.init_from_data (metrics.py:31-48).  Pass 1: per-block
+// (sum, sumsq in double, min, max) partials; pass 2: one block per job sums
+// partials in block order: mean = S/n, m2 = SS - n*mean^2 (double).
+// ---------------------------------------------------------------------------
+struct MetricJobs {
+    mlearn_metric_job j[16];
+};
+constexpr int kMetricBlocks = 64;
+
+__global__ __launch_bounds__(256) void metrics_partial_kernel(MetricJobs jobs, double* part) {
+    __shared__ double sh[4];
+    __shared__ float shf[4];
+    const mlearn_metric_job& J = jobs.j[blockIdx.y];
+    double s = 0, q = 0;
+    float mn = 3.402823466e+38f, mx = -3.402823466e+38f;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * 256) {
+        float x = J.x[i];
+        if (J.abs_value) x = fabsf(x);
+        s += x;
+        q += (double)x * x;
+        mn = fminf(mn, x);
+        mx = fmaxf(mx, x);
+    }
+    s = block_sum_d<256>(s, sh);
+    q = block_sum_d<256>(q, sh);
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    int w = threadIdx.x / 64;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) shf[w] = mn;
+    __syncthreads();
+    float bmn = fminf(fminf(shf[0], shf[1]), fminf(shf[2], shf[3]));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) shf[w] = mx;
+    __syncthreads();
+    float bmx = fmaxf(fmaxf(shf[0], shf[1]), fmaxf(shf[2], shf[3]));
+    if (threadIdx.x == 0) {
+        double* p = part + ((int64_t)blockIdx.y * kMetricBlocks + blockIdx.x) * 4;
+        p[0] = s;
+        p[1] = q;
+        p[2] = bmn;
+        p[3] = bmx;
+    }
+}
+
+__global__ void metrics_finish_kernel(MetricJobs jobs, const double* part, float* out) {
+    const mlearn_metric_job& J = jobs.j[blockIdx.x];
+    if (threadIdx.x != 0) return;
+    double s = 0, q = 0, mn = 3.402823466e+38, mx = -3.402823466e+38;
+    for (int b = 0; b < kMetricBlocks; ++b) {
+        const double* p = part + ((int64_t)blockIdx.x * kMetricBlocks + b) * 4;
+        s += p[0];
+        q += p[1];
+        mn = fmin(mn, p[2]);
+        mx = fmax(mx, p[3]);
+    }
+    double n = (double)J.n;
+    double mean = n > 0 ? s / n : 0.0;
+    double m2 = n > 0 ? q - n * mean * mean : 0.0;
+    if (m2 < 0) m2 = 0;
+    float* o = out + blockIdx.x * 5;
+    o[0] = (float)mean;
+    o[1] = (float)m2;
+    o[2] = (float)mn;
+    o[3] = (float)mx;
+    o[4] = (float)J.n;
+}
+
+// ---------------------------------------------------------------------------
+// z-score over a whole array (algo_common.py:133-140).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sum_partial_kernel(const float* x, int64_t n, double* part) {
+    __shared__ double sh[4];
+    double s = 0, q = 0;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        double v = x[i];
+        s += v;
+        q += v * v;
+    }
+    s = block_sum_d<256>(s, sh);
+    q = block_sum_d<256>(q, sh);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x * 2] = s;
+        part[blockIdx.x * 2 + 1] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void zscore_apply_kernel(const float* x, int64_t n,
+                                                           const double* part, int nparts,
+                                                           float* out) {
+    double s = 0, q = 0;
+    for (int b = 0; b < nparts; ++b) {
+        s += part[2 * b];
+        q += part[2 * b + 1];
+    }
+    double dn = (double)n;
+    float mean = (float)(s / dn);
+    float var = (float)(q / dn - (s / dn) * (s / dn));
+    float rs = rsqrtf(fmaxf(var, 1e-5f));
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        out[i] = (x[i] - mean) * rs;
+}
+
+// ---------------------------------------------------------------------------
+// Discrete distributions (dists.py:26-77).  One lane per (row, group).
+// ---------------------------------------------------------------------------
+struct Layout {
+    int K, A;
+    int off[MLEARN_MAX_GROUPS + 1];
+};
+
+static inline Layout to_layout(const mlearn_action_layout& l) {
+    Layout r;
+    r.K = l.num_groups;
+    r.A = l.num_logits;
+    for (int i = 0; i <= MLEARN_MAX_GROUPS; ++i) r.off[i] = l.offsets[i];
+    return r;
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ logits, int64_t ld,
+                                                     Layout lay, int64_t N, uint32_t k0,
+                                                     uint32_t k1, const uint64_t* step_ctr,
+                                                     uint64_t step_add, uint32_t env_off,
+                                                     int sample, int32_t* actions, float* logp) {
+    const uint64_t step = (step_ctr ? *step_ctr : 0ull) + step_add;
+    int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (task >= N * lay.K) return;
+    int64_t n = task / lay.K;
+    int g = (int)(task % lay.K);
+    float lg[32];
+    int nb = lay.off[g + 1] - lay.off[g];
+    for (int j = 0; j < nb; ++j) lg[j] = logits[n * ld + lay.off[g] + j];
+    int a;
+    float lp;
+    sample_group(lg, nb, lay.off[g], k0, k1, env_off + (uint32_t)n, step, sample, &a, &lp);
+    actions[task] = a;
+    if (logp) logp[task] = lp;
+}
+
+__global__ __launch_bounds__(256) void action_stats_kernel(const float* __restrict__ logits,
+                                                           int64_t ld, Layout lay, int64_t N,
+                                                           const int32_t* actions, float* logp,
+                                                           float* ent) {
+    int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (task >= N * lay.K) return;
+    int64_t n = task / lay.K;
+    int g = (int)(task % lay.K);
+    const float* lg = logits + n * ld + lay.off[g];
+    int nb = lay.off[g + 1] - lay.off[g];
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    float lse = mx + __logf(se);
+    float h = 0.f;
+    for (int j = 0; j < nb; ++j) {
+        float lp = lg[j] - lse;
+        h -= __expf(lg[j] - mx) / se * lp;
+    }
+    int a = actions[task];
+    logp[task] = lg[a] - lse;
+    ent[task] = h;
+}
+
+// ---------------------------------------------------------------------------
+// Epoch permutation (ppo.py:445-458): bitonic sort of (philox key, index)
+// pairs in LDS, one workgroup.
+// ---------------------------------------------------------------------------
+constexpr int kPermMax = 16384;
+
+__global__ __launch_bounds__(1024) void perm_kernel(uint32_t k0, uint32_t k1,
+                                                    const uint64_t* epoch_ctr, uint64_t epoch_add,
+                                                    uint32_t rank, int n, int npow2,
+                                                    int32_t* perm) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+    const uint64_t epoch = (epoch_ctr ? *epoch_ctr : 0ull) + epoch_add;
+    for (int i = threadIdx.x; i < npow2; i += blockDim.x) {
+        unsigned long long k;
+        if (i < n) {
+            u32x4 r = philox4x32(u32x4{(uint32_t)i, rank, (uint32_t)epoch, (uint32_t)(epoch >> 32)},
+                                 k0, k1);
+            k = ((unsigned long long)r.x << 32) | (uint32_t)i;
+        } else {
+            k = ~0ull;
+        }
+        keys[i] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= npow2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < npow2 / 2; i += blockDim.x) {
+                int lo = 2 * i - (i & (stride - 1));
+                int hi = lo + stride;
+                bool up = (lo & size) == 0;
+                unsigned long long a = keys[lo], b = keys[hi];
+                if ((a > b) == up) {
+                    keys[lo] = b;
+                    keys[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = (int32_t)(keys[i] & 0xffffffffu);
+}
+
+// ---------------------------------------------------------------------------
+// Advantage statistics per minibatch (zscore_data, algo_common.py:133-140).
+// Grid (num_mb, kStatBlocks); sequence s -> (chunk c = s / N, env b = s % N).
+// ---------------------------------------------------------------------------
+constexpr int kStatBlocks = 32;
+
+__global__ __launch_bounds__(256) void adv_stats_kernel(mlearn_rollout_view ro,
+                                                        const int32_t* __restrict__ perm,
+                                                        int mb_size, double* part) {
+    __shared__ double sh[4];
+    int m = blockIdx.x;
+    const int32_t* seqs = perm + (int64_t)m * mb_size;
+    int64_t total = (int64_t)mb_size * ro.bptt_len;
+    double s = 0, q = 0;
+    for (int64_t i = blockIdx.y * 256 + threadIdx.x; i < total; i += (int64_t)kStatBlocks * 256) {
+        int tl = (int)(i / mb_size);
+        int j = (int)(i % mb_size);
+        int64_t seq = seqs[j];
+        int64_t c = seq / ro.N, b = seq % ro.N;
+        int64_t t = c * ro.bptt_len + tl;
+        double x = ro.advantages[t * ro.N + b];
+        s += x;
+        q += x * x;
+    }
+    s = block_sum_d<256>(s, sh);
+    q = block_sum_d<256>(q, sh);
+    if (threadIdx.x == 0) {
+        double* p = part + ((int64_t)m * kStatBlocks + blockIdx.y) * 2;
+        p[0] = s;
+        p[1] = q;
+    }
+}
+
+__global__ void adv_stats_reduce_kernel(const double* part, int num_mb, double* out) {
+    int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= num_mb) return;
+    double s = 0, q = 0;
+    for (int b = 0; b < kStatBlocks; ++b) {
+        s += part[((int64_t)m * kStatBlocks + b) * 2];
+        q += part[((int64_t)m * kStatBlocks + b) * 2 + 1];
+    }
+    out[2 * m] = s;
+    out[2 * m + 1] = q;
+}
+
+__global__ void adv_stats_finish_kernel(const double* sums, int num_mb, double count, float* st) {
+    int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= num_mb) return;
+    double mean = sums[2 * m] / count;
+    double var = sums[2 * m + 1] / count - mean * mean;
+    float fm = (float)mean, fv = (float)var;
+    st[2 * m] = fm;
+    st[2 * m + 1] = rsqrtf(fmaxf(fv, 1e-5f));
+}
+
+// ---------------------------------------------------------------------------
+// Rollout post-step (rollouts.py:933-973).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void post_step_kernel(const float* __restrict__ rew,
+                                                        const uint8_t* __restrict__ done,
+                                                        int64_t N, float* srew, uint8_t* sdone,
+                                                        float* env_ret, float* trace, float gamma) {
+#pragma clang fp contract(off)
+    int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float r = rew[n];
+    uint8_t d = done[n] ? 1 : 0;
+    float er = r + gamma * env_ret[n];
+    if (trace) trace[n] = er;
+    srew[n] = r;
+    sdone[n] = d;
+    env_ret[n] = d ? 0.f : er;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic dummy vec-env (bench/test sim plugin).
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int env_episode_len(uint32_t g) { return 16 + (int)((g * 7u) % 33u); }
+
+__device__ inline float env_obs_feature(uint32_t k0, uint32_t k1, uint32_t g, int f, uint64_t step) {
+#pragma clang fp contract(off)
+    u32x4 r = philox4x32(u32x4{g, (uint32_t)f, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
+                         k1 ^ 0x5eedu);
+    float s = ((u32_to_unit(r.x) + u32_to_unit(r.y)) + u32_to_unit(r.z)) + u32_to_unit(r.w);
+    return (s - 2.0f) * 1.73205077648162841796875f;
+}
+
+// state[n] = {episode step, env step lo, env step hi, 0}; one lane per
+// (env, feature); the f == 0 lane also advances the env and emits reward/done.
+__global__ __launch_bounds__(256) void env_step_kernel(int4* state, const int32_t* actions,
+                                                       int K, int64_t N, int D, uint32_t k0,
+                                                       uint32_t k1, uint32_t eoff, float* obs,
+                                                       float* rew, uint8_t* done) {
+#pragma clang fp contract(off)
+    int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (task >= N * D) return;
+    int64_t n = task / D;
+    int f = (int)(task % D);
+    uint32_t g = eoff + (uint32_t)n;
+    int4 st = state[n];
+    const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
+    obs[task] = env_obs_feature(k0, k1, g, f, step);
+    if (f == 0) {
+        int s = st.x + 1;
+        int L = env_episode_len(g);
+        bool d = s >= L;
+        u32x4 r = philox4x32(u32x4{g, 0x80000000u, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
+                             k1 ^ 0x5eedu);
+        float u = u32_to_unit(r.x);
+        float a0 = actions ? (float)actions[n * K] : 0.f;
+        rew[n] = (u * 2.0f - 1.0f) + 0.01f * a0;
+        done[n] = d ? 1 : 0;
+        const uint64_t ns = step + 1;
+        state[n] = make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void env_reset_kernel(int4* state, int64_t N, int D,
+                                                        uint32_t k0, uint32_t k1, uint32_t eoff,
+                                                        float* obs) {
+    int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (task >= N * D) return;
+    int64_t n = task / D;
+    int f = (int)(task % D);
+    uint32_t g = eoff + (uint32_t)n;
+    obs[task] = env_obs_feature(k0, k1, g, f, 0xffffffffffffffffull);
+    if (f == 0) state[n] = make_int4((int)(g % (uint32_t)env_episode_len(g)), 0, 0, 0);
+}
+
+struct Deltas {
+    uint64_t d[8];
+};
+__global__ void counters_add_kernel(uint64_t* ctr, int n, Deltas d) {
+    int i = threadIdx.x;
+    if (i < n) ctr[i] += d.d[i];
+}
+
+}  // namespace ml
+
+using namespace ml;
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char* mlearn_last_error(void) { return ml::g_err; }
+int mlearn_abi_version(void) { return MLEARN_ABI_VERSION; }
+
+int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, int64_t n,
+                      mlearn_stream_t stream) {
+    ML_REQUIRE(n >= 0, "philox: n < 0");
+    ML_REQUIRE(n == 0 || (ctr && out), "philox: null pointer");
+    if (n == 0) return MLEARN_OK;
+    hipLaunchKernelGGL(philox_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, S(stream),
+                       (const uint4*)ctr, k0, k1, (uint4*)out, n);
+    return check_launch("philox");
+}
+
+int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
+                   const float* bootstrap, float* advantages, float* returns, int32_t T, int64_t N,
+                   float gamma, float gae_lambda, mlearn_stream_t stream) {
+    ML_REQUIRE(T >= 0 && N >= 0, "gae: negative size");
+    if (T == 0 || N == 0) return MLEARN_OK;
+    ML_REQUIRE(rewards && values && dones && bootstrap && advantages && returns,
+               "gae: null pointer");
+    float gl = gamma * gae_lambda;  // cfg.gamma * cfg.gae_lambda (algo_common.py:120)
+    bool vec = (N % 4 == 0) && ((uintptr_t)rewards % 16 == 0) && ((uintptr_t)values % 16 == 0) &&
+               ((uintptr_t)bootstrap % 16 == 0) && ((uintptr_t)advantages % 16 == 0) &&
+               ((uintptr_t)returns % 16 == 0) && ((uintptr_t)dones % 4 == 0);
+    if (vec) {
+        hipLaunchKernelGGL(gae_kernel<4>, dim3(grid_for(N / 4, 256)), dim3(256), 0, S(stream),
+                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma, gl);
+    } else {
+        hipLaunchKernelGGL(gae_kernel<1>, dim3(grid_for(N, 256)), dim3(256), 0, S(stream),
+                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma, gl);
+    }
+    return check_launch("gae");
+}
+
+int mlearn_returns_f32(const float* rewards, const uint8_t* dones, const float* bootstrap,
+                       float* returns, int32_t T, int64_t N, float gamma, mlearn_stream_t stream) {
+    ML_REQUIRE(T >= 0 && N >= 0, "returns: negative size");
+    if (T == 0 || N == 0) return MLEARN_OK;
+    ML_REQUIRE(rewards && dones && bootstrap && returns, "returns: null pointer");
+    hipLaunchKernelGGL(returns_kernel, dim3(grid_for(N, 256)), dim3(256), 0, S(stream), rewards,
+                       dones, bootstrap, returns, T, N, gamma);
+    return check_launch("returns");
+}
+
+int64_t mlearn_zscore_workspace_bytes(int64_t n) { return 256 * 2 * sizeof(double); }
+
+int mlearn_zscore_f32(const float* x, int64_t n, float* out, void* ws, mlearn_stream_t stream) {
+    ML_REQUIRE(n > 0, "zscore: n must be > 0");
+    ML_REQUIRE(x && out && ws, "zscore: null pointer");
+    int g = grid_for(n, 256, 256);
+    hipLaunchKernelGGL(sum_partial_kernel, dim3(g), dim3(256), 0, S(stream), x, n, (double*)ws);
+    hipLaunchKernelGGL(zscore_apply_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, S(stream),
+                       x, n, (const double*)ws, g, out);
+    return check_launch("zscore");
+}
+
+static int check_layout(const mlearn_action_layout& l) {
+    ML_REQUIRE(l.num_groups >= 1 && l.num_groups <= MLEARN_MAX_GROUPS, "action layout: bad K=%d",
+               l.num_groups);
+    ML_REQUIRE(l.num_logits >= 1 && l.num_logits < MLEARN_HEAD_COLS, "action layout: bad A=%d",
+               l.num_logits);
+    ML_REQUIRE(l.offsets[0] == 0 && l.offsets[l.num_groups] == l.num_logits,
+               "action layout: offsets do not span the logits");
+    for (int k = 0; k < l.num_groups; ++k)
+        ML_REQUIRE(l.offsets[k + 1] > l.offsets[k], "action layout: empty group %d", k);
+    return MLEARN_OK;
+}
+
+int mlearn_counters_add(uint64_t* ctr, int32_t n, const uint64_t* deltas, mlearn_stream_t stream) {
+    ML_REQUIRE(ctr && deltas && n >= 1 && n <= 8, "counters_add: bad args");
+    Deltas d{};
+    for (int i = 0; i < n; ++i) d.d[i] = deltas[i];
+    hipLaunchKernelGGL(counters_add_kernel, dim3(1), dim3(64), 0, S(stream), ctr, n, d);
+    return check_launch("counters_add");
+}
+
+int mlearn_discrete_sample_f32(const float* logits, int64_t ld, mlearn_action_layout layout,
+                               int64_t N, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
+                               uint64_t step, uint32_t env_offset, int32_t sample,
+                               int32_t* actions, float* log_probs, mlearn_stream_t stream) {
+    int rc = check_layout(layout);
+    if (rc) return rc;
+    ML_REQUIRE(N >= 0 && ld >= layout.num_logits, "sample: bad N/ld");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(logits && actions && (log_probs || !sample), "sample: null pointer");
+    int64_t tasks = N * layout.num_groups;
+    hipLaunchKernelGGL(sample_kernel, dim3(grid_for(tasks, 256)), dim3(256), 0, S(stream), logits,
+                       ld, to_layout(layout), N, k0, k1, step_ctr, step, env_offset, sample,
+                       actions, log_probs);
+    return check_launch("discrete_sample");
+}
+
+int mlearn_action_stats_f32(const float* logits, int64_t ld, mlearn_action_layout layout,
+                            int64_t N, const int32_t* actions, float* log_probs, float* entropies,
+                            mlearn_stream_t stream) {
+    int rc = check_layout(layout);
+    if (rc) return rc;
+    ML_REQUIRE(N >= 0 && ld >= layout.num_logits, "action_stats: bad N/ld");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(logits && actions && log_probs && entropies, "action_stats: null pointer");
+    int64_t tasks = N * layout.num_groups;
+    hipLaunchKernelGGL(action_stats_kernel, dim3(grid_for(tasks, 256)), dim3(256), 0, S(stream),
+                       logits, ld, to_layout(layout), N, actions, log_probs, entropies);
+    return check_launch("action_stats");
+}
+
+int64_t mlearn_metrics_workspace_bytes(int32_t num_jobs) {
+    return (int64_t)num_jobs * kMetricBlocks * 4 * sizeof(double);
+}
+
+int mlearn_metrics_f32(const mlearn_metric_job* jobs, int32_t num_jobs, float* out, void* ws,
+                       mlearn_stream_t stream) {
+    ML_REQUIRE(num_jobs >= 1 && num_jobs <= 16, "metrics: 1..16 jobs");
+    ML_REQUIRE(jobs && out && ws, "metrics: null pointer");
+    MetricJobs J;
+    for (int i = 0; i < num_jobs; ++i) {
+        ML_REQUIRE(jobs[i].n >= 0 && (jobs[i].n == 0 || jobs[i].x), "metrics: bad job %d", i);
+        J.j[i] = jobs[i];
+    }
+    hipLaunchKernelGGL(metrics_partial_kernel, dim3(kMetricBlocks, num_jobs), dim3(256), 0,
+                       S(stream), J, (double*)ws);
+    hipLaunchKernelGGL(metrics_finish_kernel, dim3(num_jobs), dim3(64), 0, S(stream), J,
+                       (const double*)ws, out);
+    return check_launch("metrics");
+}
+
+int mlearn_minibatch_perm(uint32_t k0, uint32_t k1, const uint64_t* epoch_ctr, uint64_t epoch,
+                          uint32_t rank, int32_t n, int32_t* perm, mlearn_stream_t stream) {
+    ML_REQUIRE(n >= 1 && n <= kPermMax, "perm: n must be in [1, %d], got %d", kPermMax, n);
+    ML_REQUIRE(perm, "perm: null pointer");
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)perm_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kPermMax * (int)sizeof(unsigned long long));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(perm_kernel, dim3(1), dim3(1024), p2 * sizeof(unsigned long long),
+                       S(stream), k0, k1, epoch_ctr, epoch, rank, n, p2, perm);
+    return check_launch("minibatch_perm");
+}
+
+int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
+                     int32_t mb_size, double* partials, mlearn_stream_t stream) {
+    ML_REQUIRE(ro && perm && partials, "adv_stats: null pointer");
+    ML_REQUIRE(num_mb >= 1 && mb_size >= 1, "adv_stats: bad minibatch sizes");
+    ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "adv_stats: bad bptt_len");
+    ML_REQUIRE((int64_t)num_mb * mb_size <= (ro->T / ro->bptt_len) * ro->N,
+               "adv_stats: minibatches exceed the sequences");
+    // partials layout: [num_mb][kStatBlocks][2] scratch followed by [num_mb][2] sums
+    double* scratch = partials + 2 * num_mb;
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb, kStatBlocks), dim3(256), 0, S(stream), *ro,
+                       perm, mb_size, scratch);
+    hipLaunchKernelGGL(adv_stats_reduce_kernel, dim3((num_mb + 63) / 64), dim3(64), 0, S(stream),
+                       (const double*)scratch, num_mb, partials);
+    return check_launch("adv_stats");
+}
+
+int mlearn_adv_stats_finish(const double* partials, int32_t num_mb, double count, float* stats,
+                            mlearn_stream_t stream) {
+    ML_REQUIRE(partials && stats && num_mb >= 1 && count > 0, "adv_stats_finish: bad args");
+    hipLaunchKernelGGL(adv_stats_finish_kernel, dim3((num_mb + 63) / 64), dim3(64), 0, S(stream),
+                       partials, num_mb, count, stats);
+    return check_launch("adv_stats_finish");
+}
+
+int mlearn_rollout_post_step(const float* rewards, const uint8_t* dones, int64_t N,
+                             float* store_rewards, uint8_t* store_dones, float* env_returns,
+                             float* env_returns_trace, float gamma, mlearn_stream_t stream) {
+    ML_REQUIRE(N >= 0, "post_step: N < 0");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(rewards && dones && store_rewards && store_dones && env_returns,
+               "post_step: null pointer");
+    hipLaunchKernelGGL(post_step_kernel, dim3(grid_for(N, 256)), dim3(256), 0, S(stream), rewards,
+                       dones, N, store_rewards, store_dones, env_returns, env_returns_trace, gamma);
+    return check_launch("post_step");
+}
+
+int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int64_t N,
+                          int32_t obs_dim, uint32_t k0, uint32_t k1, uint32_t env_offset,
+                          float* obs, float* rewards, uint8_t* dones, mlearn_stream_t stream) {
+    ML_REQUIRE(N >= 0 && obs_dim >= 1 && K >= 1, "env_step: bad sizes");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(state && obs && rewards && dones, "env_step: null pointer");
+    ML_REQUIRE((uintptr_t)state % 16 == 0, "env_step: state must be 16-byte aligned");
+    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(N * obs_dim, 256)), dim3(256), 0, S(stream),
+                       (int4*)state, actions, K, N, obs_dim, k0, k1, env_offset, obs, rewards,
+                       dones);
+    return check_launch("env_step");
+}
+
+int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t k0, uint32_t k1,
+                           uint32_t env_offset, float* obs, mlearn_stream_t stream) {
+    ML_REQUIRE(N >= 0 && obs_dim >= 1, "env_reset: bad sizes");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(state && obs, "env_reset: null pointer");
+    ML_REQUIRE((uintptr_t)state % 16 == 0, "env_reset: state must be 16-byte aligned");
+    hipLaunchKernelGGL(env_reset_kernel, dim3(grid_for(N * obs_dim, 256)), dim3(256), 0,
+                       S(stream), (int4*)state, N, obs_dim, k0, k1, env_offset, obs);
+    return check_launch("env_reset");
+}
+
+}  // extern "C"

@@ -1,0 +1,250 @@
+// Optimizer step (ppo.py:283-338):
+//   optax.chain(clip_by_global_norm(max_grad_norm), adam(lr))  (ppo.py:84-90)
+//   -> weight-norm re-projection of every backbone kernel to its initial
+//      Frobenius norm (ppo.py:303-310, train_state.py:413-423)
+//   -> LayerNorm renorm so that |scale|^2 + |bias|^2 = features (ppo.py:312-338)
+//   -> refresh of the compute-dtype weight copies the MLP kernels read
+//      (transposed [out][in] and [in][out] images, padded head).
+// Five short launches over the flat 90K-float parameter vector; global
+// reductions go through fixed-order double partials (deterministic).
+
+#include "common.h"
+#include "mlp_tile.h"
+
+namespace ml {
+
+constexpr int kNormBlocks = 64;
+
+struct CopiesK {
+    void* wt[MLEARN_MAX_LAYERS];
+    void* w[MLEARN_MAX_LAYERS];
+    void* head_t;
+    void* head;
+    float* head_b;
+};
+
+static CopiesK make_copies(const mlearn_mlp_policy& p) {
+    CopiesK c;
+    for (int l = 0; l < MLEARN_MAX_LAYERS; ++l) {
+        c.wt[l] = (void*)p.w_t[l];
+        c.w[l] = (void*)p.w[l];
+    }
+    c.head_t = (void*)p.head_t;
+    c.head = (void*)p.head;
+    c.head_b = (float*)p.head_bias;
+    return c;
+}
+
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
+                                                            double* part) {
+    __shared__ double sh[4];
+    double s = 0;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        double v = g[i];
+        s += v * v;
+    }
+    s = wave_sum64d(s);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+__global__ void sumsq_finish_kernel(const double* part, int nparts, float* out) {
+    if (threadIdx.x == 0) {
+        double s = 0;
+        for (int i = 0; i < nparts; ++i) s += part[i];
+        out[0] = sqrtf((float)s);  // optax.global_norm in f32
+    }
+}
+
+// tensor id of parameter p for the projection partials: 2*l = W_l, 2*l+1 = LN_l, -1 = head
+__device__ inline int proj_slot(const LayoutK& k, int64_t p) {
+    if (p >= k.hw_off) return -1;
+    int l = k.L - 1;
+    while (l > 0 && p < k.w_off[l]) --l;
+    return p < k.s_off[l] ? 2 * l : 2 * l + 1;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict__ params,
+                                                   const float* __restrict__ grads,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   const int32_t* step, const float* gnorm, float lr,
+                                                   float b1, float b2, float eps, float max_norm,
+                                                   double* proj_part) {
+    __shared__ float sh[4][2 * MLEARN_MAX_LAYERS];
+    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
+    const int nslot = 2 * Lk.L;
+    float contrib = 0.f;
+    int slot = -2;
+    if (p < Lk.total) {
+        const float gn = gnorm[0];
+        float g = grads[p];
+        if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
+        const int count = step[0] + 1;
+        const float mm = (1.f - b1) * g + b1 * m[p];
+        const float vv = (1.f - b2) * (g * g) + b2 * v[p];
+        const float mhat = mm / (1.f - powf(b1, (float)count));
+        const float vhat = vv / (1.f - powf(b2, (float)count));
+        const float u = mhat / (sqrtf(vhat) + eps);
+        const float np = params[p] + (-lr) * u;
+        m[p] = mm;
+        v[p] = vv;
+        params[p] = np;
+        slot = proj_slot(Lk, p);
+        contrib = np * np;
+    }
+    // per-block partial sums of squares per projection slot
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int s = 0; s < nslot; ++s) {
+        float x = slot == s ? contrib : 0.f;
+        x = wave_sum64(x);
+        if (lane == 0) sh[w][s] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < nslot) {
+        int s = threadIdx.x;
+        proj_part[blockIdx.x * (int64_t)nslot + s] =
+            ((double)sh[0][s] + sh[1][s]) + ((double)sh[2][s] + sh[3][s]);
+    }
+}
+
+__global__ void proj_finish_kernel(const double* part, int nblocks, int nslot, float* out) {
+    int s = threadIdx.x;
+    if (s >= nslot) return;
+    double t = 0;
+    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * nslot + s];
+    out[s] = (float)t;
+}
+
+template <typename T>
+__device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t p, float val) {
+    const int H = Lk.H;
+    if (p >= Lk.hb_off) {
+        C.head_b[p - Lk.hb_off] = val;
+    } else if (p >= Lk.hw_off) {
+        int64_t q = p - Lk.hw_off;
+        int c = (int)(q / Lk.A1), k = (int)(q % Lk.A1);
+        ((T*)C.head_t)[(int64_t)k * H + c] = cvt<T>(val);
+        ((T*)C.head)[(int64_t)c * MLEARN_HEAD_COLS + k] = cvt<T>(val);
+    } else {
+        int l = Lk.L - 1;
+        while (l > 0 && p < Lk.w_off[l]) --l;
+        if (p < Lk.s_off[l]) {
+            const int in = l == 0 ? Lk.D : H;
+            int64_t q = p - Lk.w_off[l];
+            int i = (int)(q / H), j = (int)(q % H);
+            ((T*)C.wt[l])[(int64_t)j * in + i] = cvt<T>(val);
+            ((T*)C.w[l])[(int64_t)i * H + j] = cvt<T>(val);
+        }
+        // LayerNorm scale/bias are read in f32 straight from the master params.
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, float* params,
+                                                      const float* init_norms, const float* sq,
+                                                      int norm_params, int norm_ln, int32_t* step) {
+    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
+    if (p == 0 && step) step[0] += 1;
+    if (p >= Lk.total) return;
+    float val = params[p];
+    const int slot = proj_slot(Lk, p);
+    if (slot >= 0) {
+        const int l = slot >> 1;
+        if ((slot & 1) == 0) {
+            if (norm_params) val = (init_norms[l] * val) / sqrtf(sq[slot]);  // ppo.py:307
+        } else if (norm_ln) {
+            // sqrt(F / (b.b + s.s)) (ppo.py:324-325)
+            val = sqrtf((float)Lk.H / sq[slot]) * val;
+        }
+        params[p] = val;
+    }
+    write_copies<T>(Lk, C, p, val);
+}
+
+// compute copies from params without any projection; zero the head padding
+template <typename T>
+__global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const float* params) {
+    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
+    const int H = Lk.H;
+    // padding: head_t rows A1..31, head cols A1..31, head_b A1..31
+    const int64_t pad = (int64_t)(MLEARN_HEAD_COLS - Lk.A1) * H;
+    if (p < pad) {
+        int k = Lk.A1 + (int)(p / H), c = (int)(p % H);
+        ((T*)C.head_t)[(int64_t)k * H + c] = cvt<T>(0.f);
+        ((T*)C.head)[(int64_t)c * MLEARN_HEAD_COLS + k] = cvt<T>(0.f);
+        if (c == 0) C.head_b[k] = 0.f;
+    }
+    if (p < Lk.total) write_copies<T>(Lk, C, p, params[p]);
+}
+
+static int64_t optim_ws_doubles(const LayoutK& k) {
+    int64_t nblk = (k.total + 255) / 256;
+    return kNormBlocks + nblk * 2 * k.L + 8 + 2 * MLEARN_MAX_LAYERS + 8;
+}
+
+}  // namespace ml
+
+using namespace ml;
+
+extern "C" {
+
+int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy) {
+    if (validate_policy(policy)) return -1;
+    return optim_ws_doubles(make_layout(*policy)) * (int64_t)sizeof(double);
+}
+
+int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state* st,
+                      void* workspace, mlearn_stream_t stream) {
+    int rc = validate_policy(policy);
+    if (rc) return rc;
+    ML_REQUIRE(st && st->params && st->grads && st->adam_m && st->adam_v && st->init_norms &&
+                   st->step && workspace,
+               "optim_step: null pointer");
+    ML_REQUIRE(st->max_grad_norm > 0 && st->lr >= 0, "optim_step: bad hyperparameters");
+    LayoutK Lk = make_layout(*policy);
+    hipStream_t s = S(stream);
+    const int64_t nblk = (Lk.total + 255) / 256;
+    double* gpart = (double*)workspace;
+    double* ppart = gpart + kNormBlocks;
+    float* gnorm = (float*)(ppart + nblk * 2 * Lk.L);
+    float* sq = gnorm + 16;
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
+                       Lk.total, gpart);
+    hipLaunchKernelGGL(sumsq_finish_kernel, dim3(1), dim3(64), 0, s, (const double*)gpart,
+                       kNormBlocks, gnorm);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk), dim3(256), 0, s, Lk, st->params,
+                       st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
+                       (const float*)gnorm, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
+                       ppart);
+    hipLaunchKernelGGL(proj_finish_kernel, dim3(1), dim3(64), 0, s, (const double*)ppart,
+                       (int)nblk, 2 * Lk.L, sq);
+    CopiesK C = make_copies(*policy);
+    if (policy->dtype == MLEARN_DTYPE_BF16)
+        hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
+                           st->params, st->init_norms, (const float*)sq, st->normalize_params,
+                           st->normalize_layernorms, st->step);
+    else
+        hipLaunchKernelGGL(project_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
+                           st->params, st->init_norms, (const float*)sq, st->normalize_params,
+                           st->normalize_layernorms, st->step);
+    return check_launch("optim_step");
+}
+
+int mlearn_policy_sync_weights(const mlearn_mlp_policy* policy, const float* params,
+                               mlearn_stream_t stream) {
+    int rc = validate_policy(policy);
+    if (rc) return rc;
+    ML_REQUIRE(params, "sync_weights: null params");
+    LayoutK Lk = make_layout(*policy);
+    CopiesK C = make_copies(*policy);
+    int64_t n = Lk.total > (int64_t)MLEARN_HEAD_COLS * Lk.H ? Lk.total : (int64_t)MLEARN_HEAD_COLS * Lk.H;
+    unsigned g = (unsigned)((n + 255) / 256);
+    if (policy->dtype == MLEARN_DTYPE_BF16)
+        hipLaunchKernelGGL(sync_kernel<bf16>, dim3(g), dim3(256), 0, S(stream), Lk, C, params);
+    else
+        hipLaunchKernelGGL(sync_kernel<float>, dim3(g), dim3(256), 0, S(stream), Lk, C, params);
+    return check_launch("sync_weights");
+}
+
+}  // extern "C"

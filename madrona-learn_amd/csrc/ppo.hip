@@ -1,0 +1,661 @@
+// PPO minibatch step up to the flat gradient (ppo.py:109-364):
+//
+//   ppo_fwd   per 64-row tile: gather the minibatch rows straight from the
+//             [T][N] rollout store (no RolloutData.minibatch copy,
+//             rollouts.py:319-329), MLP trunk + heads, PPO loss terms
+//             (ppo.py:129-262) and d loss / d {logits, value}.
+//   ppo_bwd   per 64-row tile: back through heads, ReLU and LayerNorm of
+//             every layer (row-local), writing dZ_l and LayerNorm
+//             scale/bias partials.
+//   wgrad     dW = X^T dZ over all rows (split-K slabs, MFMA with the
+//             rows as the reduction axis staged transposed through LDS).
+//   reduce    fixed-order sum of slabs and tile partials into the flat f32
+//             gradient + loss/metric outputs.  Deterministic: no atomics.
+//
+// Minibatch row f (time-major like mb['obs'] of shape [T/C, mb]):
+//   tl = f / mb, m = f % mb, seq = mb_seq[m], c = seq / N, b = seq % N,
+//   store row = (c * bptt + tl) * N + b.
+
+#include "common.h"
+#include "mlp_tile.h"
+
+namespace ml {
+
+struct RolloutK {
+    const void* obs;
+    const int32_t* actions;
+    const float* logp;
+    const float* adv;
+    const float* ret;
+    const float* values;
+    int T, bptt;
+    int64_t N;
+};
+
+struct HpK {
+    float clip, vcoef;
+    float ecoef[MLEARN_MAX_GROUPS];
+    int norm_adv, clip_vl, huber;
+    float loss_scale;
+    float inv_sk, inv_s;
+};
+
+constexpr int kSplits = 16;
+constexpr int kLossSlots = 20;  // per tile doubles
+
+struct WsK {
+    void* x0;
+    void* z[MLEARN_MAX_LAYERS];
+    float* st[MLEARN_MAX_LAYERS];
+    void* a[MLEARN_MAX_LAYERS];
+    void* dhead;
+    void* dz[MLEARN_MAX_LAYERS];
+    float* ln_part;    // [tiles][L][2 rb][2 (beta, gamma)][H]
+    float* hb_part;    // [tiles][32]
+    double* loss_part; // [tiles][kLossSlots]
+    float* slab;       // [splits][sum of weight sizes]
+    int64_t slab_stride;
+    int64_t slab_off[MLEARN_MAX_LAYERS + 1];  // layer weights, then head [H][32]
+    int ntiles;
+};
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Carve the workspace; returns total bytes (ws may be null to size only).
+static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
+    const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
+    const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
+    const int64_t tiles = (M + kTileRows - 1) / kTileRows;
+    const int64_t Mp = tiles * kTileRows;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* ptr = base ? base + off : nullptr;
+        off = align256(off + bytes);
+        return (void*)ptr;
+    };
+    WsK w{};
+    w.x0 = take(Mp * D * es);
+    for (int l = 0; l < L; ++l) {
+        w.z[l] = take(Mp * H * es);
+        w.st[l] = (float*)take(Mp * 2 * sizeof(float));
+        w.a[l] = take(Mp * H * es);
+        w.dz[l] = take(Mp * H * es);
+    }
+    w.dhead = take(Mp * MLEARN_HEAD_COLS * es);
+    w.ln_part = (float*)take(tiles * L * 2 * 2 * H * sizeof(float));
+    w.hb_part = (float*)take(tiles * MLEARN_HEAD_COLS * sizeof(float));
+    w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
+    int64_t so = 0;
+    for (int l = 0; l < L; ++l) {
+        w.slab_off[l] = so;
+        so += (int64_t)(l == 0 ? D : H) * H;
+    }
+    w.slab_off[L] = so;
+    so += (int64_t)H * MLEARN_HEAD_COLS;
+    w.slab_stride = so;
+    w.slab = (float*)take(kSplits * so * sizeof(float));
+    w.ntiles = (int)tiles;
+    if (W) *W = w;
+    return off;
+}
+
+// ---------------------------------------------------------------------------
+// Forward + loss + d(loss)/d(head outputs)
+// ---------------------------------------------------------------------------
+template <typename T, int H>
+__global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
+                                                      const int32_t* __restrict__ mb_seq, int mb,
+                                                      int64_t M, const float* __restrict__ adv_st,
+                                                      HpK hp, WsK ws) {
+    constexpr int NB = H / 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int D = P.D;
+    const int ld = (D > H ? D : H) + Pad<T>::v;
+    T* act = (T*)smem;
+    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));
+    float* lgt = red + 4 * 64 * 2;                   // [64][33]
+    float* dl = lgt + kTileRows * 33;                // [64][33] d loss / d head
+    int64_t* srow = (int64_t*)(dl + kTileRows * 33); // [64]
+    double* dred = (double*)(srow + kTileRows);      // [4][kLossSlots]
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
+
+    if (tid < kTileRows) {
+        int64_t f = row0 + tid;
+        int64_t sr = -1;
+        if (f < M) {
+            int tl = (int)(f / mb);
+            int m = (int)(f - (int64_t)tl * mb);
+            int64_t seq = mb_seq[m];
+            int64_t c = seq / ro.N, b = seq - c * ro.N;
+            sr = (c * ro.bptt + tl) * ro.N + b;
+        }
+        srow[tid] = sr;
+    }
+    __syncthreads();
+
+    // gather the observation rows
+    const T* obs = (const T*)ro.obs;
+    T* x0 = (T*)ws.x0;
+    for (int idx = tid; idx < kTileRows * D; idx += 256) {
+        int rr = idx / D, c = idx - rr * D;
+        int64_t sr = srow[rr];
+        T v = sr >= 0 ? obs[sr * D + c] : cvt<T>(0.f);
+        act[rr * ld + c] = v;
+        if (sr >= 0) x0[(row0 + rr) * D + c] = v;
+    }
+    __syncthreads();
+
+    for (int l = 0; l < P.L; ++l) {
+        const int K = l == 0 ? D : H;
+        f32x16 acc[NB];
+        zero_acc<NB>(acc);
+        tile_gemm<T, NB>(acc, act, ld, w & 1, (const T*)P.wt[l], K, K, w, lane);
+        __syncthreads();
+        ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, row0, M,
+                                (T*)ws.z[l], ws.st[l], (T*)ws.a[l]);
+        __syncthreads();
+    }
+    heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
+    __syncthreads();
+
+    // loss terms: tasks (row, group) then (row, value)
+    const float adv_mean = adv_st[0], adv_rstd = adv_st[1];
+    double sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
+    float mnobj = 3.4e38f, mxobj = -3.4e38f, mnent = 3.4e38f, mxent = -3.4e38f;
+    float mnvl = 3.4e38f, mxvl = -3.4e38f, mnerr = 3.4e38f, mxerr = -3.4e38f;
+    const int K = P.K, A = P.A;
+    for (int task = tid; task < kTileRows * (K + 1); task += 256) {
+        int rr = task / (K + 1), g = task - rr * (K + 1);
+        int64_t sr = srow[rr];
+        if (sr < 0) {
+            if (g == K)
+                for (int j = 0; j < 33; ++j) dl[rr * 33 + j] = 0.f;
+            continue;
+        }
+        if (g < K) {
+            const float* lg = &lgt[rr * 33 + P.off[g]];
+            const int nb = P.off[g + 1] - P.off[g];
+            float mx = lg[0];
+            for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+            float se = 0.f;
+            for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+            const float lse = mx + __logf(se);
+            float ent = 0.f;
+            for (int j = 0; j < nb; ++j) {
+                float lp = lg[j] - lse;
+                ent -= (__expf(lg[j] - mx) / se) * lp;  // softmax * log_softmax (dists.py:68-69)
+            }
+            const int a = ro.actions[sr * K + g];
+            const float lpa = lg[a] - lse;
+            const float old = ro.logp[sr * K + g];
+            float adv = ro.adv[sr];
+            if (hp.norm_adv) adv = (adv - adv_mean) * adv_rstd;
+            const float ratio = __expf(lpa - old);
+            const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
+            const float s1 = adv * ratio;
+            const float y = fmaxf(ratio, lo);
+            const float cr = fminf(y, hi);
+            const float s2 = adv * cr;
+            const float obj = fminf(s1, s2);
+            // JAX's balanced min/max derivatives (0.5 on ties)
+            const float dmx = ratio > lo ? 1.f : (ratio == lo ? 0.5f : 0.f);
+            const float dmn = y < hi ? 1.f : (y == hi ? 0.5f : 0.f);
+            const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+            const float dobj = w1 * adv + (1.f - w1) * adv * (dmx * dmn);
+            const float g_lp = -hp.inv_sk * dobj * ratio;          // d loss / d logp[a]
+            const float ce = hp.ecoef[g] * hp.inv_sk;               // entropy term weight
+            for (int j = 0; j < nb; ++j) {
+                float p = __expf(lg[j] - mx) / se;
+                float lp = lg[j] - lse;
+                float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * (lp + ent);
+                dl[rr * 33 + P.off[g] + j] = d * hp.loss_scale;
+            }
+            sobj += obj;
+            qobj += (double)obj * obj;
+            mnobj = fminf(mnobj, obj);
+            mxobj = fmaxf(mxobj, obj);
+            sent += ent;
+            qent += (double)ent * ent;
+            mnent = fminf(mnent, ent);
+            mxent = fmaxf(mxent, ent);
+            sentw += (double)hp.ecoef[g] * ent;
+        } else {
+            const float V = lgt[rr * 33 + A];
+            const float R = ro.ret[sr];
+            float vpred = V, dvp = 1.f;
+            if (hp.clip_vl) {  // ppo.py:197-203
+                const float ov = ro.values[sr];
+                const float vlo = ov - hp.clip, vhi = ov + hp.clip;
+                const float yy = fmaxf(V, vlo);
+                vpred = fminf(yy, vhi);
+                dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) * (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
+            }
+            const float e = vpred - R;
+            float vl, dvl;
+            if (hp.huber) {  // optax.huber_loss, delta = 1
+                const float ae = fabsf(e);
+                const float quad = fminf(ae, 1.f);
+                vl = 0.5f * quad * quad + (ae - quad);
+                dvl = ae < 1.f ? e : (e > 0.f ? 1.f : -1.f);
+            } else {         // optax.l2_loss
+                vl = 0.5f * e * e;
+                dvl = e;
+            }
+            dl[rr * 33 + A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
+            for (int j = A + 1; j < 33; ++j) dl[rr * 33 + j] = 0.f;
+            const float verr = fabsf(V - R);
+            svl += vl;
+            qvl += (double)vl * vl;
+            mnvl = fminf(mnvl, vl);
+            mxvl = fmaxf(mxvl, vl);
+            serr += verr;
+            qerr += (double)verr * verr;
+            mnerr = fminf(mnerr, verr);
+            mxerr = fmaxf(mxerr, verr);
+        }
+    }
+    __syncthreads();
+
+    // d head -> HBM (compute dtype), head-bias partial sums
+    T* dh = (T*)ws.dhead;
+    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
+        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
+        int64_t f = row0 + rr;
+        if (f < M) dh[f * MLEARN_HEAD_COLS + j] = cvt<T>(dl[rr * 33 + j]);
+    }
+    if (tid < MLEARN_HEAD_COLS) {
+        float s = 0.f;
+        for (int rr = 0; rr < kTileRows; ++rr) s += rnd<T>(dl[rr * 33 + tid]);
+        ws.hb_part[(int64_t)blockIdx.x * MLEARN_HEAD_COLS + tid] = s;
+    }
+
+    // tile loss/metric partials
+    double vals[kLossSlots] = {sobj, qobj, mnobj, mxobj, svl, qvl, mnvl, mxvl,
+                               serr, qerr, mnerr, mxerr, sent, qent, mnent, mxent, sentw, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < kLossSlots; ++s) {
+        double v = vals[s];
+        const int kind = (s < 16) ? (s & 3) : 0;  // 0,1 sum; 2 min; 3 max
+        for (int o = 1; o < 64; o <<= 1) {
+            double u = __shfl_xor(v, o);
+            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
+        }
+        if (lane == 0) dred[w * kLossSlots + s] = v;
+    }
+    __syncthreads();
+    if (tid < kLossSlots) {
+        const int kind = (tid < 16) ? (tid & 3) : 0;
+        double v = dred[tid];
+        for (int ww = 1; ww < 4; ++ww) {
+            double u = dred[ww * kLossSlots + tid];
+            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
+        }
+        ws.loss_part[(int64_t)blockIdx.x * kLossSlots + tid] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Backward through heads and the trunk (row-local)
+// ---------------------------------------------------------------------------
+template <typename T, int H>
+__global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK ws) {
+    constexpr int NB = H / 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int ld = H + Pad<T>::v;
+    const int ldh = MLEARN_HEAD_COLS + Pad<T>::v;
+    T* act = (T*)smem;
+    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rb = w & 1, r = lane & 31;
+    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
+
+    const T* dh = (const T*)ws.dhead;
+    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
+        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
+        int64_t f = row0 + rr;
+        act[rr * ldh + j] = f < M ? dh[f * MLEARN_HEAD_COLS + j] : cvt<T>(0.f);
+    }
+    __syncthreads();
+
+    f32x16 acc[NB];
+    zero_acc<NB>(acc);
+    // dA_{L-1} = dHead . Head^T    (B^T = head [H][32])
+    tile_gemm<T, NB>(acc, act, ldh, rb, (const T*)P.head, MLEARN_HEAD_COLS, MLEARN_HEAD_COLS, w,
+                     lane);
+
+    for (int l = P.L - 1; l >= 0; --l) {
+        __syncthreads();
+        const T* z = (const T*)ws.z[l];
+        const float* st = ws.st[l];
+        const float* gamma = P.lns[l];
+        const float* beta = P.lnb[l];
+        float u[NB][16], v[NB][16], xh[NB][16];
+        float mean[16], rstd[16];
+        float pg[NB], pb[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) pg[i] = pb[i] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t f = row0 + rb * 32 + acc_row(e, lane);
+            const bool live = f < M;
+            mean[e] = live ? st[f * 2] : 0.f;
+            rstd[e] = live ? st[f * 2 + 1] : 0.f;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int col = ((w >> 1) + 2 * i) * 32 + r;
+                float zz = live ? to_f32(z[f * H + col]) : 0.f;
+                float x = (zz - mean[e]) * rstd[e];
+                float y = (zz - mean[e]) * (rstd[e] * gamma[col]) + beta[col];
+                float dy = (live && rnd<T>(y) > 0.f) ? acc[i][e] : 0.f;  // ReLU'
+                xh[i][e] = x;
+                u[i][e] = dy * gamma[col];
+                v[i][e] = u[i][e] * x;
+                pg[i] += dy * x;
+                pb[i] += dy;
+            }
+        }
+        // LayerNorm scale/bias partials: fold the two half-waves, one writer per column
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            pg[i] += __shfl_xor(pg[i], 32);
+            pb[i] += __shfl_xor(pb[i], 32);
+            if (lane < 32) {
+                const int col = ((w >> 1) + 2 * i) * 32 + r;
+                float* lp = ws.ln_part + ((((int64_t)blockIdx.x * P.L + l) * 2 + rb) * 2) * H;
+                lp[col] = pb[i];
+                lp[H + col] = pg[i];
+            }
+        }
+        float su[16], sv[16];
+        row_sums2<NB>(u, v, su, sv, red, w, lane);
+        const float invH = 1.0f / (float)H;
+        T* dzo = (T*)ws.dz[l];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = rb * 32 + acc_row(e, lane);
+            const int64_t f = row0 + row;
+            const float mu = su[e] * invH, mv = sv[e] * invH;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int col = ((w >> 1) + 2 * i) * 32 + r;
+                float dz = rstd[e] * (u[i][e] - mu - xh[i][e] * mv);
+                T dzt = cvt<T>(dz);
+                act[row * ld + col] = dzt;
+                if (f < M) dzo[f * H + col] = dzt;
+            }
+        }
+        if (l > 0) {
+            __syncthreads();
+            zero_acc<NB>(acc);
+            // dA_{l-1} = dZ_l . W_l^T   (B^T = W_l [in][H])
+            tile_gemm<T, NB>(acc, act, ld, rb, (const T*)P.w[l], H, H, w, lane);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient: C[i][j] = sum_r X[r][i] * Y[r][j] over this split's rows.
+// Tile 64 (i) x 64 (j), 4 waves = 2x2 32x32 blocks; rows staged transposed
+// through LDS in chunks of 128.
+// ---------------------------------------------------------------------------
+constexpr int kWgChunk = 128;
+
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_kernel(const T* __restrict__ X, int ldx,
+                                                    const T* __restrict__ Y, int ldy, int64_t M,
+                                                    int I, int J, int64_t rows_per_split,
+                                                    float* slab, int64_t slab_stride) {
+    constexpr int E = MT<T>::E, KS = MT<T>::KS;
+    constexpr int LDT = kWgChunk + Pad<T>::v;
+    __shared__ __attribute__((aligned(16))) T XT[64 * LDT];
+    __shared__ __attribute__((aligned(16))) T YT[64 * LDT];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ib = w & 1, jb = w >> 1, r = lane & 31, h = lane >> 5;
+    const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+    const int64_t rbeg = blockIdx.z * rows_per_split;
+    const int64_t rend = rbeg + rows_per_split < M ? rbeg + rows_per_split : M;
+    const bool active = j0 + jb * 32 < J;
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    for (int64_t rc = rbeg; rc < rend; rc += kWgChunk) {
+        for (int idx = tid; idx < kWgChunk * 64; idx += 256) {
+            int rr = idx >> 6, c = idx & 63;
+            int64_t row = rc + rr;
+            bool ok = row < rend;
+            XT[c * LDT + rr] = (ok && i0 + c < I) ? X[row * ldx + i0 + c] : cvt<T>(0.f);
+            YT[c * LDT + rr] = (ok && j0 + c < J) ? Y[row * ldy + j0 + c] : cvt<T>(0.f);
+        }
+        __syncthreads();
+        if (active) {
+            const T* ap = XT + (ib * 32 + r) * LDT + h * E;
+            const T* bp = YT + (jb * 32 + r) * LDT + h * E;
+#pragma unroll 4
+            for (int k0 = 0; k0 < kWgChunk; k0 += KS)
+                acc[0] = MT<T>::mma(MT<T>::load(ap + k0), MT<T>::load(bp + k0), acc[0]);
+        }
+        __syncthreads();
+    }
+    if (active) {
+        float* out = slab + blockIdx.z * slab_stride;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            int i = i0 + ib * 32 + acc_row(e, lane);
+            int j = j0 + jb * 32 + r;
+            if (i < I && j < J) out[(int64_t)i * J + j] = acc[0][e];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-order reduction into the flat gradient.
+// ---------------------------------------------------------------------------
+LayoutK make_layout(const mlearn_mlp_policy& p) {
+    LayoutK k{};
+    k.L = p.num_layers;
+    k.D = p.obs_dim;
+    k.H = p.hidden;
+    k.A1 = p.actions.num_logits + 1;
+    int64_t o = 0;
+    for (int l = 0; l < k.L; ++l) {
+        k.w_off[l] = o;
+        o += (int64_t)(l == 0 ? k.D : k.H) * k.H;
+        k.s_off[l] = o;
+        o += k.H;
+        k.b_off[l] = o;
+        o += k.H;
+    }
+    k.hw_off = o;
+    o += (int64_t)k.H * k.A1;
+    k.hb_off = o;
+    o += k.A1;
+    k.total = o;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad) {
+    int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
+    if (p >= Lk.total) return;
+    const int H = Lk.H;
+    float g = 0.f;
+    if (p >= Lk.hb_off) {
+        int j = (int)(p - Lk.hb_off);
+        for (int t = 0; t < ws.ntiles; ++t) g += ws.hb_part[(int64_t)t * MLEARN_HEAD_COLS + j];
+    } else if (p >= Lk.hw_off) {
+        int64_t q = p - Lk.hw_off;
+        int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
+        const float* s = ws.slab + ws.slab_off[Lk.L] + (int64_t)i * MLEARN_HEAD_COLS + j;
+        for (int k = 0; k < kSplits; ++k) g += s[k * ws.slab_stride];
+    } else {
+        int l = Lk.L - 1;
+        while (l > 0 && p < Lk.w_off[l]) --l;
+        if (p >= Lk.b_off[l] || p >= Lk.s_off[l]) {
+            const int which = p >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
+            const int col = (int)(p - (which ? Lk.s_off[l] : Lk.b_off[l]));
+            for (int t = 0; t < ws.ntiles; ++t)
+                for (int rb = 0; rb < 2; ++rb)
+                    g += ws.ln_part[((((int64_t)t * Lk.L + l) * 2 + rb) * 2 + which) * H + col];
+        } else {
+            const float* s = ws.slab + ws.slab_off[l] + (p - Lk.w_off[l]);
+            for (int k = 0; k < kSplits; ++k) g += s[k * ws.slab_stride];
+        }
+    }
+    grad[p] = g;
+}
+
+// loss_out: five Metric vectors {mean, m2, min, max, count} in the order of
+// PPO.add_metrics (ppo.py:95-106): 'Loss' (scalar: {loss, 0, loss, loss, 1}),
+// 'Action Obj', 'Value Loss', 'Value Errors', 'Entropy'.
+__global__ void reduce_loss_kernel(WsK ws, HpK hp, int64_t M, int K, float* out) {
+    __shared__ double tot[kLossSlots];
+    int s = threadIdx.x;
+    if (s < kLossSlots) {
+        const int kind = (s < 16) ? (s & 3) : 0;
+        double v = ws.loss_part[s];
+        for (int t = 1; t < ws.ntiles; ++t) {
+            double u = ws.loss_part[(int64_t)t * kLossSlots + s];
+            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
+        }
+        tot[s] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double nk = (double)M * K, n = (double)M;
+        const double obj_mean = tot[0] / nk, vl_mean = tot[4] / n;
+        // loss = -mean(obj) + c_v * mean(vl) - sum_k c_e[k] * mean(H_k)   (ppo.py:241-252)
+        const double loss = -obj_mean + hp.vcoef * vl_mean - tot[16] / nk;
+        out[0] = (float)loss;
+        out[1] = 0.f;
+        out[2] = (float)loss;
+        out[3] = (float)loss;
+        out[4] = 1.f;
+        const double cnt[4] = {nk, n, n, nk};
+        for (int m = 0; m < 4; ++m) {
+            double mean = tot[4 * m] / cnt[m];
+            double m2 = tot[4 * m + 1] - cnt[m] * mean * mean;
+            out[5 + 5 * m + 0] = (float)mean;
+            out[5 + 5 * m + 1] = (float)(m2 > 0 ? m2 : 0);
+            out[5 + 5 * m + 2] = (float)tot[4 * m + 2];
+            out[5 + 5 * m + 3] = (float)tot[4 * m + 3];
+            out[5 + 5 * m + 4] = (float)cnt[m];
+        }
+    }
+}
+
+static size_t fwd_lds(int D, int H, int es) {
+    int ld = (D > H ? D : H) + 16 / es;
+    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4 + 2 * kTileRows * 33 * 4 + kTileRows * 8 +
+           4 * kLossSlots * 8;
+}
+static size_t bwd_lds(int H, int es) {
+    int ld = H + 16 / es;
+    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4;
+}
+
+template <typename T, int H>
+static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
+                            const int32_t* mb_seq, int mb, const float* adv_st,
+                            const mlearn_ppo_hparams& h, float* grad, float* loss_out, void* wsp,
+                            hipStream_t s) {
+    const int64_t M = (int64_t)mb * ro.bptt_len;
+    WsK ws;
+    carve(p, M, (char*)wsp, &ws);
+    PolicyK P = make_policy_k(p);
+    RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
+               ro.T, ro.bptt_len, ro.N};
+    HpK hp{};
+    hp.clip = h.clip_coef;
+    hp.vcoef = h.value_loss_coef;
+    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
+    hp.norm_adv = h.normalize_advantages;
+    hp.clip_vl = h.clip_value_loss;
+    hp.huber = h.huber_value_loss;
+    hp.loss_scale = h.loss_scale;
+    hp.inv_s = (float)(1.0 / (double)M);
+    hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
+
+    const int es = sizeof(T);
+    size_t lf = fwd_lds(p.obs_dim, H, es), lb = bwd_lds(H, es);
+    auto kf = ppo_fwd_kernel<T, H>;
+    auto kb = ppo_bwd_kernel<T, H>;
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        (void)hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(kf, dim3(ws.ntiles), dim3(256), lf, s, P, R, mb_seq, mb, M, adv_st, hp, ws);
+    hipLaunchKernelGGL(kb, dim3(ws.ntiles), dim3(256), lb, s, P, M, ws);
+
+    const int64_t rps = ((M + kSplits - 1) / kSplits + kWgChunk - 1) / kWgChunk * kWgChunk;
+    for (int l = 0; l < p.num_layers; ++l) {
+        const int I = l == 0 ? p.obs_dim : H;
+        const T* X = l == 0 ? (const T*)ws.x0 : (const T*)ws.a[l - 1];
+        hipLaunchKernelGGL(wgrad_kernel<T>, dim3((I + 63) / 64, (H + 63) / 64, kSplits), dim3(256),
+                           0, s, X, I, (const T*)ws.dz[l], H, M, I, H, rps,
+                           ws.slab + ws.slab_off[l], ws.slab_stride);
+    }
+    hipLaunchKernelGGL(wgrad_kernel<T>, dim3((H + 63) / 64, 1, kSplits), dim3(256), 0, s,
+                       (const T*)ws.a[p.num_layers - 1], H, (const T*)ws.dhead, MLEARN_HEAD_COLS, M,
+                       H, MLEARN_HEAD_COLS, rps, ws.slab + ws.slab_off[p.num_layers],
+                       ws.slab_stride);
+    LayoutK Lk = make_layout(p);
+    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 255) / 256)), dim3(256), 0,
+                       s, Lk, ws, grad);
+    if (loss_out)
+        hipLaunchKernelGGL(reduce_loss_kernel, dim3(1), dim3(64), 0, s, ws, hp, M,
+                           p.actions.num_groups, loss_out);
+    return check_launch("ppo_minibatch_grad");
+}
+
+}  // namespace ml
+
+using namespace ml;
+
+extern "C" {
+
+int64_t mlearn_param_count(const mlearn_mlp_policy* policy) {
+    if (validate_policy(policy)) return -1;
+    return make_layout(*policy).total;
+}
+
+int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows) {
+    if (validate_policy(policy) || rows < 1) return -1;
+    return (int64_t)carve(*policy, rows, nullptr, nullptr);
+}
+
+int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                              const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                              const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
+                              void* workspace, mlearn_stream_t stream) {
+    int rc = validate_policy(policy);
+    if (rc) return rc;
+    ML_REQUIRE(ro && mb_seq && adv_stats && hp && grad && workspace, "ppo: null pointer");
+    ML_REQUIRE(mb_size >= 1, "ppo: mb_size must be >= 1");
+    ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");
+    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
+               "ppo: null rollout array");
+    ML_REQUIRE(!hp->clip_value_loss || ro->values, "ppo: clip_value_loss needs values");
+    hipStream_t s = S(stream);
+#define ML_DISPATCH(T)                                                                           \
+    switch (policy->hidden) {                                                                   \
+        case 64: return launch_minibatch<T, 64>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp,  \
+                                                grad, loss_out, workspace, s);                  \
+        case 128: return launch_minibatch<T, 128>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp, \
+                                                  grad, loss_out, workspace, s);                \
+        default: return launch_minibatch<T, 256>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp, \
+                                                 grad, loss_out, workspace, s);                 \
+    }
+    if (policy->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
+}
+
+}  // extern "C"

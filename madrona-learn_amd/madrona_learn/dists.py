@@ -1,0 +1,85 @@
+"""Action distributions (mirrors src/madrona_learn/dists.py:12-96).
+
+``DiscreteActionDistributions`` wraps [N, sum(buckets)] logits (torch, on
+the GPU) and dispatches to the HIP kernels.  RNG: the reference's
+``prng_key`` becomes a Philox key (two uint32 words) plus a counter; see
+DESIGN.md "RNG".
+"""
+
+import torch
+
+from . import _native as nat
+
+
+class PhiloxKey:
+    """Counter-based key replacing jax.random keys: (k0, k1) plus a step."""
+
+    def __init__(self, k0, k1, step=0, env_offset=0):
+        self.k0 = int(k0) & 0xFFFFFFFF
+        self.k1 = int(k1) & 0xFFFFFFFF
+        self.step = int(step)
+        self.env_offset = int(env_offset)
+
+
+class DiscreteActionDistributions:
+    def __init__(self, actions_num_buckets, all_logits: torch.Tensor):
+        self.actions_num_buckets = list(actions_num_buckets)
+        self.all_logits = all_logits
+        self._layout = nat.action_layout(self.actions_num_buckets)
+
+    def _logits_f32(self):
+        # dists.py:22 upcasts each slice to f32
+        lg = self.all_logits.float().contiguous()
+        if lg.shape[-1] != self._layout.num_logits:
+            raise ValueError("logits width does not match the action buckets")
+        return lg.reshape(-1, lg.shape[-1])
+
+    def _sample(self, key: PhiloxKey, sample):
+        lg = self._logits_f32()
+        N = lg.shape[0]
+        K = len(self.actions_num_buckets)
+        actions = torch.empty((N, K), dtype=torch.int32, device=lg.device)
+        logp = torch.empty((N, K), dtype=torch.float32, device=lg.device) if sample else None
+        L = nat.lib()
+        nat.check(L.mlearn_discrete_sample_f32(
+            nat.ptr(lg), lg.shape[1], self._layout, N, key.k0, key.k1, None, key.step,
+            key.env_offset, 1 if sample else 0, nat.ptr(actions), nat.ptr(logp),
+            nat.stream_handle()), "discrete_sample")
+        shape = self.all_logits.shape[:-1] + (K,)
+        return actions.reshape(shape), (logp.reshape(shape) if logp is not None else None)
+
+    def sample(self, prng_key: PhiloxKey):  # dists.py:26-44
+        return self._sample(prng_key, True)
+
+    def best(self):  # dists.py:46-52
+        return self._sample(PhiloxKey(0, 0), False)[0]
+
+    def action_stats(self, all_actions: torch.Tensor):  # dists.py:54-77
+        lg = self._logits_f32()
+        N = lg.shape[0]
+        K = len(self.actions_num_buckets)
+        acts = all_actions.to(torch.int32).reshape(N, K).contiguous()
+        logp = torch.empty((N, K), dtype=torch.float32, device=lg.device)
+        ent = torch.empty((N, K), dtype=torch.float32, device=lg.device)
+        nat.check(nat.lib().mlearn_action_stats_f32(
+            nat.ptr(lg), lg.shape[1], self._layout, N, nat.ptr(acts), nat.ptr(logp),
+            nat.ptr(ent), nat.stream_handle()), "action_stats")
+        shape = self.all_logits.shape[:-1] + (K,)
+        return logp.reshape(shape), ent.reshape(shape)
+
+    def probs(self):  # dists.py:79-88
+        out = []
+        off = 0
+        lg = self.all_logits.float()
+        for b in self.actions_num_buckets:
+            out.append(torch.softmax(lg[..., off:off + b], dim=-1))
+            off += b
+        return out
+
+    def logits(self):  # dists.py:90-96
+        out = []
+        off = 0
+        for b in self.actions_num_buckets:
+            out.append(self.all_logits[..., off:off + b].float())
+            off += b
+        return out

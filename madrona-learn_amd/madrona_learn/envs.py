@@ -1,0 +1,49 @@
+"""Synthetic dummy vec-env (test/bench sim plugin).
+
+Stands in for a Madrona simulator behind the reference's ``sim_fns``
+protocol (rollouts.py:206-215, 905-936): ``init() -> {'state', 'obs'}`` and
+``step({'state', 'actions', 'resets', 'sim_ctrl', 'pbt'}) -> {'state', 'obs',
+'rewards', 'dones'}``.  One HIP launch per step (misc.hip env_step_kernel).
+Deterministic: staggered fixed episode lengths, Philox observations and
+rewards, reward depends on action[0].
+"""
+
+import torch
+
+from . import _native as nat
+
+
+class DummyVecEnv:
+    def __init__(self, num_envs, obs_dim=64, num_actions=6, seed=0, env_offset=0,
+                 device="cuda"):
+        self.N = int(num_envs)
+        self.D = int(obs_dim)
+        self.K = int(num_actions)
+        self.k0 = (seed * 0x9E3779B9 + 0x1234) & 0xFFFFFFFF
+        self.k1 = (seed * 0x85EBCA6B + 0x5678) & 0xFFFFFFFF
+        self.env_offset = int(env_offset)
+        dev = torch.device(device)
+        self.state = torch.zeros((self.N, 4), dtype=torch.int32, device=dev)
+        self.obs = torch.zeros((self.N, self.D), dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros((self.N, 1), dtype=torch.float32, device=dev)
+        self.dones = torch.zeros((self.N, 1), dtype=torch.bool, device=dev)
+
+    def init(self):
+        nat.check(nat.lib().mlearn_dummy_env_reset(
+            nat.ptr(self.state), self.N, self.D, self.k0, self.k1, self.env_offset,
+            nat.ptr(self.obs), nat.stream_handle()), "env_reset")
+        return {"state": self.state, "obs": self.obs}
+
+    def step(self, inp):
+        acts = inp["actions"]
+        if acts.dtype != torch.int32 or not acts.is_contiguous():
+            acts = acts.to(torch.int32).contiguous()
+        nat.check(nat.lib().mlearn_dummy_env_step(
+            nat.ptr(self.state), nat.ptr(acts), acts.shape[-1], self.N, self.D, self.k0, self.k1,
+            self.env_offset, nat.ptr(self.obs), nat.ptr(self.rewards), nat.ptr(self.dones),
+            nat.stream_handle()), "env_step")
+        return {"state": self.state, "obs": self.obs, "rewards": self.rewards,
+                "dones": self.dones}
+
+    def sim_fns(self):
+        return {"init": self.init, "step": self.step}

@@ -1,0 +1,106 @@
+"""Training metrics (mirrors src/madrona_learn/metrics.py:12-188).
+
+A ``Metric`` is (mean, m2, min, max, count) with the reference's Chan merge.
+Values are produced on the GPU by the native metrics/loss kernels as
+[5]-float device vectors; ``TrainingMetrics`` keeps the latest record of
+every metric in one fixed device buffer (graph-capture safe) and copies it
+into a ``metrics_buffer_size`` ring on ``advance()``.  Host readback happens
+only when the user asks for values.
+
+As in the reference, every ``record`` of a metric overwrites its slot for
+the current update, so the PPO metrics reflect the last minibatch
+(metrics.py:161-181).
+"""
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+FLT_MAX = float(np.finfo(np.float32).max)
+
+
+@dataclass
+class Metric:
+    per_policy: bool
+    mean: float = 0.0
+    m2: float = 0.0
+    min: float = FLT_MAX
+    max: float = -FLT_MAX
+    count: int = 0
+
+    @staticmethod
+    def init(per_policy):  # metrics.py:20-29
+        return Metric(per_policy)
+
+    @staticmethod
+    def init_from_data(per_policy, data):  # metrics.py:31-48
+        d = np.asarray(data, dtype=np.float64)
+        mean = float(d.mean()) if d.size else 0.0
+        return Metric(per_policy, mean, float(((d - mean) ** 2).sum()),
+                      float(d.min()) if d.size else FLT_MAX,
+                      float(d.max()) if d.size else -FLT_MAX, int(d.size))
+
+    @staticmethod
+    def from_vector(per_policy, v):
+        v = [float(x) for x in v]
+        return Metric(per_policy, v[0], v[1], v[2], v[3], int(round(v[4])))
+
+    def merge(self, o):  # metrics.py:79-98 (Chan et al.)
+        n = self.count + o.count
+        delta = o.mean - self.mean
+        inv = 1.0 / max(n, 1)
+        mean = self.mean + delta * o.count * inv
+        m2 = self.m2 + o.m2 + delta * delta * self.count * o.count * inv
+        return Metric(self.per_policy, mean, m2, min(self.min, o.min), max(self.max, o.max), n)
+
+    @property
+    def var(self):
+        return self.m2 / self.count if self.count > 0 else 0.0
+
+
+class TrainingMetrics:
+    def __init__(self, names, buffer_size, device, per_policy=True):
+        self.names = list(names)
+        self.index = {n: i for i, n in enumerate(self.names)}
+        self.buffer_size = int(buffer_size)
+        self.per_policy = per_policy
+        self.latest = torch.zeros((len(self.names), 5), dtype=torch.float32, device=device)
+        self.latest[:, 2] = FLT_MAX
+        self.latest[:, 3] = -FLT_MAX
+        self.ring = self.latest.unsqueeze(0).repeat(self.buffer_size, 1, 1)
+        self.update_idx = 0
+        self.cur_buffer_offset = 0
+
+    def slot(self, name):
+        """[5] device view of the latest record of `name` (kernels write here)."""
+        return self.latest[self.index[name]]
+
+    def record_tensor(self, name, vec5):
+        self.latest[self.index[name]].copy_(vec5)
+
+    def record_scalar(self, name, value):
+        s = self.latest[self.index[name]]
+        s[0] = value
+        s[1] = 0.0
+        s[2] = value
+        s[3] = value
+        s[4] = 1.0
+
+    def advance(self):  # metrics.py:183-188
+        self.ring[self.cur_buffer_offset].copy_(self.latest)
+        self.update_idx += 1
+        self.cur_buffer_offset = (self.cur_buffer_offset + 1) % self.buffer_size
+
+    def last(self):
+        """Host dict name -> Metric of the most recently completed update."""
+        idx = (self.cur_buffer_offset - 1) % self.buffer_size
+        host = self.ring[idx].cpu().numpy()
+        return {n: Metric.from_vector(self.per_policy, host[i]) for i, n in enumerate(self.names)}
+
+    def pretty_print(self, tab=2):
+        out = []
+        for n, m in self.last().items():
+            out.append(" " * tab + f"{n}: mean {m.mean:.4e} std {np.sqrt(max(m.var, 0)):.4e} "
+                       f"min {m.min:.4e} max {m.max:.4e} count {m.count}")
+        print("\n".join(out))

@@ -1,0 +1,164 @@
+"""PPO (mirrors src/madrona_learn/ppo.py).
+
+``PPO.update_program`` restates ``_ppo`` (ppo.py:366-488) for the default
+minibatch mode: per epoch a fresh permutation of the C*B sequences
+(ppo.py:445-458), then for every minibatch one native call that runs the
+forward, loss and backward to a flat gradient (ppo.py:109-281), the data
+parallel gradient all-reduce, and one native optimizer step
+(ppo.py:283-338).  It is a generator: it yields ('allreduce', tensor) at
+every collective so the caller can run it eagerly or capture the compute
+between collectives into HIP graphs.
+"""
+
+from dataclasses import dataclass
+from typing import Union
+
+import torch
+
+from . import _native as nat
+from .algo_common import AlgoBase, HyperParams
+from .cfg import AlgoConfig, ParamExplore
+
+__all__ = ["PPOConfig"]
+
+PPO_METRICS = ["Loss", "Action Obj", "Value Loss", "Value Errors", "Entropy"]
+
+
+@dataclass(frozen=True)
+class PPOConfig(AlgoConfig):  # ppo.py:24-39
+    num_epochs: int
+    minibatch_size: int
+    clip_coef: float
+    value_loss_coef: float
+    entropy_coef: Union[float, ParamExplore, dict]
+    max_grad_norm: float
+    clip_value_loss: bool = False
+    huber_value_loss: bool = False
+
+    def name(self):
+        return "ppo"
+
+    def setup(self):
+        return PPO()
+
+
+@dataclass(frozen=True)
+class PPOHyperParams(HyperParams):  # ppo.py:42-46
+    clip_coef: float = 0.2
+    value_loss_coef: float = 0.5
+    entropy_coef: object = 0.0
+    max_grad_norm: float = 0.5
+
+
+def _base(x):
+    return x.base if isinstance(x, ParamExplore) else x
+
+
+class PPO(AlgoBase):  # ppo.py:49-106
+    def init_hyperparams(self, cfg):
+        if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
+            assert not cfg.algo.clip_value_loss
+            assert not cfg.algo.huber_value_loss
+            assert not cfg.normalize_values
+        return PPOHyperParams(
+            lr=_base(cfg.lr), gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
+            normalize_values=cfg.normalize_values,
+            value_normalizer_decay=cfg.value_normalizer_decay,
+            max_advantage_est_decay=cfg.max_advantage_est_decay,
+            clip_coef=cfg.algo.clip_coef, value_loss_coef=cfg.algo.value_loss_coef,
+            entropy_coef=cfg.algo.entropy_coef, max_grad_norm=cfg.algo.max_grad_norm)
+
+    def make_optimizer(self, hyper_params):
+        # optax.chain(clip_by_global_norm, adam) (ppo.py:84-90): implemented natively
+        return ("clip_by_global_norm+adam", hyper_params.max_grad_norm, hyper_params.lr)
+
+    def add_metrics(self, cfg, names):
+        return list(names) + PPO_METRICS
+
+    # ------------------------------------------------------------------
+    def prepare(self, cfg, policy_state, train_state, store, dp):
+        """Allocate the per-update buffers once (graph-capture safe)."""
+        algo = cfg.algo
+        if cfg.filter_advantages or cfg.importance_sample_trajectories:
+            raise NotImplementedError(
+                "filter_advantages / importance_sample_trajectories (ppo.py:374-435) are "
+                "non-default modes outside the fused path")
+        if cfg.normalize_values:
+            raise NotImplementedError("value normalisation is SURVEY §8(f) row 2")
+        C = cfg.num_bptt_chunks
+        self.bptt = cfg.steps_per_update // C
+        self.num_seq = C * store.N                    # per rank
+        self.mb = int(algo.minibatch_size)            # per rank
+        if self.num_seq % self.mb != 0:               # ppo.py:439
+            raise ValueError(f"{self.num_seq} sequences not divisible by minibatch_size "
+                             f"{self.mb}")
+        self.num_mb = self.num_seq // self.mb
+        self.E = int(algo.num_epochs)
+        dev = policy_state.device
+        self.perm = torch.zeros((self.E, self.num_seq), dtype=torch.int32, device=dev)
+        self.adv_part = torch.zeros((self.E, self.num_mb * 66), dtype=torch.float64, device=dev)
+        self.adv_stats = torch.zeros((self.E, self.num_mb, 2), dtype=torch.float32, device=dev)
+        rows = self.mb * self.bptt
+        nbytes = nat.lib().mlearn_ppo_workspace_bytes(policy_state.desc, rows)
+        self.ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
+        self.view = store.view(self.bptt)
+        K = policy_state.arch.num_groups
+        hp = nat.PPOHparams()
+        hp.clip_coef = float(algo.clip_coef)
+        hp.value_loss_coef = float(algo.value_loss_coef)
+        ec = algo.entropy_coef
+        # entropy coefficients are per action-group name (ppo.py:231-239); the fused
+        # head is the single discrete group, so one coefficient covers its K sub-actions
+        if isinstance(ec, dict):
+            if len(ec) != 1:
+                raise NotImplementedError("one discrete action group supported")
+            ec = next(iter(ec.values()))
+        ec = float(_base(ec))
+        for k in range(K):
+            hp.entropy_coef[k] = ec
+        hp.normalize_advantages = 1 if (cfg.normalize_advantages and cfg.compute_advantages) \
+            else 0
+        if not cfg.compute_advantages:
+            raise NotImplementedError("compute_advantages=False (returns as the objective) is "
+                                      "not on the fused path yet")
+        hp.clip_value_loss = 1 if algo.clip_value_loss else 0
+        hp.huber_value_loss = 1 if algo.huber_value_loss else 0
+        hp.loss_scale = 1.0 / dp.world_size
+        self.hp = hp
+        self.dp = dp
+        self.count = float(self.mb * dp.world_size * self.bptt)
+
+    def update_program(self, cfg, policy_state, train_state, rollout_data, user_metrics_cb,
+                       metrics, epoch_ctr):
+        L = nat.lib()
+        strm = nat.stream_handle()
+        k0, k1 = train_state.update_prng_key
+        # epoch permutations + advantage statistics for every minibatch of the update
+        for e in range(self.E):
+            nat.check(L.mlearn_minibatch_perm(k0, k1, nat.ptr(epoch_ctr), e, self.dp.rank,
+                                              self.num_seq, nat.ptr(self.perm[e]), strm), "perm")
+            nat.check(L.mlearn_adv_stats(self.view, nat.ptr(self.perm[e]), self.num_mb, self.mb,
+                                         nat.ptr(self.adv_part[e]), strm), "adv_stats")
+        if self.dp.world_size > 1:
+            for e in range(self.E):
+                yield ("allreduce", self.adv_part[e, :2 * self.num_mb])
+        for e in range(self.E):
+            nat.check(L.mlearn_adv_stats_finish(nat.ptr(self.adv_part[e]), self.num_mb,
+                                                self.count, nat.ptr(self.adv_stats[e]), strm),
+                      "adv_stats_finish")
+        loss_out = metrics.latest[metrics.index["Loss"]:metrics.index["Loss"] + 5]
+        for e in range(self.E):
+            for m in range(self.num_mb):
+                seqs = self.perm[e, m * self.mb:(m + 1) * self.mb]
+                nat.check(L.mlearn_ppo_minibatch_grad(
+                    policy_state.desc, self.view, nat.ptr(seqs), self.mb,
+                    nat.ptr(self.adv_stats[e, m]), self.hp, nat.ptr(train_state.grads),
+                    nat.ptr(loss_out), nat.ptr(self.ws), strm), "ppo_minibatch_grad")
+                if self.dp.world_size > 1:
+                    yield ("allreduce", train_state.grads)
+                train_state.optimizer_step(policy_state)
+                metrics = user_metrics_cb(metrics, e, {"sequence_ids": seqs}, policy_state,
+                                          train_state)
+        nat.check(L.mlearn_counters_add(nat.ptr(epoch_ctr), 1, (nat.c_uint64 * 1)(self.E), strm),
+                  "epoch counter")
+        return metrics

@@ -1,0 +1,271 @@
+"""Rollout engine (mirrors src/madrona_learn/rollouts.py).
+
+``RolloutManager.collect`` runs the reference's rollout_loop (rollouts.py:
+829-978) as, per step: one fused HIP launch for preprocess + policy +
+sample + store (policy.hip), the user's sim step, and one post-step launch
+(rewards/dones store, env returns).  Then the bootstrap critic, GAE/returns
+and the rollout metrics.  No finalize transpose (rollouts.py:786-804): the
+store stays [T][N] = [C][T/C][P][B] and the PPO kernels index sequences
+directly.
+"""
+
+import math
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, Optional
+
+import torch
+
+from . import _native as nat
+from .algo_common import compute_advantages, compute_returns
+from .cfg import DiscreteActionsConfig
+
+
+@dataclass(frozen=True)
+class RolloutConfig:  # rollouts.py:28-134 (self-play / single-policy path)
+    sim_batch_size: int
+    num_worlds: int
+    actions_cfg: Dict
+    policy_chunk_size: int
+    num_policy_chunks: int
+    total_policy_batch_size: int
+    reward_gamma: float
+    policy_dtype: torch.dtype
+    reward_dtype: torch.dtype = torch.float32
+    prob_dtype: torch.dtype = torch.float32
+    pbt: Any = None
+
+    @staticmethod
+    def setup(num_current_policies, num_past_policies, num_teams, team_size, sim_batch_size,
+              actions_cfg, self_play_portion, cross_play_portion, past_play_portion,
+              static_play_portion, reward_gamma, custom_policy_ids, policy_dtype,
+              reward_dtype=torch.float32, prob_dtype=torch.float32,
+              policy_chunk_size_override=0):
+        complex_mm = (num_current_policies > 1 and self_play_portion != 1.0) or \
+            num_past_policies > 0 or cross_play_portion > 0 or past_play_portion > 0
+        if complex_mm or num_current_policies != 1:
+            raise NotImplementedError(
+                "PBT matchmaking / multi-policy rollouts are SURVEY §8(f) row 3; the fused "
+                "path runs one policy per device (PBT = one policy per GPU)")
+        assert num_past_policies == 0
+        policy_chunk_size = sim_batch_size // num_current_policies  # rollouts.py:104-108
+        if policy_chunk_size_override != 0:
+            policy_chunk_size = policy_chunk_size_override
+        num_policy_chunks = -(sim_batch_size // -policy_chunk_size)
+        return RolloutConfig(
+            sim_batch_size=sim_batch_size,
+            num_worlds=sim_batch_size // (team_size * num_teams),
+            actions_cfg=actions_cfg,
+            policy_chunk_size=policy_chunk_size,
+            num_policy_chunks=num_policy_chunks,
+            total_policy_batch_size=num_policy_chunks * policy_chunk_size,
+            reward_gamma=reward_gamma,
+            policy_dtype=policy_dtype,
+            reward_dtype=reward_dtype,
+            prob_dtype=prob_dtype,
+        )
+
+
+class RolloutState:  # rollouts.py:171-309
+    def __init__(self, cfg, step_fn, sim_state, cur_obs, prng_key, rnn_states, sim_ctrl,
+                 env_returns, counters, policy_assignments):
+        self.cfg = cfg
+        self.step_fn = step_fn
+        self.sim_state = sim_state
+        self.cur_obs = cur_obs
+        self.prng_key = prng_key
+        self.rnn_states = rnn_states
+        self.sim_ctrl = sim_ctrl
+        self.env_returns = env_returns
+        self.counters = counters  # device int64[8]: [0] rollout step, [1] epoch
+        self.policy_assignments = policy_assignments
+
+    @staticmethod
+    def create(rollout_cfg, sim_fns, prng_key, rnn_states, init_sim_ctrl,
+               static_play_assignments=None, device="cuda"):
+        init_out = sim_fns["init"]()
+        dev = torch.device(device)
+        return RolloutState(
+            cfg=rollout_cfg,
+            step_fn=sim_fns["step"],
+            sim_state=init_out["state"],
+            cur_obs=init_out["obs"],
+            prng_key=prng_key,
+            rnn_states=rnn_states,
+            sim_ctrl=init_sim_ctrl,
+            env_returns=torch.zeros(rollout_cfg.sim_batch_size, dtype=torch.float32, device=dev),
+            counters=torch.zeros(8, dtype=torch.int64, device=dev),
+            # self-play: every agent runs policy 0 (pbt.py:130-133)
+            policy_assignments=torch.zeros((rollout_cfg.sim_batch_size, 1), dtype=torch.int32,
+                                           device=dev),
+        )
+
+
+class RolloutData:  # rollouts.py:311-334
+    """Views of the [T][N] store.  ``minibatch`` gathers whole sequences
+    ([T/C, mb, ...], time-major) like the reference for user hooks; the PPO
+    kernels never materialise it."""
+
+    def __init__(self, store, num_bptt_chunks):
+        self.store = store
+        self.C = num_bptt_chunks
+
+    def all(self):
+        return self.store.as_dict()
+
+    def minibatch(self, indices):
+        s = self.store
+        T, N, C = s.T, s.N, self.C
+        Tc = T // C
+        idx = indices.to(torch.int64)
+        c, b = idx // N, idx % N
+        t = (c[None, :] * Tc + torch.arange(Tc, device=idx.device)[:, None])  # [Tc, mb]
+        rows = t * N + b[None, :]
+        out = {}
+        for k, v in s.as_dict().items():
+            flat = v.reshape(T * N, *v.shape[2:])
+            out[k] = flat[rows.reshape(-1)].reshape(Tc, idx.numel(), *v.shape[2:])
+        return out
+
+
+class RolloutStore:
+    def __init__(self, T, N, obs_dim, K, compute_dtype, device):
+        self.T, self.N = T, N
+        f32 = torch.float32
+        self.obs = torch.zeros((T, N, obs_dim), dtype=compute_dtype, device=device)
+        self.actions = torch.zeros((T, N, K), dtype=torch.int32, device=device)
+        self.log_probs = torch.zeros((T, N, K), dtype=f32, device=device)
+        self.values = torch.zeros((T, N), dtype=f32, device=device)
+        self.rewards = torch.zeros((T, N), dtype=f32, device=device)
+        self.dones = torch.zeros((T, N), dtype=torch.uint8, device=device)
+        self.advantages = torch.zeros((T, N), dtype=f32, device=device)
+        self.returns = torch.zeros((T, N), dtype=f32, device=device)
+        self.env_returns_trace = torch.zeros((T, N), dtype=f32, device=device)
+        self.bootstrap = torch.zeros((N,), dtype=f32, device=device)
+
+    def as_dict(self):
+        return {"obs": self.obs, "actions": self.actions, "log_probs": self.log_probs,
+                "values": self.values, "rewards": self.rewards, "dones": self.dones,
+                "advantages": self.advantages, "returns": self.returns}
+
+    def view(self, bptt_len):
+        v = nat.RolloutView()
+        v.obs = self.obs.data_ptr()
+        v.actions = self.actions.data_ptr()
+        v.log_probs = self.log_probs.data_ptr()
+        v.advantages = self.advantages.data_ptr()
+        v.returns = self.returns.data_ptr()
+        v.values = self.values.data_ptr()
+        v.T = self.T
+        v.bptt_len = bptt_len
+        v.N = self.N
+        return v
+
+
+ROLLOUT_METRICS = ["Rewards", "Values", "Est Returns", "Env Returns", "Advantages",
+                   "Bootstrap Values"]
+
+
+def obs_to_matrix(obs, N):
+    """Identity prefix: a tensor, or a dict holding exactly one tensor."""
+    if isinstance(obs, dict):
+        if len(obs) != 1:
+            raise ValueError("obs dict with several entries needs a BackboneShared prefix "
+                             "that returns one [N, obs_dim] tensor")
+        obs = next(iter(obs.values()))
+    x = obs.reshape(N, -1)
+    if x.dtype != torch.float32:
+        x = x.float()
+    return x.contiguous()
+
+
+class RolloutManager:  # rollouts.py:373-826
+    def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_state, env_offset=0):
+        self.train_cfg = train_cfg
+        self._cfg = init_rollout_state.cfg
+        assert train_cfg.steps_per_update % train_cfg.num_bptt_chunks == 0  # rollouts.py:387
+        self.T = train_cfg.steps_per_update
+        self.C = train_cfg.num_bptt_chunks
+        self.bptt = self.T // self.C
+        self.N = self._cfg.sim_batch_size
+        self.policy_state = policy_state
+        self.prefix = policy_state.actor_critic.backbone.prefix
+        arch = policy_state.arch
+        self.store = RolloutStore(self.T, self.N, arch.obs_dim, arch.num_groups, arch.dtype,
+                                  policy_state.device)
+        self.env_offset = int(env_offset)
+        self.use_advantages = train_cfg.compute_advantages
+        dev = policy_state.device
+        self._resets = torch.zeros((self._cfg.num_worlds, 1), dtype=torch.int32, device=dev)
+        self._metrics_ws = torch.zeros(int(nat.lib().mlearn_metrics_workspace_bytes(6)),
+                                       dtype=torch.uint8, device=dev)
+        s = self.store
+        jobs = (nat.MetricJob * 6)()
+        for i, (x, n, a) in enumerate([(s.rewards, self.T * self.N, 0),
+                                       (s.values, self.T * self.N, 0),
+                                       (s.returns, self.T * self.N, 0),
+                                       (s.env_returns_trace, self.T * self.N, 0),
+                                       (s.advantages, self.T * self.N, 0),
+                                       (s.bootstrap, self.N, 0)]):
+            jobs[i].x = x.data_ptr()
+            jobs[i].n = n
+            jobs[i].abs_value = a
+        self._jobs = jobs
+
+    def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
+        return list(names) + ROLLOUT_METRICS
+
+    def prep_obs(self, obs):
+        x = self.prefix(obs, train=False)
+        return obs_to_matrix(x, self.N)
+
+    def collect(self, train_state_mgr, rollout_state: RolloutState, metrics, user_hooks):
+        """rollouts.py:501-577 restated on the fused kernels."""
+        ps = self.policy_state
+        s = self.store
+        L = nat.lib()
+        strm = nat.stream_handle()
+        gamma = float(self._cfg.reward_gamma)
+        rollout_state, train_state_mgr.user_state = user_hooks.start_rollouts(
+            rollout_state, train_state_mgr.user_state)
+        key = rollout_state.prng_key
+        step_ctr = rollout_state.counters[0:1]
+        for t in range(self.T):
+            obs = self.prep_obs(rollout_state.cur_obs)
+            ps.rollout_step(obs, s.obs[t], s.actions[t], s.log_probs[t], s.values[t], key,
+                            step_ctr, t, self.env_offset, sample=True)
+            step_input = {
+                "state": rollout_state.sim_state,
+                "actions": s.actions[t],
+                "resets": self._resets,
+                "sim_ctrl": rollout_state.sim_ctrl,
+                "pbt": {"policy_assignments": rollout_state.policy_assignments},
+            }
+            out = rollout_state.step_fn(step_input)
+            rew = out["rewards"].reshape(-1)
+            if rew.dtype != torch.float32:
+                rew = rew.float()
+            dn = out["dones"].reshape(-1)
+            dn = dn.view(torch.uint8) if dn.dtype == torch.bool else (dn != 0).view(torch.uint8)
+            nat.check(L.mlearn_rollout_post_step(
+                nat.ptr(rew.contiguous()), nat.ptr(dn.contiguous()), self.N, nat.ptr(s.rewards[t]),
+                nat.ptr(s.dones[t]), nat.ptr(rollout_state.env_returns),
+                nat.ptr(s.env_returns_trace[t]), gamma, strm), "post_step")
+            rollout_state.sim_state = out["state"]
+            rollout_state.cur_obs = out["obs"]
+        # bootstrap values (rollouts.py:607-635)
+        ps.critic_only(self.prep_obs(rollout_state.cur_obs), s.bootstrap)
+        rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
+            s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
+        if self.use_advantages:
+            compute_advantages(self.train_cfg, s.rewards, s.values, s.dones, s.bootstrap,
+                               out_adv=s.advantages, out_ret=s.returns)
+        else:
+            compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s.returns)
+        i0 = metrics.index["Rewards"]
+        nat.check(L.mlearn_metrics_f32(self._jobs, 6, nat.ptr(metrics.latest[i0:i0 + 6]),
+                                       nat.ptr(self._metrics_ws), strm), "rollout metrics")
+        nat.check(L.mlearn_counters_add(nat.ptr(rollout_state.counters), 1,
+                                        (nat.c_uint64 * 1)(self.T), strm), "counters")
+        data = RolloutData(s, self.C)
+        metrics = user_hooks.rollout_metrics(metrics, data, train_state_mgr.user_state)
+        return train_state_mgr, rollout_state, data, None, metrics

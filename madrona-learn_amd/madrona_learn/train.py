@@ -1,0 +1,232 @@
+"""Training orchestration (mirrors src/madrona_learn/train.py:35-391).
+
+``init_training`` builds the same pieces as the reference's _init_training
+(train.py:268-391); ``TrainingManager.update_iter`` runs one PPO iteration
+(``_update_impl``, train.py:155-225).  The reference compiles an update into
+one XLA executable (utils.py:42-57); here the whole update (T fused rollout
+steps, the sim, bootstrap, GAE, metrics, every minibatch step) is captured
+into HIP graphs after one eager warm-up iteration and replayed, with the
+data-parallel collectives (if any) issued between graph segments.
+"""
+
+import os
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .cfg import TrainConfig
+from .dist import DataParallel
+from .metrics import TrainingMetrics
+from .policy import Policy
+from .profile import profile
+from .rollouts import RolloutConfig, RolloutManager, RolloutState
+from .train_state import PolicyState, PolicyTrainState, TrainStateManager, compile_arch
+
+
+@dataclass(frozen=True)
+class TrainHooks:  # train.py:75-128
+    def init_user_state(self):
+        return None
+
+    def start_rollouts(self, rollout_state, user_state):
+        return rollout_state, user_state
+
+    def finish_rollouts(self, rollouts, bootstrap_values, unnormalized_values,
+                        unnormalized_bootstrap_values, user_state):
+        return rollouts, user_state
+
+    def add_metrics(self, metrics):
+        return metrics
+
+    def rollout_metrics(self, metrics, rollouts, user_state):
+        return metrics
+
+    def optimize_metrics(self, metrics, epoch_idx, minibatch, policy_state, train_state):
+        return metrics
+
+
+def _split_seed(seed, stream):
+    """Deterministic 2x32-bit key for an RNG stream from the config seed."""
+    ss = np.random.SeedSequence([int(seed) & 0xFFFFFFFF, stream])
+    w = ss.generate_state(2, dtype=np.uint32)
+    return int(w[0]), int(w[1])
+
+
+class TrainingManager:  # train.py:35-64
+    def __init__(self, state, rollout, metrics, cfg, rollout_mgr, algo, user_hooks, dp,
+                 update_idx=0, use_graph=True, profile_port=None):
+        self.state = state
+        self.rollout = rollout
+        self.metrics = metrics
+        self.cfg = cfg
+        self.rollout_mgr = rollout_mgr
+        self.algo = algo
+        self.user_hooks = user_hooks
+        self.dp = dp
+        self.update_idx = int(update_idx)
+        self.use_graph = use_graph
+        self.profile_port = profile_port
+        self._segments = None
+        self._eager_iters = 0
+
+    # -- one update as a generator over collectives --------------------------
+    def _program(self):
+        with profile("Update Iter"):
+            with profile("Collect Rollouts"):
+                (self.state, self.rollout, rollout_data, _obs_stats,
+                 self.metrics) = self.rollout_mgr.collect(self.state, self.rollout, self.metrics,
+                                                          self.user_hooks)
+            with profile("Learn"):
+                self.metrics = yield from self.algo.update_program(
+                    self.cfg, self.state.policy_states, self.state.train_states, rollout_data,
+                    self.user_hooks.optimize_metrics, self.metrics, self.rollout.counters[1:2])
+
+    def _run_eager(self):
+        gen = self._program()
+        try:
+            while True:
+                op, t = next(gen)
+                if op == "allreduce":
+                    self.dp.all_reduce_sum_(t)
+        except StopIteration:
+            pass
+
+    def _capture(self):
+        """Capture the update into HIP graphs split at the collectives."""
+        gen = self._program()
+        segments = []
+        done = False
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        while not done:
+            g = torch.cuda.CUDAGraph()
+            coll = None
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    try:
+                        op, coll = next(gen)
+                    except StopIteration:
+                        done = True
+            segments.append((g, coll))
+        torch.cuda.current_stream().wait_stream(s)
+        return segments
+
+    def _replay(self):
+        for g, coll in self._segments:
+            g.replay()
+            if coll is not None:
+                self.dp.all_reduce_sum_(coll)
+
+    def update_iter(self):
+        """One PPO iteration; returns self (the reference returns a new pytree)."""
+        if self.use_graph and self._segments is None and self._eager_iters >= 1:
+            # capture runs the program once: it performs this iteration's work
+            self._segments = self._capture()
+            self._replay_collectives_of_capture()
+        elif self._segments is not None:
+            self._replay()
+        else:
+            self._run_eager()
+            self._eager_iters += 1
+        self.metrics.advance()
+        self.update_idx += 1
+        return self
+
+    def _replay_collectives_of_capture(self):
+        # Capturing records kernels without executing them: run the captured
+        # graphs once now so this call still performs exactly one update.
+        self._replay()
+
+    def save_ckpt(self, path):  # train.py:44-46
+        os.makedirs(path, exist_ok=True)
+        self.state.save(self.update_idx, os.path.join(path, f"{self.update_idx}.pt"))
+
+    def load_ckpt(self, path):  # train.py:48-49
+        self.state, self.update_idx = self.state.load(path)
+        return self
+
+
+def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: Policy,
+                  init_sim_ctrl=None, user_hooks: TrainHooks = TrainHooks(),
+                  restore_ckpt: Optional[str] = None, profile_port: Optional[int] = None,
+                  use_graph: bool = True) -> TrainingManager:
+    """train.py:131-146 / 268-391."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("madrona_learn (MI355X build) needs a ROCm GPU; there is no CPU path")
+    device = torch.device(dev) if not isinstance(dev, torch.device) else dev
+    if device.type != "cuda":
+        raise ValueError(f"device must be a GPU, got {device}")
+    torch.cuda.set_device(device)
+    dp = DataParallel()
+    algo = cfg.algo.setup()
+    if cfg.pbt is not None:
+        raise NotImplementedError("PBT populations are SURVEY §8(f) row 3")
+    if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
+        raise NotImplementedError(
+            "the fused path implements the scalar DenseLayerCritic: set "
+            "TrainConfig(dreamer_v3_critic=False) (DreamerV3 two-hot is SURVEY §8(f) row 2)")
+
+    sim_batch = cfg.num_agents_per_world * cfg.num_worlds
+    rollout_cfg = RolloutConfig.setup(
+        num_current_policies=1, num_past_policies=0, num_teams=1,
+        team_size=cfg.num_agents_per_world, sim_batch_size=sim_batch, actions_cfg=cfg.actions,
+        self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0,
+        static_play_portion=0.0, reward_gamma=cfg.gamma,
+        custom_policy_ids=cfg.custom_policy_ids, policy_dtype=cfg.compute_dtype)
+    rollout_key = _split_seed(cfg.seed, 1)
+    update_key = _split_seed(cfg.seed, 2)
+    rnn_states = policy.actor_critic.init_recurrent_state(sim_batch)
+    rollout_state = RolloutState.create(rollout_cfg, sim_fns, rollout_key, rnn_states,
+                                        init_sim_ctrl, device=device)
+
+    prefix = policy.actor_critic.backbone.prefix
+    from .rollouts import obs_to_matrix
+    obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
+    arch = compile_arch(policy.actor_critic, obs0.shape[1], cfg.compute_dtype)
+    preprocess = policy.obs_preprocess
+    if preprocess is not None:
+        preprocess.fused_cast_dtype(cfg.compute_dtype)
+    rng = np.random.default_rng(int(cfg.seed))
+    ps = PolicyState(policy.actor_critic, arch, preprocess, device, rng)
+    dp.broadcast_(ps.params)
+    ps.sync_weights()
+    ts = PolicyTrainState(cfg, algo.init_hyperparams(cfg), ps, update_key)
+    tsm = TrainStateManager(policy_states=ps, train_states=ts, pbt_rng=None,
+                            user_state=user_hooks.init_user_state())
+    start = 0
+    if restore_ckpt is not None:
+        tsm, start = tsm.load(restore_ckpt)
+
+    rollout_mgr = RolloutManager(cfg, rollout_state, ps, env_offset=dp.rank * sim_batch)
+    names = algo.add_metrics(cfg, [])
+    names = rollout_mgr.add_metrics(cfg, names)
+    names = user_hooks.add_metrics(names)
+    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device)
+    algo.prepare(cfg, ps, ts, rollout_mgr.store, dp)
+    print(cfg)
+    return TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algo, user_hooks, dp,
+                           update_idx=start, use_graph=use_graph, profile_port=profile_port)
+
+
+def stop_training(training_mgr: TrainingManager):  # train.py:148-153
+    torch.cuda.synchronize()
+
+
+def train(dev, cfg: TrainConfig, sim_fns, policy: Policy, init_sim_ctrl=None,
+          user_hooks: TrainHooks = TrainHooks(), restore_ckpt=None, log_every=0,
+          use_graph=True, callback=None):
+    """Convenience loop: cfg.num_updates iterations of update_iter."""
+    mgr = init_training(dev, cfg, sim_fns, policy, init_sim_ctrl, user_hooks, restore_ckpt,
+                        use_graph=use_graph)
+    for i in range(cfg.num_updates):
+        mgr = mgr.update_iter()
+        if log_every and (i + 1) % log_every == 0 and mgr.dp.rank == 0:
+            print(f"update {mgr.update_idx}")
+            mgr.metrics.pretty_print()
+        if callback is not None:
+            callback(mgr)
+    stop_training(mgr)
+    return mgr

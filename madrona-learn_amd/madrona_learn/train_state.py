@@ -1,0 +1,261 @@
+"""Policy / train state (mirrors src/madrona_learn/train_state.py:34-488).
+
+``compile_policy`` recognises the ActorCritic tree the fused kernels
+implement and builds a ``PolicyState``: one flat f32 parameter arena in HBM
+(layout of ``mlearn_param_count``) plus the compute-dtype weight images the
+kernels read, all bound into one ``mlearn_mlp_policy`` descriptor.
+``PolicyTrainState`` holds Adam moments, the Adam step counter, the initial
+weight norms (train_state.py:413-423) and the minibatch RNG key.
+"""
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .actor_critic import ActorCritic, BackboneEncoder, BackboneShared
+from .cfg import DiscreteActionsConfig, TrainConfig
+from .models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+from .observations import ObservationsPreprocessNoop
+
+
+@dataclass(frozen=True)
+class MlpArch:
+    obs_dim: int
+    hidden: int
+    num_layers: int
+    buckets: tuple
+    dtype: torch.dtype
+
+    @property
+    def num_logits(self):
+        return int(sum(self.buckets))
+
+    @property
+    def num_groups(self):
+        return len(self.buckets)
+
+
+def param_layout(arch: MlpArch):
+    """Python mirror of LayoutK / mlearn_param_count (csrc/ppo.hip)."""
+    H, A1 = arch.hidden, arch.num_logits + 1
+    off = 0
+    lay = {"w": [], "s": [], "b": []}
+    for l in range(arch.num_layers):
+        fin = arch.obs_dim if l == 0 else H
+        lay["w"].append((off, (fin, H)))
+        off += fin * H
+        lay["s"].append((off, (H,)))
+        off += H
+        lay["b"].append((off, (H,)))
+        off += H
+    lay["hw"] = (off, (H, A1))
+    off += H * A1
+    lay["hb"] = (off, (A1,))
+    off += A1
+    lay["total"] = off
+    return lay
+
+
+def _actions_buckets(actor, cfg_actions):
+    if not isinstance(actor, DenseLayerDiscreteActor):
+        raise NotImplementedError(
+            "fused path supports DenseLayerDiscreteActor (models.py:122-139); got "
+            f"{type(actor).__name__}")
+    return tuple(int(b) for b in actor.cfg.actions_num_buckets)
+
+
+def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpArch:
+    bb = actor_critic.backbone
+    enc = bb.encoder if isinstance(bb, BackboneShared) else bb
+    if not isinstance(enc, BackboneEncoder):
+        raise NotImplementedError(
+            "fused path supports BackboneShared(encoder=BackboneEncoder(net=MLP)) "
+            "(actor_critic.py:131-153, 202-244); recurrent / separate backbones are the next "
+            "SURVEY §8(f) rows")
+    net = enc.net
+    if not isinstance(net, MLP):
+        raise NotImplementedError(f"fused path needs an MLP trunk, got {type(net).__name__}")
+    if not isinstance(actor_critic.critic, DenseLayerCritic):
+        raise NotImplementedError(
+            "fused path supports DenseLayerCritic (models.py:142-154); pass "
+            "dreamer_v3_critic=False in TrainConfig")
+    buckets = _actions_buckets(actor_critic.actor, None)
+    return MlpArch(obs_dim=int(obs_dim), hidden=net.num_channels, num_layers=net.num_layers,
+                   buckets=buckets, dtype=compute_dtype)
+
+
+class PolicyState:
+    """Parameters + compute images of one policy (train_state.py:34-82)."""
+
+    def __init__(self, actor_critic, arch: MlpArch, obs_preprocess, device, rng):
+        self.actor_critic = actor_critic
+        self.arch = arch
+        self.obs_preprocess = obs_preprocess or ObservationsPreprocessNoop.create()
+        self.device = torch.device(device)
+        self.layout = param_layout(arch)
+        H, D, L, A1 = arch.hidden, arch.obs_dim, arch.num_layers, arch.num_logits + 1
+        dt = arch.dtype
+
+        host = np.zeros(self.layout["total"], dtype=np.float32)
+        net = actor_critic.backbone.encoder.net if isinstance(
+            actor_critic.backbone, BackboneShared) else actor_critic.backbone.net
+        init_norms = []
+        for l in range(L):
+            o, shp = self.layout["w"][l]
+            w = net.weight_init(rng, shp)
+            host[o:o + w.size] = w.reshape(-1)
+            init_norms.append(float(np.linalg.norm(w.astype(np.float64))))
+            o, shp = self.layout["s"][l]
+            host[o:o + H] = 1.0
+        o, _ = self.layout["hw"]
+        wa = actor_critic.actor.weight_init(rng, (H, arch.num_logits))
+        wv = actor_critic.critic.weight_init(rng, (H, 1))
+        host[o:o + H * A1] = np.concatenate([wa, wv], axis=1).reshape(-1)
+
+        self.params = torch.from_numpy(host).to(self.device)
+        self.init_norms = torch.tensor(init_norms, dtype=torch.float32, device=self.device)
+        # compute-dtype images read by the kernels
+        self.w_t, self.w = [], []
+        for l in range(L):
+            fin = D if l == 0 else H
+            self.w_t.append(torch.zeros((H, fin), dtype=dt, device=self.device))
+            self.w.append(torch.zeros((fin, H), dtype=dt, device=self.device))
+        self.head_t = torch.zeros((nat.HEAD_COLS, H), dtype=dt, device=self.device)
+        self.head = torch.zeros((H, nat.HEAD_COLS), dtype=dt, device=self.device)
+        self.head_b = torch.zeros((nat.HEAD_COLS,), dtype=torch.float32, device=self.device)
+
+        d = nat.MlpPolicy()
+        d.dtype = nat.dtype_code(dt)
+        d.obs_dim = D
+        d.hidden = H
+        d.num_layers = L
+        d.actions = nat.action_layout(arch.buckets)
+        for l in range(L):
+            d.w_t[l] = self.w_t[l].data_ptr()
+            d.w[l] = self.w[l].data_ptr()
+            d.ln_scale[l] = self.params.data_ptr() + 4 * self.layout["s"][l][0]
+            d.ln_bias[l] = self.params.data_ptr() + 4 * self.layout["b"][l][0]
+        d.head_t = self.head_t.data_ptr()
+        d.head = self.head.data_ptr()
+        d.head_bias = self.head_b.data_ptr()
+        self.desc = d
+        n = nat.lib().mlearn_param_count(d)
+        if n != self.layout["total"]:
+            raise RuntimeError(f"param layout mismatch: native {n} vs {self.layout['total']}")
+        self.sync_weights()
+
+    # -- views --------------------------------------------------------------
+    def view(self, key, l=None):
+        o, shp = self.layout[key][l] if l is not None else self.layout[key]
+        return self.params[o:o + int(np.prod(shp))].view(*shp)
+
+    @property
+    def param_tree(self):
+        """flax-style nested dict of views into the arena (train_state.py:65)."""
+        L, A = self.arch.num_layers, self.arch.num_logits
+        net = {}
+        for l in range(L):
+            net[f"Dense_{l}"] = {"kernel": self.view("w", l)}
+            net[f"LayerNorm_{l}"] = {"impl": {"scale": self.view("s", l),
+                                              "bias": self.view("b", l)}}
+        hw, hb = self.view("hw"), self.view("hb")
+        return {
+            "backbone": {"encoder": {"net": net}},
+            "actor": {"impl": {"kernel": hw[:, :A], "bias": hb[:A]}},
+            "critic": {"Dense_0": {"kernel": hw[:, A:], "bias": hb[A:]}},
+        }
+
+    def sync_weights(self):
+        nat.check(nat.lib().mlearn_policy_sync_weights(self.desc, nat.ptr(self.params),
+                                                       nat.stream_handle()), "sync_weights")
+
+    # -- kernels ------------------------------------------------------------
+    def rollout_step(self, obs, obs_store, actions, log_probs, values, key, step_ctr, step,
+                     env_offset=0, sample=True):
+        """ActorCritic.rollout + store (actor_critic.py:74-96, rollouts.py:637-668)."""
+        N = obs.shape[0]
+        nat.check(nat.lib().mlearn_policy_rollout_step(
+            self.desc, nat.ptr(obs, torch.float32, name="obs"), N, nat.ptr(obs_store),
+            nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values), key[0], key[1],
+            nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, nat.stream_handle()),
+            "policy_rollout_step")
+
+    def critic_only(self, obs, values):
+        """ActorCritic.critic_only (actor_critic.py:65-72)."""
+        N = obs.shape[0]
+        nat.check(nat.lib().mlearn_policy_rollout_step(
+            self.desc, nat.ptr(obs, torch.float32, name="obs"), N, None, None, None,
+            nat.ptr(values), 0, 0, None, 0, 0, 0, nat.stream_handle()), "critic_only")
+
+    def state_dict(self):
+        return {"params": self.params.detach().cpu()}
+
+    def load_state_dict(self, sd):
+        self.params.copy_(sd["params"].to(self.device))
+        self.sync_weights()
+
+
+class PolicyTrainState:
+    """Optimizer + per-policy training state (train_state.py:85-136)."""
+
+    def __init__(self, cfg: TrainConfig, hyper_params, policy_state: PolicyState, key):
+        self.hyper_params = hyper_params
+        dev = policy_state.device
+        P = policy_state.layout["total"]
+        self.adam_m = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.adam_v = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.initial_weight_norms = policy_state.init_norms
+        self.update_prng_key = (int(key[0]) & 0xFFFFFFFF, int(key[1]) & 0xFFFFFFFF)
+        nbytes = nat.lib().mlearn_optim_workspace_bytes(policy_state.desc)
+        self.optim_ws = torch.zeros(max(nbytes, 16), dtype=torch.uint8, device=dev)
+        o = nat.OptimState()
+        o.params = policy_state.params.data_ptr()
+        o.grads = self.grads.data_ptr()
+        o.adam_m = self.adam_m.data_ptr()
+        o.adam_v = self.adam_v.data_ptr()
+        o.init_norms = self.initial_weight_norms.data_ptr()
+        o.step = self.step.data_ptr()
+        o.lr = float(hyper_params.lr)
+        o.b1, o.b2, o.eps = 0.9, 0.999, 1e-8  # optax.adam defaults (optax 0.1.9)
+        o.max_grad_norm = float(hyper_params.max_grad_norm)
+        o.normalize_params = 1
+        o.normalize_layernorms = 1
+        self.optim_desc = o
+
+    def optimizer_step(self, policy_state: PolicyState):
+        nat.check(nat.lib().mlearn_optim_step(policy_state.desc, self.optim_desc,
+                                              nat.ptr(self.optim_ws), nat.stream_handle()),
+                  "optim_step")
+
+    def state_dict(self):
+        return {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu()}
+
+    def load_state_dict(self, sd):
+        self.adam_m.copy_(sd["adam_m"])
+        self.adam_v.copy_(sd["adam_v"])
+        self.step.copy_(sd["step"])
+
+
+@dataclass
+class TrainStateManager:  # train_state.py:139-304
+    policy_states: PolicyState
+    train_states: PolicyTrainState
+    pbt_rng: Any = None
+    user_state: Any = None
+
+    def save(self, update_idx, path):
+        torch.save({"update_idx": int(update_idx),
+                    "policy": self.policy_states.state_dict(),
+                    "train": self.train_states.state_dict()}, path)
+
+    def load(self, path):
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        self.policy_states.load_state_dict(sd["policy"])
+        self.train_states.load_state_dict(sd["train"])
+        return self, sd["update_idx"]

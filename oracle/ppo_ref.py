@@ -1,0 +1,490 @@
+"""NumPy restatement of the reference's batched-PPO iteration.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  Every function cites the
+reference file:line (relative to shacklettbp/madrona-learn src/madrona_learn/)
+whose arithmetic it restates.  Third-party arithmetic the reference calls is
+restated from its published definition (flax 0.8.1 LayerNorm / Dense, optax
+0.1.9 clip_by_global_norm / adam / l2_loss / huber_loss, jax.nn.logsumexp /
+softmax); the replaced RNG (jax.random threefry) is documented in DESIGN.md.
+
+Modes
+  'f64'   float64 arithmetic, no rounding (accuracy reference)
+  'f32'   float32 values at every reference dtype boundary
+  'bf16'  compute_dtype=bfloat16: values rounded to bf16 (RNE) where the
+          reference's flax modules emit bf16 (Dense outputs, LayerNorm
+          outputs, head outputs, bf16 cotangents at Dense boundaries)
+Arithmetic runs in ``ad`` (float64 by default; float32 for the timed CPU
+baseline).
+"""
+
+import numpy as np
+
+from . import native
+
+LN_EPS = 1e-6  # flax.linen.LayerNorm default epsilon (flax 0.8.1)
+ADAM_B1, ADAM_B2, ADAM_EPS = 0.9, 0.999, 1e-8  # optax.adam defaults (optax 0.1.9)
+
+
+# ---------------------------------------------------------------------------
+# dtype helpers
+# ---------------------------------------------------------------------------
+def round_bf16(x):
+    """float32 -> bfloat16 (round to nearest even) -> float32."""
+    x = np.asarray(x, dtype=np.float32)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32)
+    out = r.view(np.float32)
+    return np.where(np.isnan(x), x, out)
+
+
+def rnd(x, mode, ad=np.float64):
+    if mode == "f64":
+        return np.asarray(x, dtype=ad)
+    x32 = np.asarray(x, dtype=np.float32)
+    if mode == "bf16":
+        x32 = round_bf16(x32)
+    return x32.astype(ad)
+
+
+# ---------------------------------------------------------------------------
+# returns / advantages
+# ---------------------------------------------------------------------------
+def gae_f32(rewards, values, dones, bootstrap, gamma, lam):
+    """compute_advantages (algo_common.py:84-130) + returns = adv + values
+    (rollouts.py:761-769), in float32 with the reference's operation order
+    (no fused multiply-add): bit-exact twin of the HIP kernel."""
+    r = np.asarray(rewards, np.float32)
+    v = np.asarray(values, np.float32)
+    d = np.asarray(dones).astype(bool)
+    T = r.shape[0]
+    g = np.float32(gamma)
+    gl = np.float32(np.float32(gamma) * np.float32(lam))
+    nv = np.asarray(bootstrap, np.float32).copy()
+    na = np.zeros_like(nv)
+    adv = np.empty_like(r)
+    for i in range(T - 1, -1, -1):
+        nv = np.where(d[i], np.float32(0), nv)
+        na = np.where(d[i], np.float32(0), na)
+        td = (r[i] + g * nv) - v[i]
+        a = td + gl * na
+        adv[i] = a
+        nv = v[i]
+        na = a
+    return adv, adv + v
+
+
+def gae(rewards, values, dones, bootstrap, gamma, lam, ad=np.float64):
+    """Same recurrence in `ad` precision (accuracy reference)."""
+    r = np.asarray(rewards, ad)
+    v = np.asarray(values, ad)
+    d = np.asarray(dones).astype(bool)
+    nv = np.asarray(bootstrap, ad).copy()
+    na = np.zeros_like(nv)
+    adv = np.empty_like(r)
+    for i in range(r.shape[0] - 1, -1, -1):
+        nv = np.where(d[i], 0, nv)
+        na = np.where(d[i], 0, na)
+        a = r[i] + gamma * nv - v[i] + gamma * lam * na
+        adv[i] = a
+        nv, na = v[i], a
+    return adv, adv + v
+
+
+def discounted_returns_f32(rewards, dones, bootstrap, gamma):
+    """compute_returns (algo_common.py:45-81), float32 operation order."""
+    r = np.asarray(rewards, np.float32)
+    d = np.asarray(dones).astype(bool)
+    g = np.float32(gamma)
+    nr = np.asarray(bootstrap, np.float32).copy()
+    out = np.empty_like(r)
+    for i in range(r.shape[0] - 1, -1, -1):
+        nr = np.where(d[i], np.float32(0), nr)
+        nr = r[i] + g * nr
+        out[i] = nr
+    return out
+
+
+def zscore(x):
+    """zscore_data (algo_common.py:133-140): population variance, clamp 1e-5."""
+    x = np.asarray(x, np.float64)
+    mean, var = x.mean(), x.var()
+    return (x - mean) / np.sqrt(max(var, 1e-5)), mean, var
+
+
+# ---------------------------------------------------------------------------
+# parameters
+# ---------------------------------------------------------------------------
+def param_layout(obs_dim, hidden, num_layers, num_logits):
+    """Flat layout shared with the HIP library (mlearn_param_count)."""
+    H, A1 = hidden, num_logits + 1
+    off, lay = 0, {"W": [], "s": [], "b": []}
+    for l in range(num_layers):
+        fin = obs_dim if l == 0 else H
+        lay["W"].append((off, (fin, H)))
+        off += fin * H
+        lay["s"].append((off, (H,)))
+        off += H
+        lay["b"].append((off, (H,)))
+        off += H
+    lay["Wh"] = (off, (H, A1))
+    off += H * A1
+    lay["bh"] = (off, (A1,))
+    off += A1
+    lay["total"] = off
+    return lay
+
+
+def unflatten(flat, lay, ad=np.float64):
+    flat = np.asarray(flat, ad)
+    P = {"W": [], "s": [], "b": []}
+    for k in ("W", "s", "b"):
+        for o, shp in lay[k]:
+            P[k].append(flat[o:o + int(np.prod(shp))].reshape(shp).copy())
+    for k in ("Wh", "bh"):
+        o, shp = lay[k]
+        P[k] = flat[o:o + int(np.prod(shp))].reshape(shp).copy()
+    return P
+
+
+def flatten(P, lay):
+    out = np.zeros(lay["total"], np.float64)
+    for k in ("W", "s", "b"):
+        for (o, shp), v in zip(lay[k], P[k]):
+            out[o:o + v.size] = v.reshape(-1)
+    for k in ("Wh", "bh"):
+        o, shp = lay[k]
+        out[o:o + P[k].size] = P[k].reshape(-1)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# actor-critic forward (models.py:46-56, 99-154; actor_critic.py:74-128)
+# ---------------------------------------------------------------------------
+def forward(P, x, mode, ad=np.float64):
+    """MLP trunk (Dense no-bias -> LayerNorm -> ReLU) + actor logits + critic.
+
+    Returns (logits [M,A] f32-valued, value [M], cache)."""
+    h = rnd(x, mode, ad)
+    cache = {"in": [], "z": [], "mean": [], "rstd": [], "a": []}
+    for l in range(len(P["W"])):
+        W = rnd(P["W"][l], mode, ad)
+        z = rnd(h @ W, mode, ad)                                    # Dense output dtype
+        mean = z.mean(-1, keepdims=True)
+        var = np.maximum((z * z).mean(-1, keepdims=True) - mean * mean, 0)  # fast variance
+        rstd = 1.0 / np.sqrt(var + LN_EPS)
+        y = (z - mean) * (rstd * P["s"][l].astype(ad)) + P["b"][l].astype(ad)
+        a = np.maximum(rnd(y, mode, ad), 0)                         # LayerNorm dtype, ReLU
+        cache["in"].append(h)
+        cache["z"].append(z)
+        cache["mean"].append(mean)
+        cache["rstd"].append(rstd)
+        cache["a"].append(a)
+        h = a
+    Wh = rnd(P["Wh"], mode, ad)
+    out = rnd(rnd(h @ Wh, mode, ad) + rnd(P["bh"], mode, ad), mode, ad)  # Dense + bias
+    A = Wh.shape[1] - 1
+    return out[:, :A], out[:, A], cache
+
+
+def log_softmax_groups(logits, buckets):
+    """Per-group log_softmax / softmax / entropy (dists.py:54-77)."""
+    res = []
+    off = 0
+    for nb in buckets:
+        sl = logits[:, off:off + nb]
+        mx = sl.max(-1, keepdims=True)
+        lse = mx + np.log(np.exp(sl - mx).sum(-1, keepdims=True))
+        lp = sl - lse
+        p = np.exp(sl - mx) / np.exp(sl - mx).sum(-1, keepdims=True)
+        ent = -(p * lp).sum(-1)
+        res.append((off, nb, lp, p, ent))
+        off += nb
+    return res
+
+
+def action_stats(logits, buckets, actions):
+    """DiscreteActionDistributions.action_stats (dists.py:54-77)."""
+    res = log_softmax_groups(np.asarray(logits, np.float64), buckets)
+    M = logits.shape[0]
+    rows = np.arange(M)
+    logp = np.stack([lp[rows, actions[:, g]] for g, (_, _, lp, _, _) in enumerate(res)], -1)
+    ent = np.stack([e for (_, _, _, _, e) in res], -1)
+    return logp, ent
+
+
+def sample_actions(logits, buckets, gumbel):
+    """DiscreteActionDistributions.sample (dists.py:26-44) with the replaced
+    RNG: argmax(logit + Gumbel noise) per group in float32, first index on ties."""
+    lg = np.asarray(logits, np.float32)
+    noisy = lg + np.asarray(gumbel, np.float32)
+    acts = []
+    off = 0
+    for nb in buckets:
+        acts.append(np.argmax(noisy[:, off:off + nb], axis=-1))
+        off += nb
+    a = np.stack(acts, -1).astype(np.int32)
+    logp, _ = action_stats(lg, buckets, a)
+    return a, logp
+
+
+# ---------------------------------------------------------------------------
+# PPO loss and its gradient (ppo.py:129-281)
+# ---------------------------------------------------------------------------
+def _dmin(a, b):
+    """JAX's balanced derivative of minimum(a, b) w.r.t. a (0.5 on ties)."""
+    return np.where(a < b, 1.0, np.where(a == b, 0.5, 0.0))
+
+
+def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale=1.0,
+                   ad=np.float64):
+    """Loss (ppo.py:129-262) and d loss / d params (jax.value_and_grad) by
+    hand-written backprop.  batch: obs [M,D], actions [M,K], log_probs [M,K],
+    advantages [M], returns [M], values [M] (all rows of one minibatch)."""
+    logits, V, cache = forward(P, batch["obs"], mode, ad)
+    M = logits.shape[0]
+    K = len(buckets)
+    acts = np.asarray(batch["actions"])
+    old = np.asarray(batch["log_probs"], ad)
+    adv = np.asarray(batch["advantages"], ad)
+    R = np.asarray(batch["returns"], ad)
+    if hp.get("normalize_advantages", True):
+        if adv_stats is None:
+            mean, var = adv.mean(), adv.var()
+        else:
+            mean, var = adv_stats
+        adv = (adv - mean) / np.sqrt(max(var, 1e-5))
+    clip = hp["clip_coef"]
+    lo, hi = 1.0 - clip, 1.0 + clip
+    inv_sk = 1.0 / (M * K)
+    inv_s = 1.0 / M
+    ce = hp["entropy_coef"]
+    dlog = np.zeros((M, logits.shape[1]), ad)
+    objs, ents = [], []
+    rows = np.arange(M)
+    for g, (off, nb, lp, p, ent) in enumerate(log_softmax_groups(logits, buckets)):
+        a = acts[:, g]
+        ratio = np.exp(lp[rows, a] - old[:, g])
+        s1 = adv * ratio
+        y = np.maximum(ratio, lo)
+        cr = np.minimum(y, hi)
+        s2 = adv * cr
+        obj = np.minimum(s1, s2)
+        dclip = np.where(ratio > lo, 1.0, np.where(ratio == lo, 0.5, 0.0)) * \
+            np.where(y < hi, 1.0, np.where(y == hi, 0.5, 0.0))
+        w1 = _dmin(s1, s2)
+        dobj = w1 * adv + (1 - w1) * adv * dclip
+        g_lp = -inv_sk * dobj * ratio
+        onehot = np.zeros((M, nb), ad)
+        onehot[rows, a] = 1.0
+        d = g_lp[:, None] * (onehot - p) + ce * inv_sk * p * (lp + ent[:, None])
+        dlog[:, off:off + nb] = d * loss_scale
+        objs.append(obj)
+        ents.append(ent)
+    obj = np.stack(objs, -1)
+    ent = np.stack(ents, -1)
+    vpred, dvp = V, np.ones_like(V)
+    if hp.get("clip_value_loss", False):
+        ov = np.asarray(batch["values"], ad)
+        yy = np.maximum(V, ov - clip)
+        vpred = np.minimum(yy, ov + clip)
+        dvp = np.where(V > ov - clip, 1.0, np.where(V == ov - clip, 0.5, 0.0)) * \
+            np.where(yy < ov + clip, 1.0, np.where(yy == ov + clip, 0.5, 0.0))
+    e = vpred - R
+    if hp.get("huber_value_loss", False):
+        ae = np.abs(e)
+        quad = np.minimum(ae, 1.0)
+        vl = 0.5 * quad * quad + (ae - quad)
+        dvl = np.where(ae < 1.0, e, np.sign(e))
+    else:
+        vl = 0.5 * e * e
+        dvl = e
+    dV = hp["value_loss_coef"] * inv_s * dvl * dvp * loss_scale
+    loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
+
+    # ---- backward ----
+    A = logits.shape[1]
+    dhead = np.concatenate([dlog, dV[:, None]], -1)
+    dhead = rnd(dhead, mode, ad)                     # cotangent in the compute dtype
+    G = {"W": [None] * len(P["W"]), "s": [None] * len(P["W"]), "b": [None] * len(P["W"])}
+    aL = cache["a"][-1]
+    G["Wh"] = aL.T @ dhead
+    G["bh"] = dhead.sum(0)
+    da = dhead @ rnd(P["Wh"], mode, ad).T
+    for l in range(len(P["W"]) - 1, -1, -1):
+        z, mean, rstd = cache["z"][l], cache["mean"][l], cache["rstd"][l]
+        gam, bet = P["s"][l].astype(ad), P["b"][l].astype(ad)
+        xh = (z - mean) * rstd
+        y = (z - mean) * (rstd * gam) + bet
+        dy = np.where(rnd(y, mode, ad) > 0, da, 0.0)
+        G["s"][l] = (dy * xh).sum(0)
+        G["b"][l] = dy.sum(0)
+        dxh = dy * gam
+        dz = rstd * (dxh - dxh.mean(-1, keepdims=True) - xh * (dxh * xh).mean(-1, keepdims=True))
+        dz = rnd(dz, mode, ad)
+        G["W"][l] = cache["in"][l].T @ dz
+        if l > 0:
+            da = dz @ rnd(P["W"][l], mode, ad).T
+    metrics = {
+        "Loss": loss, "Action Obj": obj, "Value Loss": vl, "Value Errors": np.abs(V - R),
+        "Entropy": ent,
+    }
+    return loss, G, metrics, {"logits": logits, "value": V}
+
+
+# ---------------------------------------------------------------------------
+# optimizer (ppo.py:84-90, 283-338; optax 0.1.9)
+# ---------------------------------------------------------------------------
+def clip_by_global_norm(g, max_norm):
+    gn = np.sqrt((g * g).sum())
+    if gn < max_norm:
+        return g, gn
+    return (g / gn) * max_norm, gn
+
+
+def adam_step(p, g, m, v, count, lr, b1=ADAM_B1, b2=ADAM_B2, eps=ADAM_EPS):
+    """optax.scale_by_adam + scale(-lr) + apply_updates; count = step before."""
+    m = (1 - b1) * g + b1 * m
+    v = (1 - b2) * (g * g) + b2 * v
+    c = count + 1
+    mhat = m / (1 - b1 ** c)
+    vhat = v / (1 - b2 ** c)
+    u = mhat / (np.sqrt(vhat) + eps)
+    return p + (-lr) * u, m, v
+
+
+def project(P, init_norms):
+    """normalize_params (ppo.py:303-310) + normalize_layernorms (312-338)."""
+    for l in range(len(P["W"])):
+        W = P["W"][l]
+        P["W"][l] = (init_norms[l] * W) / np.sqrt((W * W).sum())
+        s, b = P["s"][l], P["b"][l]
+        f = np.sqrt(s.shape[-1] / (np.dot(b, b) + np.dot(s, s)))
+        P["s"][l] = f * s
+        P["b"][l] = f * b
+    return P
+
+
+def optimizer_step(flat_p, flat_g, m, v, count, lay, init_norms, lr, max_grad_norm):
+    g, gn = clip_by_global_norm(flat_g, max_grad_norm)
+    p, m, v = adam_step(flat_p, g, m, v, count, lr)
+    P = project(unflatten(p, lay), init_norms)
+    return flatten(P, lay), m, v, gn
+
+
+def grads_to_flat(G, lay):
+    return flatten(G, lay)
+
+
+# ---------------------------------------------------------------------------
+# minibatching (ppo.py:437-482, rollouts.py:319-329)
+# ---------------------------------------------------------------------------
+def epoch_permutation(k0, k1, epoch, rank, n):
+    """random.permutation restated on Philox keys (see DESIGN.md RNG)."""
+    i = np.arange(n, dtype=np.uint32)
+    ctr = np.stack([i, np.full(n, rank, np.uint32), np.full(n, epoch & 0xFFFFFFFF, np.uint32),
+                    np.full(n, epoch >> 32, np.uint32)], -1)
+    keys = native.philox(ctr, k0, k1)[:, 0]
+    return np.lexsort((i, keys)).astype(np.int32)
+
+
+def minibatch_rows(seq_ids, N, bptt):
+    """Store rows (t*N + b) of the minibatch, time-major [T/C, mb] like
+    RolloutData.minibatch + swapaxes (rollouts.py:319-329)."""
+    seq = np.asarray(seq_ids, np.int64)
+    c, b = seq // N, seq % N
+    tl = np.arange(bptt)[:, None]
+    return ((c[None, :] * bptt + tl) * N + b[None, :]).reshape(-1)
+
+
+def gather_minibatch(store, rows):
+    T, N = store["rewards"].shape
+    flat = lambda x: np.asarray(x).reshape(T * N, *np.asarray(x).shape[2:])
+    return {
+        "obs": flat(store["obs"])[rows],
+        "actions": flat(store["actions"])[rows],
+        "log_probs": flat(store["log_probs"])[rows],
+        "advantages": flat(store["advantages"])[rows],
+        "returns": flat(store["returns"])[rows],
+        "values": flat(store["values"])[rows],
+    }
+
+
+def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs, minibatch_size,
+               bptt, key, epoch_base, mode="f64", lr, max_grad_norm, ad=np.float64):
+    """_ppo (ppo.py:366-488) for the default minibatch mode, over one or more
+    data-parallel ranks (stores[r] = rank r's [T][N] store).  Each optimizer
+    step uses the union of the ranks' minibatches: advantage statistics of the
+    union, gradient = mean over ranks of the local-mean gradients (equal
+    sizes: the union mean).  Returns (params, opt, last-minibatch metrics)."""
+    world = len(stores)
+    T, N = stores[0]["rewards"].shape
+    nseq = (T // bptt) * N
+    nmb = nseq // minibatch_size
+    m, v, count = opt
+    metrics = None
+    for e in range(num_epochs):
+        perms = [epoch_permutation(key[0], key[1], epoch_base + e, r, nseq) for r in range(world)]
+        for mb_i in range(nmb):
+            batches = []
+            for r in range(world):
+                ids = perms[r][mb_i * minibatch_size:(mb_i + 1) * minibatch_size]
+                batches.append(gather_minibatch(stores[r], minibatch_rows(ids, N, bptt)))
+            alladv = np.concatenate([np.asarray(b["advantages"], np.float64) for b in batches])
+            stats = (alladv.mean(), alladv.var())
+            P = unflatten(flat_p, lay, ad)
+            gsum = None
+            for b in batches:
+                loss, G, met, _ = ppo_loss_grads(P, b, hp, buckets, mode, adv_stats=stats,
+                                                 loss_scale=1.0 / world, ad=ad)
+                gf = flatten(G, lay)
+                gsum = gf if gsum is None else gsum + gf
+                if metrics is None or b is batches[0]:
+                    metrics = met
+            flat_p, m, v, _ = optimizer_step(flat_p, gsum, m, v, count, lay, init_norms, lr,
+                                             max_grad_norm)
+            count += 1
+    return flat_p, (m, v, count), metrics
+
+
+# ---------------------------------------------------------------------------
+# rollout (rollouts.py:829-978) with the synthetic env
+# ---------------------------------------------------------------------------
+def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99,
+            env_returns=None, ad=np.float64, actions_override=None):
+    """rollout_loop restated: per step policy forward + Gumbel-max sample,
+    store, env step, env-return bookkeeping; then the bootstrap critic.
+    actions_override[t] (e.g. the GPU's actions) drives the env instead of
+    the oracle's own samples (used to replay a GPU trajectory exactly)."""
+    P = unflatten(flat_p, lay, ad)
+    N = env.N
+    A = int(sum(buckets))
+    K = len(buckets)
+    store = {k: [] for k in ("obs", "actions", "log_probs", "values", "rewards", "dones")}
+    store["logits"] = []
+    er = np.zeros(N, np.float32) if env_returns is None else env_returns
+    trace = []
+    obs = env.obs.copy()
+    for t in range(T):
+        x = rnd(obs, mode, ad)
+        logits, V, _ = forward(P, x, mode, ad)
+        gum = native.gumbel_table(key[0], key[1], step_base + t, env.eoff, N, A)
+        acts, logp = sample_actions(logits.astype(np.float32), buckets, gum)
+        if actions_override is not None:
+            acts = np.asarray(actions_override[t], np.int32)
+            logp, _ = action_stats(logits, buckets, acts)
+        store["obs"].append(x.astype(np.float32))
+        store["actions"].append(acts)
+        store["log_probs"].append(logp.astype(np.float32))
+        store["values"].append(V.astype(np.float32))
+        store["logits"].append(logits.astype(np.float32))
+        obs, rew, done = env.step(acts)
+        er = (rew + np.float32(gamma) * er).astype(np.float32)
+        trace.append(er.copy())
+        store["rewards"].append(rew)
+        store["dones"].append(done)
+        er = np.where(done.astype(bool), np.float32(0), er).astype(np.float32)
+    _, boot, _ = forward(P, rnd(obs, mode, ad), mode, ad)
+    out = {k: np.stack(v) for k, v in store.items()}
+    out["bootstrap"] = boot.astype(np.float32)
+    out["env_returns_trace"] = np.stack(trace)
+    return out, er

@@ -1,0 +1,128 @@
+"""End-to-end GPU parity of one full PPO iteration (config C0 shape:
+64 envs, MLP[64,64], T=32, 2 epochs, minibatch 16 sequences) against the
+oracle replaying the same trajectory, plus HIP-graph replay == eager.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import native as onat
+from oracle import ppo_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+BUCKETS = [4, 8, 5, 5, 2, 2]
+
+
+def make_cfg(dtype, N=64, H=64, T=32, chunks=1, mb=16, epochs=2, seed=5):
+    import madrona_learn as ml
+    return ml.TrainConfig(
+        num_worlds=N, num_agents_per_world=1, num_updates=1,
+        actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
+        lr=3e-4, algo=ml.PPOConfig(num_epochs=epochs, minibatch_size=mb, clip_coef=0.2,
+                                   value_loss_coef=0.5, entropy_coef={"actions": 0.01},
+                                   max_grad_norm=0.5),
+        num_bptt_chunks=chunks, gamma=0.99, gae_lambda=0.95, seed=seed, metrics_buffer_size=4,
+        dreamer_v3_critic=False, compute_dtype=dtype)
+
+
+def make_policy(dtype, H, L=2):
+    import madrona_learn as ml
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    return ml.Policy(actor_critic=ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(H, L, dtype))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
+        critic=DenseLayerCritic(dtype)), obs_preprocess=ml.ObservationsCaster.create(dtype))
+
+
+def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=16, use_graph=False):
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    env = DummyVecEnv(N, D, 6, seed=2, device=gpu)
+    cfg = make_cfg(dtype, N=N, H=H, chunks=chunks, mb=mb)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(dtype, H), use_graph=use_graph)
+    return cfg, env, mgr
+
+
+@pytest.mark.parametrize("mode,dtype,chunks", [("f32", torch.float32, 1),
+                                               ("f32", torch.float32, 2),
+                                               ("bf16", torch.bfloat16, 1)])
+def test_full_update_matches_oracle(gpu, mode, dtype, chunks):
+    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks)
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    lay = ref.param_layout(64, 64, 2, 26)
+    p0 = ps.params.cpu().numpy().astype(np.float64)
+    oenv = onat.Env(env.N, env.D, env.k0, env.k1, 0)
+    oenv.reset()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    g_acts = s.actions.cpu().numpy()
+    # replay the GPU's trajectory on the oracle env + oracle policy
+    ro, _ = ref.rollout(p0, lay, oenv, cfg.steps_per_update, BUCKETS, mgr.rollout.prng_key, 0,
+                        mode=mode, gamma=cfg.gamma, actions_override=g_acts)
+    assert np.array_equal(s.obs.float().cpu().numpy(), ro["obs"])
+    assert np.array_equal(s.rewards.cpu().numpy(), ro["rewards"])
+    assert np.array_equal(s.dones.cpu().numpy(), ro["dones"])
+    tol = 1e-4 if mode == "f32" else 3e-2
+    np.testing.assert_allclose(s.values.cpu().numpy(), ro["values"], rtol=tol, atol=tol)
+    np.testing.assert_allclose(s.bootstrap.cpu().numpy(), ro["bootstrap"], rtol=tol, atol=tol)
+    np.testing.assert_allclose(s.log_probs.cpu().numpy(), ro["log_probs"], rtol=tol, atol=tol)
+    np.testing.assert_allclose(s.env_returns_trace.cpu().numpy(), ro["env_returns_trace"],
+                               rtol=1e-6, atol=1e-6)
+    # actions equal the oracle's own samples wherever the margin is clear
+    gum = np.stack([onat.gumbel_table(*mgr.rollout.prng_key, t, 0, env.N, 26)
+                    for t in range(cfg.steps_per_update)])
+    noisy = ro["logits"] + gum
+    off = 0
+    for g, nb in enumerate(BUCKETS):
+        sl = noisy[..., off:off + nb]
+        srt = np.sort(sl, -1)
+        clear = (srt[..., -1] - srt[..., -2]) > 1e-3
+        assert np.array_equal(np.argmax(sl, -1)[clear], g_acts[..., g][clear])
+        off += nb
+    # GAE on the GPU's own store is bit-exact with the oracle's f32 recurrence
+    adv, ret = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(),
+                           s.dones.cpu().numpy(), s.bootstrap.cpu().numpy(), cfg.gamma,
+                           cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)
+    assert np.array_equal(s.returns.cpu().numpy(), ret)
+    # PPO epochs on the GPU's store from the same initial parameters
+    store = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+             for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    zeros = np.zeros_like(p0)
+    p1, _, met = ref.ppo_update(
+        p0, (zeros, zeros.copy(), 0), [store], hp, BUCKETS, lay,
+        ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=16,
+        bptt=cfg.steps_per_update // chunks, key=ts.update_prng_key, epoch_base=0, mode=mode,
+        lr=3e-4, max_grad_norm=0.5)
+    got = ps.params.cpu().numpy()
+    delta_ref = p1 - p0
+    delta_got = got - p0
+    cos = delta_got @ delta_ref / (np.linalg.norm(delta_got) * np.linalg.norm(delta_ref))
+    if mode == "f32":
+        np.testing.assert_allclose(got, p1, rtol=1e-4, atol=2e-5)
+        assert cos > 0.999
+    else:
+        assert cos > 0.97, cos
+    assert int(ts.step.item()) == 2 * (cfg.num_worlds * chunks // 16)
+    last = mgr.metrics.last()
+    np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
+    assert last["Advantages"].count == 32 * 64
+
+
+def test_graph_replay_matches_eager(gpu):
+    """Two independent managers, same seed: eager iterations vs captured graph
+    replays must produce bit-identical parameters."""
+    _, _, eager = _setup(gpu, torch.bfloat16, use_graph=False)
+    _, _, graph = _setup(gpu, torch.bfloat16, use_graph=True)
+    for _ in range(3):
+        eager.update_iter()
+        graph.update_iter()
+    torch.cuda.synchronize()
+    assert graph._segments is not None
+    assert torch.equal(eager.state.policy_states.params, graph.state.policy_states.params)
+    assert torch.equal(eager.rollout_mgr.store.actions, graph.rollout_mgr.store.actions)
