@@ -93,14 +93,48 @@ struct PolicyK {
 PolicyK make_policy_k(const mlearn_mlp_policy& p);
 int validate_policy(const mlearn_mlp_policy* p);
 
+// Store 4 consecutive elements (one 8-byte bf16 / 16-byte f32 store).
+__device__ inline void store4(bf16* p, float a, float b, float c, float d) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+    *(bf16x4*)p = v;
+}
+__device__ inline void store4(float* p, float a, float b, float c, float d) {
+    *(float4*)p = make_float4(a, b, c, d);
+}
+
+// Write a wave's accumulator-layout values v[i][e] (rows rb*32.., columns of
+// its blocks) transposed into XT[col][row0 + row]: per block 4 stores of 4
+// consecutive rows.  Rows >= M are written as zeros (padding of the K axis of
+// the weight-gradient GEMMs).
+template <typename T, int NB>
+__device__ inline void store_transposed(const float (&v)[NB][16], T* XT, int64_t ldT, int w,
+                                        int lane, int64_t row0, int64_t M) {
+    const int rb = w & 1, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int col = ((w >> 1) + 2 * i) * 32 + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = row0 + rb * 32 + 8 * q + 4 * h;
+            float x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = row + u < M ? v[i][4 * q + u] : 0.f;
+            store4(XT + (int64_t)col * ldT + row, x[0], x[1], x[2], x[3]);
+        }
+    }
+}
+
 // LayerNorm + ReLU epilogue on a wave's accumulators (rows rb*32.., its
 // column blocks).  Writes the compute-dtype activation into act (LDS) and,
-// when given, z (Dense output), stats (mean, rstd) and a (post-ReLU) to HBM.
+// when given, z (Dense output, row-major), stats (mean, rstd) and the
+// activation transposed (aT[col][row], for the weight-gradient GEMM).
 template <typename T, int NB>
 __device__ inline void ln_relu_epilogue(f32x16 (&acc)[NB], const float* __restrict__ gamma,
                                         const float* __restrict__ beta, T* act, int ld,
                                         float* red, int w, int lane, int H, int64_t row0,
-                                        int64_t M, T* z_out, float* st_out, T* a_out) {
+                                        int64_t M, T* z_out, float* st_out, T* aT_out,
+                                        int64_t ldT) {
     const int rb = w & 1, r = lane & 31;
     float u[NB][16], v[NB][16];
 #pragma unroll
@@ -132,14 +166,12 @@ __device__ inline void ln_relu_epilogue(f32x16 (&acc)[NB], const float* __restri
             const int col = ((w >> 1) + 2 * i) * 32 + r;
             float y = (acc[i][e] - mean) * (rstd * gamma[col]) + beta[col];
             y = fmaxf(rnd<T>(y), 0.f);
-            T yt = cvt<T>(y);
-            act[row * ld + col] = yt;
-            if (live) {
-                if (z_out) z_out[grow * H + col] = cvt<T>(acc[i][e]);
-                if (a_out) a_out[grow * H + col] = yt;
-            }
+            act[row * ld + col] = cvt<T>(y);
+            u[i][e] = y;
+            if (live && z_out) z_out[grow * H + col] = cvt<T>(acc[i][e]);
         }
     }
+    if (aT_out) store_transposed<T, NB>(u, aT_out, ldT, w, lane, row0, M);
 }
 
 // Heads: out[64][32] = act[64][H] x head_t^T, waves 0 and 1 (one row block each).

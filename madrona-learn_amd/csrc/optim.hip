@@ -108,12 +108,17 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     }
 }
 
-__global__ void proj_finish_kernel(const double* part, int nblocks, int nslot, float* out) {
-    int s = threadIdx.x;
-    if (s >= nslot) return;
+// one block per projection slot; fixed-order tree over the block partials
+__global__ __launch_bounds__(256) void proj_finish_kernel(const double* part, int nblocks, int nslot,
+                                                          float* out) {
+    __shared__ double sh[4];
+    const int sl = blockIdx.x;
     double t = 0;
-    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * nslot + s];
-    out[s] = (float)t;
+    for (int b = threadIdx.x; b < nblocks; b += 256) t += part[(int64_t)b * nslot + sl];
+    t = wave_sum64d(t);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) out[sl] = (float)(((sh[0] + sh[1]) + sh[2]) + sh[3]);
 }
 
 template <typename T>
@@ -217,7 +222,7 @@ int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state*
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
                        (const float*)gnorm, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
                        ppart);
-    hipLaunchKernelGGL(proj_finish_kernel, dim3(1), dim3(64), 0, s, (const double*)ppart,
+    hipLaunchKernelGGL(proj_finish_kernel, dim3(2 * Lk.L), dim3(256), 0, s, (const double*)ppart,
                        (int)nblk, 2 * Lk.L, sq);
     CopiesK C = make_copies(*policy);
     if (policy->dtype == MLEARN_DTYPE_BF16)

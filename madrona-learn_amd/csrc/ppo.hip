@@ -40,28 +40,46 @@ struct HpK {
     float inv_sk, inv_s;
 };
 
-constexpr int kSplits = 16;
-constexpr int kLossSlots = 20;  // per tile doubles
+constexpr int kLossSlots = 20;   // per tile doubles
+constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
+constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
+constexpr int kWgChunk = 64;     // weight-gradient K chunk (rows of the minibatch)
 
 struct WsK {
-    void* x0;
-    void* z[MLEARN_MAX_LAYERS];
-    float* st[MLEARN_MAX_LAYERS];
-    void* a[MLEARN_MAX_LAYERS];
-    void* dhead;
-    void* dz[MLEARN_MAX_LAYERS];
-    float* ln_part;    // [tiles][L][2 rb][2 (beta, gamma)][H]
-    float* hb_part;    // [tiles][32]
-    double* loss_part; // [tiles][kLossSlots]
-    float* slab;       // [splits][sum of weight sizes]
-    int64_t slab_stride;
-    int64_t slab_off[MLEARN_MAX_LAYERS + 1];  // layer weights, then head [H][32]
+    void* x0T;                          // [D][Mp]   gathered obs, transposed
+    void* z[MLEARN_MAX_LAYERS];         // [Mp][H]   Dense outputs (row-major)
+    float* st[MLEARN_MAX_LAYERS];       // [Mp][2]   LayerNorm mean, rstd
+    void* aT[MLEARN_MAX_LAYERS];        // [H][Mp]   post-ReLU activations, transposed
+    void* dhead;                        // [Mp][32]  d loss / d head outputs
+    void* dheadT;                       // [32][Mp]
+    void* dzT[MLEARN_MAX_LAYERS];       // [H][Mp]   d loss / d Dense outputs, transposed
+    float* colpart;                     // [tiles][CP] per-tile column partials
+    float* colpart2;                    // [kColChunks][CP]
+    double* loss_part;                  // [tiles][kLossSlots]
+    float* slab;                        // split-K partial weight gradients
+    int64_t slab_off[MLEARN_MAX_LAYERS + 1];
+    int splits[MLEARN_MAX_LAYERS + 1];
+    int64_t rps[MLEARN_MAX_LAYERS + 1];  // rows per split
+    int64_t Mp;
     int ntiles;
+    int CP;                             // L*4*H + 32
 };
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Carve the workspace; returns total bytes (ws may be null to size only).
+// Split-K plan of one weight gradient [I][J] over Mp rows: ~256 workgroups.
+static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
+    int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
+    int64_t chunks = Mp / kWgChunk;
+    int64_t s = 256 / tiles;
+    if (s < 1) s = 1;
+    if (s > chunks) s = chunks;
+    int64_t per = (chunks + s - 1) / s;
+    *rps = per * kWgChunk;
+    *splits = (int)((Mp + *rps - 1) / *rps);
+}
+
+// Carve the workspace; returns total bytes (base may be null to size only).
 static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
@@ -74,27 +92,30 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
         return (void*)ptr;
     };
     WsK w{};
-    w.x0 = take(Mp * D * es);
+    w.Mp = Mp;
+    w.ntiles = (int)tiles;
+    w.CP = L * 4 * H + MLEARN_HEAD_COLS;
+    w.x0T = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
         w.z[l] = take(Mp * H * es);
         w.st[l] = (float*)take(Mp * 2 * sizeof(float));
-        w.a[l] = take(Mp * H * es);
-        w.dz[l] = take(Mp * H * es);
+        w.aT[l] = take(Mp * H * es);
+        w.dzT[l] = take(Mp * H * es);
     }
     w.dhead = take(Mp * MLEARN_HEAD_COLS * es);
-    w.ln_part = (float*)take(tiles * L * 2 * 2 * H * sizeof(float));
-    w.hb_part = (float*)take(tiles * MLEARN_HEAD_COLS * sizeof(float));
+    w.dheadT = take(Mp * MLEARN_HEAD_COLS * es);
+    w.colpart = (float*)take(tiles * w.CP * sizeof(float));
+    w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
     int64_t so = 0;
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l <= L; ++l) {
+        const int I = l == L ? H : (l == 0 ? D : H);
+        const int J = l == L ? MLEARN_HEAD_COLS : H;
+        plan_splits(I, J, Mp, &w.splits[l], &w.rps[l]);
         w.slab_off[l] = so;
-        so += (int64_t)(l == 0 ? D : H) * H;
+        so += (int64_t)w.splits[l] * I * J;
     }
-    w.slab_off[L] = so;
-    so += (int64_t)H * MLEARN_HEAD_COLS;
-    w.slab_stride = so;
-    w.slab = (float*)take(kSplits * so * sizeof(float));
-    w.ntiles = (int)tiles;
+    w.slab = (float*)take(so * sizeof(float));
     if (W) *W = w;
     return off;
 }
@@ -137,15 +158,22 @@ __global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
 
     // gather the observation rows
     const T* obs = (const T*)ro.obs;
-    T* x0 = (T*)ws.x0;
     for (int idx = tid; idx < kTileRows * D; idx += 256) {
         int rr = idx / D, c = idx - rr * D;
         int64_t sr = srow[rr];
-        T v = sr >= 0 ? obs[sr * D + c] : cvt<T>(0.f);
-        act[rr * ld + c] = v;
-        if (sr >= 0) x0[(row0 + rr) * D + c] = v;
+        act[rr * ld + c] = sr >= 0 ? obs[sr * D + c] : cvt<T>(0.f);
     }
     __syncthreads();
+    // x0^T for the layer-0 weight gradient: 4 rows per store
+    {
+        T* x0T = (T*)ws.x0T;
+        for (int idx = tid; idx < D * (kTileRows / 4); idx += 256) {
+            int c = idx % D, g = idx / D;
+            store4(x0T + (int64_t)c * ws.Mp + row0 + 4 * g, to_f32(act[(4 * g) * ld + c]),
+                   to_f32(act[(4 * g + 1) * ld + c]), to_f32(act[(4 * g + 2) * ld + c]),
+                   to_f32(act[(4 * g + 3) * ld + c]));
+        }
+    }
 
     for (int l = 0; l < P.L; ++l) {
         const int K = l == 0 ? D : H;
@@ -154,7 +182,7 @@ __global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
         tile_gemm<T, NB>(acc, act, ld, w & 1, (const T*)P.wt[l], K, K, w, lane);
         __syncthreads();
         ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, row0, M,
-                                (T*)ws.z[l], ws.st[l], (T*)ws.a[l]);
+                                (T*)ws.z[l], ws.st[l], (T*)ws.aT[l], ws.Mp);
         __syncthreads();
     }
     heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
@@ -258,17 +286,24 @@ __global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
     }
     __syncthreads();
 
-    // d head -> HBM (compute dtype), head-bias partial sums
+    // d head -> HBM (compute dtype, row-major and transposed), head-bias partials
     T* dh = (T*)ws.dhead;
     for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
         int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
-        int64_t f = row0 + rr;
-        if (f < M) dh[f * MLEARN_HEAD_COLS + j] = cvt<T>(dl[rr * 33 + j]);
+        dh[(row0 + rr) * MLEARN_HEAD_COLS + j] = cvt<T>(dl[rr * 33 + j]);
+    }
+    {
+        T* dhT = (T*)ws.dheadT;
+        for (int idx = tid; idx < MLEARN_HEAD_COLS * (kTileRows / 4); idx += 256) {
+            int j = idx % MLEARN_HEAD_COLS, g = idx / MLEARN_HEAD_COLS;
+            store4(dhT + (int64_t)j * ws.Mp + row0 + 4 * g, dl[(4 * g) * 33 + j],
+                   dl[(4 * g + 1) * 33 + j], dl[(4 * g + 2) * 33 + j], dl[(4 * g + 3) * 33 + j]);
+        }
     }
     if (tid < MLEARN_HEAD_COLS) {
         float s = 0.f;
         for (int rr = 0; rr < kTileRows; ++rr) s += rnd<T>(dl[rr * 33 + tid]);
-        ws.hb_part[(int64_t)blockIdx.x * MLEARN_HEAD_COLS + tid] = s;
+        ws.colpart[(int64_t)blockIdx.x * ws.CP + P.L * 4 * H + tid] = s;
     }
 
     // tile loss/metric partials
@@ -315,8 +350,7 @@ __global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK 
     const T* dh = (const T*)ws.dhead;
     for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
         int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
-        int64_t f = row0 + rr;
-        act[rr * ldh + j] = f < M ? dh[f * MLEARN_HEAD_COLS + j] : cvt<T>(0.f);
+        act[rr * ldh + j] = dh[(row0 + rr) * MLEARN_HEAD_COLS + j];
     }
     __syncthreads();
 
@@ -364,7 +398,7 @@ __global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK 
             pb[i] += __shfl_xor(pb[i], 32);
             if (lane < 32) {
                 const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float* lp = ws.ln_part + ((((int64_t)blockIdx.x * P.L + l) * 2 + rb) * 2) * H;
+                float* lp = ws.colpart + (int64_t)blockIdx.x * ws.CP + ((l * 2 + rb) * 2) * H;
                 lp[col] = pb[i];
                 lp[H + col] = pg[i];
             }
@@ -372,21 +406,19 @@ __global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK 
         float su[16], sv[16];
         row_sums2<NB>(u, v, su, sv, red, w, lane);
         const float invH = 1.0f / (float)H;
-        T* dzo = (T*)ws.dz[l];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int row = rb * 32 + acc_row(e, lane);
-            const int64_t f = row0 + row;
             const float mu = su[e] * invH, mv = sv[e] * invH;
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
                 const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float dz = rstd[e] * (u[i][e] - mu - xh[i][e] * mv);
-                T dzt = cvt<T>(dz);
-                act[row * ld + col] = dzt;
-                if (f < M) dzo[f * H + col] = dzt;
+                float dz = rnd<T>(rstd[e] * (u[i][e] - mu - xh[i][e] * mv));
+                act[row * ld + col] = cvt<T>(dz);
+                u[i][e] = dz;
             }
         }
+        store_transposed<T, NB>(u, (T*)ws.dzT[l], ws.Mp, w, lane, row0, M);
         if (l > 0) {
             __syncthreads();
             zero_acc<NB>(acc);
@@ -397,56 +429,104 @@ __global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK 
 }
 
 // ---------------------------------------------------------------------------
-// Weight gradient: C[i][j] = sum_r X[r][i] * Y[r][j] over this split's rows.
-// Tile 64 (i) x 64 (j), 4 waves = 2x2 32x32 blocks; rows staged transposed
-// through LDS in chunks of 128.
+// Weight gradient dW[i][j] = sum_k XT[i][k] * YT[j][k] (NT GEMM, both operands
+// feature-major so every lane streams whole 128-B lines along k).
+// Tile 128 (i) x 128 (j): 4 waves in 2x2, each 64x64 = 2x2 MFMA blocks.
+// Split-K over the minibatch rows; each split writes an f32 slab that the
+// reduce kernel sums in split order.  Within a 64-row K chunk, half-wave h
+// supplies k in [32h, 32h+32): the same permutation for A and B, so the
+// MFMA reduction covers the chunk exactly once.
 // ---------------------------------------------------------------------------
-constexpr int kWgChunk = 128;
+template <typename T>
+__device__ inline void load_row32(const T* p, typename MT<T>::frag (&f)[32 / MT<T>::E]);
+
+template <>
+__device__ inline void load_row32<bf16>(const bf16* p, bf16x8 (&f)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f[s] = *(const bf16x8*)(p + 8 * s);
+}
+template <>
+__device__ inline void load_row32<float>(const float* p, float (&f)[32]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        float4 v = *(const float4*)(p + 4 * s);
+        f[4 * s] = v.x;
+        f[4 * s + 1] = v.y;
+        f[4 * s + 2] = v.z;
+        f[4 * s + 3] = v.w;
+    }
+}
 
 template <typename T>
-__global__ __launch_bounds__(256) void wgrad_kernel(const T* __restrict__ X, int ldx,
-                                                    const T* __restrict__ Y, int ldy, int64_t M,
-                                                    int I, int J, int64_t rows_per_split,
-                                                    float* slab, int64_t slab_stride) {
-    constexpr int E = MT<T>::E, KS = MT<T>::KS;
-    constexpr int LDT = kWgChunk + Pad<T>::v;
-    __shared__ __attribute__((aligned(16))) T XT[64 * LDT];
-    __shared__ __attribute__((aligned(16))) T YT[64 * LDT];
+__global__ __launch_bounds__(256) void wgrad_nt_kernel(const T* __restrict__ XT,
+                                                       const T* __restrict__ YT, int64_t ldk,
+                                                       int I, int J, int64_t rps, float* slab) {
+    constexpr int E = MT<T>::E, NS = 32 / E;
+    typedef typename MT<T>::frag frag;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int ib = w & 1, jb = w >> 1, r = lane & 31, h = lane >> 5;
-    const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
-    const int64_t rbeg = blockIdx.z * rows_per_split;
-    const int64_t rend = rbeg + rows_per_split < M ? rbeg + rows_per_split : M;
-    const bool active = j0 + jb * 32 < J;
-    f32x16 acc[1];
-    zero_acc<1>(acc);
-    for (int64_t rc = rbeg; rc < rend; rc += kWgChunk) {
-        for (int idx = tid; idx < kWgChunk * 64; idx += 256) {
-            int rr = idx >> 6, c = idx & 63;
-            int64_t row = rc + rr;
-            bool ok = row < rend;
-            XT[c * LDT + rr] = (ok && i0 + c < I) ? X[row * ldx + i0 + c] : cvt<T>(0.f);
-            YT[c * LDT + rr] = (ok && j0 + c < J) ? Y[row * ldy + j0 + c] : cvt<T>(0.f);
-        }
-        __syncthreads();
-        if (active) {
-            const T* ap = XT + (ib * 32 + r) * LDT + h * E;
-            const T* bp = YT + (jb * 32 + r) * LDT + h * E;
-#pragma unroll 4
-            for (int k0 = 0; k0 < kWgChunk; k0 += KS)
-                acc[0] = MT<T>::mma(MT<T>::load(ap + k0), MT<T>::load(bp + k0), acc[0]);
-        }
-        __syncthreads();
-    }
-    if (active) {
-        float* out = slab + blockIdx.z * slab_stride;
+    const int r = lane & 31, h = lane >> 5;
+    const int wi = w & 1, wj = w >> 1;
+    const int i0 = blockIdx.x * kWgTile + wi * 64;
+    const int j0 = blockIdx.y * kWgTile + wj * 64;
+    const bool ai[2] = {i0 < I, i0 + 32 < I};
+    const bool bj[2] = {j0 < J, j0 + 32 < J};
+    if (!ai[0] || !bj[0]) return;  // whole wave out of range (no barriers below)
+    const int64_t k0 = blockIdx.z * rps;
+    const int64_t k1 = k0 + rps < ldk ? k0 + rps : ldk;
+    f32x16 acc[2][2];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            int i = i0 + ib * 32 + acc_row(e, lane);
-            int j = j0 + jb * 32 + r;
-            if (i < I && j < J) out[(int64_t)i * J + j] = acc[0][e];
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+    const T* xp[2];
+    const T* yp[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        xp[a] = XT + (int64_t)(ai[a] ? i0 + 32 * a + r : i0 + r) * ldk + 32 * h;
+        yp[a] = YT + (int64_t)(bj[a] ? j0 + 32 * a + r : j0 + r) * ldk + 32 * h;
+    }
+    for (int64_t k = k0; k < k1; k += kWgChunk) {
+        frag fa[2][NS], fb[2][NS];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            load_row32<T>(xp[a] + k, fa[a]);
+            load_row32<T>(yp[a] + k, fb[a]);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a][s], fb[b][s], acc[a][b]);
+    }
+    float* out = slab + (int64_t)blockIdx.z * I * J;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        if (!ai[a]) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            if (!bj[b]) continue;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                int i = i0 + 32 * a + acc_row(e, lane);
+                int j = j0 + 32 * b + r;
+                out[(int64_t)i * J + j] = acc[a][b][e];
+            }
         }
     }
+}
+
+// First level of the per-tile column partials (LayerNorm scale/bias grads,
+// head-bias grad): colpart2[c][col] = sum over tiles t = c, c + 32, ...
+__global__ __launch_bounds__(256) void colsum_kernel(WsK ws) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (col >= ws.CP) return;
+    float s = 0.f;
+    for (int t = c; t < ws.ntiles; t += kColChunks) s += ws.colpart[(int64_t)t * ws.CP + col];
+    ws.colpart2[(int64_t)c * ws.CP + col] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -478,28 +558,33 @@ LayoutK make_layout(const mlearn_mlp_policy& p) {
 __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad) {
     int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     if (p >= Lk.total) return;
-    const int H = Lk.H;
+    const int H = Lk.H, L = Lk.L;
     float g = 0.f;
+    auto colsum = [&](int col) {
+        float t = 0.f;
+        for (int c = 0; c < kColChunks; ++c) t += ws.colpart2[(int64_t)c * ws.CP + col];
+        return t;
+    };
     if (p >= Lk.hb_off) {
-        int j = (int)(p - Lk.hb_off);
-        for (int t = 0; t < ws.ntiles; ++t) g += ws.hb_part[(int64_t)t * MLEARN_HEAD_COLS + j];
+        g = colsum(L * 4 * H + (int)(p - Lk.hb_off));
     } else if (p >= Lk.hw_off) {
         int64_t q = p - Lk.hw_off;
         int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
-        const float* s = ws.slab + ws.slab_off[Lk.L] + (int64_t)i * MLEARN_HEAD_COLS + j;
-        for (int k = 0; k < kSplits; ++k) g += s[k * ws.slab_stride];
+        const float* s = ws.slab + ws.slab_off[L] + (int64_t)i * MLEARN_HEAD_COLS + j;
+        const int64_t stride = (int64_t)H * MLEARN_HEAD_COLS;
+        for (int k = 0; k < ws.splits[L]; ++k) g += s[k * stride];
     } else {
-        int l = Lk.L - 1;
+        int l = L - 1;
         while (l > 0 && p < Lk.w_off[l]) --l;
-        if (p >= Lk.b_off[l] || p >= Lk.s_off[l]) {
+        if (p >= Lk.s_off[l]) {
             const int which = p >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
             const int col = (int)(p - (which ? Lk.s_off[l] : Lk.b_off[l]));
-            for (int t = 0; t < ws.ntiles; ++t)
-                for (int rb = 0; rb < 2; ++rb)
-                    g += ws.ln_part[((((int64_t)t * Lk.L + l) * 2 + rb) * 2 + which) * H + col];
+            g = colsum(((l * 2 + 0) * 2 + which) * H + col) + colsum(((l * 2 + 1) * 2 + which) * H + col);
         } else {
+            const int I = l == 0 ? Lk.D : H;
             const float* s = ws.slab + ws.slab_off[l] + (p - Lk.w_off[l]);
-            for (int k = 0; k < kSplits; ++k) g += s[k * ws.slab_stride];
+            const int64_t stride = (int64_t)I * H;
+            for (int k = 0; k < ws.splits[l]; ++k) g += s[k * stride];
         }
     }
     grad[p] = g;
@@ -508,20 +593,47 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
 // loss_out: five Metric vectors {mean, m2, min, max, count} in the order of
 // PPO.add_metrics (ppo.py:95-106): 'Loss' (scalar: {loss, 0, loss, loss, 1}),
 // 'Action Obj', 'Value Loss', 'Value Errors', 'Entropy'.
-__global__ void reduce_loss_kernel(WsK ws, HpK hp, int64_t M, int K, float* out) {
+__global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64_t M, int K,
+                                                            float* out) {
+    __shared__ double sh[16][kLossSlots];
     __shared__ double tot[kLossSlots];
-    int s = threadIdx.x;
-    if (s < kLossSlots) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    double v[kLossSlots];
+#pragma unroll
+    for (int s = 0; s < kLossSlots; ++s) {
         const int kind = (s < 16) ? (s & 3) : 0;
-        double v = ws.loss_part[s];
-        for (int t = 1; t < ws.ntiles; ++t) {
+        v[s] = kind == 2 ? 3.4e38 : (kind == 3 ? -3.4e38 : 0.0);
+    }
+    for (int t = tid; t < ws.ntiles; t += 1024) {
+#pragma unroll
+        for (int s = 0; s < kLossSlots; ++s) {
+            const int kind = (s < 16) ? (s & 3) : 0;
             double u = ws.loss_part[(int64_t)t * kLossSlots + s];
-            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
+            v[s] = kind == 2 ? fmin(v[s], u) : (kind == 3 ? fmax(v[s], u) : v[s] + u);
         }
-        tot[s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < kLossSlots; ++s) {
+        const int kind = (s < 16) ? (s & 3) : 0;
+        double x = v[s];
+        for (int o = 1; o < 64; o <<= 1) {
+            double u = __shfl_xor(x, o);
+            x = kind == 2 ? fmin(x, u) : (kind == 3 ? fmax(x, u) : x + u);
+        }
+        if (lane == 0) sh[w][s] = x;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid < kLossSlots) {
+        const int kind = (tid < 16) ? (tid & 3) : 0;
+        double x = sh[0][tid];
+        for (int i = 1; i < 16; ++i) {
+            double u = sh[i][tid];
+            x = kind == 2 ? fmin(x, u) : (kind == 3 ? fmax(x, u) : x + u);
+        }
+        tot[tid] = x;
+    }
+    __syncthreads();
+    if (tid == 0) {
         const double nk = (double)M * K, n = (double)M;
         const double obj_mean = tot[0] / nk, vl_mean = tot[4] / n;
         // loss = -mean(obj) + c_v * mean(vl) - sum_k c_e[k] * mean(H_k)   (ppo.py:241-252)
@@ -591,23 +703,22 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hipLaunchKernelGGL(kf, dim3(ws.ntiles), dim3(256), lf, s, P, R, mb_seq, mb, M, adv_st, hp, ws);
     hipLaunchKernelGGL(kb, dim3(ws.ntiles), dim3(256), lb, s, P, M, ws);
 
-    const int64_t rps = ((M + kSplits - 1) / kSplits + kWgChunk - 1) / kWgChunk * kWgChunk;
-    for (int l = 0; l < p.num_layers; ++l) {
-        const int I = l == 0 ? p.obs_dim : H;
-        const T* X = l == 0 ? (const T*)ws.x0 : (const T*)ws.a[l - 1];
-        hipLaunchKernelGGL(wgrad_kernel<T>, dim3((I + 63) / 64, (H + 63) / 64, kSplits), dim3(256),
-                           0, s, X, I, (const T*)ws.dz[l], H, M, I, H, rps,
-                           ws.slab + ws.slab_off[l], ws.slab_stride);
+    const int L = p.num_layers;
+    for (int l = 0; l <= L; ++l) {
+        const int I = l == L ? H : (l == 0 ? p.obs_dim : H);
+        const int J = l == L ? MLEARN_HEAD_COLS : H;
+        const T* X = l == 0 ? (const T*)ws.x0T : (const T*)ws.aT[l - 1];
+        const T* Y = l == L ? (const T*)ws.dheadT : (const T*)ws.dzT[l];
+        dim3 g((I + kWgTile - 1) / kWgTile, (J + kWgTile - 1) / kWgTile, ws.splits[l]);
+        hipLaunchKernelGGL(wgrad_nt_kernel<T>, g, dim3(256), 0, s, X, Y, ws.Mp, I, J, ws.rps[l],
+                           ws.slab + ws.slab_off[l]);
     }
-    hipLaunchKernelGGL(wgrad_kernel<T>, dim3((H + 63) / 64, 1, kSplits), dim3(256), 0, s,
-                       (const T*)ws.a[p.num_layers - 1], H, (const T*)ws.dhead, MLEARN_HEAD_COLS, M,
-                       H, MLEARN_HEAD_COLS, rps, ws.slab + ws.slab_off[p.num_layers],
-                       ws.slab_stride);
+    hipLaunchKernelGGL(colsum_kernel, dim3((ws.CP + 255) / 256, kColChunks), dim3(256), 0, s, ws);
     LayoutK Lk = make_layout(p);
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 255) / 256)), dim3(256), 0,
                        s, Lk, ws, grad);
     if (loss_out)
-        hipLaunchKernelGGL(reduce_loss_kernel, dim3(1), dim3(64), 0, s, ws, hp, M,
+        hipLaunchKernelGGL(reduce_loss_kernel, dim3(1), dim3(1024), 0, s, ws, hp, M,
                            p.actions.num_groups, loss_out);
     return check_launch("ppo_minibatch_grad");
 }
