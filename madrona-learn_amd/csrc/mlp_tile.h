@@ -42,39 +42,31 @@ template <int NB> __device__ inline void zero_acc(f32x16 (&acc)[NB]) {
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
 }
 
-// Row sums of two per-element quantities over all H columns of the tile.
-// u[i][e], v[i][e] are this lane's values; returns per-register row totals
-// (identical in every lane that holds that row).  red: LDS [4][64][2] floats.
-template <int NB>
-__device__ inline void row_sums2(const float (&u)[NB][16], const float (&v)[NB][16], float (&su)[16],
-                                 float (&sv)[16], float* red, int w, int lane) {
+// In-place row totals: s[e], q[e] hold this lane's partial sums (over its
+// column blocks) for the rows of its 16 accumulator registers; on return they
+// hold the totals over all H columns (identical in every lane holding a row).
+// red: LDS [4][64][2] floats.  Contains one workgroup barrier.
+__device__ inline void row_reduce2(float (&s)[16], float (&q)[16], float* red, int w, int lane) {
     const int rb = w & 1;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            a += u[i][e];
-            b += v[i][e];
-        }
-        su[e] = wave_sum32(a);
-        sv[e] = wave_sum32(b);
+        s[e] = wave_sum32(s[e]);
+        q[e] = wave_sum32(q[e]);
     }
     if ((lane & 31) == 0) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             int row = rb * 32 + acc_row(e, lane);
-            red[(w * 64 + row) * 2 + 0] = su[e];
-            red[(w * 64 + row) * 2 + 1] = sv[e];
+            red[(w * 64 + row) * 2 + 0] = s[e];
+            red[(w * 64 + row) * 2 + 1] = q[e];
         }
     }
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         int row = rb * 32 + acc_row(e, lane);
-        // fixed order: the wave with the lower column blocks first
-        su[e] = red[(rb * 64 + row) * 2 + 0] + red[((rb + 2) * 64 + row) * 2 + 0];
-        sv[e] = red[(rb * 64 + row) * 2 + 1] + red[((rb + 2) * 64 + row) * 2 + 1];
+        s[e] = red[(rb * 64 + row) * 2 + 0] + red[((rb + 2) * 64 + row) * 2 + 0];
+        q[e] = red[(rb * 64 + row) * 2 + 1] + red[((rb + 2) * 64 + row) * 2 + 1];
     }
 }
 
@@ -125,6 +117,24 @@ __device__ inline void store_transposed(const float (&v)[NB][16], T* XT, int64_t
     }
 }
 
+template <typename T, int NB>
+__device__ inline void store_transposed(const f32x16 (&v)[NB], T* XT, int64_t ldT, int w,
+                                        int lane, int64_t row0, int64_t M) {
+    const int rb = w & 1, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int col = ((w >> 1) + 2 * i) * 32 + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = row0 + rb * 32 + 8 * q + 4 * h;
+            float x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = row + u < M ? v[i][4 * q + u] : 0.f;
+            store4(XT + (int64_t)col * ldT + row, x[0], x[1], x[2], x[3]);
+        }
+    }
+}
+
 // LayerNorm + ReLU epilogue on a wave's accumulators (rows rb*32.., its
 // column blocks).  Writes the compute-dtype activation into act (LDS) and,
 // when given, z (Dense output, row-major), stats (mean, rstd) and the
@@ -132,46 +142,37 @@ __device__ inline void store_transposed(const float (&v)[NB][16], T* XT, int64_t
 template <typename T, int NB>
 __device__ inline void ln_relu_epilogue(f32x16 (&acc)[NB], const float* __restrict__ gamma,
                                         const float* __restrict__ beta, T* act, int ld,
-                                        float* red, int w, int lane, int H, int64_t row0,
-                                        int64_t M, T* z_out, float* st_out, T* aT_out,
-                                        int64_t ldT) {
+                                        float* red, int w, int lane, int H) {
     const int rb = w & 1, r = lane & 31;
-    float u[NB][16], v[NB][16];
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            float x = rnd<T>(acc[i][e]);  // Dense output in the compute dtype
-            acc[i][e] = x;
-            u[i][e] = x;
-            v[i][e] = x * x;
-        }
     float s[16], q[16];
-    row_sums2<NB>(u, v, s, q, red, w, lane);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const float x = rnd<T>(acc[i][e]);  // Dense output in the compute dtype
+            acc[i][e] = x;
+            a += x;
+            b += x * x;
+        }
+        s[e] = a;
+        q[e] = b;
+    }
+    row_reduce2(s, q, red, w, lane);
     const float invH = 1.0f / (float)H;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int row = rb * 32 + acc_row(e, lane);
-        float mean = s[e] * invH;
-        float var = fmaxf(q[e] * invH - mean * mean, 0.f);
-        float rstd = rsqrtf(var + 1e-6f);
-        const int64_t grow = row0 + row;
-        const bool live = grow < M;
-        if (st_out && live && (w >> 1) == 0 && r == 0) {
-            st_out[grow * 2 + 0] = mean;
-            st_out[grow * 2 + 1] = rstd;
-        }
+        const float mean = s[e] * invH;
+        const float var = fmaxf(q[e] * invH - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + 1e-6f);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const int col = ((w >> 1) + 2 * i) * 32 + r;
             float y = (acc[i][e] - mean) * (rstd * gamma[col]) + beta[col];
-            y = fmaxf(rnd<T>(y), 0.f);
-            act[row * ld + col] = cvt<T>(y);
-            u[i][e] = y;
-            if (live && z_out) z_out[grow * H + col] = cvt<T>(acc[i][e]);
+            act[row * ld + col] = cvt<T>(fmaxf(rnd<T>(y), 0.f));
         }
     }
-    if (aT_out) store_transposed<T, NB>(u, aT_out, ldT, w, lane, row0, M);
 }
 
 // Heads: out[64][32] = act[64][H] x head_t^T, waves 0 and 1 (one row block each).

@@ -95,8 +95,7 @@ __global__ __launch_bounds__(256) void policy_step_kernel(PolicyK P, const float
         zero_acc<NB>(acc);
         tile_gemm<T, NB>(acc, act, ld, w & 1, (const T*)P.wt[l], K, K, w, lane);
         __syncthreads();
-        ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, row0, N,
-                                (T*)nullptr, nullptr, (T*)nullptr, 0);
+        ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H);
         __syncthreads();
     }
 

@@ -47,11 +47,8 @@ constexpr int kWgChunk = 64;     // weight-gradient K chunk (rows of the minibat
 
 struct WsK {
     void* x0T;                          // [D][Mp]   gathered obs, transposed
-    void* z[MLEARN_MAX_LAYERS];         // [Mp][H]   Dense outputs (row-major)
-    float* st[MLEARN_MAX_LAYERS];       // [Mp][2]   LayerNorm mean, rstd
     void* aT[MLEARN_MAX_LAYERS];        // [H][Mp]   post-ReLU activations, transposed
-    void* dhead;                        // [Mp][32]  d loss / d head outputs
-    void* dheadT;                       // [32][Mp]
+    void* dheadT;                       // [32][Mp]  d loss / d head outputs, transposed
     void* dzT[MLEARN_MAX_LAYERS];       // [H][Mp]   d loss / d Dense outputs, transposed
     float* colpart;                     // [tiles][CP] per-tile column partials
     float* colpart2;                    // [kColChunks][CP]
@@ -97,12 +94,9 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     w.CP = L * 4 * H + MLEARN_HEAD_COLS;
     w.x0T = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
-        w.z[l] = take(Mp * H * es);
-        w.st[l] = (float*)take(Mp * 2 * sizeof(float));
         w.aT[l] = take(Mp * H * es);
         w.dzT[l] = take(Mp * H * es);
     }
-    w.dhead = take(Mp * MLEARN_HEAD_COLS * es);
     w.dheadT = take(Mp * MLEARN_HEAD_COLS * es);
     w.colpart = (float*)take(tiles * w.CP * sizeof(float));
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
@@ -121,73 +115,38 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
 }
 
 // ---------------------------------------------------------------------------
-// Forward + loss + d(loss)/d(head outputs)
+// Fused minibatch step per 64-row tile: gather -> trunk forward -> heads ->
+// PPO loss terms and d loss / d head -> backward through heads, ReLU and
+// LayerNorm of every layer.  Each layer's Dense output stays in registers
+// (packed bf16 pairs in bf16 mode) between the forward and the backward, so
+// the only HBM writes are the weight-gradient operands (x0^T, a_l^T, dHead^T,
+// dZ_l^T, feature-major) and the per-tile column / loss partials.
 // ---------------------------------------------------------------------------
-template <typename T, int H>
-__global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
-                                                      const int32_t* __restrict__ mb_seq, int mb,
-                                                      int64_t M, const float* __restrict__ adv_st,
-                                                      HpK hp, WsK ws) {
-    constexpr int NB = H / 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int D = P.D;
-    const int ld = (D > H ? D : H) + Pad<T>::v;
-    T* act = (T*)smem;
-    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));
-    float* lgt = red + 4 * 64 * 2;                   // [64][33]
-    float* dl = lgt + kTileRows * 33;                // [64][33] d loss / d head
-    int64_t* srow = (int64_t*)(dl + kTileRows * 33); // [64]
-    double* dred = (double*)(srow + kTileRows);      // [4][kLossSlots]
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
-
-    if (tid < kTileRows) {
-        int64_t f = row0 + tid;
-        int64_t sr = -1;
-        if (f < M) {
-            int tl = (int)(f / mb);
-            int m = (int)(f - (int64_t)tl * mb);
-            int64_t seq = mb_seq[m];
-            int64_t c = seq / ro.N, b = seq - c * ro.N;
-            sr = (c * ro.bptt + tl) * ro.N + b;
-        }
-        srow[tid] = sr;
+template <typename T, int NB> struct ZStore;
+template <int NB> struct ZStore<bf16, NB> {
+    uint32_t d[NB][8];
+    __device__ void set(int i, int e, float x) {  // x is already bf16-valued
+        const uint32_t b = __builtin_bit_cast(uint32_t, x) >> 16;
+        d[i][e >> 1] = (e & 1) ? ((d[i][e >> 1] & 0x0000ffffu) | (b << 16))
+                               : ((d[i][e >> 1] & 0xffff0000u) | b);
     }
-    __syncthreads();
-
-    // gather the observation rows
-    const T* obs = (const T*)ro.obs;
-    for (int idx = tid; idx < kTileRows * D; idx += 256) {
-        int rr = idx / D, c = idx - rr * D;
-        int64_t sr = srow[rr];
-        act[rr * ld + c] = sr >= 0 ? obs[sr * D + c] : cvt<T>(0.f);
+    __device__ float get(int i, int e) const {
+        const uint32_t b = (e & 1) ? (d[i][e >> 1] & 0xffff0000u) : (d[i][e >> 1] << 16);
+        return __builtin_bit_cast(float, b);
     }
-    __syncthreads();
-    // x0^T for the layer-0 weight gradient: 4 rows per store
-    {
-        T* x0T = (T*)ws.x0T;
-        for (int idx = tid; idx < D * (kTileRows / 4); idx += 256) {
-            int c = idx % D, g = idx / D;
-            store4(x0T + (int64_t)c * ws.Mp + row0 + 4 * g, to_f32(act[(4 * g) * ld + c]),
-                   to_f32(act[(4 * g + 1) * ld + c]), to_f32(act[(4 * g + 2) * ld + c]),
-                   to_f32(act[(4 * g + 3) * ld + c]));
-        }
-    }
+};
+template <int NB> struct ZStore<float, NB> {
+    float d[NB][16];
+    __device__ void set(int i, int e, float x) { d[i][e] = x; }
+    __device__ float get(int i, int e) const { return d[i][e]; }
+};
 
-    for (int l = 0; l < P.L; ++l) {
-        const int K = l == 0 ? D : H;
-        f32x16 acc[NB];
-        zero_acc<NB>(acc);
-        tile_gemm<T, NB>(acc, act, ld, w & 1, (const T*)P.wt[l], K, K, w, lane);
-        __syncthreads();
-        ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, row0, M,
-                                (T*)ws.z[l], ws.st[l], (T*)ws.aT[l], ws.Mp);
-        __syncthreads();
-    }
-    heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
-    __syncthreads();
-
+// PPO loss terms of the tile (ppo.py:129-262) and d loss / d {logits, value}
+// into dl[64][33]; per-tile loss/metric partials into ws.loss_part.
+template <typename T>
+__device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const float* adv_st,
+                                 const HpK& hp, const WsK& ws, const float* lgt, float* dl,
+                                 const int64_t* srow, double* dred, int tid, int lane, int w) {
     // loss terms: tasks (row, group) then (row, value)
     const float adv_mean = adv_st[0], adv_rstd = adv_st[1];
     double sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
@@ -285,27 +244,6 @@ __global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
         }
     }
     __syncthreads();
-
-    // d head -> HBM (compute dtype, row-major and transposed), head-bias partials
-    T* dh = (T*)ws.dhead;
-    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
-        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
-        dh[(row0 + rr) * MLEARN_HEAD_COLS + j] = cvt<T>(dl[rr * 33 + j]);
-    }
-    {
-        T* dhT = (T*)ws.dheadT;
-        for (int idx = tid; idx < MLEARN_HEAD_COLS * (kTileRows / 4); idx += 256) {
-            int j = idx % MLEARN_HEAD_COLS, g = idx / MLEARN_HEAD_COLS;
-            store4(dhT + (int64_t)j * ws.Mp + row0 + 4 * g, dl[(4 * g) * 33 + j],
-                   dl[(4 * g + 1) * 33 + j], dl[(4 * g + 2) * 33 + j], dl[(4 * g + 3) * 33 + j]);
-        }
-    }
-    if (tid < MLEARN_HEAD_COLS) {
-        float s = 0.f;
-        for (int rr = 0; rr < kTileRows; ++rr) s += rnd<T>(dl[rr * 33 + tid]);
-        ws.colpart[(int64_t)blockIdx.x * ws.CP + P.L * 4 * H + tid] = s;
-    }
-
     // tile loss/metric partials
     double vals[kLossSlots] = {sobj, qobj, mnobj, mxobj, svl, qvl, mnvl, mxvl,
                                serr, qerr, mnerr, mxerr, sent, qent, mnent, mxent, sentw, 0, 0, 0};
@@ -331,65 +269,179 @@ __global__ __launch_bounds__(256) void ppo_fwd_kernel(PolicyK P, RolloutK ro,
     }
 }
 
-// ---------------------------------------------------------------------------
-// Backward through heads and the trunk (row-local)
-// ---------------------------------------------------------------------------
-template <typename T, int H>
-__global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK ws) {
+template <typename T, int H, int L>
+__global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
+                                                       const int32_t* __restrict__ mb_seq, int mb,
+                                                       int64_t M, const float* __restrict__ adv_st,
+                                                       HpK hp, WsK ws) {
     constexpr int NB = H / 64;
+    constexpr int PAD = Pad<T>::v;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int ld = H + Pad<T>::v;
-    const int ldh = MLEARN_HEAD_COLS + Pad<T>::v;
+    const int D = P.D;
+    const int ld = (D > H ? D : H) + PAD;
+    const int ldh = MLEARN_HEAD_COLS + PAD;
     T* act = (T*)smem;
-    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));
+    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));  // [4][64][2]
+    float* lgt = red + 4 * 64 * 2;                                      // [64][33]
+    float* dl = lgt + kTileRows * 33;                                   // [64][33]
+    float* stat = dl + kTileRows * 33;                                  // [L][64][2]
+    int64_t* srow = (int64_t*)(stat + L * kTileRows * 2);               // [64]
+    double* dred = (double*)(srow + kTileRows);                         // [4][kLossSlots]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int rb = w & 1, r = lane & 31;
     const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
 
-    const T* dh = (const T*)ws.dhead;
-    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
-        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
-        act[rr * ldh + j] = dh[(row0 + rr) * MLEARN_HEAD_COLS + j];
+    if (tid < kTileRows) {
+        int64_t f = row0 + tid;
+        int64_t sr = -1;
+        if (f < M) {
+            int tl = (int)(f / mb);
+            int m = (int)(f - (int64_t)tl * mb);
+            int64_t seq = mb_seq[m];
+            int64_t c = seq / ro.N, b = seq - c * ro.N;
+            sr = (c * ro.bptt + tl) * ro.N + b;
+        }
+        srow[tid] = sr;
     }
     __syncthreads();
 
+    // gather the observation rows, 16 B per lane
+    {
+        constexpr int V = 16 / sizeof(T);
+        typedef __attribute__((ext_vector_type(4))) uint32_t u32x4v;
+        const T* obs = (const T*)ro.obs;
+        const int cpr = D / V;  // 16-B chunks per row
+        for (int idx = tid; idx < kTileRows * cpr; idx += 256) {
+            int rr = idx / cpr, c = (idx - rr * cpr) * V;
+            int64_t sr = srow[rr];
+            u32x4v v = {0u, 0u, 0u, 0u};
+            if (sr >= 0) v = *(const u32x4v*)(obs + sr * D + c);
+            *(u32x4v*)(act + rr * ld + c) = v;
+        }
+    }
+    __syncthreads();
+    {
+        T* x0T = (T*)ws.x0T;
+        for (int idx = tid; idx < D * (kTileRows / 4); idx += 256) {
+            int c = idx % D, g = idx / D;
+            store4(x0T + (int64_t)c * ws.Mp + row0 + 4 * g, to_f32(act[(4 * g) * ld + c]),
+                   to_f32(act[(4 * g + 1) * ld + c]), to_f32(act[(4 * g + 2) * ld + c]),
+                   to_f32(act[(4 * g + 3) * ld + c]));
+        }
+    }
+
+    // ---- forward ----
+    ZStore<T, NB> z[L];
     f32x16 acc[NB];
+    const float invH = 1.0f / (float)H;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        const int K = l == 0 ? D : H;
+        zero_acc<NB>(acc);
+        tile_gemm<T, NB>(acc, act, ld, rb, (const T*)P.wt[l], K, K, w, lane);
+        __syncthreads();
+        float s[16], q[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            float a = 0.f, b = 0.f;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const float x = rnd<T>(acc[i][e]);  // Dense output in the compute dtype
+                acc[i][e] = x;
+                z[l].set(i, e, x);
+                a += x;
+                b += x * x;
+            }
+            s[e] = a;
+            q[e] = b;
+        }
+        row_reduce2(s, q, red, w, lane);
+        const float* gamma = P.lns[l];
+        const float* beta = P.lnb[l];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = rb * 32 + acc_row(e, lane);
+            const float mean = s[e] * invH;
+            const float var = fmaxf(q[e] * invH - mean * mean, 0.f);
+            const float rstd = rsqrtf(var + 1e-6f);
+            if ((w >> 1) == 0 && r == 0) {
+                stat[(l * kTileRows + row) * 2] = mean;
+                stat[(l * kTileRows + row) * 2 + 1] = rstd;
+            }
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int col = ((w >> 1) + 2 * i) * 32 + r;
+                float y = (acc[i][e] - mean) * (rstd * gamma[col]) + beta[col];
+                y = fmaxf(rnd<T>(y), 0.f);
+                act[row * ld + col] = cvt<T>(y);
+                acc[i][e] = y;
+            }
+        }
+        store_transposed<T, NB>(acc, (T*)ws.aT[l], ws.Mp, w, lane, row0, M);
+        __syncthreads();
+    }
+    heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
+    __syncthreads();
+
+    // ---- loss ----
+    tile_loss<T>(P, ro, adv_st, hp, ws, lgt, dl, srow, dred, tid, lane, w);
+    // (tile_loss ends with a barrier: dl is complete)
+    {
+        T* dhT = (T*)ws.dheadT;
+        for (int idx = tid; idx < MLEARN_HEAD_COLS * (kTileRows / 4); idx += 256) {
+            int j = idx % MLEARN_HEAD_COLS, g = idx / MLEARN_HEAD_COLS;
+            store4(dhT + (int64_t)j * ws.Mp + row0 + 4 * g, dl[(4 * g) * 33 + j],
+                   dl[(4 * g + 1) * 33 + j], dl[(4 * g + 2) * 33 + j], dl[(4 * g + 3) * 33 + j]);
+        }
+    }
+    if (tid < MLEARN_HEAD_COLS) {
+        float sum = 0.f;
+        for (int rr = 0; rr < kTileRows; ++rr) sum += rnd<T>(dl[rr * 33 + tid]);
+        ws.colpart[(int64_t)blockIdx.x * ws.CP + L * 4 * H + tid] = sum;
+    }
+    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
+        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
+        act[rr * ldh + j] = cvt<T>(dl[rr * 33 + j]);
+    }
+    __syncthreads();
+
+    // ---- backward ----
     zero_acc<NB>(acc);
     // dA_{L-1} = dHead . Head^T    (B^T = head [H][32])
     tile_gemm<T, NB>(acc, act, ldh, rb, (const T*)P.head, MLEARN_HEAD_COLS, MLEARN_HEAD_COLS, w,
                      lane);
-
-    for (int l = P.L - 1; l >= 0; --l) {
+#pragma unroll
+    for (int l = L - 1; l >= 0; --l) {
         __syncthreads();
-        const T* z = (const T*)ws.z[l];
-        const float* st = ws.st[l];
         const float* gamma = P.lns[l];
         const float* beta = P.lnb[l];
-        float u[NB][16], v[NB][16], xh[NB][16];
-        float mean[16], rstd[16];
-        float pg[NB], pb[NB];
+        float su[16], sv[16], pg[NB], pb[NB];
 #pragma unroll
         for (int i = 0; i < NB; ++i) pg[i] = pb[i] = 0.f;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int64_t f = row0 + rb * 32 + acc_row(e, lane);
-            const bool live = f < M;
-            mean[e] = live ? st[f * 2] : 0.f;
-            rstd[e] = live ? st[f * 2 + 1] : 0.f;
+            const int row = rb * 32 + acc_row(e, lane);
+            const bool live = row0 + row < M;
+            const float mean = stat[(l * kTileRows + row) * 2];
+            const float rstd = stat[(l * kTileRows + row) * 2 + 1];
+            float a = 0.f, b = 0.f;
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
                 const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float zz = live ? to_f32(z[f * H + col]) : 0.f;
-                float x = (zz - mean[e]) * rstd[e];
-                float y = (zz - mean[e]) * (rstd[e] * gamma[col]) + beta[col];
-                float dy = (live && rnd<T>(y) > 0.f) ? acc[i][e] : 0.f;  // ReLU'
-                xh[i][e] = x;
-                u[i][e] = dy * gamma[col];
-                v[i][e] = u[i][e] * x;
-                pg[i] += dy * x;
+                const float zz = z[l].get(i, e);
+                const float xh = (zz - mean) * rstd;
+                const float y = (zz - mean) * (rstd * gamma[col]) + beta[col];
+                const float dy = (live && rnd<T>(y) > 0.f) ? acc[i][e] : 0.f;  // ReLU'
+                const float u = dy * gamma[col];
+                acc[i][e] = u;
+                a += u;
+                b += u * xh;
+                pg[i] += dy * xh;
                 pb[i] += dy;
             }
+            su[e] = a;
+            sv[e] = b;
         }
         // LayerNorm scale/bias partials: fold the two half-waves, one writer per column
 #pragma unroll
@@ -403,22 +455,23 @@ __global__ __launch_bounds__(256) void ppo_bwd_kernel(PolicyK P, int64_t M, WsK 
                 lp[H + col] = pg[i];
             }
         }
-        float su[16], sv[16];
-        row_sums2<NB>(u, v, su, sv, red, w, lane);
-        const float invH = 1.0f / (float)H;
+        row_reduce2(su, sv, red, w, lane);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int row = rb * 32 + acc_row(e, lane);
+            const float mean = stat[(l * kTileRows + row) * 2];
+            const float rstd = stat[(l * kTileRows + row) * 2 + 1];
             const float mu = su[e] * invH, mv = sv[e] * invH;
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
                 const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float dz = rnd<T>(rstd[e] * (u[i][e] - mu - xh[i][e] * mv));
+                const float xh = (z[l].get(i, e) - mean) * rstd;
+                const float dz = rnd<T>(rstd * (acc[i][e] - mu - xh * mv));
                 act[row * ld + col] = cvt<T>(dz);
-                u[i][e] = dz;
+                acc[i][e] = dz;
             }
         }
-        store_transposed<T, NB>(u, (T*)ws.dzT[l], ws.Mp, w, lane, row0, M);
+        store_transposed<T, NB>(acc, (T*)ws.dzT[l], ws.Mp, w, lane, row0, M);
         if (l > 0) {
             __syncthreads();
             zero_acc<NB>(acc);
@@ -484,8 +537,12 @@ __global__ __launch_bounds__(256) void wgrad_nt_kernel(const T* __restrict__ XT,
     const T* yp[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        xp[a] = XT + (int64_t)(ai[a] ? i0 + 32 * a + r : i0 + r) * ldk + 32 * h;
-        yp[a] = YT + (int64_t)(bj[a] ? j0 + 32 * a + r : j0 + r) * ldk + 32 * h;
+        // rows past I / J (I = obs_dim may be a multiple of 16 only) read a valid
+        // row; their outputs are dropped below
+        const int xi = i0 + 32 * a + r < I ? i0 + 32 * a + r : I - 1;
+        const int yj = j0 + 32 * a + r < J ? j0 + 32 * a + r : J - 1;
+        xp[a] = XT + (int64_t)xi * ldk + 32 * h;
+        yp[a] = YT + (int64_t)yj * ldk + 32 * h;
     }
     for (int64_t k = k0; k < k1; k += kWgChunk) {
         frag fa[2][NS], fb[2][NS];
@@ -512,7 +569,7 @@ __global__ __launch_bounds__(256) void wgrad_nt_kernel(const T* __restrict__ XT,
             for (int e = 0; e < 16; ++e) {
                 int i = i0 + 32 * a + acc_row(e, lane);
                 int j = j0 + 32 * b + r;
-                out[(int64_t)i * J + j] = acc[a][b][e];
+                if (i < I && j < J) out[(int64_t)i * J + j] = acc[a][b][e];
             }
         }
     }
@@ -656,14 +713,25 @@ __global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64
     }
 }
 
-static size_t fwd_lds(int D, int H, int es) {
+static size_t step_lds(int D, int H, int L, int es) {
     int ld = (D > H ? D : H) + 16 / es;
-    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4 + 2 * kTileRows * 33 * 4 + kTileRows * 8 +
-           4 * kLossSlots * 8;
+    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4 + 2 * kTileRows * 33 * 4 +
+           (size_t)L * kTileRows * 2 * 4 + kTileRows * 8 + 4 * kLossSlots * 8;
 }
-static size_t bwd_lds(int H, int es) {
-    int ld = H + 16 / es;
-    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4;
+
+template <typename T, int H, int L>
+static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                        int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                        hipStream_t s) {
+    auto k = ppo_step_kernel<T, H, L>;
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    size_t lds = step_lds(P.D, H, L, sizeof(T));
+    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(256), lds, s, P, R, mb_seq, mb, M, adv_st, hp, ws);
 }
 
 template <typename T, int H>
@@ -688,21 +756,12 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
 
-    const int es = sizeof(T);
-    size_t lf = fwd_lds(p.obs_dim, H, es), lb = bwd_lds(H, es);
-    auto kf = ppo_fwd_kernel<T, H>;
-    auto kb = ppo_bwd_kernel<T, H>;
-    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  128 * 1024);
-        (void)hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  128 * 1024);
-        attr_set = true;
+    switch (p.num_layers) {
+        case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
-    hipLaunchKernelGGL(kf, dim3(ws.ntiles), dim3(256), lf, s, P, R, mb_seq, mb, M, adv_st, hp, ws);
-    hipLaunchKernelGGL(kb, dim3(ws.ntiles), dim3(256), lb, s, P, M, ws);
-
     const int L = p.num_layers;
     for (int l = 0; l <= L; ++l) {
         const int I = l == L ? H : (l == 0 ? p.obs_dim : H);
