@@ -114,18 +114,25 @@ int mlearn_action_stats_f32(const float* logits, int64_t ld, mlearn_action_layou
 /* BackboneEncoder 131-153, models.py MLP 99-119, LayerNorm 46-56,          */
 /* DenseLayerDiscreteActor 122-139, DenseLayerCritic 142-154).             */
 /* ---------------------------------------------------------------------- */
+/* The compute-dtype weight copies are "fragment-order" images (written by
+ * mlearn_policy_sync_weights / mlearn_optim_step): a logical matrix Bt[N][K]
+ * stores element (n, k) at
+ *   ((n/32 * K/KS + k/KS) * 64 + n%32 + 32*((k%KS)/E)) * E + k%E
+ * with (E, KS) = (8, 16) for bf16 and (1, 2) for f32, so that one wave's
+ * matrix-core B operand is a single contiguous run. */
 typedef struct mlearn_mlp_policy {
     int32_t dtype;       /* compute dtype: MLEARN_DTYPE_F32 / MLEARN_DTYPE_BF16 */
     int32_t obs_dim;     /* multiple of 16, <= 256 */
     int32_t hidden;      /* 64, 128 or 256 */
     int32_t num_layers;  /* 1..MLEARN_MAX_LAYERS */
     mlearn_action_layout actions;
-    const void* w_t[MLEARN_MAX_LAYERS];    /* [hidden][in_l] compute dtype (Dense kernel^T) */
-    const void* w[MLEARN_MAX_LAYERS];      /* [in_l][hidden] compute dtype (Dense kernel) */
+    const void* w_t[MLEARN_MAX_LAYERS];  /* hidden*in_l: Bt[n=out][k=in] = W_l[k][n] */
+    const void* w[MLEARN_MAX_LAYERS];    /* hidden*in_l: Bt[n=in][k=out] = W_l[n][k];
+                                            w[0] is not used */
     const float* ln_scale[MLEARN_MAX_LAYERS];  /* [hidden] f32 */
     const float* ln_bias[MLEARN_MAX_LAYERS];   /* [hidden] f32 */
-    const void* head_t;      /* [32][hidden] compute dtype; rows 0..A-1 actor, row A critic */
-    const void* head;        /* [hidden][32] compute dtype */
+    const void* head_t;      /* 32*hidden: Bt[n=head col][k=unit]; cols 0..A-1 actor, A critic */
+    const void* head;        /* 32*hidden: Bt[n=unit][k=head col] */
     const float* head_bias;  /* [32] f32 */
 } mlearn_mlp_policy;
 

@@ -52,60 +52,66 @@ int validate_policy(const mlearn_mlp_policy* p) {
     for (int k = 0; k < l.num_groups; ++k)
         ML_REQUIRE(l.offsets[k + 1] > l.offsets[k], "policy: empty action group %d", k);
     for (int i = 0; i < p->num_layers; ++i)
-        ML_REQUIRE(p->w_t[i] && p->w[i] && p->ln_scale[i] && p->ln_bias[i],
+        ML_REQUIRE(p->w_t[i] && (i == 0 || p->w[i]) && p->ln_scale[i] && p->ln_bias[i],
                    "policy: null layer %d weights", i);
     ML_REQUIRE(p->head_t && p->head && p->head_bias, "policy: null head weights");
     return MLEARN_OK;
 }
 
+// One workgroup = 32 rows x H/32 waves; wave w computes output column block w
+// of every layer (NB = 1), so a 8192-env step runs 256 workgroups x 8 waves.
 template <typename T, int H>
-__global__ __launch_bounds__(256) void policy_step_kernel(PolicyK P, const float* __restrict__ obs,
-                                                          int64_t N, T* obs_store, int32_t* actions,
-                                                          float* logp, float* values, uint32_t k0,
-                                                          uint32_t k1, const uint64_t* step_ctr,
-                                                          uint64_t step_add, uint32_t eoff,
-                                                          int sample) {
-    constexpr int NB = H / 64;
+__global__ __launch_bounds__(2 * H) void policy_step_kernel(PolicyK P, const float* __restrict__ obs,
+                                                            int64_t N, T* obs_store,
+                                                            int32_t* actions, float* logp,
+                                                            float* values, uint32_t k0,
+                                                            uint32_t k1, const uint64_t* step_ctr,
+                                                            uint64_t step_add, uint32_t eoff,
+                                                            int sample) {
+    constexpr int W = H / 32, CG = W, ROWS = 32, THREADS = 64 * W;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D;
     const int ld = (D > H ? D : H) + Pad<T>::v;
     T* act = (T*)smem;
-    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));
-    float* lgt = red + 4 * 64 * 2;
+    float* red = (float*)(act + ROWS * ld);  // [W][32][2]
+    float* lgt = red + W * ROWS * 2;         // [32][33]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const uint64_t step = (step_ctr ? *step_ctr : 0ull) + step_add;
 
-    // 1. preprocess (cast) + store the observation tile
-    for (int idx = tid; idx < kTileRows * D; idx += 256) {
-        int rr = idx / D, c = idx - rr * D;
-        int64_t n = row0 + rr;
-        float x = n < N ? obs[n * D + c] : 0.f;
-        T xt = cvt<T>(x);
-        act[rr * ld + c] = xt;
-        if (obs_store && n < N) obs_store[n * D + c] = xt;
+    // 1. preprocess (cast) + store the observation tile, 16 B loads
+    {
+        const int cpr = D / 4;
+        for (int idx = tid; idx < ROWS * cpr; idx += THREADS) {
+            int rr = idx / cpr, c = (idx - rr * cpr) * 4;
+            int64_t n = row0 + rr;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < N) x = *(const float4*)(obs + n * D + c);
+            store4(act + rr * ld + c, x.x, x.y, x.z, x.w);
+            if (obs_store && n < N) store4(obs_store + n * D + c, x.x, x.y, x.z, x.w);
+        }
     }
-    __syncthreads();
+    lds_barrier();
 
     // 2. trunk
     for (int l = 0; l < P.L; ++l) {
         const int K = l == 0 ? D : H;
-        f32x16 acc[NB];
-        zero_acc<NB>(acc);
-        tile_gemm<T, NB>(acc, act, ld, w & 1, (const T*)P.wt[l], K, K, w, lane);
-        __syncthreads();
-        ln_relu_epilogue<T, NB>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H);
-        __syncthreads();
+        f32x16 acc[1];
+        zero_acc<1>(acc);
+        gemm_direct<T, 1, CG>(acc, act, ld, 0, (const T*)P.wt[l], K, H, w, lane);
+        ln_relu_epilogue<T, 1, 1, CG>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, nullptr,
+                                      nullptr);
+        lds_barrier();
     }
 
     // 3. actor + critic heads
-    heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
-    __syncthreads();
+    heads_to_lds<T, 1, CG>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
+    lds_barrier();
 
     // 4. sample + store
     if (actions) {
-        for (int task = tid; task < kTileRows * P.K; task += 256) {
+        for (int task = tid; task < ROWS * P.K; task += THREADS) {
             int rr = task / P.K, g = task - rr * P.K;
             int64_t n = row0 + rr;
             if (n >= N) continue;
@@ -118,7 +124,7 @@ __global__ __launch_bounds__(256) void policy_step_kernel(PolicyK P, const float
         }
     }
     if (values) {
-        for (int rr = tid; rr < kTileRows; rr += 256) {
+        for (int rr = tid; rr < ROWS; rr += THREADS) {
             int64_t n = row0 + rr;
             if (n < N) values[n] = lgt[rr * 33 + P.A];
         }
@@ -127,7 +133,8 @@ __global__ __launch_bounds__(256) void policy_step_kernel(PolicyK P, const float
 
 size_t policy_step_lds(int D, int H, int esize) {
     int ld = (D > H ? D : H) + 16 / esize;
-    return (size_t)kTileRows * ld * esize + 4 * 64 * 2 * sizeof(float) + kTileRows * 33 * sizeof(float);
+    return (size_t)32 * ld * esize + (size_t)(H / 32) * 32 * 2 * sizeof(float) +
+           32 * 33 * sizeof(float);
 }
 
 template <typename T, int H>
@@ -140,12 +147,12 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  64 * 1024 * 2);
+                                  128 * 1024);
         attr_set = true;
     }
-    int grid = (int)((N + kTileRows - 1) / kTileRows);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, P, obs, N, (T*)obs_store, actions, logp,
-                       values, k0, k1, step_ctr, step, eoff, sample);
+    int grid = (int)((N + 31) / 32);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(2 * H), lds, s, P, obs, N, (T*)obs_store, actions,
+                       logp, values, k0, k1, step_ctr, step, eoff, sample);
     return check_launch("policy_rollout_step");
 }
 
@@ -166,6 +173,9 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
     ML_REQUIRE(obs, "policy_rollout_step: null obs");
     ML_REQUIRE(!actions || log_probs || !sample, "policy_rollout_step: sampling needs log_probs");
     ML_REQUIRE(actions || values, "policy_rollout_step: nothing to compute");
+    ML_REQUIRE((uintptr_t)obs % 16 == 0, "policy_rollout_step: obs must be 16-byte aligned");
+    ML_REQUIRE(!obs_store || (uintptr_t)obs_store % 16 == 0,
+               "policy_rollout_step: obs_store must be 16-byte aligned");
     PolicyK P = make_policy_k(*policy);
     hipStream_t s = S(stream);
 #define ML_DISPATCH(T)                                                                              \

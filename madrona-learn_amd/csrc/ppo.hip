@@ -41,6 +41,10 @@ struct HpK {
 };
 
 constexpr int kLossSlots = 20;   // per tile doubles
+constexpr int kStepRows = 32;    // rows per fused-step tile
+#ifndef ML_STEP_WAVES
+#define ML_STEP_WAVES 2
+#endif
 constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 constexpr int kWgChunk = 64;     // weight-gradient K chunk (rows of the minibatch)
@@ -59,8 +63,24 @@ struct WsK {
     int64_t rps[MLEARN_MAX_LAYERS + 1];  // rows per split
     int64_t Mp;
     int ntiles;
-    int CP;                             // L*4*H + 32
+    int CP;                             // L*2*H + 32
+    uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
+
+#ifdef ML_STAMPS
+static uint64_t* g_stamp_buf = nullptr;
+#define STAMP(i)                                                                   \
+    do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+        if (ws.stamps && threadIdx.x == 0)                                         \
+            ws.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -80,8 +100,8 @@ static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
 static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
-    const int64_t tiles = (M + kTileRows - 1) / kTileRows;
-    const int64_t Mp = tiles * kTileRows;
+    const int64_t tiles = (M + kStepRows - 1) / kStepRows;
+    const int64_t Mp = ((tiles * kStepRows + kWgChunk - 1) / kWgChunk) * kWgChunk;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char* ptr = base ? base + off : nullptr;
@@ -91,7 +111,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     WsK w{};
     w.Mp = Mp;
     w.ntiles = (int)tiles;
-    w.CP = L * 4 * H + MLEARN_HEAD_COLS;
+    w.CP = L * 2 * H + MLEARN_HEAD_COLS;
     w.x0T = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
         w.aT[l] = take(Mp * H * es);
@@ -141,22 +161,29 @@ template <int NB> struct ZStore<float, NB> {
     __device__ float get(int i, int e) const { return d[i][e]; }
 };
 
+// Per-row loss inputs gathered from the store at the start of the tile.
+struct LossIn {
+    int32_t* act;  // [ROWS][K]
+    float* lp;     // [ROWS][K]
+    float* adv;    // [ROWS]
+    float* ret;    // [ROWS]
+    float* val;    // [ROWS]
+};
+
 // PPO loss terms of the tile (ppo.py:129-262) and d loss / d {logits, value}
-// into dl[64][33]; per-tile loss/metric partials into ws.loss_part.
-template <typename T>
-__device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const float* adv_st,
-                                 const HpK& hp, const WsK& ws, const float* lgt, float* dl,
-                                 const int64_t* srow, double* dred, int tid, int lane, int w) {
-    // loss terms: tasks (row, group) then (row, value)
+// into dl[ROWS][33]; per-tile loss/metric partials into ws.loss_part.
+template <typename T, int ROWS, int THREADS>
+__device__ inline void tile_loss(const PolicyK& P, const float* adv_st, const HpK& hp,
+                                 const WsK& ws, const float* lgt, float* dl, const LossIn& in,
+                                 const int64_t* srow, float* dred, int tid, int lane, int w) {
     const float adv_mean = adv_st[0], adv_rstd = adv_st[1];
-    double sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
+    float sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
     float mnobj = 3.4e38f, mxobj = -3.4e38f, mnent = 3.4e38f, mxent = -3.4e38f;
     float mnvl = 3.4e38f, mxvl = -3.4e38f, mnerr = 3.4e38f, mxerr = -3.4e38f;
     const int K = P.K, A = P.A;
-    for (int task = tid; task < kTileRows * (K + 1); task += 256) {
-        int rr = task / (K + 1), g = task - rr * (K + 1);
-        int64_t sr = srow[rr];
-        if (sr < 0) {
+    for (int task = tid; task < ROWS * (K + 1); task += THREADS) {
+        const int rr = task / (K + 1), g = task - rr * (K + 1);
+        if (srow[rr] < 0) {
             if (g == K)
                 for (int j = 0; j < 33; ++j) dl[rr * 33 + j] = 0.f;
             continue;
@@ -166,20 +193,21 @@ __device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const flo
             const int nb = P.off[g + 1] - P.off[g];
             float mx = lg[0];
             for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+            float ex[32];
             float se = 0.f;
-            for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+            for (int j = 0; j < nb; ++j) {
+                ex[j] = __expf(lg[j] - mx);
+                se += ex[j];
+            }
+            const float inv = 1.0f / se;
             const float lse = mx + __logf(se);
             float ent = 0.f;
-            for (int j = 0; j < nb; ++j) {
-                float lp = lg[j] - lse;
-                ent -= (__expf(lg[j] - mx) / se) * lp;  // softmax * log_softmax (dists.py:68-69)
-            }
-            const int a = ro.actions[sr * K + g];
+            for (int j = 0; j < nb; ++j) ent -= (ex[j] * inv) * (lg[j] - lse);  // dists.py:68-69
+            const int a = in.act[rr * K + g];
             const float lpa = lg[a] - lse;
-            const float old = ro.logp[sr * K + g];
-            float adv = ro.adv[sr];
+            float adv = in.adv[rr];
             if (hp.norm_adv) adv = (adv - adv_mean) * adv_rstd;
-            const float ratio = __expf(lpa - old);
+            const float ratio = __expf(lpa - in.lp[rr * K + g]);
             const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
             const float s1 = adv * ratio;
             const float y = fmaxf(ratio, lo);
@@ -191,33 +219,33 @@ __device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const flo
             const float dmn = y < hi ? 1.f : (y == hi ? 0.5f : 0.f);
             const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
             const float dobj = w1 * adv + (1.f - w1) * adv * (dmx * dmn);
-            const float g_lp = -hp.inv_sk * dobj * ratio;          // d loss / d logp[a]
-            const float ce = hp.ecoef[g] * hp.inv_sk;               // entropy term weight
+            const float g_lp = -hp.inv_sk * dobj * ratio;  // d loss / d logp[a]
+            const float ce = hp.ecoef[g] * hp.inv_sk;       // entropy term weight
             for (int j = 0; j < nb; ++j) {
-                float p = __expf(lg[j] - mx) / se;
-                float lp = lg[j] - lse;
-                float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * (lp + ent);
+                const float p = ex[j] * inv;
+                const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lg[j] - lse) + ent);
                 dl[rr * 33 + P.off[g] + j] = d * hp.loss_scale;
             }
             sobj += obj;
-            qobj += (double)obj * obj;
+            qobj += obj * obj;
             mnobj = fminf(mnobj, obj);
             mxobj = fmaxf(mxobj, obj);
             sent += ent;
-            qent += (double)ent * ent;
+            qent += ent * ent;
             mnent = fminf(mnent, ent);
             mxent = fmaxf(mxent, ent);
-            sentw += (double)hp.ecoef[g] * ent;
+            sentw += hp.ecoef[g] * ent;
         } else {
             const float V = lgt[rr * 33 + A];
-            const float R = ro.ret[sr];
+            const float R = in.ret[rr];
             float vpred = V, dvp = 1.f;
             if (hp.clip_vl) {  // ppo.py:197-203
-                const float ov = ro.values[sr];
+                const float ov = in.val[rr];
                 const float vlo = ov - hp.clip, vhi = ov + hp.clip;
                 const float yy = fmaxf(V, vlo);
                 vpred = fminf(yy, vhi);
-                dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) * (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
+                dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) *
+                      (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
             }
             const float e = vpred - R;
             float vl, dvl;
@@ -226,7 +254,7 @@ __device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const flo
                 const float quad = fminf(ae, 1.f);
                 vl = 0.5f * quad * quad + (ae - quad);
                 dvl = ae < 1.f ? e : (e > 0.f ? 1.f : -1.f);
-            } else {         // optax.l2_loss
+            } else {  // optax.l2_loss
                 vl = 0.5f * e * e;
                 dvl = e;
             }
@@ -234,102 +262,133 @@ __device__ inline void tile_loss(const PolicyK& P, const RolloutK& ro, const flo
             for (int j = A + 1; j < 33; ++j) dl[rr * 33 + j] = 0.f;
             const float verr = fabsf(V - R);
             svl += vl;
-            qvl += (double)vl * vl;
+            qvl += vl * vl;
             mnvl = fminf(mnvl, vl);
             mxvl = fmaxf(mxvl, vl);
             serr += verr;
-            qerr += (double)verr * verr;
+            qerr += verr * verr;
             mnerr = fminf(mnerr, verr);
             mxerr = fmaxf(mxerr, verr);
         }
     }
-    __syncthreads();
-    // tile loss/metric partials
-    double vals[kLossSlots] = {sobj, qobj, mnobj, mxobj, svl, qvl, mnvl, mxvl,
-                               serr, qerr, mnerr, mxerr, sent, qent, mnent, mxent, sentw, 0, 0, 0};
+    // tile loss/metric partials: DPP over each half-wave, then the half-wave
+    // partials in fixed order (f32 within the tile, f64 across tiles)
+    const float vals[kLossSlots] = {sobj, qobj, mnobj, mxobj, svl, qvl, mnvl, mxvl,
+                                    serr, qerr, mnerr, mxerr, sent, qent, mnent, mxent,
+                                    sentw, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kLossSlots; ++s) {
-        double v = vals[s];
-        const int kind = (s < 16) ? (s & 3) : 0;  // 0,1 sum; 2 min; 3 max
-        for (int o = 1; o < 64; o <<= 1) {
-            double u = __shfl_xor(v, o);
-            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
-        }
-        if (lane == 0) dred[w * kLossSlots + s] = v;
+        const int kind = (s < 16) ? (s & 3) : 0;
+        float v = vals[s];
+        v = kind == 2 ? half_reduce<2>(v) : (kind == 3 ? half_reduce<3>(v) : half_reduce<0>(v));
+        if ((lane & 31) == 0) dred[(w * 2 + (lane >> 5)) * kLossSlots + s] = v;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < kLossSlots) {
         const int kind = (tid < 16) ? (tid & 3) : 0;
         double v = dred[tid];
-        for (int ww = 1; ww < 4; ++ww) {
-            double u = dred[ww * kLossSlots + tid];
+        for (int q = 1; q < 2 * (THREADS / 64); ++q) {
+            double u = dred[q * kLossSlots + tid];
             v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
         }
         ws.loss_part[(int64_t)blockIdx.x * kLossSlots + tid] = v;
     }
 }
 
+template <int H> struct StepCfg {
+    static constexpr int W = H >= 128 ? 4 : 2;  // waves per workgroup
+    static constexpr int CG = W;               // column groups (one row block)
+    static constexpr int NB = H / 32 / W;      // column blocks per wave
+    static constexpr int ROWS = 32;
+    static constexpr int THREADS = 64 * W;
+};
+
+template <typename T, int H, int L> static size_t step_lds(int D, int K) {
+    typedef StepCfg<H> C;
+    const int ld = (D > H ? D : H) + 16 / (int)sizeof(T);
+    size_t b = (size_t)C::ROWS * ld * sizeof(T);      // act
+    b += (size_t)C::W * C::ROWS * 2 * 4;               // red
+    b += 2 * (size_t)C::ROWS * 33 * 4;                 // lgt, dl
+    b += (size_t)L * C::ROWS * 2 * 4;                  // stat
+    b += 2 * (size_t)C::ROWS * K * 4 + 3 * C::ROWS * 4; // loss inputs
+    b += (size_t)2 * C::W * kLossSlots * 4;            // dred
+    b += (size_t)C::ROWS * 8;                           // srow
+    return b;
+}
+
 template <typename T, int H, int L>
-__global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
-                                                       const int32_t* __restrict__ mb_seq, int mb,
-                                                       int64_t M, const float* __restrict__ adv_st,
-                                                       HpK hp, WsK ws) {
-    constexpr int NB = H / 64;
+__global__ __launch_bounds__(StepCfg<H>::THREADS) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
+    PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
+    const float* __restrict__ adv_st, HpK hp, WsK ws) {
+    typedef StepCfg<H> C;
+    constexpr int NB = C::NB, CG = C::CG, ROWS = C::ROWS, THREADS = C::THREADS;
     constexpr int PAD = Pad<T>::v;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int D = P.D;
+    const int D = P.D, K = P.K;
     const int ld = (D > H ? D : H) + PAD;
     const int ldh = MLEARN_HEAD_COLS + PAD;
-    T* act = (T*)smem;
-    float* red = (float*)(smem + (size_t)kTileRows * ld * sizeof(T));  // [4][64][2]
-    float* lgt = red + 4 * 64 * 2;                                      // [64][33]
-    float* dl = lgt + kTileRows * 33;                                   // [64][33]
-    float* stat = dl + kTileRows * 33;                                  // [L][64][2]
-    int64_t* srow = (int64_t*)(stat + L * kTileRows * 2);               // [64]
-    double* dred = (double*)(srow + kTileRows);                         // [4][kLossSlots]
+    T* act = (T*)smem;                                  // [ROWS][ld]
+    float* red = (float*)(act + ROWS * ld);             // [W][ROWS][2]
+    float* lgt = red + C::W * ROWS * 2;                 // [ROWS][33]
+    float* dl = lgt + ROWS * 33;                        // [ROWS][33]
+    float* stat = dl + ROWS * 33;                       // [L][ROWS][2]
+    LossIn in;
+    in.act = (int32_t*)(stat + L * ROWS * 2);           // [ROWS][K]
+    in.lp = (float*)(in.act + ROWS * K);                // [ROWS][K]
+    in.adv = in.lp + ROWS * K;
+    in.ret = in.adv + ROWS;
+    in.val = in.ret + ROWS;
+    float* dred = in.val + ROWS;                        // [2W][kLossSlots]
+    int64_t* srow = (int64_t*)(((uintptr_t)(dred + 2 * C::W * kLossSlots) + 7) & ~(uintptr_t)7);
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int rb = w & 1, r = lane & 31;
-    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
+    const int cg = w, r = lane & 31;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    STAMP(0);
 
-    if (tid < kTileRows) {
-        int64_t f = row0 + tid;
+    if (tid < ROWS) {
+        const int64_t f = row0 + tid;
         int64_t sr = -1;
         if (f < M) {
-            int tl = (int)(f / mb);
-            int m = (int)(f - (int64_t)tl * mb);
-            int64_t seq = mb_seq[m];
-            int64_t c = seq / ro.N, b = seq - c * ro.N;
+            const int tl = (int)(f / mb);
+            const int m = (int)(f - (int64_t)tl * mb);
+            const int64_t seq = mb_seq[m];
+            const int64_t c = seq / ro.N, b = seq - c * ro.N;
             sr = (c * ro.bptt + tl) * ro.N + b;
         }
         srow[tid] = sr;
     }
-    __syncthreads();
+    lds_barrier();
 
-    // gather the observation rows, 16 B per lane
+    // gather the observation rows (16 B per lane) and the loss inputs
     {
         constexpr int V = 16 / sizeof(T);
-        typedef __attribute__((ext_vector_type(4))) uint32_t u32x4v;
+        typedef __attribute__((ext_vector_type(4))) uint32_t u4;
         const T* obs = (const T*)ro.obs;
-        const int cpr = D / V;  // 16-B chunks per row
-        for (int idx = tid; idx < kTileRows * cpr; idx += 256) {
-            int rr = idx / cpr, c = (idx - rr * cpr) * V;
-            int64_t sr = srow[rr];
-            u32x4v v = {0u, 0u, 0u, 0u};
-            if (sr >= 0) v = *(const u32x4v*)(obs + sr * D + c);
-            *(u32x4v*)(act + rr * ld + c) = v;
+        const int cpr = D / V;
+        for (int idx = tid; idx < ROWS * cpr; idx += THREADS) {
+            const int rr = idx / cpr, c = (idx - rr * cpr) * V;
+            const int64_t sr = srow[rr];
+            u4 v = {0u, 0u, 0u, 0u};
+            if (sr >= 0) v = *(const u4*)(obs + sr * D + c);
+            *(u4*)(act + rr * ld + c) = v;
+        }
+        for (int idx = tid; idx < ROWS * K; idx += THREADS) {
+            const int rr = idx / K, g = idx - rr * K;
+            const int64_t sr = srow[rr];
+            in.act[idx] = sr >= 0 ? ro.actions[sr * K + g] : 0;
+            in.lp[idx] = sr >= 0 ? ro.logp[sr * K + g] : 0.f;
+        }
+        for (int rr = tid; rr < ROWS; rr += THREADS) {
+            const int64_t sr = srow[rr];
+            in.adv[rr] = sr >= 0 ? ro.adv[sr] : 0.f;
+            in.ret[rr] = sr >= 0 ? ro.ret[sr] : 0.f;
+            in.val[rr] = (sr >= 0 && ro.values) ? ro.values[sr] : 0.f;
         }
     }
-    __syncthreads();
-    {
-        T* x0T = (T*)ws.x0T;
-        for (int idx = tid; idx < D * (kTileRows / 4); idx += 256) {
-            int c = idx % D, g = idx / D;
-            store4(x0T + (int64_t)c * ws.Mp + row0 + 4 * g, to_f32(act[(4 * g) * ld + c]),
-                   to_f32(act[(4 * g + 1) * ld + c]), to_f32(act[(4 * g + 2) * ld + c]),
-                   to_f32(act[(4 * g + 3) * ld + c]));
-        }
-    }
+    lds_barrier();
+    store_tile_transposed<T, ROWS, THREADS>(act, ld, D, (T*)ws.x0T, ws.Mp, row0, M, tid);
+    STAMP(1);
 
     // ---- forward ----
     ZStore<T, NB> z[L];
@@ -337,10 +396,10 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
     const float invH = 1.0f / (float)H;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-        const int K = l == 0 ? D : H;
+        const int Kl = l == 0 ? D : H;
         zero_acc<NB>(acc);
-        tile_gemm<T, NB>(acc, act, ld, rb, (const T*)P.wt[l], K, K, w, lane);
-        __syncthreads();
+        gemm_direct<T, NB, CG>(acc, act, ld, 0, (const T*)P.wt[l], Kl, H, cg, lane);
+        STAMP(2 + 2 * l);
         float s[16], q[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -356,84 +415,87 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
             s[e] = a;
             q[e] = b;
         }
-        row_reduce2(s, q, red, w, lane);
-        const float* gamma = P.lns[l];
-        const float* beta = P.lnb[l];
+        row_reduce2<1, CG>(s, q, red, w, lane);  // (barrier: every wave is past its GEMM)
+        float g[NB], bt[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            g[i] = P.lns[l][(cg + CG * i) * 32 + r];
+            bt[i] = P.lnb[l][(cg + CG * i) * 32 + r];
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int row = rb * 32 + acc_row(e, lane);
+            const int row = acc_row(e, lane);
             const float mean = s[e] * invH;
             const float var = fmaxf(q[e] * invH - mean * mean, 0.f);
             const float rstd = rsqrtf(var + 1e-6f);
-            if ((w >> 1) == 0 && r == 0) {
-                stat[(l * kTileRows + row) * 2] = mean;
-                stat[(l * kTileRows + row) * 2 + 1] = rstd;
+            if (cg == 0 && r == 0) {
+                stat[(l * ROWS + row) * 2] = mean;
+                stat[(l * ROWS + row) * 2 + 1] = rstd;
             }
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
-                const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float y = (acc[i][e] - mean) * (rstd * gamma[col]) + beta[col];
-                y = fmaxf(rnd<T>(y), 0.f);
+                const int col = (cg + CG * i) * 32 + r;
+                const float y = fmaxf(rnd<T>((acc[i][e] - mean) * (rstd * g[i]) + bt[i]), 0.f);
                 act[row * ld + col] = cvt<T>(y);
-                acc[i][e] = y;
             }
         }
-        store_transposed<T, NB>(acc, (T*)ws.aT[l], ws.Mp, w, lane, row0, M);
-        __syncthreads();
+        lds_barrier();
+        store_tile_transposed<T, ROWS, THREADS>(act, ld, H, (T*)ws.aT[l], ws.Mp, row0, M, tid);
+        STAMP(3 + 2 * l);
     }
-    heads_to_lds<T>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
-    __syncthreads();
+    heads_to_lds<T, 1, CG>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
+    lds_barrier();
+    STAMP(6);
 
     // ---- loss ----
-    tile_loss<T>(P, ro, adv_st, hp, ws, lgt, dl, srow, dred, tid, lane, w);
-    // (tile_loss ends with a barrier: dl is complete)
-    {
-        T* dhT = (T*)ws.dheadT;
-        for (int idx = tid; idx < MLEARN_HEAD_COLS * (kTileRows / 4); idx += 256) {
-            int j = idx % MLEARN_HEAD_COLS, g = idx / MLEARN_HEAD_COLS;
-            store4(dhT + (int64_t)j * ws.Mp + row0 + 4 * g, dl[(4 * g) * 33 + j],
-                   dl[(4 * g + 1) * 33 + j], dl[(4 * g + 2) * 33 + j], dl[(4 * g + 3) * 33 + j]);
-        }
+    tile_loss<T, ROWS, THREADS>(P, adv_st, hp, ws, lgt, dl, in, srow, dred, tid, lane, w);
+    lds_barrier();
+    STAMP(7);
+    for (int idx = tid; idx < MLEARN_HEAD_COLS * (ROWS / 4); idx += THREADS) {
+        const int j = idx % MLEARN_HEAD_COLS, gq = idx / MLEARN_HEAD_COLS;
+        store4((T*)ws.dheadT + (int64_t)j * ws.Mp + row0 + 4 * gq, dl[(4 * gq) * 33 + j],
+               dl[(4 * gq + 1) * 33 + j], dl[(4 * gq + 2) * 33 + j], dl[(4 * gq + 3) * 33 + j]);
     }
     if (tid < MLEARN_HEAD_COLS) {
         float sum = 0.f;
-        for (int rr = 0; rr < kTileRows; ++rr) sum += rnd<T>(dl[rr * 33 + tid]);
-        ws.colpart[(int64_t)blockIdx.x * ws.CP + L * 4 * H + tid] = sum;
+        for (int rr = 0; rr < ROWS; ++rr) sum += rnd<T>(dl[rr * 33 + tid]);
+        ws.colpart[(int64_t)blockIdx.x * ws.CP + L * 2 * H + tid] = sum;
     }
-    for (int idx = tid; idx < kTileRows * MLEARN_HEAD_COLS; idx += 256) {
-        int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
+    for (int idx = tid; idx < ROWS * MLEARN_HEAD_COLS; idx += THREADS) {
+        const int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
         act[rr * ldh + j] = cvt<T>(dl[rr * 33 + j]);
     }
-    __syncthreads();
+    lds_barrier();
+    STAMP(8);
 
     // ---- backward ----
     zero_acc<NB>(acc);
     // dA_{L-1} = dHead . Head^T    (B^T = head [H][32])
-    tile_gemm<T, NB>(acc, act, ldh, rb, (const T*)P.head, MLEARN_HEAD_COLS, MLEARN_HEAD_COLS, w,
-                     lane);
+    gemm_direct<T, NB, CG>(acc, act, ldh, 0, (const T*)P.head, MLEARN_HEAD_COLS, H, cg, lane);
+    STAMP(9);
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
-        __syncthreads();
-        const float* gamma = P.lns[l];
-        const float* beta = P.lnb[l];
-        float su[16], sv[16], pg[NB], pb[NB];
+        float su[16], sv[16], pg[NB], pb[NB], gm[NB], bt[NB];
 #pragma unroll
-        for (int i = 0; i < NB; ++i) pg[i] = pb[i] = 0.f;
+        for (int i = 0; i < NB; ++i) {
+            pg[i] = pb[i] = 0.f;
+            gm[i] = P.lns[l][(cg + CG * i) * 32 + r];
+            bt[i] = P.lnb[l][(cg + CG * i) * 32 + r];
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int row = rb * 32 + acc_row(e, lane);
+            const int row = acc_row(e, lane);
             const bool live = row0 + row < M;
-            const float mean = stat[(l * kTileRows + row) * 2];
-            const float rstd = stat[(l * kTileRows + row) * 2 + 1];
+            const float mean = stat[(l * ROWS + row) * 2];
+            const float rstd = stat[(l * ROWS + row) * 2 + 1];
             float a = 0.f, b = 0.f;
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
-                const int col = ((w >> 1) + 2 * i) * 32 + r;
-                const float zz = z[l].get(i, e);
-                const float xh = (zz - mean) * rstd;
-                const float y = (zz - mean) * (rstd * gamma[col]) + beta[col];
+                const float zc = z[l].get(i, e) - mean;
+                const float xh = zc * rstd;
+                const float y = zc * (rstd * gm[i]) + bt[i];
                 const float dy = (live && rnd<T>(y) > 0.f) ? acc[i][e] : 0.f;  // ReLU'
-                const float u = dy * gamma[col];
+                const float u = dy * gm[i];
                 acc[i][e] = u;
                 a += u;
                 b += u * xh;
@@ -449,36 +511,52 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
             pg[i] += __shfl_xor(pg[i], 32);
             pb[i] += __shfl_xor(pb[i], 32);
             if (lane < 32) {
-                const int col = ((w >> 1) + 2 * i) * 32 + r;
-                float* lp = ws.colpart + (int64_t)blockIdx.x * ws.CP + ((l * 2 + rb) * 2) * H;
+                const int col = (cg + CG * i) * 32 + r;
+                float* lp = ws.colpart + (int64_t)blockIdx.x * ws.CP + (l * 2) * H;
                 lp[col] = pb[i];
                 lp[H + col] = pg[i];
             }
         }
-        row_reduce2(su, sv, red, w, lane);
+        row_reduce2<1, CG>(su, sv, red, w, lane);  // (barrier: every wave is past its GEMM)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int row = rb * 32 + acc_row(e, lane);
-            const float mean = stat[(l * kTileRows + row) * 2];
-            const float rstd = stat[(l * kTileRows + row) * 2 + 1];
+            const int row = acc_row(e, lane);
+            const float mean = stat[(l * ROWS + row) * 2];
+            const float rstd = stat[(l * ROWS + row) * 2 + 1];
             const float mu = su[e] * invH, mv = sv[e] * invH;
 #pragma unroll
             for (int i = 0; i < NB; ++i) {
-                const int col = ((w >> 1) + 2 * i) * 32 + r;
+                const int col = (cg + CG * i) * 32 + r;
                 const float xh = (z[l].get(i, e) - mean) * rstd;
-                const float dz = rnd<T>(rstd * (acc[i][e] - mu - xh * mv));
-                act[row * ld + col] = cvt<T>(dz);
-                acc[i][e] = dz;
+                act[row * ld + col] = cvt<T>(rstd * (acc[i][e] - mu - xh * mv));
             }
         }
-        store_transposed<T, NB>(acc, (T*)ws.dzT[l], ws.Mp, w, lane, row0, M);
+        lds_barrier();
+        store_tile_transposed<T, ROWS, THREADS>(act, ld, H, (T*)ws.dzT[l], ws.Mp, row0, M, tid);
+        STAMP(10 + 2 * (L - 1 - l));
         if (l > 0) {
-            __syncthreads();
             zero_acc<NB>(acc);
             // dA_{l-1} = dZ_l . W_l^T   (B^T = W_l [in][H])
-            tile_gemm<T, NB>(acc, act, ld, rb, (const T*)P.w[l], H, H, w, lane);
+            gemm_direct<T, NB, CG>(acc, act, ld, 0, (const T*)P.w[l], H, H, cg, lane);
+            STAMP(11 + 2 * (L - 1 - l));
         }
     }
+}
+
+template <typename T, int H, int L>
+static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                        int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                        hipStream_t s) {
+    auto k = ppo_step_kernel<T, H, L>;
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        attr_set = true;
+    }
+    const size_t lds = step_lds<T, H, L>(P.D, P.K);
+    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(StepCfg<H>::THREADS), lds, s, P, R, mb_seq, mb, M,
+                       adv_st, hp, ws);
 }
 
 // ---------------------------------------------------------------------------
@@ -623,7 +701,7 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
         return t;
     };
     if (p >= Lk.hb_off) {
-        g = colsum(L * 4 * H + (int)(p - Lk.hb_off));
+        g = colsum(L * 2 * H + (int)(p - Lk.hb_off));
     } else if (p >= Lk.hw_off) {
         int64_t q = p - Lk.hw_off;
         int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
@@ -636,7 +714,7 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
         if (p >= Lk.s_off[l]) {
             const int which = p >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
             const int col = (int)(p - (which ? Lk.s_off[l] : Lk.b_off[l]));
-            g = colsum(((l * 2 + 0) * 2 + which) * H + col) + colsum(((l * 2 + 1) * 2 + which) * H + col);
+            g = colsum((l * 2 + which) * H + col);
         } else {
             const int I = l == 0 ? Lk.D : H;
             const float* s = ws.slab + ws.slab_off[l] + (p - Lk.w_off[l]);
@@ -713,27 +791,6 @@ __global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64
     }
 }
 
-static size_t step_lds(int D, int H, int L, int es) {
-    int ld = (D > H ? D : H) + 16 / es;
-    return (size_t)kTileRows * ld * es + 4 * 64 * 2 * 4 + 2 * kTileRows * 33 * 4 +
-           (size_t)L * kTileRows * 2 * 4 + kTileRows * 8 + 4 * kLossSlots * 8;
-}
-
-template <typename T, int H, int L>
-static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
-                        int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
-                        hipStream_t s) {
-    auto k = ppo_step_kernel<T, H, L>;
-    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr_set = true;
-    }
-    size_t lds = step_lds(P.D, H, L, sizeof(T));
-    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(256), lds, s, P, R, mb_seq, mb, M, adv_st, hp, ws);
-}
-
 template <typename T, int H>
 static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
                             const int32_t* mb_seq, int mb, const float* adv_st,
@@ -742,6 +799,9 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     const int64_t M = (int64_t)mb * ro.bptt_len;
     WsK ws;
     carve(p, M, (char*)wsp, &ws);
+#ifdef ML_STAMPS
+    ws.stamps = g_stamp_buf;
+#endif
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
                ro.T, ro.bptt_len, ro.N};
@@ -787,6 +847,11 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 using namespace ml;
 
 extern "C" {
+
+#ifdef ML_STAMPS
+// diagnostic builds only: phase timestamps of the fused minibatch kernel
+void mlearn_debug_set_stamp_buffer(uint64_t* buf) { g_stamp_buf = buf; }
+#endif
 
 int64_t mlearn_param_count(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;

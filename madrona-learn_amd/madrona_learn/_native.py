@@ -14,7 +14,9 @@ from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so")
+LIB_PATH = os.environ.get(
+    "MADRONA_LEARN_LIB",
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
 ABI_VERSION = 1
 
 DTYPE_F32 = 0

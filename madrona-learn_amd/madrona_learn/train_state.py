@@ -118,14 +118,14 @@ class PolicyState:
 
         self.params = torch.from_numpy(host).to(self.device)
         self.init_norms = torch.tensor(init_norms, dtype=torch.float32, device=self.device)
-        # compute-dtype images read by the kernels
+        # compute-dtype fragment-order images read by the kernels (frag.py)
         self.w_t, self.w = [], []
         for l in range(L):
             fin = D if l == 0 else H
-            self.w_t.append(torch.zeros((H, fin), dtype=dt, device=self.device))
-            self.w.append(torch.zeros((fin, H), dtype=dt, device=self.device))
-        self.head_t = torch.zeros((nat.HEAD_COLS, H), dtype=dt, device=self.device)
-        self.head = torch.zeros((H, nat.HEAD_COLS), dtype=dt, device=self.device)
+            self.w_t.append(torch.zeros(H * fin, dtype=dt, device=self.device))
+            self.w.append(torch.zeros(fin * H if l > 0 else 0, dtype=dt, device=self.device))
+        self.head_t = torch.zeros(nat.HEAD_COLS * H, dtype=dt, device=self.device)
+        self.head = torch.zeros(H * nat.HEAD_COLS, dtype=dt, device=self.device)
         self.head_b = torch.zeros((nat.HEAD_COLS,), dtype=torch.float32, device=self.device)
 
         d = nat.MlpPolicy()
@@ -136,7 +136,7 @@ class PolicyState:
         d.actions = nat.action_layout(arch.buckets)
         for l in range(L):
             d.w_t[l] = self.w_t[l].data_ptr()
-            d.w[l] = self.w[l].data_ptr()
+            d.w[l] = self.w[l].data_ptr() if l > 0 else None
             d.ln_scale[l] = self.params.data_ptr() + 4 * self.layout["s"][l][0]
             d.ln_bias[l] = self.params.data_ptr() + 4 * self.layout["b"][l][0]
         d.head_t = self.head_t.data_ptr()
