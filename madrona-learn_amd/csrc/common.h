@@ -171,18 +171,6 @@ template <> struct MT<float> {
     }
 };
 
-// B-operand images ("fragment order").  A logical matrix Bt[N][K] (N output
-// columns, K reduction) is stored so that the 64 lane fragments of one MFMA
-// step are contiguous: element (n, k) lives at
-//   ((n/32 * K/KS + k/KS) * 64 + (n%32) + 32*((k%KS)/E)) * E + k%E,
-// so a wave's B load is one contiguous 64*E*sizeof(T) run (1 KiB for bf16).
-template <typename T>
-__host__ __device__ inline int64_t frag_index(int n, int k, int K) {
-    constexpr int E = MT<T>::E, KS = MT<T>::KS;
-    const int kk = k % KS;
-    return ((int64_t)((n >> 5) * (K / KS) + k / KS) * 64 + (n & 31) + 32 * (kk / E)) * E + kk % E;
-}
-
 __device__ inline int acc_row(int i, int lane) { return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5); }
 
 __device__ inline float wave_sum32(float v) {

@@ -9,7 +9,7 @@
 // reductions go through fixed-order double partials (deterministic).
 
 #include "common.h"
-#include "mlp_tile.h"
+#include "rowtile.h"
 
 namespace ml {
 
@@ -129,8 +129,8 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
     } else if (p >= Lk.hw_off) {
         int64_t q = p - Lk.hw_off;
         int c = (int)(q / Lk.A1), k = (int)(q % Lk.A1);
-        ((T*)C.head_t)[frag_index<T>(k, c, H)] = cvt<T>(val);
-        ((T*)C.head)[frag_index<T>(c, k, MLEARN_HEAD_COLS)] = cvt<T>(val);
+        ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(val);
+        ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(val);
     } else {
         int l = Lk.L - 1;
         while (l > 0 && p < Lk.w_off[l]) --l;
@@ -138,8 +138,8 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
             const int in = l == 0 ? Lk.D : H;
             int64_t q = p - Lk.w_off[l];
             int i = (int)(q / H), j = (int)(q % H);
-            ((T*)C.wt[l])[frag_index<T>(j, i, in)] = cvt<T>(val);
-            if (l > 0) ((T*)C.w[l])[frag_index<T>(i, j, H)] = cvt<T>(val);
+            ((T*)C.wt[l])[img_index<T>(j, i, in, l > 0)] = cvt<T>(val);
+            if (l > 0) ((T*)C.w[l])[img_index<T>(i, j, H, true)] = cvt<T>(val);
         }
         // LayerNorm scale/bias are read in f32 straight from the master params.
     }
@@ -176,8 +176,8 @@ __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const 
     const int64_t pad = (int64_t)(MLEARN_HEAD_COLS - Lk.A1) * H;
     if (p < pad) {
         int k = Lk.A1 + (int)(p / H), c = (int)(p % H);
-        ((T*)C.head_t)[frag_index<T>(k, c, H)] = cvt<T>(0.f);
-        ((T*)C.head)[frag_index<T>(c, k, MLEARN_HEAD_COLS)] = cvt<T>(0.f);
+        ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(0.f);
+        ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(0.f);
         if (c == 0) C.head_b[k] = 0.f;
     }
     if (p < Lk.total) write_copies<T>(Lk, C, p, params[p]);

@@ -11,7 +11,7 @@
 
 #include "common.h"
 #include "dists.h"
-#include "mlp_tile.h"
+#include "rowtile.h"
 
 namespace ml {
 
@@ -58,83 +58,132 @@ int validate_policy(const mlearn_mlp_policy* p) {
     return MLEARN_OK;
 }
 
-// One workgroup = 32 rows x H/32 waves; wave w computes output column block w
-// of every layer (NB = 1), so a 8192-env step runs 256 workgroups x 8 waves.
+// One wave = 32 environments (one per lane pair), all H features: the trunk,
+// heads and sampling of its rows run without any workgroup barrier.  The
+// workgroup's waves share the LayerNorm parameters staged once in LDS.
+constexpr int kPolicyWaves = 1;  // waves per workgroup (grid = one wave per 32 envs)
+
 template <typename T, int H>
-__global__ __launch_bounds__(2 * H) void policy_step_kernel(PolicyK P, const float* __restrict__ obs,
-                                                            int64_t N, T* obs_store,
-                                                            int32_t* actions, float* logp,
-                                                            float* values, uint32_t k0,
-                                                            uint32_t k1, const uint64_t* step_ctr,
-                                                            uint64_t step_add, uint32_t eoff,
-                                                            int sample) {
-    constexpr int W = H / 32, CG = W, ROWS = 32, THREADS = 64 * W;
+__global__ __launch_bounds__(64 * kPolicyWaves) void policy_step_kernel(
+    PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
+    float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
+    uint64_t step_add, uint32_t eoff, int sample) {
+    typedef typename RT<T>::frag frag;
+    constexpr int NB = H / 32, KS = RT<T>::KS, SPB = RT<T>::SPB, KSH = H / KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int D = P.D;
-    const int ld = (D > H ? D : H) + Pad<T>::v;
-    T* act = (T*)smem;
-    float* red = (float*)(act + ROWS * ld);  // [W][32][2]
-    float* lgt = red + W * ROWS * 2;         // [32][33]
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int D = P.D, L = P.L;
+    float* gb = (float*)smem;            // [L][2][H]
+    float* hbias = gb + L * 2 * H;       // [32]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += blockDim.x) {
+        float v;
+        if (i < L * 2 * H) {
+            const int l = i / (2 * H), c = i - l * 2 * H;
+            v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
+        } else {
+            v = P.head_b[i - L * 2 * H];
+        }
+        gb[i] = v;
+    }
+    __syncthreads();
+    float* lg = hbias + MLEARN_HEAD_COLS + w * (32 * 33);  // [32][33] per wave
+    const int64_t row0 = ((int64_t)blockIdx.x * kPolicyWaves + w) * 32;
+    if (row0 >= N) return;
+    const int64_t row = row0 + r;
+    const bool live = row < N;
     const uint64_t step = (step_ctr ? *step_ctr : 0ull) + step_add;
+    const float invH = 1.0f / (float)H;
 
-    // 1. preprocess (cast) + store the observation tile, 16 B loads
+    // layer 0: observation fragments straight from the env output (cast to
+    // the compute dtype = ObservationsCaster), copied to the rollout store
+    f32x16 acc[NB];
+    zero_acc<NB>(acc);
     {
-        const int cpr = D / 4;
-        for (int idx = tid; idx < ROWS * cpr; idx += THREADS) {
-            int rr = idx / cpr, c = (idx - rr * cpr) * 4;
-            int64_t n = row0 + rr;
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n < N) x = *(const float4*)(obs + n * D + c);
-            store4(act + rr * ld + c, x.x, x.y, x.z, x.w);
-            if (obs_store && n < N) store4(obs_store + n * D + c, x.x, x.y, x.z, x.w);
+        const float* orow = obs + (live ? row : 0) * D;
+        T* srow = obs_store ? obs_store + (live ? row : 0) * D : nullptr;
+        const int nks = D / KS;
+        const T* img = (const T*)P.wt[0] + lane * RT<T>::E;
+        for (int s = 0; s < nks; ++s) {
+            const frag b = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
+            if (srow && live) RT<T>::put_row(srow, s, h, b);
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+                acc[nb] = MT<T>::mma(MT<T>::load(img + (nb * nks + s) * 64 * RT<T>::E), b, acc[nb]);
         }
     }
-    lds_barrier();
-
-    // 2. trunk
-    for (int l = 0; l < P.L; ++l) {
-        const int K = l == 0 ? D : H;
-        f32x16 acc[1];
-        zero_acc<1>(acc);
-        gemm_direct<T, 1, CG>(acc, act, ld, 0, (const T*)P.wt[l], K, H, w, lane);
-        ln_relu_epilogue<T, 1, 1, CG>(acc, P.lns[l], P.lnb[l], act, ld, red, w, lane, H, nullptr,
-                                      nullptr);
-        lds_barrier();
+    frag bf[KSH];
+    for (int l = 0;; ++l) {
+        // LayerNorm + ReLU (models.py:46-56), statistics per row = per lane
+        float sum = 0.f, sq = 0.f;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float x = rnd<T>(acc[nb][q]);
+                acc[nb][q] = x;
+                sum += x;
+                sq += x * x;
+            }
+        sum = sum_halves(sum);
+        sq = sum_halves(sq);
+        const float mean = sum * invH;
+        const float var = fmaxf(sq * invH - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + 1e-6f);
+        const float* gm = gb + l * 2 * H;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int f0 = nb * 32 + 8 * g + 4 * h;
+                const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
+                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = 4 * g + j;
+                    acc[nb][q] = fmaxf(rnd<T>((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j]), 0.f);
+                }
+            }
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
+        if (l + 1 == L) break;
+        zero_acc<NB>(acc);
+        gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.wt[l + 1], lane);
     }
 
-    // 3. actor + critic heads
-    heads_to_lds<T, 1, CG>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
-    lds_barrier();
-
-    // 4. sample + store
-    if (actions) {
-        for (int task = tid; task < ROWS * P.K; task += THREADS) {
-            int rr = task / P.K, g = task - rr * P.K;
-            int64_t n = row0 + rr;
-            if (n >= N) continue;
-            int a;
-            float lp;
-            sample_group(&lgt[rr * 33 + P.off[g]], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
-                         eoff + (uint32_t)n, step, sample, &a, &lp);
-            actions[n * P.K + g] = a;
-            if (logp) logp[n * P.K + g] = lp;
+    // actor + critic heads: lg[row][j] = rnd(rnd(a . W) + rnd(b)) (dists.py:22)
+    {
+        f32x16 ha[1];
+        zero_acc<1>(ha);
+        gemm_rb<T, 1, KSH>(ha, bf, (const T*)P.head_t, lane);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int j = feat(0, q, h);
+            lg[r * 33 + j] = rnd<T>(rnd<T>(ha[0][q]) + rnd<T>(hbias[j]));
         }
     }
-    if (values) {
-        for (int rr = tid; rr < ROWS; rr += THREADS) {
-            int64_t n = row0 + rr;
-            if (n < N) values[n] = lgt[rr * 33 + P.A];
+    wave_lds_sync();
+
+    // sample: lane half h takes the action groups g = h, h + 2, ...
+    if (live) {
+        const float* lr = lg + r * 33;
+        if (actions) {
+            for (int g = h; g < P.K; g += 2) {
+                int a;
+                float lp;
+                sample_group(lr + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
+                             eoff + (uint32_t)row, step, sample, &a, &lp);
+                actions[row * P.K + g] = a;
+                if (logp) logp[row * P.K + g] = lp;
+            }
         }
+        if (values && h == 0) values[row] = lr[P.A];
     }
 }
 
-size_t policy_step_lds(int D, int H, int esize) {
-    int ld = (D > H ? D : H) + 16 / esize;
-    return (size_t)32 * ld * esize + (size_t)(H / 32) * 32 * 2 * sizeof(float) +
-           32 * 33 * sizeof(float);
+static size_t policy_step_lds(int L, int H) {
+    return (size_t)(L * 2 * H + MLEARN_HEAD_COLS) * 4 + (size_t)kPolicyWaves * 32 * 33 * 4;
 }
 
 template <typename T, int H>
@@ -142,17 +191,12 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
                               hipStream_t s) {
-    size_t lds = policy_step_lds(P.D, H, sizeof(T));
-    auto kern = policy_step_kernel<T, H>;
-    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  128 * 1024);
-        attr_set = true;
-    }
-    int grid = (int)((N + 31) / 32);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(2 * H), lds, s, P, obs, N, (T*)obs_store, actions,
-                       logp, values, k0, k1, step_ctr, step, eoff, sample);
+    const size_t lds = policy_step_lds(P.L, H);
+    const int64_t tiles = (N + 31) / 32;
+    const int grid = (int)((tiles + kPolicyWaves - 1) / kPolicyWaves);
+    hipLaunchKernelGGL((policy_step_kernel<T, H>), dim3(grid), dim3(64 * kPolicyWaves), lds, s, P,
+                       obs, N, (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff,
+                       sample);
     return check_launch("policy_rollout_step");
 }
 

@@ -1,14 +1,17 @@
 // PPO minibatch step up to the flat gradient (ppo.py:109-364):
 //
-//   ppo_fwd   per 64-row tile: gather the minibatch rows straight from the
-//             [T][N] rollout store (no RolloutData.minibatch copy,
-//             rollouts.py:319-329), MLP trunk + heads, PPO loss terms
-//             (ppo.py:129-262) and d loss / d {logits, value}.
-//   ppo_bwd   per 64-row tile: back through heads, ReLU and LayerNorm of
-//             every layer (row-local), writing dZ_l and LayerNorm
-//             scale/bias partials.
-//   wgrad     dW = X^T dZ over all rows (split-K slabs, MFMA with the
-//             rows as the reduction axis staged transposed through LDS).
+//   ppo_step  one wave per 32 minibatch rows (row-on-lane orientation,
+//             rowtile.h): gather the rows straight from the [T][N] rollout
+//             store (no RolloutData.minibatch copy, rollouts.py:319-329), MLP
+//             trunk + heads, PPO loss terms (ppo.py:129-262), d loss /
+//             d {logits, value}, and back through heads, ReLU and LayerNorm
+//             of every layer.  Dense outputs are kept in lane-private LDS,
+//             everything else in registers; the wave writes the weight-
+//             gradient operands X_l and dZ_l row-major plus LayerNorm
+//             scale/bias and head-bias partials.
+//   wgrad     dW_l = X_l^T dZ_l over all rows, every weight in one launch
+//             (split-K slabs; MFMA operands transposed on the LDS read with
+//             ds_read_b64_tr_b16).
 //   reduce    fixed-order sum of slabs and tile partials into the flat f32
 //             gradient + loss/metric outputs.  Deterministic: no atomics.
 //
@@ -17,7 +20,7 @@
 //   store row = (c * bptt + tl) * N + b.
 
 #include "common.h"
-#include "mlp_tile.h"
+#include "rowtile.h"
 
 namespace ml {
 
@@ -41,19 +44,16 @@ struct HpK {
 };
 
 constexpr int kLossSlots = 20;   // per tile doubles
-constexpr int kStepRows = 32;    // rows per fused-step tile
-#ifndef ML_STEP_WAVES
-#define ML_STEP_WAVES 2
-#endif
 constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
-constexpr int kWgChunk = 64;     // weight-gradient K chunk (rows of the minibatch)
+constexpr int kWgChunk = 32;     // weight-gradient K chunk (rows of the minibatch)
+constexpr int kRowAlign = 64;    // Mp granularity
 
 struct WsK {
-    void* x0T;                          // [D][Mp]   gathered obs, transposed
-    void* aT[MLEARN_MAX_LAYERS];        // [H][Mp]   post-ReLU activations, transposed
-    void* dheadT;                       // [32][Mp]  d loss / d head outputs, transposed
-    void* dzT[MLEARN_MAX_LAYERS];       // [H][Mp]   d loss / d Dense outputs, transposed
+    void* x0;                           // [Mp][D]  gathered obs (compute dtype)
+    void* a[MLEARN_MAX_LAYERS];         // [Mp][H]  post-ReLU activations
+    void* dhead;                        // [Mp][32] d loss / d head outputs
+    void* dz[MLEARN_MAX_LAYERS];        // [Mp][H]  d loss / d Dense outputs
     float* colpart;                     // [tiles][CP] per-tile column partials
     float* colpart2;                    // [kColChunks][CP]
     double* loss_part;                  // [tiles][kLossSlots]
@@ -62,25 +62,9 @@ struct WsK {
     int splits[MLEARN_MAX_LAYERS + 1];
     int64_t rps[MLEARN_MAX_LAYERS + 1];  // rows per split
     int64_t Mp;
-    int ntiles;
+    int ntiles;                         // Mp / 32
     int CP;                             // L*2*H + 32
-    uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
-
-#ifdef ML_STAMPS
-static uint64_t* g_stamp_buf = nullptr;
-#define STAMP(i)                                                                   \
-    do {                                                                           \
-        __builtin_amdgcn_sched_barrier(0);                                         \
-        if (ws.stamps && threadIdx.x == 0)                                         \
-            ws.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
-        __builtin_amdgcn_sched_barrier(0);                                         \
-    } while (0)
-#else
-#define STAMP(i) \
-    do {         \
-    } while (0)
-#endif
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -100,8 +84,8 @@ static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
 static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
-    const int64_t tiles = (M + kStepRows - 1) / kStepRows;
-    const int64_t Mp = ((tiles * kStepRows + kWgChunk - 1) / kWgChunk) * kWgChunk;
+    const int64_t Mp = (M + kRowAlign - 1) / kRowAlign * kRowAlign;
+    const int64_t tiles = Mp / 32;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char* ptr = base ? base + off : nullptr;
@@ -112,12 +96,12 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     w.Mp = Mp;
     w.ntiles = (int)tiles;
     w.CP = L * 2 * H + MLEARN_HEAD_COLS;
-    w.x0T = take(Mp * D * es);
+    w.x0 = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
-        w.aT[l] = take(Mp * H * es);
-        w.dzT[l] = take(Mp * H * es);
+        w.a[l] = take(Mp * H * es);
+        w.dz[l] = take(Mp * H * es);
     }
-    w.dheadT = take(Mp * MLEARN_HEAD_COLS * es);
+    w.dhead = take(Mp * MLEARN_HEAD_COLS * es);
     w.colpart = (float*)take(tiles * w.CP * sizeof(float));
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
@@ -135,410 +119,384 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused minibatch step per 64-row tile: gather -> trunk forward -> heads ->
-// PPO loss terms and d loss / d head -> backward through heads, ReLU and
-// LayerNorm of every layer.  Each layer's Dense output stays in registers
-// (packed bf16 pairs in bf16 mode) between the forward and the backward, so
-// the only HBM writes are the weight-gradient operands (x0^T, a_l^T, dHead^T,
-// dZ_l^T, feature-major) and the per-tile column / loss partials.
+// PPO loss terms of one (row, action group) / (row, value) task
+// (ppo.py:129-262), writing d loss / d logits (or d value) in place of the
+// logits.
 // ---------------------------------------------------------------------------
-template <typename T, int NB> struct ZStore;
-template <int NB> struct ZStore<bf16, NB> {
-    uint32_t d[NB][8];
-    __device__ void set(int i, int e, float x) {  // x is already bf16-valued
-        const uint32_t b = __builtin_bit_cast(uint32_t, x) >> 16;
-        d[i][e >> 1] = (e & 1) ? ((d[i][e >> 1] & 0x0000ffffu) | (b << 16))
-                               : ((d[i][e >> 1] & 0xffff0000u) | b);
-    }
-    __device__ float get(int i, int e) const {
-        const uint32_t b = (e & 1) ? (d[i][e >> 1] & 0xffff0000u) : (d[i][e >> 1] << 16);
-        return __builtin_bit_cast(float, b);
-    }
-};
-template <int NB> struct ZStore<float, NB> {
-    float d[NB][16];
-    __device__ void set(int i, int e, float x) { d[i][e] = x; }
-    __device__ float get(int i, int e) const { return d[i][e]; }
-};
-
-// Per-row loss inputs gathered from the store at the start of the tile.
-struct LossIn {
-    int32_t* act;  // [ROWS][K]
-    float* lp;     // [ROWS][K]
-    float* adv;    // [ROWS]
-    float* ret;    // [ROWS]
-    float* val;    // [ROWS]
-};
-
-// PPO loss terms of the tile (ppo.py:129-262) and d loss / d {logits, value}
-// into dl[ROWS][33]; per-tile loss/metric partials into ws.loss_part.
-template <typename T, int ROWS, int THREADS>
-__device__ inline void tile_loss(const PolicyK& P, const float* adv_st, const HpK& hp,
-                                 const WsK& ws, const float* lgt, float* dl, const LossIn& in,
-                                 const int64_t* srow, float* dred, int tid, int lane, int w) {
-    const float adv_mean = adv_st[0], adv_rstd = adv_st[1];
+struct LossAcc {
     float sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
     float mnobj = 3.4e38f, mxobj = -3.4e38f, mnent = 3.4e38f, mxent = -3.4e38f;
     float mnvl = 3.4e38f, mxvl = -3.4e38f, mnerr = 3.4e38f, mxerr = -3.4e38f;
-    const int K = P.K, A = P.A;
-    for (int task = tid; task < ROWS * (K + 1); task += THREADS) {
-        const int rr = task / (K + 1), g = task - rr * (K + 1);
-        if (srow[rr] < 0) {
-            if (g == K)
-                for (int j = 0; j < 33; ++j) dl[rr * 33 + j] = 0.f;
-            continue;
-        }
-        if (g < K) {
-            const float* lg = &lgt[rr * 33 + P.off[g]];
-            const int nb = P.off[g + 1] - P.off[g];
-            float mx = lg[0];
-            for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
-            float ex[32];
-            float se = 0.f;
-            for (int j = 0; j < nb; ++j) {
-                ex[j] = __expf(lg[j] - mx);
-                se += ex[j];
-            }
-            const float inv = 1.0f / se;
-            const float lse = mx + __logf(se);
-            float ent = 0.f;
-            for (int j = 0; j < nb; ++j) ent -= (ex[j] * inv) * (lg[j] - lse);  // dists.py:68-69
-            const int a = in.act[rr * K + g];
-            const float lpa = lg[a] - lse;
-            float adv = in.adv[rr];
-            if (hp.norm_adv) adv = (adv - adv_mean) * adv_rstd;
-            const float ratio = __expf(lpa - in.lp[rr * K + g]);
-            const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
-            const float s1 = adv * ratio;
-            const float y = fmaxf(ratio, lo);
-            const float cr = fminf(y, hi);
-            const float s2 = adv * cr;
-            const float obj = fminf(s1, s2);
-            // JAX's balanced min/max derivatives (0.5 on ties)
-            const float dmx = ratio > lo ? 1.f : (ratio == lo ? 0.5f : 0.f);
-            const float dmn = y < hi ? 1.f : (y == hi ? 0.5f : 0.f);
-            const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
-            const float dobj = w1 * adv + (1.f - w1) * adv * (dmx * dmn);
-            const float g_lp = -hp.inv_sk * dobj * ratio;  // d loss / d logp[a]
-            const float ce = hp.ecoef[g] * hp.inv_sk;       // entropy term weight
-            for (int j = 0; j < nb; ++j) {
-                const float p = ex[j] * inv;
-                const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lg[j] - lse) + ent);
-                dl[rr * 33 + P.off[g] + j] = d * hp.loss_scale;
-            }
-            sobj += obj;
-            qobj += obj * obj;
-            mnobj = fminf(mnobj, obj);
-            mxobj = fmaxf(mxobj, obj);
-            sent += ent;
-            qent += ent * ent;
-            mnent = fminf(mnent, ent);
-            mxent = fmaxf(mxent, ent);
-            sentw += hp.ecoef[g] * ent;
-        } else {
-            const float V = lgt[rr * 33 + A];
-            const float R = in.ret[rr];
-            float vpred = V, dvp = 1.f;
-            if (hp.clip_vl) {  // ppo.py:197-203
-                const float ov = in.val[rr];
-                const float vlo = ov - hp.clip, vhi = ov + hp.clip;
-                const float yy = fmaxf(V, vlo);
-                vpred = fminf(yy, vhi);
-                dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) *
-                      (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
-            }
-            const float e = vpred - R;
-            float vl, dvl;
-            if (hp.huber) {  // optax.huber_loss, delta = 1
-                const float ae = fabsf(e);
-                const float quad = fminf(ae, 1.f);
-                vl = 0.5f * quad * quad + (ae - quad);
-                dvl = ae < 1.f ? e : (e > 0.f ? 1.f : -1.f);
-            } else {  // optax.l2_loss
-                vl = 0.5f * e * e;
-                dvl = e;
-            }
-            dl[rr * 33 + A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
-            for (int j = A + 1; j < 33; ++j) dl[rr * 33 + j] = 0.f;
-            const float verr = fabsf(V - R);
-            svl += vl;
-            qvl += vl * vl;
-            mnvl = fminf(mnvl, vl);
-            mxvl = fmaxf(mxvl, vl);
-            serr += verr;
-            qerr += verr * verr;
-            mnerr = fminf(mnerr, verr);
-            mxerr = fmaxf(mxerr, verr);
-        }
+};
+
+__device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float old_lp, float adv,
+                                  float ecoef, LossAcc& m) {
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float ex[32];
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) {
+        ex[j] = __expf(lg[j] - mx);
+        se += ex[j];
     }
-    // tile loss/metric partials: DPP over each half-wave, then the half-wave
-    // partials in fixed order (f32 within the tile, f64 across tiles)
-    const float vals[kLossSlots] = {sobj, qobj, mnobj, mxobj, svl, qvl, mnvl, mxvl,
-                                    serr, qerr, mnerr, mxerr, sent, qent, mnent, mxent,
-                                    sentw, 0.f, 0.f, 0.f};
+    const float inv = 1.0f / se;
+    const float lse = mx + __logf(se);
+    float ent = 0.f;
+    for (int j = 0; j < nb; ++j) ent -= (ex[j] * inv) * (lg[j] - lse);  // dists.py:68-69
+    const float lpa = lg[a] - lse;
+    const float ratio = __expf(lpa - old_lp);
+    const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
+    const float s1 = adv * ratio;
+    const float y = fmaxf(ratio, lo);
+    const float cr = fminf(y, hi);
+    const float s2 = adv * cr;
+    const float obj = fminf(s1, s2);
+    // JAX's balanced min/max derivatives (0.5 on ties)
+    const float dmx = ratio > lo ? 1.f : (ratio == lo ? 0.5f : 0.f);
+    const float dmn = y < hi ? 1.f : (y == hi ? 0.5f : 0.f);
+    const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    const float dobj = w1 * adv + (1.f - w1) * adv * (dmx * dmn);
+    const float g_lp = -hp.inv_sk * dobj * ratio;  // d loss / d logp[a]
+    const float ce = ecoef * hp.inv_sk;             // entropy term weight
+    for (int j = 0; j < nb; ++j) {
+        const float p = ex[j] * inv;
+        const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lg[j] - lse) + ent);
+        lg[j] = d * hp.loss_scale;
+    }
+    m.sobj += obj;
+    m.qobj += obj * obj;
+    m.mnobj = fminf(m.mnobj, obj);
+    m.mxobj = fmaxf(m.mxobj, obj);
+    m.sent += ent;
+    m.qent += ent * ent;
+    m.mnent = fminf(m.mnent, ent);
+    m.mxent = fmaxf(m.mxent, ent);
+    m.sentw += ecoef * ent;
+}
+
+// lg points at the row; value logit at column A; zeroes columns A+1..31.
+__device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, float ov,
+                                  LossAcc& m) {
+    const float V = lg[A];
+    float vpred = V, dvp = 1.f;
+    if (hp.clip_vl) {  // ppo.py:197-203
+        const float vlo = ov - hp.clip, vhi = ov + hp.clip;
+        const float yy = fmaxf(V, vlo);
+        vpred = fminf(yy, vhi);
+        dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) * (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
+    }
+    const float e = vpred - R;
+    float vl, dvl;
+    if (hp.huber) {  // optax.huber_loss, delta = 1
+        const float ae = fabsf(e);
+        const float quad = fminf(ae, 1.f);
+        vl = 0.5f * quad * quad + (ae - quad);
+        dvl = ae < 1.f ? e : (e > 0.f ? 1.f : -1.f);
+    } else {  // optax.l2_loss
+        vl = 0.5f * e * e;
+        dvl = e;
+    }
+    lg[A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
+    for (int j = A + 1; j < MLEARN_HEAD_COLS; ++j) lg[j] = 0.f;
+    const float verr = fabsf(V - R);
+    m.svl += vl;
+    m.qvl += vl * vl;
+    m.mnvl = fminf(m.mnvl, vl);
+    m.mxvl = fmaxf(m.mxvl, vl);
+    m.serr += verr;
+    m.qerr += verr * verr;
+    m.mnerr = fminf(m.mnerr, verr);
+    m.mxerr = fmaxf(m.mxerr, verr);
+}
+
+// Wave reduction of the lane metrics into the tile's kLossSlots doubles.
+__device__ inline void store_loss_partials(const LossAcc& m, double* out, int lane) {
+    const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
+                                    m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
+                                    m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kLossSlots; ++s) {
         const int kind = (s < 16) ? (s & 3) : 0;
         float v = vals[s];
         v = kind == 2 ? half_reduce<2>(v) : (kind == 3 ? half_reduce<3>(v) : half_reduce<0>(v));
-        if ((lane & 31) == 0) dred[(w * 2 + (lane >> 5)) * kLossSlots + s] = v;
-    }
-    lds_barrier();
-    if (tid < kLossSlots) {
-        const int kind = (tid < 16) ? (tid & 3) : 0;
-        double v = dred[tid];
-        for (int q = 1; q < 2 * (THREADS / 64); ++q) {
-            double u = dred[q * kLossSlots + tid];
-            v = kind == 2 ? fmin(v, u) : (kind == 3 ? fmax(v, u) : v + u);
-        }
-        ws.loss_part[(int64_t)blockIdx.x * kLossSlots + tid] = v;
+        const float u = __shfl_xor(v, 32);
+        v = kind == 2 ? fminf(v, u) : (kind == 3 ? fmaxf(v, u) : v + u);
+        if (lane == 0) out[s] = (double)v;
     }
 }
 
-template <int H> struct StepCfg {
-    static constexpr int W = H >= 128 ? 4 : 2;  // waves per workgroup
-    static constexpr int CG = W;               // column groups (one row block)
-    static constexpr int NB = H / 32 / W;      // column blocks per wave
-    static constexpr int ROWS = 32;
-    static constexpr int THREADS = 64 * W;
+// ---------------------------------------------------------------------------
+// Fused minibatch step: one wave per 32 rows.
+// LDS: shared [L][2][H] LayerNorm scale/bias + [32] head bias; per wave the
+// Dense outputs z_l (lane-private, [L][H/32][CH][64] x 16 B) and the logits /
+// d logits tile lg[32][33] f32.
+// ---------------------------------------------------------------------------
+template <typename T, int H, int L> struct StepLds {
+    static constexpr size_t shared = (size_t)(L * 2 * H + MLEARN_HEAD_COLS) * 4;
+    static constexpr size_t z = (size_t)L * 32 * H * sizeof(T);
+    static constexpr size_t wave = z + 32 * 33 * 4;
+    static int waves() {
+        for (int w = 4; w > 1; w >>= 1)
+            if (shared + w * wave <= 160 * 1024) return w;
+        return 1;
+    }
 };
 
-template <typename T, int H, int L> static size_t step_lds(int D, int K) {
-    typedef StepCfg<H> C;
-    const int ld = (D > H ? D : H) + 16 / (int)sizeof(T);
-    size_t b = (size_t)C::ROWS * ld * sizeof(T);      // act
-    b += (size_t)C::W * C::ROWS * 2 * 4;               // red
-    b += 2 * (size_t)C::ROWS * 33 * 4;                 // lgt, dl
-    b += (size_t)L * C::ROWS * 2 * 4;                  // stat
-    b += 2 * (size_t)C::ROWS * K * 4 + 3 * C::ROWS * 4; // loss inputs
-    b += (size_t)2 * C::W * kLossSlots * 4;            // dred
-    b += (size_t)C::ROWS * 8;                           // srow
-    return b;
-}
-
 template <typename T, int H, int L>
-__global__ __launch_bounds__(StepCfg<H>::THREADS) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
-    PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
-    const float* __restrict__ adv_st, HpK hp, WsK ws) {
-    typedef StepCfg<H> C;
-    constexpr int NB = C::NB, CG = C::CG, ROWS = C::ROWS, THREADS = C::THREADS;
-    constexpr int PAD = Pad<T>::v;
+__global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
+                                                       const int32_t* __restrict__ mb_seq, int mb,
+                                                       int64_t M, const float* __restrict__ adv_st,
+                                                       HpK hp, WsK ws) {
+    typedef typename RT<T>::frag frag;
+    typedef ZIO<T> Z;
+    typedef typename Z::u4 u4;
+    constexpr int NB = H / 32, E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB;
+    constexpr int KSH = H / KS, KSHD = MLEARN_HEAD_COLS / KS, CH = Z::CH;
+    typedef StepLds<T, H, L> LDS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, K = P.K;
-    const int ld = (D > H ? D : H) + PAD;
-    const int ldh = MLEARN_HEAD_COLS + PAD;
-    T* act = (T*)smem;                                  // [ROWS][ld]
-    float* red = (float*)(act + ROWS * ld);             // [W][ROWS][2]
-    float* lgt = red + C::W * ROWS * 2;                 // [ROWS][33]
-    float* dl = lgt + ROWS * 33;                        // [ROWS][33]
-    float* stat = dl + ROWS * 33;                       // [L][ROWS][2]
-    LossIn in;
-    in.act = (int32_t*)(stat + L * ROWS * 2);           // [ROWS][K]
-    in.lp = (float*)(in.act + ROWS * K);                // [ROWS][K]
-    in.adv = in.lp + ROWS * K;
-    in.ret = in.adv + ROWS;
-    in.val = in.ret + ROWS;
-    float* dred = in.val + ROWS;                        // [2W][kLossSlots]
-    int64_t* srow = (int64_t*)(((uintptr_t)(dred + 2 * C::W * kLossSlots) + 7) & ~(uintptr_t)7);
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cg = w, r = lane & 31;
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
-    STAMP(0);
-
-    if (tid < ROWS) {
-        const int64_t f = row0 + tid;
-        int64_t sr = -1;
-        if (f < M) {
-            const int tl = (int)(f / mb);
-            const int m = (int)(f - (int64_t)tl * mb);
-            const int64_t seq = mb_seq[m];
-            const int64_t c = seq / ro.N, b = seq - c * ro.N;
-            sr = (c * ro.bptt + tl) * ro.N + b;
+    float* gb = (float*)smem;         // [L][2][H]
+    float* hbias = gb + L * 2 * H;    // [32]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += blockDim.x) {
+        float v;
+        if (i < L * 2 * H) {
+            const int l = i / (2 * H), c = i - l * 2 * H;
+            v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
+        } else {
+            v = P.head_b[i - L * 2 * H];
         }
-        srow[tid] = sr;
+        gb[i] = v;
     }
-    lds_barrier();
-
-    // gather the observation rows (16 B per lane) and the loss inputs
-    {
-        constexpr int V = 16 / sizeof(T);
-        typedef __attribute__((ext_vector_type(4))) uint32_t u4;
-        const T* obs = (const T*)ro.obs;
-        const int cpr = D / V;
-        for (int idx = tid; idx < ROWS * cpr; idx += THREADS) {
-            const int rr = idx / cpr, c = (idx - rr * cpr) * V;
-            const int64_t sr = srow[rr];
-            u4 v = {0u, 0u, 0u, 0u};
-            if (sr >= 0) v = *(const u4*)(obs + sr * D + c);
-            *(u4*)(act + rr * ld + c) = v;
-        }
-        for (int idx = tid; idx < ROWS * K; idx += THREADS) {
-            const int rr = idx / K, g = idx - rr * K;
-            const int64_t sr = srow[rr];
-            in.act[idx] = sr >= 0 ? ro.actions[sr * K + g] : 0;
-            in.lp[idx] = sr >= 0 ? ro.logp[sr * K + g] : 0.f;
-        }
-        for (int rr = tid; rr < ROWS; rr += THREADS) {
-            const int64_t sr = srow[rr];
-            in.adv[rr] = sr >= 0 ? ro.adv[sr] : 0.f;
-            in.ret[rr] = sr >= 0 ? ro.ret[sr] : 0.f;
-            in.val[rr] = (sr >= 0 && ro.values) ? ro.values[sr] : 0.f;
-        }
+    __syncthreads();
+    char* wb = smem + LDS::shared + (size_t)w * LDS::wave;
+    u4* zb = (u4*)wb;                    // [L][NB][CH][64]
+    float* lg = (float*)(wb + LDS::z);   // [32][33]
+    const int tile = blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= ws.ntiles) return;
+    const int64_t row = (int64_t)tile * 32 + r;
+    const bool live = row < M;
+    int64_t sr = 0;
+    if (live) {
+        const int tl = (int)(row / mb);
+        const int m = (int)(row - (int64_t)tl * mb);
+        const int64_t seq = mb_seq[m];
+        const int64_t c = seq / ro.N, b = seq - c * ro.N;
+        sr = (c * ro.bptt + tl) * ro.N + b;
     }
-    lds_barrier();
-    store_tile_transposed<T, ROWS, THREADS>(act, ld, D, (T*)ws.x0T, ws.Mp, row0, M, tid);
-    STAMP(1);
+    // loss inputs of the first four tasks of this lane (groups h, h+2, ...)
+    int pa[4];
+    float pl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int g = h + 2 * i;
+        const bool ok = live && g < K;
+        pa[i] = ok ? ro.actions[sr * K + g] : 0;
+        pl[i] = ok ? ro.logp[sr * K + g] : 0.f;
+    }
+    float adv = 0.f, ret = 0.f, oval = 0.f;
+    if (live) {
+        adv = ro.adv[sr];
+        ret = ro.ret[sr];
+        if (ro.values) oval = ro.values[sr];
+        if (hp.norm_adv) adv = (adv - adv_st[0]) * adv_st[1];
+    }
 
     // ---- forward ----
-    ZStore<T, NB> z[L];
     f32x16 acc[NB];
+    zero_acc<NB>(acc);
+    {
+        const T* orow = (const T*)ro.obs + sr * D;
+        T* xrow = (T*)ws.x0 + row * D;
+        const int nks = D / KS;
+        const T* img = (const T*)P.wt[0] + lane * E;
+        for (int s = 0; s < nks; ++s) {
+            const frag b = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
+            RT<T>::put_row(xrow, s, h, b);
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+                acc[nb] = MT<T>::mma(MT<T>::load(img + (nb * nks + s) * 64 * E), b, acc[nb]);
+        }
+    }
+    frag bf[KSH];
+    float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-        const int Kl = l == 0 ? D : H;
-        zero_acc<NB>(acc);
-        gemm_direct<T, NB, CG>(acc, act, ld, 0, (const T*)P.wt[l], Kl, H, cg, lane);
-        STAMP(2 + 2 * l);
-        float s[16], q[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            float a = 0.f, b = 0.f;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const float x = rnd<T>(acc[i][e]);  // Dense output in the compute dtype
-                acc[i][e] = x;
-                z[l].set(i, e, x);
-                a += x;
-                b += x * x;
-            }
-            s[e] = a;
-            q[e] = b;
-        }
-        row_reduce2<1, CG>(s, q, red, w, lane);  // (barrier: every wave is past its GEMM)
-        float g[NB], bt[NB];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            g[i] = P.lns[l][(cg + CG * i) * 32 + r];
-            bt[i] = P.lnb[l][(cg + CG * i) * 32 + r];
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int row = acc_row(e, lane);
-            const float mean = s[e] * invH;
-            const float var = fmaxf(q[e] * invH - mean * mean, 0.f);
-            const float rstd = rsqrtf(var + 1e-6f);
-            if (cg == 0 && r == 0) {
-                stat[(l * ROWS + row) * 2] = mean;
-                stat[(l * ROWS + row) * 2 + 1] = rstd;
-            }
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const int col = (cg + CG * i) * 32 + r;
-                const float y = fmaxf(rnd<T>((acc[i][e] - mean) * (rstd * g[i]) + bt[i]), 0.f);
-                act[row * ld + col] = cvt<T>(y);
-            }
-        }
-        lds_barrier();
-        store_tile_transposed<T, ROWS, THREADS>(act, ld, H, (T*)ws.aT[l], ws.Mp, row0, M, tid);
-        STAMP(3 + 2 * l);
-    }
-    heads_to_lds<T, 1, CG>(act, ld, (const T*)P.head_t, P.head_b, H, lgt, w, lane);
-    lds_barrier();
-    STAMP(6);
-
-    // ---- loss ----
-    tile_loss<T, ROWS, THREADS>(P, adv_st, hp, ws, lgt, dl, in, srow, dred, tid, lane, w);
-    lds_barrier();
-    STAMP(7);
-    for (int idx = tid; idx < MLEARN_HEAD_COLS * (ROWS / 4); idx += THREADS) {
-        const int j = idx % MLEARN_HEAD_COLS, gq = idx / MLEARN_HEAD_COLS;
-        store4((T*)ws.dheadT + (int64_t)j * ws.Mp + row0 + 4 * gq, dl[(4 * gq) * 33 + j],
-               dl[(4 * gq + 1) * 33 + j], dl[(4 * gq + 2) * 33 + j], dl[(4 * gq + 3) * 33 + j]);
-    }
-    if (tid < MLEARN_HEAD_COLS) {
-        float sum = 0.f;
-        for (int rr = 0; rr < ROWS; ++rr) sum += rnd<T>(dl[rr * 33 + tid]);
-        ws.colpart[(int64_t)blockIdx.x * ws.CP + L * 2 * H + tid] = sum;
-    }
-    for (int idx = tid; idx < ROWS * MLEARN_HEAD_COLS; idx += THREADS) {
-        const int rr = idx / MLEARN_HEAD_COLS, j = idx - rr * MLEARN_HEAD_COLS;
-        act[rr * ldh + j] = cvt<T>(dl[rr * 33 + j]);
-    }
-    lds_barrier();
-    STAMP(8);
-
-    // ---- backward ----
-    zero_acc<NB>(acc);
-    // dA_{L-1} = dHead . Head^T    (B^T = head [H][32])
-    gemm_direct<T, NB, CG>(acc, act, ldh, 0, (const T*)P.head, MLEARN_HEAD_COLS, H, cg, lane);
-    STAMP(9);
-#pragma unroll
-    for (int l = L - 1; l >= 0; --l) {
-        float su[16], sv[16], pg[NB], pb[NB], gm[NB], bt[NB];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            pg[i] = pb[i] = 0.f;
-            gm[i] = P.lns[l][(cg + CG * i) * 32 + r];
-            bt[i] = P.lnb[l][(cg + CG * i) * 32 + r];
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int row = acc_row(e, lane);
-            const bool live = row0 + row < M;
-            const float mean = stat[(l * ROWS + row) * 2];
-            const float rstd = stat[(l * ROWS + row) * 2 + 1];
-            float a = 0.f, b = 0.f;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const float zc = z[l].get(i, e) - mean;
-                const float xh = zc * rstd;
-                const float y = zc * (rstd * gm[i]) + bt[i];
-                const float dy = (live && rnd<T>(y) > 0.f) ? acc[i][e] : 0.f;  // ReLU'
-                const float u = dy * gm[i];
-                acc[i][e] = u;
-                a += u;
-                b += u * xh;
-                pg[i] += dy * xh;
-                pb[i] += dy;
-            }
-            su[e] = a;
-            sv[e] = b;
-        }
-        // LayerNorm scale/bias partials: fold the two half-waves, one writer per column
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            pg[i] += __shfl_xor(pg[i], 32);
-            pb[i] += __shfl_xor(pb[i], 32);
-            if (lane < 32) {
-                const int col = (cg + CG * i) * 32 + r;
-                float* lp = ws.colpart + (int64_t)blockIdx.x * ws.CP + (l * 2) * H;
-                lp[col] = pb[i];
-                lp[H + col] = pg[i];
-            }
-        }
-        row_reduce2<1, CG>(su, sv, red, w, lane);  // (barrier: every wave is past its GEMM)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int row = acc_row(e, lane);
-            const float mean = stat[(l * ROWS + row) * 2];
-            const float rstd = stat[(l * ROWS + row) * 2 + 1];
-            const float mu = su[e] * invH, mv = sv[e] * invH;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const int col = (cg + CG * i) * 32 + r;
-                const float xh = (z[l].get(i, e) - mean) * rstd;
-                act[row * ld + col] = cvt<T>(rstd * (acc[i][e] - mu - xh * mv));
-            }
-        }
-        lds_barrier();
-        store_tile_transposed<T, ROWS, THREADS>(act, ld, H, (T*)ws.dzT[l], ws.Mp, row0, M, tid);
-        STAMP(10 + 2 * (L - 1 - l));
         if (l > 0) {
             zero_acc<NB>(acc);
-            // dA_{l-1} = dZ_l . W_l^T   (B^T = W_l [in][H])
-            gemm_direct<T, NB, CG>(acc, act, ld, 0, (const T*)P.w[l], H, H, cg, lane);
-            STAMP(11 + 2 * (L - 1 - l));
+            gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.wt[l], lane);
+        }
+        float sum = 0.f, sq = 0.f;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float x = rnd<T>(acc[nb][q]);  // Dense output in the compute dtype
+                acc[nb][q] = x;
+                sum += x;
+                sq += x * x;
+            }
+            Z::put(zb + (l * NB + nb) * CH * 64, lane, acc[nb]);
+        }
+        sum = sum_halves(sum);
+        sq = sum_halves(sq);
+        const float mean = sum * invH;
+        const float var = fmaxf(sq * invH - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + 1e-6f);
+        mean_r[l] = mean;
+        rstd_r[l] = rstd;
+        const float* gm = gb + l * 2 * H;
+        T* arow = (T*)ws.a[l] + row * H;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int f0 = nb * 32 + 8 * g + 4 * h;
+                const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
+                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = 4 * g + j;
+                    acc[nb][q] = fmaxf(rnd<T>((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j]), 0.f);
+                }
+                store4(arow + f0, acc[nb][4 * g], acc[nb][4 * g + 1], acc[nb][4 * g + 2],
+                       acc[nb][4 * g + 3]);
+            }
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
+    }
+    {
+        f32x16 ha[1];
+        zero_acc<1>(ha);
+        gemm_rb<T, 1, KSH>(ha, bf, (const T*)P.head_t, lane);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int j = feat(0, q, h);
+            lg[r * 33 + j] = rnd<T>(rnd<T>(ha[0][q]) + rnd<T>(hbias[j]));
+        }
+    }
+    wave_lds_sync();
+
+    // ---- loss: lane half h takes tasks h, h + 2, ... (task K = value) ----
+    {
+        LossAcc m;
+        float* lr = lg + r * 33;
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int g = h + 2 * i;
+                if (g < K)
+                    loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], pa[i], pl[i], adv,
+                               hp.ecoef[g], m);
+                else if (g == K)
+                    loss_value(hp, lr, P.A, ret, oval, m);
+            }
+            for (int g = h + 8; g <= K; g += 2) {
+                if (g < K)
+                    loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], ro.actions[sr * K + g],
+                               ro.logp[sr * K + g], adv, hp.ecoef[g], m);
+                else
+                    loss_value(hp, lr, P.A, ret, oval, m);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) lr[16 * h + j] = 0.f;
+        }
+        store_loss_partials(m, ws.loss_part + (int64_t)tile * kLossSlots, lane);
+    }
+    wave_lds_sync();
+
+    // d head: row-major store (wgrad operand) and the head-bias column partial
+    {
+        const float* lr = lg + r * 33 + 16 * h;
+        T* drow = (T*)ws.dhead + row * MLEARN_HEAD_COLS + 16 * h;
+#pragma unroll
+        for (int j = 0; j < 16; j += 4) store4(drow + j, lr[j], lr[j + 1], lr[j + 2], lr[j + 3]);
+        float cs = 0.f;
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) cs += rnd<T>(lg[(16 * h + mm) * 33 + r]);
+        cs = sum_halves(cs);
+        if (h == 0) ws.colpart[(int64_t)tile * ws.CP + L * 2 * H + r] = cs;
+    }
+
+    // ---- backward ----
+    {
+        frag db[KSHD];
+#pragma unroll
+        for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * 33, s, h);
+        zero_acc<NB>(acc);
+        // dA_{L-1}^T = Head . dHead^T
+        gemm_rb<T, NB, KSHD>(acc, db, (const T*)P.head, lane);
+    }
+    const int qs = col_sum16_index(lane);
+#pragma unroll
+    for (int l = L - 1; l >= 0; --l) {
+        const float mean = mean_r[l], rstd = rstd_r[l];
+        const float* gm = gb + l * 2 * H;
+        float* cp = ws.colpart + (int64_t)tile * ws.CP + l * 2 * H;
+        float su = 0.f, sv = 0.f;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+            float z[16], pg[16], pb[16];
+            Z::get(zb + (l * NB + nb) * CH * 64, lane, z);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int f0 = nb * 32 + 8 * g + 4 * h;
+                const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
+                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = 4 * g + j;
+                    const float zc = z[q] - mean;
+                    const float xh = zc * rstd;
+                    const float y = zc * (rstd * gg[j]) + bb[j];
+                    const float dy = (live && rnd<T>(y) > 0.f) ? acc[nb][q] : 0.f;  // ReLU'
+                    const float u = dy * gg[j];
+                    acc[nb][q] = u;
+                    su += u;
+                    sv += u * xh;
+                    pg[q] = dy * xh;
+                    pb[q] = dy;
+                }
+            }
+            // LayerNorm scale/bias partials: column sums over the tile's rows
+            const float tg = col_sum16(pg, lane);
+            const float tb = col_sum16(pb, lane);
+            if ((lane & 16) == 0) {
+                const int f = feat(nb, qs, h);
+                cp[f] = tb;
+                cp[H + f] = tg;
+            }
+        }
+        su = sum_halves(su);
+        sv = sum_halves(sv);
+        const float mu = su * invH, mv = sv * invH;
+        T* dzrow = (T*)ws.dz[l] + row * H;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+            float z[16];
+            Z::get(zb + (l * NB + nb) * CH * 64, lane, z);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float xh = (z[q] - mean) * rstd;
+                acc[nb][q] = rnd<T>(rstd * (acc[nb][q] - mu - xh * mv));
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                store4(dzrow + nb * 32 + 8 * g + 4 * h, acc[nb][4 * g], acc[nb][4 * g + 1],
+                       acc[nb][4 * g + 2], acc[nb][4 * g + 3]);
+        }
+        if (l > 0) {
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
+            zero_acc<NB>(acc);
+            // dA_{l-1}^T = W_l . dZ_l^T
+            gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.w[l], lane);
         }
     }
 }
@@ -547,111 +505,169 @@ template <typename T, int H, int L>
 static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                         int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                         hipStream_t s) {
+    typedef StepLds<T, H, L> LDS;
     auto k = ppo_step_kernel<T, H, L>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  128 * 1024);
+                                  160 * 1024);
         attr_set = true;
     }
-    const size_t lds = step_lds<T, H, L>(P.D, P.K);
-    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(StepCfg<H>::THREADS), lds, s, P, R, mb_seq, mb, M,
-                       adv_st, hp, ws);
+    const int wpb = LDS::waves();
+    const size_t lds = LDS::shared + wpb * LDS::wave;
+    hipLaunchKernelGGL(k, dim3((ws.ntiles + wpb - 1) / wpb), dim3(64 * wpb), lds, s, P, R, mb_seq,
+                       mb, M, adv_st, hp, ws);
 }
 
 // ---------------------------------------------------------------------------
-// Weight gradient dW[i][j] = sum_k XT[i][k] * YT[j][k] (NT GEMM, both operands
-// feature-major so every lane streams whole 128-B lines along k).
-// Tile 128 (i) x 128 (j): 4 waves in 2x2, each 64x64 = 2x2 MFMA blocks.
-// Split-K over the minibatch rows; each split writes an f32 slab that the
-// reduce kernel sums in split order.  Within a 64-row K chunk, half-wave h
-// supplies k in [32h, 32h+32): the same permutation for A and B, so the
-// MFMA reduction covers the chunk exactly once.
+// Weight gradients dW[i][j] = sum_m X[m][i] * Y[m][j] for every weight of the
+// policy in one launch (X, Y row-major [Mp][I] / [Mp][J], written by the step
+// kernel).  Workgroup tile 128 (i) x 128 (j): 4 waves in 2x2, each 64x64 =
+// 2x2 MFMA blocks.  K = minibatch rows in chunks of 32, double-buffered
+// through LDS; the MFMA wants both operands k-contiguous, i.e. COLUMNS of the
+// row-major tiles: bf16 fragments come from ds_read_b64_tr_b16 (4 rows x 16
+// columns per 16-lane group, delivered column-major), f32 from plain reads.
+// LDS rows are 160 elements (80 dwords = 16 mod 64): the 32 lanes of a half
+// wave cover all 64 banks on the transposed reads.  Split-K over the rows;
+// each split writes an f32 slab that reduce_grads sums in split order.
 // ---------------------------------------------------------------------------
-template <typename T>
-__device__ inline void load_row32(const T* p, typename MT<T>::frag (&f)[32 / MT<T>::E]);
+struct WgJob {
+    const void* X;
+    const void* Y;
+    float* out;
+    int64_t rps;
+    int I, J, ti, tj, splits, wg0;
+};
+struct WgJobs {
+    WgJob job[MLEARN_MAX_LAYERS + 1];
+    int n;
+    int64_t Mp;
+};
 
-template <>
-__device__ inline void load_row32<bf16>(const bf16* p, bf16x8 (&f)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = *(const bf16x8*)(p + 8 * s);
-}
-template <>
-__device__ inline void load_row32<float>(const float* p, float (&f)[32]) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        float4 v = *(const float4*)(p + 4 * s);
-        f[4 * s] = v.x;
-        f[4 * s + 1] = v.y;
-        f[4 * s + 2] = v.z;
-        f[4 * s + 3] = v.w;
+template <typename T> struct WgCfg {
+    static constexpr int LD = sizeof(T) == 2 ? 160 : 132;  // LDS row (elements)
+    static constexpr size_t buf = (size_t)kWgChunk * LD * sizeof(T);  // one operand, one stage
+    static constexpr size_t lds = 4 * buf;
+};
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+template <typename T> struct WgFrag;
+template <> struct WgFrag<bf16> {
+    typedef bf16x8 frag;
+    // lane (r, h): tile[k = 16 ks + 8 h + e][c0 + r], e = 0..7
+    __device__ static frag load(const bf16* tile, int ks, int c0, int lane) {
+        const int g = lane >> 4, hh = g >> 1, cc = g & 1, q = (lane >> 2) & 3, p = lane & 3;
+        const bf16* base = tile + (16 * ks + 8 * hh + q) * WgCfg<bf16>::LD + c0 + 16 * cc + 4 * p;
+        typedef __attribute__((address_space(3))) short4v* lp;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base + 4 * WgCfg<bf16>::LD));
+        typedef short short8v __attribute__((ext_vector_type(8)));
+        short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(frag, v);
     }
-}
+};
+template <> struct WgFrag<float> {
+    typedef float frag;
+    // lane (r, h): tile[k = 2 ks + h][c0 + r]
+    __device__ static frag load(const float* tile, int ks, int c0, int lane) {
+        return tile[(2 * ks + (lane >> 5)) * WgCfg<float>::LD + c0 + (lane & 31)];
+    }
+};
 
 template <typename T>
-__global__ __launch_bounds__(256) void wgrad_nt_kernel(const T* __restrict__ XT,
-                                                       const T* __restrict__ YT, int64_t ldk,
-                                                       int I, int J, int64_t rps, float* slab) {
-    constexpr int E = MT<T>::E, NS = 32 / E;
-    typedef typename MT<T>::frag frag;
+__global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs) {
+    constexpr int VPC = 16 / sizeof(T);                  // elements per 16-B chunk
+    constexpr int CPR = kWgTile / VPC;                   // chunks per tile row
+    constexpr int PER = kWgChunk * CPR / 256;            // chunks per thread per operand
+    constexpr int LD = WgCfg<T>::LD, KSTEPS = kWgChunk / MT<T>::KS;
+    typedef __attribute__((ext_vector_type(4))) uint32_t u4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* lds = (T*)smem;  // [stage][operand][kWgChunk][LD]
+
+    int jb = 0;
+    while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
+    const WgJob& J = jobs.job[jb];
+    const int local = blockIdx.x - J.wg0;
+    const int nt = J.ti * J.tj;
+    const int split = local / nt, t = local - split * nt;
+    const int i0 = (t % J.ti) * kWgTile, j0 = (t / J.ti) * kWgTile;
+    const int64_t m0 = split * J.rps;
+    const int64_t m1 = m0 + J.rps < jobs.Mp ? m0 + J.rps : jobs.Mp;  // whole chunks
+    const int nchunks = (int)((m1 - m0) / kWgChunk);
+    const T* X = (const T*)J.X;
+    const T* Y = (const T*)J.Y;
+
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int wi = w & 1, wj = w >> 1;
-    const int i0 = blockIdx.x * kWgTile + wi * 64;
-    const int j0 = blockIdx.y * kWgTile + wj * 64;
-    const bool ai[2] = {i0 < I, i0 + 32 < I};
-    const bool bj[2] = {j0 < J, j0 + 32 < J};
-    if (!ai[0] || !bj[0]) return;  // whole wave out of range (no barriers below)
-    const int64_t k0 = blockIdx.z * rps;
-    const int64_t k1 = k0 + rps < ldk ? k0 + rps : ldk;
+    const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
+    const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
+
+    u4 rx[PER], ry[PER];
+    auto gload = [&](int c) {
+        const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = tid + 256 * u;
+            const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
+            const u4 zero = {0u, 0u, 0u, 0u};
+            rx[u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
+            ry[u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
+        }
+    };
+    auto sstore = [&](int stage) {
+        T* xs = lds + (size_t)stage * 2 * kWgChunk * LD;
+        T* ys = xs + kWgChunk * LD;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = tid + 256 * u;
+            const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
+            *(u4*)(xs + rr * LD + cc) = rx[u];
+            *(u4*)(ys + rr * LD + cc) = ry[u];
+        }
+    };
+
     f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) zero_acc<2>(acc[a]);
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) gload(c + 1);
+        const T* xs = lds + (size_t)(c & 1) * 2 * kWgChunk * LD;
+        const T* ys = xs + kWgChunk * LD;
+        if (wi_on && wj_on) {
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ++ks) {
+                typename WgFrag<T>::frag fa[2], fb[2];
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    fa[a] = WgFrag<T>::load(xs, ks, iw + 32 * a, lane);
+                    fb[a] = WgFrag<T>::load(ys, ks, jw + 32 * a, lane);
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a], fb[b], acc[a][b]);
+            }
+        }
+        if (c + 1 < nchunks) sstore((c + 1) & 1);
+        __syncthreads();
+    }
+    if (!wi_on || !wj_on) return;
+    float* out = J.out + (int64_t)split * J.I * J.J;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-    const T* xp[2];
-    const T* yp[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        // rows past I / J (I = obs_dim may be a multiple of 16 only) read a valid
-        // row; their outputs are dropped below
-        const int xi = i0 + 32 * a + r < I ? i0 + 32 * a + r : I - 1;
-        const int yj = j0 + 32 * a + r < J ? j0 + 32 * a + r : J - 1;
-        xp[a] = XT + (int64_t)xi * ldk + 32 * h;
-        yp[a] = YT + (int64_t)yj * ldk + 32 * h;
-    }
-    for (int64_t k = k0; k < k1; k += kWgChunk) {
-        frag fa[2][NS], fb[2][NS];
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            load_row32<T>(xp[a] + k, fa[a]);
-            load_row32<T>(yp[a] + k, fb[a]);
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a][s], fb[b][s], acc[a][b]);
-    }
-    float* out = slab + (int64_t)blockIdx.z * I * J;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        if (!ai[a]) continue;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            if (!bj[b]) continue;
-#pragma unroll
             for (int e = 0; e < 16; ++e) {
-                int i = i0 + 32 * a + acc_row(e, lane);
-                int j = j0 + 32 * b + r;
-                if (i < I && j < J) out[(int64_t)i * J + j] = acc[a][b][e];
+                const int i = i0 + iw + 32 * a + acc_row(e, lane);
+                const int j = j0 + jw + 32 * b + (lane & 31);
+                if (i < J.I && j < J.J) out[(int64_t)i * J.J + j] = acc[a][b][e];
             }
-        }
-    }
 }
+
 
 // First level of the per-tile column partials (LayerNorm scale/bias grads,
 // head-bias grad): colpart2[c][col] = sum over tiles t = c, c + 32, ...
@@ -799,9 +815,6 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     const int64_t M = (int64_t)mb * ro.bptt_len;
     WsK ws;
     carve(p, M, (char*)wsp, &ws);
-#ifdef ML_STAMPS
-    ws.stamps = g_stamp_buf;
-#endif
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
                ro.T, ro.bptt_len, ro.N};
@@ -823,14 +836,33 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
         default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
     const int L = p.num_layers;
+    WgJobs jobs{};
+    jobs.n = L + 1;
+    jobs.Mp = ws.Mp;
+    int wg = 0;
     for (int l = 0; l <= L; ++l) {
-        const int I = l == L ? H : (l == 0 ? p.obs_dim : H);
-        const int J = l == L ? MLEARN_HEAD_COLS : H;
-        const T* X = l == 0 ? (const T*)ws.x0T : (const T*)ws.aT[l - 1];
-        const T* Y = l == L ? (const T*)ws.dheadT : (const T*)ws.dzT[l];
-        dim3 g((I + kWgTile - 1) / kWgTile, (J + kWgTile - 1) / kWgTile, ws.splits[l]);
-        hipLaunchKernelGGL(wgrad_nt_kernel<T>, g, dim3(256), 0, s, X, Y, ws.Mp, I, J, ws.rps[l],
-                           ws.slab + ws.slab_off[l]);
+        WgJob& J = jobs.job[l];
+        J.I = l == L ? H : (l == 0 ? p.obs_dim : H);
+        J.J = l == L ? MLEARN_HEAD_COLS : H;
+        J.X = l == 0 ? ws.x0 : ws.a[l - 1];
+        J.Y = l == L ? ws.dhead : ws.dz[l];
+        J.out = ws.slab + ws.slab_off[l];
+        J.rps = ws.rps[l];
+        J.ti = (J.I + kWgTile - 1) / kWgTile;
+        J.tj = (J.J + kWgTile - 1) / kWgTile;
+        J.splits = ws.splits[l];
+        J.wg0 = wg;
+        wg += J.ti * J.tj * J.splits;
+    }
+    {
+        auto k = wgrad_kernel<T>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)WgCfg<T>::lds);
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(k, dim3(wg), dim3(256), WgCfg<T>::lds, s, jobs);
     }
     hipLaunchKernelGGL(colsum_kernel, dim3((ws.CP + 255) / 256, kColChunks), dim3(256), 0, s, ws);
     LayoutK Lk = make_layout(p);
@@ -847,11 +879,6 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 using namespace ml;
 
 extern "C" {
-
-#ifdef ML_STAMPS
-// diagnostic builds only: phase timestamps of the fused minibatch kernel
-void mlearn_debug_set_stamp_buffer(uint64_t* buf) { g_stamp_buf = buf; }
-#endif
 
 int64_t mlearn_param_count(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;

@@ -1,0 +1,286 @@
+// Row-on-lane building blocks of the fused MLP kernels (rollout step and PPO
+// minibatch step).
+//
+// Orientation.  Every layer is computed transposed, Z^T = W^T . X^T: the
+// weights are the MFMA A operand and the activations the B operand, so the
+// 32x32 accumulator of a wave holds 32 output FEATURES (in its 16 registers,
+// feature (q&3) + 8(q>>2) + 4h of the block for register q of lane half h)
+// for 32 batch ROWS (one per lane, row = lane & 31).  Consequences:
+//   - a wave owns whole rows: LayerNorm statistics are per-lane sums over the
+//     lane's registers plus one exchange with lane ^ 32; no LDS, no barrier;
+//   - the next layer sums over the features, i.e. over the registers, so the
+//     post-activation accumulators ARE the next layer's B fragments (no LDS
+//     round trip); the weights' A-operand images use the matching permuted k
+//     order (img_index perm = true, include/mlearn.h);
+//   - only the weights travel: contiguous 1 KiB fragment runs from L2.
+// A workgroup is a set of independent waves (one tile of 32 rows each) that
+// share the LayerNorm parameters staged once in LDS.
+#pragma once
+#include "common.h"
+
+namespace ml {
+
+// ---------------------------------------------------------------------------
+// A-operand weight images.  Logical Wimg[n][k] (n = output feature of the
+// product, k = reduction index); perm selects the k order of B fragments that
+// come straight from accumulator registers.
+// ---------------------------------------------------------------------------
+template <typename T> struct ImgK;
+template <> struct ImgK<bf16> {
+    __host__ __device__ static inline int64_t index(int n, int k, int K, bool perm) {
+        const int kk = k & 15, s = k >> 4;
+        const int h = perm ? (kk >> 2) & 1 : kk >> 3;
+        const int e = perm ? (((kk >> 3) << 2) | (kk & 3)) : (kk & 7);
+        return ((int64_t)((n >> 5) * (K >> 4) + s) * 64 + (n & 31) + 32 * h) * 8 + e;
+    }
+};
+template <> struct ImgK<float> {
+    __host__ __device__ static inline int64_t index(int n, int k, int K, bool perm) {
+        int s, h;
+        if (perm) {
+            const int kk = k & 31;
+            h = (kk >> 2) & 1;
+            s = ((k >> 5) << 4) | ((kk >> 3) << 2) | (kk & 3);
+        } else {
+            h = k & 1;
+            s = k >> 1;
+        }
+        return (int64_t)((n >> 5) * (K >> 1) + s) * 64 + (n & 31) + 32 * h;
+    }
+};
+template <typename T>
+__host__ __device__ inline int64_t img_index(int n, int k, int K, bool perm) {
+    return ImgK<T>::index(n, k, K, perm);
+}
+
+// ---------------------------------------------------------------------------
+// B fragments.
+// ---------------------------------------------------------------------------
+template <typename T> struct RT;
+template <> struct RT<bf16> {
+    static constexpr int E = 8, KS = 16, SPB = 2;  // SPB: k-steps per 32-feature block
+    typedef bf16x8 frag;
+    __device__ static frag zero() {
+        frag f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (bf16)0.f;
+        return f;
+    }
+    // k-step t of a block held in accumulator layout (permuted k order)
+    __device__ static frag from_acc(const f32x16& a, int t) {
+        frag f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (bf16)a[8 * t + e];
+        return f;
+    }
+    // natural k order: elements k = 16 s + 8 h + e of a row in memory
+    __device__ static frag row(const bf16* p, int s, int h) {
+        return *(const bf16x8*)(p + 16 * s + 8 * h);
+    }
+    __device__ static frag row(const float* p, int s, int h) {
+        const float4 a = *(const float4*)(p + 16 * s + 8 * h);
+        const float4 b = *(const float4*)(p + 16 * s + 8 * h + 4);
+        frag f = {(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w,
+                  (bf16)b.x, (bf16)b.y, (bf16)b.z, (bf16)b.w};
+        return f;
+    }
+    __device__ static void put_row(bf16* p, int s, int h, frag f) {
+        *(bf16x8*)(p + 16 * s + 8 * h) = f;
+    }
+    // natural-order fragment from an f32 LDS row with arbitrary alignment
+    __device__ static frag row_lds(const float* p, int s, int h) {
+        frag f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (bf16)p[16 * s + 8 * h + e];
+        return f;
+    }
+};
+template <> struct RT<float> {
+    static constexpr int E = 1, KS = 2, SPB = 16;
+    typedef float frag;
+    __device__ static frag zero() { return 0.f; }
+    __device__ static frag from_acc(const f32x16& a, int t) { return a[t]; }
+    __device__ static frag row(const float* p, int s, int h) { return p[2 * s + h]; }
+    __device__ static void put_row(float* p, int s, int h, frag f) { p[2 * s + h] = f; }
+    __device__ static frag row_lds(const float* p, int s, int h) { return p[2 * s + h]; }
+};
+
+template <int NB> __device__ inline void zero_acc(f32x16 (&acc)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+}
+
+// Wave-uniform buffer descriptor over a weight image (raw buffer loads: one
+// 32-bit lane offset VGPR for every fragment, block/step offsets in SGPRs).
+__device__ inline __amdgpu_buffer_rsrc_t img_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7FFFFFFF, 0x00020000);
+}
+template <typename T> __device__ inline typename RT<T>::frag img_load(__amdgpu_buffer_rsrc_t rs,
+                                                                        int voff, int soff);
+template <> __device__ inline bf16x8 img_load<bf16>(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+template <> __device__ inline float img_load<float>(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+}
+
+// acc[nb] += sum_s Img[block nb][step s] x b[s]   (NOUT blocks of 32 outputs).
+// The A fragments of step s+1 are in flight while the MFMAs of step s run
+// (two register sets; sched_barrier fences keep the compiler from sinking
+// each load down to its MFMA, which would expose a full L2 round trip per
+// MFMA at one wave per SIMD).
+template <typename T, int NOUT, int NKS>
+__device__ inline void gemm_rb(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&b)[NKS],
+                               const T* __restrict__ img, int lane) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);  // bytes per fragment run
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    frag ra[2][NOUT];
+#pragma unroll
+    for (int nb = 0; nb < NOUT; ++nb) ra[0][nb] = img_load<T>(rs, voff, (nb * NKS) * FB);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        if (s + 1 < NKS) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb)
+                ra[(s + 1) & 1][nb] = img_load<T>(rs, voff, (nb * NKS + s + 1) * FB);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ra[s & 1][nb], b[s], acc[nb]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Feature index of accumulator register q of block nb for lane half h.
+__device__ inline int feat(int nb, int q, int h) { return nb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h; }
+
+// Sum of a per-row value over both lane halves (features 4h-interleaved).
+__device__ inline float sum_halves(float v) { return v + __shfl_xor(v, 32); }
+
+// ---------------------------------------------------------------------------
+// Cross-lane helpers.
+// ---------------------------------------------------------------------------
+#define ML_DPP(v, ctrl) \
+    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, true))
+#define ML_SWZ(v, pat) \
+    __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), pat))
+
+template <int D> __device__ inline float xlane(float v) {
+    if constexpr (D == 1) return ML_DPP(v, 0xB1);       // quad_perm [1,0,3,2]
+    else if constexpr (D == 2) return ML_DPP(v, 0x4E);  // quad_perm [2,3,0,1]
+    else if constexpr (D == 8) return ML_DPP(v, 0x128); // row_ror:8 (= xor 8 in a row)
+    else if constexpr (D == 4) return ML_SWZ(v, 0x101F);
+    else return ML_SWZ(v, 0x401F);                       // xor 16
+}
+
+// Reductions over the 32 lanes of each half-wave (result in every lane).
+template <int KIND> __device__ inline float red_op(float a, float b) {
+    return KIND == 2 ? fminf(a, b) : (KIND == 3 ? fmaxf(a, b) : a + b);
+}
+template <int KIND> __device__ inline float half_reduce(float v) {
+    v = red_op<KIND>(v, xlane<1>(v));
+    v = red_op<KIND>(v, xlane<2>(v));
+    v = red_op<KIND>(v, ML_DPP(v, 0x124));  // row_ror:4
+    v = red_op<KIND>(v, xlane<8>(v));
+    v = red_op<KIND>(v, xlane<16>(v));
+    return v;
+}
+
+// Column sums: the 16 values v[q] of every lane summed over the 32 lanes
+// (rows) of its half-wave, by recursive halving (each step sends half the
+// values to the partner lane).  Returns the total of value index
+// col_sum16_index(lane); lanes r and r ^ 16 return the same total.
+template <int D, int N> __device__ inline void bfly(float (&v)[16], int lane) {
+    const bool hi = (lane & D) != 0;
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+        const float a = v[i], b = v[i + N / 2];
+        const float keep = hi ? b : a, send = hi ? a : b;
+        v[i] = keep + xlane<D>(send);
+    }
+}
+__device__ inline float col_sum16(float (&v)[16], int lane) {
+    bfly<1, 16>(v, lane);
+    bfly<2, 8>(v, lane);
+    bfly<8, 4>(v, lane);
+    bfly<4, 2>(v, lane);
+    return v[0] + xlane<16>(v[0]);
+}
+__device__ inline int col_sum16_index(int lane) {
+    return ((lane & 1) << 3) | ((lane & 2) << 1) | ((lane >> 2) & 2) | ((lane >> 2) & 1);
+}
+
+// Order LDS traffic between the lanes of one wave.
+__device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Store 4 consecutive elements (one 8-byte bf16 / 16-byte f32 store).
+__device__ inline void store4(bf16* p, float a, float b, float c, float d) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+    *(bf16x4*)p = v;
+}
+__device__ inline void store4(float* p, float a, float b, float c, float d) {
+    *(float4*)p = make_float4(a, b, c, d);
+}
+
+// Lane-private LDS spill of one accumulator block (16 values) in the compute
+// dtype: CH 16-byte chunks, chunk-major over the 64 lanes (conflict-free).
+template <typename T> struct ZIO {
+    static constexpr int VPC = 16 / sizeof(T), CH = 16 / VPC;
+    typedef __attribute__((ext_vector_type(4))) uint32_t u4;
+    __device__ static void put(u4* base, int lane, const f32x16& a) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            union {
+                T v[VPC];
+                u4 q;
+            } u;
+#pragma unroll
+            for (int j = 0; j < VPC; ++j) u.v[j] = cvt<T>(a[c * VPC + j]);
+            base[c * 64 + lane] = u.q;
+        }
+    }
+    __device__ static void get(const u4* base, int lane, float (&z)[16]) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            union {
+                T v[VPC];
+                u4 q;
+            } u;
+            u.q = base[c * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < VPC; ++j) z[c * VPC + j] = to_f32(u.v[j]);
+        }
+    }
+};
+
+struct PolicyK {
+    int D, H, L, K, A;
+    int off[MLEARN_MAX_GROUPS + 1];
+    const void* wt[MLEARN_MAX_LAYERS];
+    const void* w[MLEARN_MAX_LAYERS];
+    const float* lns[MLEARN_MAX_LAYERS];
+    const float* lnb[MLEARN_MAX_LAYERS];
+    const void* head_t;
+    const void* head;
+    const float* head_b;
+};
+
+PolicyK make_policy_k(const mlearn_mlp_policy& p);
+int validate_policy(const mlearn_mlp_policy* p);
+
+// Flat f32 parameter layout (mlearn_param_count): per layer W_l [in][H],
+// LN scale [H], LN bias [H]; then head W [H][A+1], head bias [A+1].
+struct LayoutK {
+    int L, D, H, A1;  // A1 = A + 1 head outputs
+    int64_t w_off[MLEARN_MAX_LAYERS], s_off[MLEARN_MAX_LAYERS], b_off[MLEARN_MAX_LAYERS];
+    int64_t hw_off, hb_off, total;
+};
+
+LayoutK make_layout(const mlearn_mlp_policy& p);
+
+}  // namespace ml

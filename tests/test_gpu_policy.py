@@ -212,16 +212,16 @@ def test_optimizer_step(gpu):
     got = ps.params.cpu().numpy()
     np.testing.assert_allclose(got, p, rtol=2e-5, atol=2e-6)
     assert int(ts.step.item()) == 3
-    # compute-dtype fragment-order images follow the master weights
+    # compute-dtype operand images follow the master weights (frag.py)
     from madrona_learn.frag import from_image
     for l in range(2):
         wl = ps.view("w", l)
         fin, H = wl.shape
-        assert torch.equal(from_image(ps.w_t[l], H, fin), wl.t())
+        assert torch.equal(from_image(ps.w_t[l], H, fin, l > 0), wl.t())
         if l > 0:
-            assert torch.equal(from_image(ps.w[l], fin, H), wl)
+            assert torch.equal(from_image(ps.w[l], fin, H, True), wl)
     hw = ps.view("hw")
     A1 = hw.shape[1]
-    assert torch.equal(from_image(ps.head_t, 32, 256)[:A1], hw.t())
-    assert torch.equal(from_image(ps.head, 256, 32)[:, :A1], hw)
-    assert not from_image(ps.head, 256, 32)[:, A1:].any()
+    assert torch.equal(from_image(ps.head_t, 32, 256, True)[:A1], hw.t())
+    assert torch.equal(from_image(ps.head, 256, 32, False)[:, :A1], hw)
+    assert not from_image(ps.head, 256, 32, False)[:, A1:].any()
