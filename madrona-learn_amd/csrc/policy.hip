@@ -149,14 +149,14 @@ __global__ __launch_bounds__(64 * kPolicyWaves) void policy_step_kernel(
             for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
         if (l + 1 == L) break;
         zero_acc<NB>(acc);
-        gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.wt[l + 1], lane);
+        gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.wt[l + 1], lane);
     }
 
     // actor + critic heads: lg[row][j] = rnd(rnd(a . W) + rnd(b)) (dists.py:22)
     {
         f32x16 ha[1];
         zero_acc<1>(ha);
-        gemm_rb<T, 1, KSH>(ha, bf, (const T*)P.head_t, lane);
+        gemm_rb<T, 1, KSH, 8>(ha, bf, (const T*)P.head_t, lane);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int j = feat(0, q, h);

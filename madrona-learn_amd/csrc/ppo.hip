@@ -64,7 +64,23 @@ struct WsK {
     int64_t Mp;
     int ntiles;                         // Mp / 32
     int CP;                             // L*2*H + 32
+    uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
+
+#ifdef ML_STAMPS
+static uint64_t* g_stamp_buf = nullptr;
+#define STAMP(i)                                                                  \
+    do {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        if (ws.stamps && lane == 0)                                               \
+            ws.stamps[(int64_t)tile * 16 + (i)] = __builtin_amdgcn_s_memtime();   \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -129,21 +145,10 @@ struct LossAcc {
     float mnvl = 3.4e38f, mxvl = -3.4e38f, mnerr = 3.4e38f, mxerr = -3.4e38f;
 };
 
-__device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float old_lp, float adv,
-                                  float ecoef, LossAcc& m) {
-    float mx = lg[0];
-    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
-    float ex[32];
-    float se = 0.f;
-    for (int j = 0; j < nb; ++j) {
-        ex[j] = __expf(lg[j] - mx);
-        se += ex[j];
-    }
-    const float inv = 1.0f / se;
-    const float lse = mx + __logf(se);
-    float ent = 0.f;
-    for (int j = 0; j < nb; ++j) ent -= (ex[j] * inv) * (lg[j] - lse);  // dists.py:68-69
-    const float lpa = lg[a] - lse;
+// PPO objective terms of one action group given its log-prob of the taken
+// action and entropy; returns d loss / d logp[a] and accumulates metrics.
+__device__ inline float ppo_obj(const HpK& hp, float lpa, float old_lp, float adv, float ent,
+                                float ecoef, LossAcc& m) {
     const float ratio = __expf(lpa - old_lp);
     const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
     const float s1 = adv * ratio;
@@ -156,13 +161,6 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
     const float dmn = y < hi ? 1.f : (y == hi ? 0.5f : 0.f);
     const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
     const float dobj = w1 * adv + (1.f - w1) * adv * (dmx * dmn);
-    const float g_lp = -hp.inv_sk * dobj * ratio;  // d loss / d logp[a]
-    const float ce = ecoef * hp.inv_sk;             // entropy term weight
-    for (int j = 0; j < nb; ++j) {
-        const float p = ex[j] * inv;
-        const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lg[j] - lse) + ent);
-        lg[j] = d * hp.loss_scale;
-    }
     m.sobj += obj;
     m.qobj += obj * obj;
     m.mnobj = fminf(m.mnobj, obj);
@@ -172,6 +170,67 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
     m.mnent = fminf(m.mnent, ent);
     m.mxent = fmaxf(m.mxent, ent);
     m.sentw += ecoef * ent;
+    return -hp.inv_sk * dobj * ratio;
+}
+
+// Group of at most MAXB logits held in registers (fixed width, masked): no
+// dynamically indexed register arrays.
+template <int MAXB>
+__device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a, float old_lp,
+                                        float adv, float ecoef, LossAcc& m) {
+    float v[MAXB];
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) v[j] = j < nb ? lg[j] : -3.4e38f;
+    float mx = v[0];
+#pragma unroll
+    for (int j = 1; j < MAXB; ++j) mx = fmaxf(mx, v[j]);
+    float ex[MAXB], se = 0.f, lpa = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+        ex[j] = j < nb ? __expf(v[j] - mx) : 0.f;
+        se += ex[j];
+    }
+    const float inv = 1.0f / se;
+    const float lse = mx + __logf(se);
+    float ent = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+        if (j < nb) ent -= (ex[j] * inv) * (v[j] - lse);  // dists.py:68-69
+        lpa = j == a ? v[j] - lse : lpa;
+    }
+    const float g_lp = ppo_obj(hp, lpa, old_lp, adv, ent, ecoef, m);
+    const float ce = ecoef * hp.inv_sk;  // entropy term weight
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+        const float p = ex[j] * inv;
+        const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((v[j] - lse) + ent);
+        if (j < nb) lg[j] = d * hp.loss_scale;
+    }
+}
+
+// Any group size (<= 31): three passes over the logits in LDS.
+__device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float old_lp, float adv,
+                                  float ecoef, LossAcc& m) {
+    if (nb <= 8) {
+        loss_group_fixed<8>(hp, lg, nb, a, old_lp, adv, ecoef, m);
+        return;
+    }
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    const float inv = 1.0f / se;
+    const float lse = mx + __logf(se);
+    float ent = 0.f;
+    for (int j = 0; j < nb; ++j) ent -= (__expf(lg[j] - mx) * inv) * (lg[j] - lse);
+    const float g_lp = ppo_obj(hp, lg[a] - lse, old_lp, adv, ent, ecoef, m);
+    const float ce = ecoef * hp.inv_sk;
+    for (int j = 0; j < nb; ++j) {
+        const float lj = lg[j];
+        const float p = __expf(lj - mx) * inv;
+        const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lj - lse) + ent);
+        lg[j] = d * hp.loss_scale;
+    }
 }
 
 // lg points at the row; value logit at column A; zeroes columns A+1..31.
@@ -242,6 +301,12 @@ template <typename T, int H, int L> struct StepLds {
     }
 };
 
+// ReLU' threshold: rnd<T>(y) > 0  <=>  y > THR (bf16 round-to-nearest-even
+// sends y <= 2^-134 to zero).
+template <typename T> __device__ inline float relu_thr();
+template <> __device__ inline float relu_thr<float>() { return 0.f; }
+template <> __device__ inline float relu_thr<bf16>() { return __builtin_bit_cast(float, 0x00008000u); }
+
 template <typename T, int H, int L>
 __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
                                                        const int32_t* __restrict__ mb_seq, int mb,
@@ -250,8 +315,9 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
     typedef typename RT<T>::frag frag;
     typedef ZIO<T> Z;
     typedef typename Z::u4 u4;
-    constexpr int NB = H / 32, E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB;
+    constexpr int NB = H / 32, KS = RT<T>::KS, SPB = RT<T>::SPB;
     constexpr int KSH = H / KS, KSHD = MLEARN_HEAD_COLS / KS, CH = Z::CH;
+    constexpr int KSD = 256 / KS;  // max k-steps over the observation
     typedef StepLds<T, H, L> LDS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, K = P.K;
@@ -284,6 +350,15 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         const int64_t c = seq / ro.N, b = seq - c * ro.N;
         sr = (c * ro.bptt + tl) * ro.N + b;
     }
+    // observation fragments (natural k order), all in flight at once
+    const int nks0 = D / KS;
+    frag ob[KSD];
+    {
+        const T* orow = (const T*)ro.obs + sr * D;
+#pragma unroll
+        for (int s = 0; s < KSD; ++s)
+            if (s < nks0) ob[s] = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
+    }
     // loss inputs of the first four tasks of this lane (groups h, h+2, ...)
     int pa[4];
     float pl[4];
@@ -299,25 +374,20 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         adv = ro.adv[sr];
         ret = ro.ret[sr];
         if (ro.values) oval = ro.values[sr];
-        if (hp.norm_adv) adv = (adv - adv_st[0]) * adv_st[1];
+    }
+    STAMP(0);
+    {
+        T* xrow = (T*)ws.x0 + row * D;
+#pragma unroll
+        for (int s = 0; s < KSD; ++s)
+            if (s < nks0) RT<T>::put_row(xrow, s, h, ob[s]);
     }
 
     // ---- forward ----
     f32x16 acc[NB];
     zero_acc<NB>(acc);
-    {
-        const T* orow = (const T*)ro.obs + sr * D;
-        T* xrow = (T*)ws.x0 + row * D;
-        const int nks = D / KS;
-        const T* img = (const T*)P.wt[0] + lane * E;
-        for (int s = 0; s < nks; ++s) {
-            const frag b = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
-            RT<T>::put_row(xrow, s, h, b);
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-                acc[nb] = MT<T>::mma(MT<T>::load(img + (nb * nks + s) * 64 * E), b, acc[nb]);
-        }
-    }
+    gemm_ring<T, NB, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0], lane);
+    STAMP(1);
     frag bf[KSH];
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
@@ -325,7 +395,8 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
     for (int l = 0; l < L; ++l) {
         if (l > 0) {
             zero_acc<NB>(acc);
-            gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.wt[l], lane);
+            gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.wt[l], lane);
+            STAMP(2 * l + 1);
         }
         float sum = 0.f, sq = 0.f;
 #pragma unroll
@@ -358,7 +429,8 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int q = 4 * g + j;
-                    acc[nb][q] = fmaxf(rnd<T>((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j]), 0.f);
+                    // LayerNorm (x - mean) * (rstd * scale) + bias, ReLU, compute dtype
+                    acc[nb][q] = rnd<T>(fmaxf((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
                 }
                 store4(arow + f0, acc[nb][4 * g], acc[nb][4 * g + 1], acc[nb][4 * g + 2],
                        acc[nb][4 * g + 3]);
@@ -367,11 +439,12 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
+        STAMP(2 * l + 2);
     }
     {
         f32x16 ha[1];
         zero_acc<1>(ha);
-        gemm_rb<T, 1, KSH>(ha, bf, (const T*)P.head_t, lane);
+        gemm_rb<T, 1, KSH, 8>(ha, bf, (const T*)P.head_t, lane);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int j = feat(0, q, h);
@@ -379,9 +452,11 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         }
     }
     wave_lds_sync();
+    STAMP(2 * L + 1);
 
     // ---- loss: lane half h takes tasks h, h + 2, ... (task K = value) ----
     {
+        if (hp.norm_adv) adv = (adv - adv_st[0]) * adv_st[1];
         LossAcc m;
         float* lr = lg + r * 33;
         if (live) {
@@ -408,6 +483,7 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         store_loss_partials(m, ws.loss_part + (int64_t)tile * kLossSlots, lane);
     }
     wave_lds_sync();
+    STAMP(2 * L + 2);
 
     // d head: row-major store (wgrad operand) and the head-bias column partial
     {
@@ -429,9 +505,11 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * 33, s, h);
         zero_acc<NB>(acc);
         // dA_{L-1}^T = Head . dHead^T
-        gemm_rb<T, NB, KSHD>(acc, db, (const T*)P.head, lane);
+        gemm_rb<T, NB, KSHD, 2>(acc, db, (const T*)P.head, lane);
     }
+    STAMP(2 * L + 3);
     const int qs = col_sum16_index(lane);
+    const float thr = relu_thr<T>();
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
         const float mean = mean_r[l], rstd = rstd_r[l];
@@ -453,7 +531,9 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
                     const float zc = z[q] - mean;
                     const float xh = zc * rstd;
                     const float y = zc * (rstd * gg[j]) + bb[j];
-                    const float dy = (live && rnd<T>(y) > 0.f) ? acc[nb][q] : 0.f;  // ReLU'
+                    const float da = acc[nb][q];
+                    const bool on = (y > thr) & live;  // ReLU'
+                    const float dy = on ? da : 0.f;
                     const float u = dy * gg[j];
                     acc[nb][q] = u;
                     su += u;
@@ -473,22 +553,22 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         }
         su = sum_halves(su);
         sv = sum_halves(sv);
-        const float mu = su * invH, mv = sv * invH;
+        // dZ = rstd * (u - mean(u) - xh * mean(u xh)) = rstd * u + (-rstd^2 mean(u xh)) zc - rstd mean(u)
+        const float ca = -(rstd * rstd) * (sv * invH), cb = -rstd * (su * invH);
         T* dzrow = (T*)ws.dz[l] + row * H;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
             float z[16];
             Z::get(zb + (l * NB + nb) * CH * 64, lane, z);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float xh = (z[q] - mean) * rstd;
-                acc[nb][q] = rnd<T>(rstd * (acc[nb][q] - mu - xh * mv));
-            }
+            for (int q = 0; q < 16; ++q)
+                acc[nb][q] = rnd<T>(rstd * acc[nb][q] + (ca * (z[q] - mean) + cb));
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 store4(dzrow + nb * 32 + 8 * g + 4 * h, acc[nb][4 * g], acc[nb][4 * g + 1],
                        acc[nb][4 * g + 2], acc[nb][4 * g + 3]);
         }
+        STAMP(2 * L + 4 + 2 * (L - 1 - l));
         if (l > 0) {
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb)
@@ -496,7 +576,8 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
                 for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
             zero_acc<NB>(acc);
             // dA_{l-1}^T = W_l . dZ_l^T
-            gemm_rb<T, NB, KSH>(acc, bf, (const T*)P.w[l], lane);
+            gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.w[l], lane);
+            STAMP(2 * L + 5 + 2 * (L - 1 - l));
         }
     }
 }
@@ -815,6 +896,9 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     const int64_t M = (int64_t)mb * ro.bptt_len;
     WsK ws;
     carve(p, M, (char*)wsp, &ws);
+#ifdef ML_STAMPS
+    ws.stamps = g_stamp_buf;
+#endif
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
                ro.T, ro.bptt_len, ro.N};
@@ -879,6 +963,11 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 using namespace ml;
 
 extern "C" {
+
+#ifdef ML_STAMPS
+// diagnostic builds only: phase timestamps of the fused minibatch kernel
+void mlearn_debug_set_stamp_buffer(uint64_t* buf) { g_stamp_buf = buf; }
+#endif
 
 int64_t mlearn_param_count(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;

@@ -127,39 +127,49 @@ template <> __device__ inline float img_load<float>(__amdgpu_buffer_rsrc_t rs, i
 }
 
 // acc[nb] += sum_s Img[block nb][step s] x b[s]   (NOUT blocks of 32 outputs).
-// The A fragments of step s+1 are in flight while the MFMAs of step s run
-// (two register sets; sched_barrier fences keep the compiler from sinking
-// each load down to its MFMA, which would expose a full L2 round trip per
-// MFMA at one wave per SIMD).
-template <typename T, int NOUT, int NKS>
-__device__ inline void gemm_rb(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&b)[NKS],
-                               const T* __restrict__ img, int lane) {
+// A ring of DEPTH k-steps of A fragments is in flight ahead of the MFMAs;
+// sched_barrier fences keep the compiler from sinking each load down to its
+// MFMA, which would expose a full L2 round trip per MFMA at one wave/SIMD.
+// nks (<= NKS) is the wave-uniform number of steps actually taken.
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_ring(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&b)[NKS],
+                                 int nks, const T* __restrict__ img, int lane) {
     typedef typename RT<T>::frag frag;
     constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);  // bytes per fragment run
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
     const int voff = lane * RT<T>::E * (int)sizeof(T);
-    frag ra[2][NOUT];
+    frag ra[DEPTH][NOUT];
 #pragma unroll
-    for (int nb = 0; nb < NOUT; ++nb) ra[0][nb] = img_load<T>(rs, voff, (nb * NKS) * FB);
+    for (int s = 0; s < DEPTH - 1; ++s)
+        if (s < nks)
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * nks + s) * FB);
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
-        if (s + 1 < NKS) {
+        if (s < nks) {
+            const int sl = s + DEPTH - 1;
+            if (sl < nks) {
+#pragma unroll
+                for (int nb = 0; nb < NOUT; ++nb)
+                    ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * nks + sl) * FB);
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int nb = 0; nb < NOUT; ++nb)
-                ra[(s + 1) & 1][nb] = img_load<T>(rs, voff, (nb * NKS + s + 1) * FB);
+                acc[nb] = MT<T>::mma(ra[s % DEPTH][nb], b[s], acc[nb]);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ra[s & 1][nb], b[s], acc[nb]);
-        __builtin_amdgcn_sched_barrier(0);
     }
+}
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_rb(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&b)[NKS],
+                               const T* __restrict__ img, int lane) {
+    gemm_ring<T, NOUT, NKS, DEPTH>(acc, b, NKS, img, lane);
 }
 
 // Feature index of accumulator register q of block nb for lane half h.
 __device__ inline int feat(int nb, int q, int h) { return nb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h; }
 
-// Sum of a per-row value over both lane halves (features 4h-interleaved).
-__device__ inline float sum_halves(float v) { return v + __shfl_xor(v, 32); }
 
 // ---------------------------------------------------------------------------
 // Cross-lane helpers.
@@ -175,6 +185,20 @@ template <int D> __device__ inline float xlane(float v) {
     else if constexpr (D == 8) return ML_DPP(v, 0x128); // row_ror:8 (= xor 8 in a row)
     else if constexpr (D == 4) return ML_SWZ(v, 0x101F);
     else return ML_SWZ(v, 0x401F);                       // xor 16
+}
+// v + (value of lane ^ 16) / (value of lane ^ 32): one v_permlane16_swap /
+// v_permlane32_swap on two copies (VALU only; the builtins' two-result form
+// miscompiles when both operands are the same value, so inline asm with the
+// hazard padding the compiler would insert).
+__device__ inline float add_xor16(float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    return a + b;
+}
+__device__ inline float add_xor32(float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    return a + b;
 }
 
 // Reductions over the 32 lanes of each half-wave (result in every lane).
@@ -207,12 +231,22 @@ __device__ inline float col_sum16(float (&v)[16], int lane) {
     bfly<1, 16>(v, lane);
     bfly<2, 8>(v, lane);
     bfly<8, 4>(v, lane);
-    bfly<4, 2>(v, lane);
-    return v[0] + xlane<16>(v[0]);
+    {  // partner lane ^ 4 (same bits 0, 1, 3) within the 16-lane row:
+       // row_ror:N delivers lane i - N, so bit-2-clear lanes take ror:12 (i + 4)
+        const bool hi = (lane & 4) != 0;
+        const float a = v[0], b = v[1];
+        const float keep = hi ? b : a, send = hi ? a : b;
+        const float r4 = ML_DPP(send, 0x124), r12 = ML_DPP(send, 0x12C);
+        v[0] = keep + (hi ? r4 : r12);
+    }
+    return add_xor16(v[0]);
 }
 __device__ inline int col_sum16_index(int lane) {
     return ((lane & 1) << 3) | ((lane & 2) << 1) | ((lane >> 2) & 2) | ((lane >> 2) & 1);
 }
+
+// Sum of a per-row value over both lane halves (features 4h-interleaved).
+__device__ inline float sum_halves(float v) { return add_xor32(v); }
 
 // Order LDS traffic between the lanes of one wave.
 __device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Diagnostic library with in-kernel phase stamps (-DML_STAMPS); never the product .so.
+set -e
+cd "$(dirname "$0")/../madrona-learn_amd"
+mkdir -p build_stamps
+for f in csrc/*.hip; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DML_STAMPS -c $f -o build_stamps/$(basename $f .hip).o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build_stamps/*.o -o build_stamps/libmlearn_stamps.so
