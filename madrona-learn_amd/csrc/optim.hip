@@ -5,8 +5,9 @@
 //   -> LayerNorm renorm so that |scale|^2 + |bias|^2 = features (ppo.py:312-338)
 //   -> refresh of the compute-dtype weight copies the MLP kernels read
 //      (transposed [out][in] and [in][out] images, padded head).
-// Five short launches over the flat 90K-float parameter vector; global
-// reductions go through fixed-order double partials (deterministic).
+// Three short launches over the flat 90K-float parameter vector; global
+// reductions go through fixed-order double partials that every consumer
+// block re-reduces identically (deterministic, no finishing launches).
 
 #include "common.h"
 #include "rowtile.h"
@@ -49,13 +50,6 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
     if (threadIdx.x == 0) part[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
 }
 
-__global__ void sumsq_finish_kernel(const double* part, int nparts, float* out) {
-    if (threadIdx.x == 0) {
-        double s = 0;
-        for (int i = 0; i < nparts; ++i) s += part[i];
-        out[0] = sqrtf((float)s);  // optax.global_norm in f32
-    }
-}
 
 // tensor id of parameter p for the projection partials: 2*l = W_l, 2*l+1 = LN_l, -1 = head
 __device__ inline int proj_slot(const LayoutK& k, int64_t p) {
@@ -65,19 +59,32 @@ __device__ inline int proj_slot(const LayoutK& k, int64_t p) {
     return p < k.s_off[l] ? 2 * l : 2 * l + 1;
 }
 
+// Global gradient norm from the kNormBlocks partials (every block computes it
+// the same way: wave 0, fixed butterfly order).
+__device__ inline float global_norm(const double* gpart) {
+    __shared__ float gn_sh;
+    if (threadIdx.x < 64) {
+        double t = threadIdx.x < kNormBlocks ? gpart[threadIdx.x] : 0.0;
+        t = wave_sum64d(t);
+        if (threadIdx.x == 0) gn_sh = sqrtf((float)t);  // optax.global_norm in f32
+    }
+    __syncthreads();
+    return gn_sh;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict__ params,
                                                    const float* __restrict__ grads,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   const int32_t* step, const float* gnorm, float lr,
-                                                   float b1, float b2, float eps, float max_norm,
-                                                   double* proj_part) {
+                                                   const int32_t* step, const double* gpart,
+                                                   float lr, float b1, float b2, float eps,
+                                                   float max_norm, double* proj_part) {
     __shared__ float sh[4][2 * MLEARN_MAX_LAYERS];
     const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     const int nslot = 2 * Lk.L;
     float contrib = 0.f;
     int slot = -2;
+    const float gn = global_norm(gpart);
     if (p < Lk.total) {
-        const float gn = gnorm[0];
         float g = grads[p];
         if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
         const int count = step[0] + 1;
@@ -108,19 +115,6 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     }
 }
 
-// one block per projection slot; fixed-order tree over the block partials
-__global__ __launch_bounds__(256) void proj_finish_kernel(const double* part, int nblocks, int nslot,
-                                                          float* out) {
-    __shared__ double sh[4];
-    const int sl = blockIdx.x;
-    double t = 0;
-    for (int b = threadIdx.x; b < nblocks; b += 256) t += part[(int64_t)b * nslot + sl];
-    t = wave_sum64d(t);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) out[sl] = (float)(((sh[0] + sh[1]) + sh[2]) + sh[3]);
-}
-
 template <typename T>
 __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t p, float val) {
     const int H = Lk.H;
@@ -147,8 +141,26 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
 
 template <typename T>
 __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, float* params,
-                                                      const float* init_norms, const float* sq,
-                                                      int norm_params, int norm_ln, int32_t* step) {
+                                                      const float* init_norms, const double* ppart,
+                                                      int nblk, int norm_params, int norm_ln,
+                                                      int32_t* step) {
+    // per-slot sums of squares of the updated tensors (ppo.py:303-338), the
+    // same fixed-order tree in every block
+    __shared__ double red[4][2 * MLEARN_MAX_LAYERS];
+    __shared__ float sq[2 * MLEARN_MAX_LAYERS];
+    const int nslot = 2 * Lk.L;
+    for (int sl = 0; sl < nslot; ++sl) {
+        double t = 0;
+        for (int b = threadIdx.x; b < nblk; b += 256) t += ppart[(int64_t)b * nslot + sl];
+        t = wave_sum64d(t);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][sl] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < nslot) {
+        const int sl = threadIdx.x;
+        sq[sl] = (float)(((red[0][sl] + red[1][sl]) + red[2][sl]) + red[3][sl]);
+    }
+    __syncthreads();
     const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     if (p == 0 && step) step[0] += 1;
     if (p >= Lk.total) return;
@@ -212,27 +224,21 @@ int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state*
     const int64_t nblk = (Lk.total + 255) / 256;
     double* gpart = (double*)workspace;
     double* ppart = gpart + kNormBlocks;
-    float* gnorm = (float*)(ppart + nblk * 2 * Lk.L);
-    float* sq = gnorm + 16;
     hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
                        Lk.total, gpart);
-    hipLaunchKernelGGL(sumsq_finish_kernel, dim3(1), dim3(64), 0, s, (const double*)gpart,
-                       kNormBlocks, gnorm);
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk), dim3(256), 0, s, Lk, st->params,
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
-                       (const float*)gnorm, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
+                       (const double*)gpart, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
                        ppart);
-    hipLaunchKernelGGL(proj_finish_kernel, dim3(2 * Lk.L), dim3(256), 0, s, (const double*)ppart,
-                       (int)nblk, 2 * Lk.L, sq);
     CopiesK C = make_copies(*policy);
     if (policy->dtype == MLEARN_DTYPE_BF16)
         hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const float*)sq, st->normalize_params,
-                           st->normalize_layernorms, st->step);
+                           st->params, st->init_norms, (const double*)ppart, (int)nblk,
+                           st->normalize_params, st->normalize_layernorms, st->step);
     else
         hipLaunchKernelGGL(project_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const float*)sq, st->normalize_params,
-                           st->normalize_layernorms, st->step);
+                           st->params, st->init_norms, (const double*)ppart, (int)nblk,
+                           st->normalize_params, st->normalize_layernorms, st->step);
     return check_launch("optim_step");
 }
 

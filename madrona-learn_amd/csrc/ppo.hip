@@ -84,11 +84,11 @@ static uint64_t* g_stamp_buf = nullptr;
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Split-K plan of one weight gradient [I][J] over Mp rows: ~256 workgroups.
+// Split-K plan of one weight gradient [I][J] over Mp rows: ~128 workgroups.
 static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
-    int64_t s = 256 / tiles;
+    int64_t s = 128 / tiles;
     if (s < 1) s = 1;
     if (s > chunks) s = chunks;
     int64_t per = (chunks + s - 1) / s;
@@ -623,6 +623,7 @@ struct WgJobs {
     WgJob job[MLEARN_MAX_LAYERS + 1];
     int n;
     int64_t Mp;
+    int nwg, ncol, ncolx;  // weight-gradient blocks, column-sum blocks (ncolx per chunk)
 };
 
 template <typename T> struct WgCfg {
@@ -656,8 +657,20 @@ template <> struct WgFrag<float> {
     }
 };
 
+__device__ inline void colsum_block(const WsK& ws, int bx, int c);
+__device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K, float* out);
+
+// Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
+// level of the column partials; one more (if loss_out) the loss metrics.
 template <typename T>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs) {
+__global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
+                                                    float* loss_out) {
+    if ((int)blockIdx.x >= jobs.nwg) {
+        const int b = blockIdx.x - jobs.nwg;
+        if (b < jobs.ncol) colsum_block(ws, b % jobs.ncolx, b / jobs.ncolx);
+        else loss_block(ws, hp, M, K, loss_out);
+        return;
+    }
     constexpr int VPC = 16 / sizeof(T);                  // elements per 16-B chunk
     constexpr int CPR = kWgTile / VPC;                   // chunks per tile row
     constexpr int PER = kWgChunk * CPR / 256;            // chunks per thread per operand
@@ -683,56 +696,72 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs) {
     const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
     const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
 
-    u4 rx[PER], ry[PER];
-    auto gload = [&](int c) {
+    // two register sets of staged rows: chunk c + 2 is in flight while chunk c
+    // is multiplied out of LDS and chunk c + 1 is written to the other buffer
+    u4 rx[2][PER], ry[2][PER];
+    auto gload = [&](int c, u4 (&gx)[PER], u4 (&gy)[PER]) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
             const u4 zero = {0u, 0u, 0u, 0u};
-            rx[u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
-            ry[u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
+            gx[u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
+            gy[u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
         }
     };
-    auto sstore = [&](int stage) {
+    auto sstore = [&](int stage, const u4 (&gx)[PER], const u4 (&gy)[PER]) {
         T* xs = lds + (size_t)stage * 2 * kWgChunk * LD;
         T* ys = xs + kWgChunk * LD;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
-            *(u4*)(xs + rr * LD + cc) = rx[u];
-            *(u4*)(ys + rr * LD + cc) = ry[u];
+            *(u4*)(xs + rr * LD + cc) = gx[u];
+            *(u4*)(ys + rr * LD + cc) = gy[u];
         }
     };
-
     f32x16 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) zero_acc<2>(acc[a]);
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int c = 0; c < nchunks; ++c) {
-        if (c + 1 < nchunks) gload(c + 1);
-        const T* xs = lds + (size_t)(c & 1) * 2 * kWgChunk * LD;
+    auto compute = [&](int stage) {
+        if (!(wi_on && wj_on)) return;
+        const T* xs = lds + (size_t)stage * 2 * kWgChunk * LD;
         const T* ys = xs + kWgChunk * LD;
-        if (wi_on && wj_on) {
 #pragma unroll
-            for (int ks = 0; ks < KSTEPS; ++ks) {
-                typename WgFrag<T>::frag fa[2], fb[2];
+        for (int ks = 0; ks < KSTEPS; ++ks) {
+            typename WgFrag<T>::frag fa[2], fb[2];
 #pragma unroll
-                for (int a = 0; a < 2; ++a) {
-                    fa[a] = WgFrag<T>::load(xs, ks, iw + 32 * a, lane);
-                    fb[a] = WgFrag<T>::load(ys, ks, jw + 32 * a, lane);
-                }
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a], fb[b], acc[a][b]);
+            for (int a = 0; a < 2; ++a) {
+                fa[a] = WgFrag<T>::load(xs, ks, iw + 32 * a, lane);
+                fb[a] = WgFrag<T>::load(ys, ks, jw + 32 * a, lane);
             }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a], fb[b], acc[a][b]);
         }
-        if (c + 1 < nchunks) sstore((c + 1) & 1);
+    };
+    gload(0, rx[0], ry[0]);
+    if (nchunks > 1) gload(1, rx[1], ry[1]);
+    sstore(0, rx[0], ry[0]);
+    if (nchunks > 2) gload(2, rx[0], ry[0]);
+    __syncthreads();
+    for (int c = 0; c < nchunks; c += 2) {
+        // even chunk c: buffer 0; chunk c + 1 waits in set 1
+        compute(0);
+        if (c + 1 < nchunks) {
+            sstore(1, rx[1], ry[1]);
+            if (c + 3 < nchunks) gload(c + 3, rx[1], ry[1]);
+        }
+        __syncthreads();
+        if (c + 1 >= nchunks) break;
+        // odd chunk c + 1: buffer 1; chunk c + 2 waits in set 0
+        compute(1);
+        if (c + 2 < nchunks) {
+            sstore(0, rx[0], ry[0]);
+            if (c + 4 < nchunks) gload(c + 4, rx[0], ry[0]);
+        }
         __syncthreads();
     }
     if (!wi_on || !wj_on) return;
@@ -751,14 +780,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs) {
 
 
 // First level of the per-tile column partials (LayerNorm scale/bias grads,
-// head-bias grad): colpart2[c][col] = sum over tiles t = c, c + 32, ...
-__global__ __launch_bounds__(256) void colsum_kernel(WsK ws) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    const int c = blockIdx.y;
+// head-bias grad): colpart2[c][col] = sum over tiles t = c, c + kColChunks, ...
+// (8 independent accumulators, combined in fixed order).  Runs as extra
+// blocks of the weight-gradient launch.
+__device__ inline void colsum_block(const WsK& ws, int bx, int c) {
+    const int col = bx * 256 + threadIdx.x;
     if (col >= ws.CP) return;
-    float s = 0.f;
-    for (int t = c; t < ws.ntiles; t += kColChunks) s += ws.colpart[(int64_t)t * ws.CP + col];
-    ws.colpart2[(int64_t)c * ws.CP + col] = s;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int t = c;
+    for (; t + 7 * kColChunks < ws.ntiles; t += 8 * kColChunks)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += ws.colpart[(int64_t)(t + u * kColChunks) * ws.CP + col];
+    for (int u = 0; t < ws.ntiles; t += kColChunks, ++u) acc[u] += ws.colpart[(int64_t)t * ws.CP + col];
+    ws.colpart2[(int64_t)c * ws.CP + col] =
+        ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
 // ---------------------------------------------------------------------------
@@ -787,47 +822,78 @@ LayoutK make_layout(const mlearn_mlp_policy& p) {
     return k;
 }
 
+// Fixed-order reduction of the split-K slabs and column partials into the
+// flat gradient.  A block owns 64 consecutive parameters (every segment of
+// the flat layout but the head bias is a multiple of 64 long): 16 column
+// threads x 16 split groups; group g sums splits g, g + 16, ... and the
+// groups are combined in order through LDS.
+constexpr int kRgGroups = 16;
 __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad) {
-    int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
-    if (p >= Lk.total) return;
+    __shared__ float red[kRgGroups][65];
+    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int64_t p0 = (int64_t)blockIdx.x * 64;
     const int H = Lk.H, L = Lk.L;
-    float g = 0.f;
-    auto colsum = [&](int col) {
-        float t = 0.f;
-        for (int c = 0; c < kColChunks; ++c) t += ws.colpart2[(int64_t)c * ws.CP + col];
-        return t;
-    };
-    if (p >= Lk.hb_off) {
-        g = colsum(L * 2 * H + (int)(p - Lk.hb_off));
-    } else if (p >= Lk.hw_off) {
-        int64_t q = p - Lk.hw_off;
-        int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
-        const float* s = ws.slab + ws.slab_off[L] + (int64_t)i * MLEARN_HEAD_COLS + j;
-        const int64_t stride = (int64_t)H * MLEARN_HEAD_COLS;
-        for (int k = 0; k < ws.splits[L]; ++k) g += s[k * stride];
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p0 >= Lk.hw_off) {  // head weight (slab [split][H][32]) and head bias
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t p = p0 + 4 * c + e;
+            if (p >= Lk.total) break;
+            if (p >= Lk.hb_off) {
+                const int col = L * 2 * H + (int)(p - Lk.hb_off);
+                for (int k = g; k < kColChunks; k += kRgGroups)
+                    v[e] += ws.colpart2[(int64_t)k * ws.CP + col];
+            } else {
+                const int64_t q = p - Lk.hw_off;
+                const int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
+                const float* sp = ws.slab + ws.slab_off[L] + (int64_t)i * MLEARN_HEAD_COLS + j;
+                const int64_t stride = (int64_t)H * MLEARN_HEAD_COLS;
+                for (int k = g; k < ws.splits[L]; k += kRgGroups) v[e] += sp[k * stride];
+            }
+        }
     } else {
         int l = L - 1;
-        while (l > 0 && p < Lk.w_off[l]) --l;
-        if (p >= Lk.s_off[l]) {
-            const int which = p >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
-            const int col = (int)(p - (which ? Lk.s_off[l] : Lk.b_off[l]));
-            g = colsum((l * 2 + which) * H + col);
-        } else {
+        while (l > 0 && p0 < Lk.w_off[l]) --l;
+        if (p0 >= Lk.s_off[l]) {  // LayerNorm scale / bias: column partials
+            const int which = p0 >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
+            const int col = (l * 2 + which) * H + (int)(p0 - (which ? Lk.s_off[l] : Lk.b_off[l])) + 4 * c;
+            for (int k = g; k < kColChunks; k += kRgGroups) {
+                const float4 x = *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col);
+                v[0] += x.x;
+                v[1] += x.y;
+                v[2] += x.z;
+                v[3] += x.w;
+            }
+        } else {  // Dense kernel: split-K slabs
             const int I = l == 0 ? Lk.D : H;
-            const float* s = ws.slab + ws.slab_off[l] + (p - Lk.w_off[l]);
+            const float* sp = ws.slab + ws.slab_off[l] + (p0 - Lk.w_off[l]) + 4 * c;
             const int64_t stride = (int64_t)I * H;
-            for (int k = 0; k < ws.splits[l]; ++k) g += s[k * stride];
+            for (int k = g; k < ws.splits[l]; k += kRgGroups) {
+                const float4 x = *(const float4*)(sp + k * stride);
+                v[0] += x.x;
+                v[1] += x.y;
+                v[2] += x.z;
+                v[3] += x.w;
+            }
         }
     }
-    grad[p] = g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[g][4 * c + e] = v[e];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int64_t p = p0 + threadIdx.x;
+        float t = red[0][threadIdx.x];
+#pragma unroll
+        for (int k = 1; k < kRgGroups; ++k) t += red[k][threadIdx.x];
+        if (p < Lk.total) grad[p] = t;
+    }
 }
 
 // loss_out: five Metric vectors {mean, m2, min, max, count} in the order of
 // PPO.add_metrics (ppo.py:95-106): 'Loss' (scalar: {loss, 0, loss, loss, 1}),
 // 'Action Obj', 'Value Loss', 'Value Errors', 'Entropy'.
-__global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64_t M, int K,
-                                                            float* out) {
-    __shared__ double sh[16][kLossSlots];
+__device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K, float* out) {
+    __shared__ double sh[4][kLossSlots];
     __shared__ double tot[kLossSlots];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double v[kLossSlots];
@@ -836,7 +902,7 @@ __global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64
         const int kind = (s < 16) ? (s & 3) : 0;
         v[s] = kind == 2 ? 3.4e38 : (kind == 3 ? -3.4e38 : 0.0);
     }
-    for (int t = tid; t < ws.ntiles; t += 1024) {
+    for (int t = tid; t < ws.ntiles; t += 256) {
 #pragma unroll
         for (int s = 0; s < kLossSlots; ++s) {
             const int kind = (s < 16) ? (s & 3) : 0;
@@ -858,7 +924,7 @@ __global__ __launch_bounds__(1024) void reduce_loss_kernel(WsK ws, HpK hp, int64
     if (tid < kLossSlots) {
         const int kind = (tid < 16) ? (tid & 3) : 0;
         double x = sh[0][tid];
-        for (int i = 1; i < 16; ++i) {
+        for (int i = 1; i < 4; ++i) {
             double u = sh[i][tid];
             x = kind == 2 ? fmin(x, u) : (kind == 3 ? fmax(x, u) : x + u);
         }
@@ -938,6 +1004,9 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
         J.wg0 = wg;
         wg += J.ti * J.tj * J.splits;
     }
+    jobs.nwg = wg;
+    jobs.ncolx = (ws.CP + 255) / 256;
+    jobs.ncol = jobs.ncolx * kColChunks;
     {
         auto k = wgrad_kernel<T>;
         static bool attr_set = false;
@@ -946,15 +1015,13 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
                                       (int)WgCfg<T>::lds);
             attr_set = true;
         }
-        hipLaunchKernelGGL(k, dim3(wg), dim3(256), WgCfg<T>::lds, s, jobs);
-    }
-    hipLaunchKernelGGL(colsum_kernel, dim3((ws.CP + 255) / 256, kColChunks), dim3(256), 0, s, ws);
-    LayoutK Lk = make_layout(p);
-    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 255) / 256)), dim3(256), 0,
-                       s, Lk, ws, grad);
-    if (loss_out)
-        hipLaunchKernelGGL(reduce_loss_kernel, dim3(1), dim3(1024), 0, s, ws, hp, M,
+        const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
                            p.actions.num_groups, loss_out);
+    }
+    LayoutK Lk = make_layout(p);
+    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
+                       dim3(256), 0, s, Lk, ws, grad);
     return check_launch("ppo_minibatch_grad");
 }
 
