@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 1
+#define MLEARN_ABI_VERSION 2
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -136,18 +136,32 @@ typedef struct mlearn_mlp_policy {
     const float* head_bias;  /* [32] f32 */
 } mlearn_mlp_policy;
 
+/* Post-step bookkeeping of the PREVIOUS env step (rollouts.py:933-973), fused
+ * into the next policy launch; same arithmetic as mlearn_rollout_post_step. */
+typedef struct mlearn_post_step {
+    const float* rewards;       /* [N] env output of step t-1 */
+    const uint8_t* dones;       /* [N] */
+    float* store_rewards;       /* [N] rollout store, step t-1 */
+    uint8_t* store_dones;       /* [N] */
+    float* env_returns;         /* [N] running discounted return (in/out) */
+    float* env_returns_trace;   /* [N] or NULL */
+    float gamma;
+} mlearn_post_step;
+
 /* One rollout step of ActorCritic.rollout (actor_critic.py:74-96) fused with
  * the post-inference store (rollouts.py:637-668): preprocess (cast to the
  * compute dtype) -> MLP trunk -> actor logits + critic -> sample -> write
  * obs_store[N][obs_dim] (may be NULL), actions[N][K] i32, log_probs[N][K] f32,
  * values[N] f32.  actions == NULL computes only the critic
  * (ActorCritic.critic_only, actor_critic.py:65-72, used for the bootstrap
- * values, rollouts.py:607-635). */
+ * values, rollouts.py:607-635).  post (may be NULL) applies the post-step of
+ * the previous env step in the same launch. */
 int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const float* obs, int64_t N,
                                void* obs_store, int32_t* actions, float* log_probs,
                                float* values, uint32_t k0, uint32_t k1,
                                const uint64_t* step_ctr, uint64_t step, uint32_t env_offset,
-                               int32_t sample, mlearn_stream_t stream);
+                               int32_t sample, const mlearn_post_step* post,
+                               mlearn_stream_t stream);
 
 /* Post-step bookkeeping of rollout_loop (rollouts.py:933-973, _post_step_cb
  * 682-714): store rewards/dones at step t, env_returns = r + gamma*env_returns,
@@ -176,8 +190,9 @@ int mlearn_metrics_f32(const mlearn_metric_job* jobs, int32_t num_jobs, float* o
 /* PPO update (ppo.py:109-488)                                             */
 /* ---------------------------------------------------------------------- */
 /* Epoch permutation of n sequence ids (ppo.py:445-458, random.permutation):
- * perm = argsort of Philox keys (ctr={i, rank, epoch lo, epoch hi}), ties
- * broken by index.  n <= 16384 per call. */
+ * perm[i] = cycle-walked 4-round Feistel bijection of i on [0, 2^b), b =
+ * ceil(log2 n) rounded up to even, round r function = Philox4x32-10 word 0 of
+ * ctr {R + (r << 24), rank, epoch lo, epoch hi}, keys (k0, k1).  n <= 2^30. */
 int mlearn_minibatch_perm(uint32_t k0, uint32_t k1, const uint64_t* epoch_ctr, uint64_t epoch,
                           uint32_t rank, int32_t n, int32_t* perm, mlearn_stream_t stream);
 

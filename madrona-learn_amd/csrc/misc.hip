@@ -331,42 +331,38 @@ __global__ __launch_bounds__(256) void action_stats_kernel(const float* __restri
 // Epoch permutation (ppo.py:445-458): bitonic sort of (philox key, index)
 // pairs in LDS, one workgroup.
 // ---------------------------------------------------------------------------
-constexpr int kPermMax = 16384;
 
-__global__ __launch_bounds__(1024) void perm_kernel(uint32_t k0, uint32_t k1,
-                                                    const uint64_t* epoch_ctr, uint64_t epoch_add,
-                                                    uint32_t rank, int n, int npow2,
-                                                    int32_t* perm) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+// Epoch permutation as a keyed bijection: a 4-round balanced Feistel network
+// on [0, 2^b) (b = ceil(log2 n) rounded up to even, round function = Philox
+// word 0 of ctr {R + (round << 24), rank, epoch lo, epoch hi}) restricted to
+// [0, n) by cycle walking.  Every element is independent: one thread each.
+__device__ inline uint32_t feistel4(uint32_t x, int half, uint32_t mask, uint32_t k0, uint32_t k1,
+                                    uint32_t rank, uint64_t epoch) {
+    uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) {
+        const u32x4 f = philox4x32(
+            u32x4{R + ((uint32_t)rd << 24), rank, (uint32_t)epoch, (uint32_t)(epoch >> 32)}, k0, k1);
+        const uint32_t nr = L ^ (f.x & mask);
+        L = R;
+        R = nr;
+    }
+    return (L << half) | R;
+}
+
+__global__ __launch_bounds__(256) void perm_kernel(uint32_t k0, uint32_t k1,
+                                                   const uint64_t* epoch_ctr, uint64_t epoch_add,
+                                                   uint32_t rank, int n, int half,
+                                                   int32_t* perm) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
     const uint64_t epoch = (epoch_ctr ? *epoch_ctr : 0ull) + epoch_add;
-    for (int i = threadIdx.x; i < npow2; i += blockDim.x) {
-        unsigned long long k;
-        if (i < n) {
-            u32x4 r = philox4x32(u32x4{(uint32_t)i, rank, (uint32_t)epoch, (uint32_t)(epoch >> 32)},
-                                 k0, k1);
-            k = ((unsigned long long)r.x << 32) | (uint32_t)i;
-        } else {
-            k = ~0ull;
-        }
-        keys[i] = k;
-    }
-    __syncthreads();
-    for (int size = 2; size <= npow2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < npow2 / 2; i += blockDim.x) {
-                int lo = 2 * i - (i & (stride - 1));
-                int hi = lo + stride;
-                bool up = (lo & size) == 0;
-                unsigned long long a = keys[lo], b = keys[hi];
-                if ((a > b) == up) {
-                    keys[lo] = b;
-                    keys[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = (int32_t)(keys[i] & 0xffffffffu);
+    const uint32_t mask = (1u << half) - 1u;
+    uint32_t x = (uint32_t)i;
+    do {
+        x = feistel4(x, half, mask, k0, k1, rank, epoch);
+    } while (x >= (uint32_t)n);  // cycle walking: the orbit of i returns below n
+    perm[i] = (int32_t)x;
 }
 
 // ---------------------------------------------------------------------------
@@ -643,19 +639,13 @@ int mlearn_metrics_f32(const mlearn_metric_job* jobs, int32_t num_jobs, float* o
 
 int mlearn_minibatch_perm(uint32_t k0, uint32_t k1, const uint64_t* epoch_ctr, uint64_t epoch,
                           uint32_t rank, int32_t n, int32_t* perm, mlearn_stream_t stream) {
-    ML_REQUIRE(n >= 1 && n <= kPermMax, "perm: n must be in [1, %d], got %d", kPermMax, n);
+    ML_REQUIRE(n >= 1 && n <= (1 << 30), "perm: n must be in [1, 2^30], got %d", n);
     ML_REQUIRE(perm, "perm: null pointer");
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)perm_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  kPermMax * (int)sizeof(unsigned long long));
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(perm_kernel, dim3(1), dim3(1024), p2 * sizeof(unsigned long long),
-                       S(stream), k0, k1, epoch_ctr, epoch, rank, n, p2, perm);
+    int b = 2;
+    while ((1ll << b) < n) ++b;
+    if (b & 1) ++b;
+    hipLaunchKernelGGL(perm_kernel, dim3((n + 255) / 256), dim3(256), 0, S(stream), k0, k1,
+                       epoch_ctr, epoch, rank, n, b / 2, perm);
     return check_launch("minibatch_perm");
 }
 

@@ -58,24 +58,63 @@ int validate_policy(const mlearn_mlp_policy* p) {
     return MLEARN_OK;
 }
 
-// One wave = 32 environments (one per lane pair), all H features: the trunk,
-// heads and sampling of its rows run without any workgroup barrier.  The
-// workgroup's waves share the LayerNorm parameters staged once in LDS.
-constexpr int kPolicyWaves = 1;  // waves per workgroup (grid = one wave per 32 envs)
+// Post-step of the previous env step, fused into the next policy launch.
+struct PostK {
+    const float* rew;
+    const uint8_t* done;
+    float* srew;
+    uint8_t* sdone;
+    float* env_ret;
+    float* trace;
+    float gamma;
+};
+
+// rollouts.py:933-973: store reward/done, env_returns = r + gamma * env_returns
+// (traced for the 'Env Returns' metric), zeroed where done.
+__device__ inline void post_step_row(const PostK& p, int64_t n) {
+#pragma clang fp contract(off)
+    const float r = p.rew[n];
+    const uint8_t d = p.done[n] ? 1 : 0;
+    const float er = r + p.gamma * p.env_ret[n];
+    if (p.trace) p.trace[n] = er;
+    p.srew[n] = r;
+    p.sdone[n] = d;
+    p.env_ret[n] = d ? 0.f : er;
+}
+
+// One workgroup = 32 environments (one per lane pair); its W waves split the
+// hidden features (wave w owns blocks w*NBW .. w*NBW+NBW-1 of every layer).
+// Per layer: each wave's MFMAs over the full input (B fragments from LDS),
+// LayerNorm statistics combined across the waves through LDS, and the
+// post-activation fragments written back to LDS for the next layer.  The
+// heads split the reduction instead: each wave multiplies its own features,
+// partials are summed in wave order.
+template <int H> struct PolCfg {
+    static constexpr int NB = H / 32;
+    static constexpr int W = NB < 4 ? NB : 4;
+    static constexpr int NBW = NB / W;
+};
 
 template <typename T, int H>
-__global__ __launch_bounds__(64 * kPolicyWaves) void policy_step_kernel(
+__global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-    uint64_t step_add, uint32_t eoff, int sample) {
+    uint64_t step_add, uint32_t eoff, int sample, PostK post) {
     typedef typename RT<T>::frag frag;
-    constexpr int NB = H / 32, KS = RT<T>::KS, SPB = RT<T>::SPB, KSH = H / KS;
+    typedef PolCfg<H> C;
+    constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
+    constexpr int E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB, KSH = H / KS;
+    constexpr int KSD = 256 / KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, L = P.L;
-    float* gb = (float*)smem;            // [L][2][H]
-    float* hbias = gb + L * 2 * H;       // [32]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += blockDim.x) {
+    frag* fr = (frag*)smem;                               // [KSH][64] B fragments
+    float* gb = (float*)(fr + KSH * 64);                  // [L][2][H]
+    float* hbias = gb + L * 2 * H;                        // [32]
+    float* red = hbias + MLEARN_HEAD_COLS;                // [W][32][2]
+    float* lgp = red + W * 64;                            // [W][32][33] head partials
+    float* lg = lgp + W * 32 * 33;                        // [32][33]
+    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += THREADS) {
         float v;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
@@ -85,53 +124,68 @@ __global__ __launch_bounds__(64 * kPolicyWaves) void policy_step_kernel(
         }
         gb[i] = v;
     }
-    __syncthreads();
-    float* lg = hbias + MLEARN_HEAD_COLS + w * (32 * 33);  // [32][33] per wave
-    const int64_t row0 = ((int64_t)blockIdx.x * kPolicyWaves + w) * 32;
-    if (row0 >= N) return;
+    const int64_t row0 = (int64_t)blockIdx.x * 32;
     const int64_t row = row0 + r;
     const bool live = row < N;
+    if (post.rew && tid < 32 && row0 + tid < N) post_step_row(post, row0 + tid);
     const uint64_t step = (step_ctr ? *step_ctr : 0ull) + step_add;
     const float invH = 1.0f / (float)H;
 
     // layer 0: observation fragments straight from the env output (cast to
-    // the compute dtype = ObservationsCaster), copied to the rollout store
-    f32x16 acc[NB];
-    zero_acc<NB>(acc);
+    // the compute dtype = ObservationsCaster); wave 0 copies them to the store
+    const int nks0 = D / KS;
+    frag ob[KSD];
     {
         const float* orow = obs + (live ? row : 0) * D;
-        T* srow = obs_store ? obs_store + (live ? row : 0) * D : nullptr;
-        const int nks = D / KS;
-        const T* img = (const T*)P.wt[0] + lane * RT<T>::E;
-        for (int s = 0; s < nks; ++s) {
-            const frag b = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
-            if (srow && live) RT<T>::put_row(srow, s, h, b);
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-                acc[nb] = MT<T>::mma(MT<T>::load(img + (nb * nks + s) * 64 * RT<T>::E), b, acc[nb]);
+        for (int s = 0; s < KSD; ++s)
+            if (s < nks0) ob[s] = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
+        if (w == 0 && obs_store && live) {
+            T* srow = obs_store + row * D;
+#pragma unroll
+            for (int s = 0; s < KSD; ++s)
+                if (s < nks0) RT<T>::put_row(srow, s, h, ob[s]);
         }
     }
+    f32x16 acc[NBW];
+    zero_acc<NBW>(acc);
+    gemm_ring<T, NBW, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0] + (int64_t)w * NBW * nks0 * 64 * E,
+                              lane);
+    __syncthreads();  // LayerNorm parameters staged
     frag bf[KSH];
     for (int l = 0;; ++l) {
-        // LayerNorm + ReLU (models.py:46-56), statistics per row = per lane
+        // LayerNorm + ReLU (models.py:46-56); row statistics over all waves
         float sum = 0.f, sq = 0.f;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+        for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const float x = rnd<T>(acc[nb][q]);
-                acc[nb][q] = x;
+                const float x = rnd<T>(acc[i][q]);
+                acc[i][q] = x;
                 sum += x;
                 sq += x * x;
             }
         sum = sum_halves(sum);
         sq = sum_halves(sq);
+        if (h == 0) {
+            red[(w * 32 + r) * 2] = sum;
+            red[(w * 32 + r) * 2 + 1] = sq;
+        }
+        __syncthreads();
+        sum = red[r * 2];
+        sq = red[r * 2 + 1];
+#pragma unroll
+        for (int v = 1; v < W; ++v) {
+            sum += red[(v * 32 + r) * 2];
+            sq += red[(v * 32 + r) * 2 + 1];
+        }
         const float mean = sum * invH;
         const float var = fmaxf(sq * invH - mean * mean, 0.f);
         const float rstd = rsqrtf(var + 1e-6f);
         const float* gm = gb + l * 2 * H;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+        for (int i = 0; i < NBW; ++i) {
+            const int nb = w * NBW + i;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int f0 = nb * 32 + 8 * g + 4 * h;
@@ -140,63 +194,89 @@ __global__ __launch_bounds__(64 * kPolicyWaves) void policy_step_kernel(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int q = 4 * g + j;
-                    acc[nb][q] = fmaxf(rnd<T>((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j]), 0.f);
+                    acc[i][q] = rnd<T>(fmaxf((acc[i][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
                 }
             }
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-            for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
+        }
         if (l + 1 == L) break;
-        zero_acc<NB>(acc);
-        gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.wt[l + 1], lane);
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int t = 0; t < SPB; ++t)
+                fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
+        zero_acc<NBW>(acc);
+        gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
+                                  (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);
     }
 
-    // actor + critic heads: lg[row][j] = rnd(rnd(a . W) + rnd(b)) (dists.py:22)
+    // actor + critic heads over this wave's features, partials summed in wave
+    // order: lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22)
     {
+        frag hb[NBW * SPB];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = RT<T>::from_acc(acc[i], t);
         f32x16 ha[1];
         zero_acc<1>(ha);
-        gemm_rb<T, 1, KSH, 8>(ha, bf, (const T*)P.head_t, lane);
+        gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int j = feat(0, q, h);
-            lg[r * 33 + j] = rnd<T>(rnd<T>(ha[0][q]) + rnd<T>(hbias[j]));
-        }
+        for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * 33 + feat(0, q, h)] = ha[0][q];
     }
-    wave_lds_sync();
+    __syncthreads();
+    for (int i = tid; i < 32 * MLEARN_HEAD_COLS; i += THREADS) {
+        const int rr = i >> 5, j = i & 31;
+        float x = lgp[rr * 33 + j];
+#pragma unroll
+        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * 33 + j];
+        lg[rr * 33 + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+    }
+    __syncthreads();
 
-    // sample: lane half h takes the action groups g = h, h + 2, ...
-    if (live) {
-        const float* lr = lg + r * 33;
-        if (actions) {
-            for (int g = h; g < P.K; g += 2) {
-                int a;
-                float lp;
-                sample_group(lr + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
-                             eoff + (uint32_t)row, step, sample, &a, &lp);
-                actions[row * P.K + g] = a;
-                if (logp) logp[row * P.K + g] = lp;
-            }
+    // sample + store: one (env, group) task per thread
+    if (actions) {
+        for (int task = tid; task < 32 * P.K; task += THREADS) {
+            const int rr = task / P.K, g = task - rr * P.K;
+            const int64_t n = row0 + rr;
+            if (n >= N) continue;
+            int a;
+            float lp;
+            sample_group(lg + rr * 33 + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
+                         eoff + (uint32_t)n, step, sample, &a, &lp);
+            actions[n * P.K + g] = a;
+            if (logp) logp[n * P.K + g] = lp;
         }
-        if (values && h == 0) values[row] = lr[P.A];
     }
+    if (values && tid < 32 && row0 + tid < N) values[row0 + tid] = lg[tid * 33 + P.A];
 }
 
-static size_t policy_step_lds(int L, int H) {
-    return (size_t)(L * 2 * H + MLEARN_HEAD_COLS) * 4 + (size_t)kPolicyWaves * 32 * 33 * 4;
+template <typename T, int H> static size_t policy_step_lds(int L) {
+    typedef PolCfg<H> C;
+    return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
+           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33) * 4;
 }
 
 template <typename T, int H>
 static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, void* obs_store,
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
-                              hipStream_t s) {
-    const size_t lds = policy_step_lds(P.L, H);
-    const int64_t tiles = (N + 31) / 32;
-    const int grid = (int)((tiles + kPolicyWaves - 1) / kPolicyWaves);
-    hipLaunchKernelGGL((policy_step_kernel<T, H>), dim3(grid), dim3(64 * kPolicyWaves), lds, s, P,
-                       obs, N, (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff,
-                       sample);
+                              const PostK& post, hipStream_t s) {
+    const size_t lds = policy_step_lds<T, H>(P.L);
+    auto kern = policy_step_kernel<T, H>;
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        attr_set = true;
+    }
+    const int grid = (int)((N + 31) / 32);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
+                       (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
+                       post);
     return check_launch("policy_rollout_step");
 }
 
@@ -209,7 +289,7 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
                                           float* log_probs, float* values, uint32_t k0,
                                           uint32_t k1, const uint64_t* step_ctr, uint64_t step,
                                           uint32_t env_offset, int32_t sample,
-                                          mlearn_stream_t stream) {
+                                          const mlearn_post_step* post, mlearn_stream_t stream) {
     int rc = validate_policy(policy);
     if (rc) return rc;
     ML_REQUIRE(N >= 0, "policy_rollout_step: N < 0");
@@ -220,16 +300,24 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
     ML_REQUIRE((uintptr_t)obs % 16 == 0, "policy_rollout_step: obs must be 16-byte aligned");
     ML_REQUIRE(!obs_store || (uintptr_t)obs_store % 16 == 0,
                "policy_rollout_step: obs_store must be 16-byte aligned");
+    PostK pk{};
+    if (post) {
+        ML_REQUIRE(post->rewards && post->dones && post->store_rewards && post->store_dones &&
+                       post->env_returns,
+                   "policy_rollout_step: null post-step pointer");
+        pk = PostK{post->rewards, post->dones, post->store_rewards, post->store_dones,
+                   post->env_returns, post->env_returns_trace, post->gamma};
+    }
     PolicyK P = make_policy_k(*policy);
     hipStream_t s = S(stream);
 #define ML_DISPATCH(T)                                                                              \
     switch (policy->hidden) {                                                                      \
         case 64: return launch_policy_step<T, 64>(P, obs, N, obs_store, actions, log_probs, values, \
-                                                  k0, k1, step_ctr, step, env_offset, sample, s);            \
+                                                  k0, k1, step_ctr, step, env_offset, sample, pk, s);            \
         case 128: return launch_policy_step<T, 128>(P, obs, N, obs_store, actions, log_probs,      \
-                                                    values, k0, k1, step_ctr, step, env_offset, sample, s);  \
+                                                    values, k0, k1, step_ctr, step, env_offset, sample, pk, s);  \
         default: return launch_policy_step<T, 256>(P, obs, N, obs_store, actions, log_probs,       \
-                                                   values, k0, k1, step_ctr, step, env_offset, sample, s);   \
+                                                   values, k0, k1, step_ctr, step, env_offset, sample, pk, s);   \
     }
     if (policy->dtype == MLEARN_DTYPE_BF16) {
         ML_DISPATCH(bf16)

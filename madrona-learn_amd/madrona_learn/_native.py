@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -41,6 +41,12 @@ class MlpPolicy(Structure):
 
 class MetricJob(Structure):
     _fields_ = [("x", c_void_p), ("n", c_int64), ("abs_value", c_int32), ("pad", c_int32)]
+
+
+class PostStep(Structure):
+    _fields_ = [("rewards", c_void_p), ("dones", c_void_p), ("store_rewards", c_void_p),
+                ("store_dones", c_void_p), ("env_returns", c_void_p),
+                ("env_returns_trace", c_void_p), ("gamma", c_float)]
 
 
 class RolloutView(Structure):
@@ -83,7 +89,7 @@ _SIGNATURES = {
     "mlearn_action_stats_f32": (c_int32, [_P, c_int64, ActionLayout, c_int64, _P, _P, _P, _S]),
     "mlearn_policy_rollout_step": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P,
                                              c_uint32, c_uint32, _P, c_uint64, c_uint32, c_int32,
-                                             _S]),
+                                             POINTER(PostStep), _S]),
     "mlearn_rollout_post_step": (c_int32, [_P, _P, c_int64, _P, _P, _P, _P, c_float, _S]),
     "mlearn_metrics_workspace_bytes": (c_int64, [c_int32]),
     "mlearn_metrics_f32": (c_int32, [POINTER(MetricJob), c_int32, _P, _P, _S]),

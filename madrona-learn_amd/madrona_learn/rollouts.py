@@ -218,6 +218,22 @@ class RolloutManager:  # rollouts.py:373-826
         x = self.prefix(obs, train=False)
         return obs_to_matrix(x, self.N)
 
+    def _post_desc(self, t, rew, dn, rollout_state, gamma):
+        """Post-step descriptor of env step t (rollouts.py:933-973); the tensors it
+        points at are kept alive until the next collect."""
+        s = self.store
+        if not hasattr(self, "_posts"):
+            self._posts = [nat.PostStep() for _ in range(self.T)]
+            self._post_keep = [None] * self.T
+        p = self._posts[t]
+        p.rewards, p.dones = nat.ptr(rew), nat.ptr(dn)
+        p.store_rewards, p.store_dones = nat.ptr(s.rewards[t]), nat.ptr(s.dones[t])
+        p.env_returns = nat.ptr(rollout_state.env_returns)
+        p.env_returns_trace = nat.ptr(s.env_returns_trace[t])
+        p.gamma = gamma
+        self._post_keep[t] = (rew, dn)
+        return p
+
     def collect(self, train_state_mgr, rollout_state: RolloutState, metrics, user_hooks):
         """rollouts.py:501-577 restated on the fused kernels."""
         ps = self.policy_state
@@ -229,10 +245,11 @@ class RolloutManager:  # rollouts.py:373-826
             rollout_state, train_state_mgr.user_state)
         key = rollout_state.prng_key
         step_ctr = rollout_state.counters[0:1]
+        post = None  # post-step of env step t-1, fused into the policy launch of step t
         for t in range(self.T):
             obs = self.prep_obs(rollout_state.cur_obs)
             ps.rollout_step(obs, s.obs[t], s.actions[t], s.log_probs[t], s.values[t], key,
-                            step_ctr, t, self.env_offset, sample=True)
+                            step_ctr, t, self.env_offset, sample=True, post=post)
             step_input = {
                 "state": rollout_state.sim_state,
                 "actions": s.actions[t],
@@ -246,14 +263,11 @@ class RolloutManager:  # rollouts.py:373-826
                 rew = rew.float()
             dn = out["dones"].reshape(-1)
             dn = dn.view(torch.uint8) if dn.dtype == torch.bool else (dn != 0).view(torch.uint8)
-            nat.check(L.mlearn_rollout_post_step(
-                nat.ptr(rew.contiguous()), nat.ptr(dn.contiguous()), self.N, nat.ptr(s.rewards[t]),
-                nat.ptr(s.dones[t]), nat.ptr(rollout_state.env_returns),
-                nat.ptr(s.env_returns_trace[t]), gamma, strm), "post_step")
+            post = self._post_desc(t, rew.contiguous(), dn.contiguous(), rollout_state, gamma)
             rollout_state.sim_state = out["state"]
             rollout_state.cur_obs = out["obs"]
-        # bootstrap values (rollouts.py:607-635)
-        ps.critic_only(self.prep_obs(rollout_state.cur_obs), s.bootstrap)
+        # bootstrap values (rollouts.py:607-635), with the last post-step
+        ps.critic_only(self.prep_obs(rollout_state.cur_obs), s.bootstrap, post=post)
         rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:

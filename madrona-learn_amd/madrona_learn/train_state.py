@@ -175,21 +175,22 @@ class PolicyState:
 
     # -- kernels ------------------------------------------------------------
     def rollout_step(self, obs, obs_store, actions, log_probs, values, key, step_ctr, step,
-                     env_offset=0, sample=True):
-        """ActorCritic.rollout + store (actor_critic.py:74-96, rollouts.py:637-668)."""
+                     env_offset=0, sample=True, post=None):
+        """ActorCritic.rollout + store (actor_critic.py:74-96, rollouts.py:637-668);
+        post: optional nat.PostStep of the previous env step."""
         N = obs.shape[0]
         nat.check(nat.lib().mlearn_policy_rollout_step(
             self.desc, nat.ptr(obs, torch.float32, name="obs"), N, nat.ptr(obs_store),
             nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values), key[0], key[1],
-            nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, nat.stream_handle()),
-            "policy_rollout_step")
+            nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post,
+            nat.stream_handle()), "policy_rollout_step")
 
-    def critic_only(self, obs, values):
+    def critic_only(self, obs, values, post=None):
         """ActorCritic.critic_only (actor_critic.py:65-72)."""
         N = obs.shape[0]
         nat.check(nat.lib().mlearn_policy_rollout_step(
             self.desc, nat.ptr(obs, torch.float32, name="obs"), N, None, None, None,
-            nat.ptr(values), 0, 0, None, 0, 0, 0, nat.stream_handle()), "critic_only")
+            nat.ptr(values), 0, 0, None, 0, 0, 0, post, nat.stream_handle()), "critic_only")
 
     def state_dict(self):
         return {"params": self.params.detach().cpu()}

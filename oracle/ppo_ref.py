@@ -378,13 +378,33 @@ def grads_to_flat(G, lay):
 # ---------------------------------------------------------------------------
 # minibatching (ppo.py:437-482, rollouts.py:319-329)
 # ---------------------------------------------------------------------------
+def _feistel4(x, half, k0, k1, rank, epoch):
+    mask = np.uint32((1 << half) - 1)
+    L, R = x >> np.uint32(half), x & mask
+    for rd in range(4):
+        ctr = np.stack([R + np.uint32(rd << 24), np.full(len(R), rank, np.uint32),
+                        np.full(len(R), epoch & 0xFFFFFFFF, np.uint32),
+                        np.full(len(R), epoch >> 32, np.uint32)], -1)
+        f = native.philox(ctr, k0, k1)[:, 0]
+        L, R = R, L ^ (f & mask)
+    return (L << np.uint32(half)) | R
+
+
 def epoch_permutation(k0, k1, epoch, rank, n):
-    """random.permutation restated on Philox keys (see DESIGN.md RNG)."""
-    i = np.arange(n, dtype=np.uint32)
-    ctr = np.stack([i, np.full(n, rank, np.uint32), np.full(n, epoch & 0xFFFFFFFF, np.uint32),
-                    np.full(n, epoch >> 32, np.uint32)], -1)
-    keys = native.philox(ctr, k0, k1)[:, 0]
-    return np.lexsort((i, keys)).astype(np.int32)
+    """random.permutation restated as a keyed bijection (see DESIGN.md RNG):
+    4-round balanced Feistel network on [0, 2^b) with Philox round functions,
+    restricted to [0, n) by cycle walking (misc.hip perm_kernel)."""
+    b = 2
+    while (1 << b) < n:
+        b += 1
+    b += b & 1
+    x = np.arange(n, dtype=np.uint32)
+    x = _feistel4(x, b // 2, k0, k1, rank, epoch)
+    out = x >= n
+    while out.any():
+        x[out] = _feistel4(x[out], b // 2, k0, k1, rank, epoch)
+        out = x >= n
+    return x.astype(np.int32)
 
 
 def minibatch_rows(seq_ids, N, bptt):

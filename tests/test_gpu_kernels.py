@@ -137,7 +137,7 @@ def test_action_stats(gpu):
     np.testing.assert_allclose(ent.cpu().numpy(), eent, rtol=1e-5, atol=2e-6)
 
 
-@pytest.mark.parametrize("n", [1, 16, 1000, 8192, 16384])
+@pytest.mark.parametrize("n", [1, 16, 1000, 8192, 16384, 100003])
 def test_minibatch_perm_bitexact(gpu, n):
     nat = _nat()
     out = torch.empty(n, dtype=torch.int32, device=gpu)
