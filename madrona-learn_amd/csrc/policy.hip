@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     constexpr int KSD = 256 / KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, L = P.L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the buffer descriptors
     frag* fr = (frag*)smem;                               // [KSH][64] B fragments
     float* gb = (float*)(fr + KSH * 64);                  // [L][2][H]
     float* hbias = gb + L * 2 * H;                        // [32]

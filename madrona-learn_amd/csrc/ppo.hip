@@ -268,38 +268,29 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, floa
     m.mxerr = fmaxf(m.mxerr, verr);
 }
 
-// Wave reduction of the lane metrics into the tile's kLossSlots doubles.
-__device__ inline void store_loss_partials(const LossAcc& m, double* out, int lane) {
-    const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
-                                    m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
-                                    m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < kLossSlots; ++s) {
-        const int kind = (s < 16) ? (s & 3) : 0;
-        float v = vals[s];
-        v = kind == 2 ? half_reduce<2>(v) : (kind == 3 ? half_reduce<3>(v) : half_reduce<0>(v));
-        const float u = __shfl_xor(v, 32);
-        v = kind == 2 ? fminf(v, u) : (kind == 3 ? fmaxf(v, u) : v + u);
-        if (lane == 0) out[s] = (double)v;
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Fused minibatch step: one wave per 32 rows.
-// LDS: shared [L][2][H] LayerNorm scale/bias + [32] head bias; per wave the
-// Dense outputs z_l (lane-private, [L][H/32][CH][64] x 16 B) and the logits /
-// d logits tile lg[32][33] f32.
+// Fused minibatch step: one workgroup per 32 rows; its W waves split the
+// hidden features (wave w owns blocks w*NBW .. w*NBW+NBW-1 of every layer).
+// Per layer the waves run their MFMAs over the full input (B fragments from
+// LDS), combine LayerNorm row statistics through LDS, and exchange
+// post-activation (forward) or dZ (backward) fragments through LDS.  Each
+// wave keeps its own Dense outputs in registers for the backward pass.
+// LDS: B fragments [KSH][64], LayerNorm scale/bias [L][2][H], head bias, row
+// statistics [W][32][2], head partials [W][32][33], logits / d logits
+// [32][33], loss partials [W][kLossSlots].
 // ---------------------------------------------------------------------------
-template <typename T, int H, int L> struct StepLds {
-    static constexpr size_t shared = (size_t)(L * 2 * H + MLEARN_HEAD_COLS) * 4;
-    static constexpr size_t z = (size_t)L * 32 * H * sizeof(T);
-    static constexpr size_t wave = z + 32 * 33 * 4;
-    static int waves() {
-        for (int w = 4; w > 1; w >>= 1)
-            if (shared + w * wave <= 160 * 1024) return w;
-        return 1;
-    }
+template <int H> struct StepCfg {
+    static constexpr int NB = H / 32;
+    static constexpr int W = NB < 4 ? NB : 4;
+    static constexpr int NBW = NB / W;
 };
+
+template <typename T, int H, int L> static size_t step_lds() {
+    typedef StepCfg<H> C;
+    return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
+           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33 +
+                    C::W * kLossSlots) * 4;
+}
 
 // ReLU' threshold: rnd<T>(y) > 0  <=>  y > THR (bf16 round-to-nearest-even
 // sends y <= 2^-134 to zero).
@@ -307,24 +298,39 @@ template <typename T> __device__ inline float relu_thr();
 template <> __device__ inline float relu_thr<float>() { return 0.f; }
 template <> __device__ inline float relu_thr<bf16>() { return __builtin_bit_cast(float, 0x00008000u); }
 
+__device__ inline float frag_elem(const bf16x8& f, int e) { return (float)f[e]; }
+__device__ inline float frag_elem(float f, int) { return f; }
+
+// Store row of minibatch row f.
+__device__ inline int64_t store_row(const RolloutK& ro, const int32_t* mb_seq, int mb, int64_t f) {
+    const int tl = (int)(f / mb);
+    const int m = (int)(f - (int64_t)tl * mb);
+    const int64_t seq = mb_seq[m];
+    const int64_t c = seq / ro.N, b = seq - c * ro.N;
+    return (c * ro.bptt + tl) * ro.N + b;
+}
+
 template <typename T, int H, int L>
-__global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
-                                                       const int32_t* __restrict__ mb_seq, int mb,
-                                                       int64_t M, const float* __restrict__ adv_st,
-                                                       HpK hp, WsK ws) {
+__global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
+    PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
+    const float* __restrict__ adv_st, HpK hp, WsK ws) {
     typedef typename RT<T>::frag frag;
-    typedef ZIO<T> Z;
-    typedef typename Z::u4 u4;
-    constexpr int NB = H / 32, KS = RT<T>::KS, SPB = RT<T>::SPB;
-    constexpr int KSH = H / KS, KSHD = MLEARN_HEAD_COLS / KS, CH = Z::CH;
-    constexpr int KSD = 256 / KS;  // max k-steps over the observation
-    typedef StepLds<T, H, L> LDS;
+    typedef StepCfg<H> C;
+    constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
+    constexpr int E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB;
+    constexpr int KSH = H / KS, KSHD = MLEARN_HEAD_COLS / KS, KSD = 256 / KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, K = P.K;
-    float* gb = (float*)smem;         // [L][2][H]
-    float* hbias = gb + L * 2 * H;    // [32]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += blockDim.x) {
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the buffer descriptors
+    frag* fr = (frag*)smem;                    // [KSH][64]
+    float* gb = (float*)(fr + KSH * 64);       // [L][2][H]
+    float* hbias = gb + L * 2 * H;             // [32]
+    float* red = hbias + MLEARN_HEAD_COLS;     // [W][32][2]
+    float* lgp = red + W * 64;                 // [W][32][33]
+    float* lg = lgp + W * 32 * 33;             // [32][33]
+    float* lred = lg + 32 * 33;                // [W][kLossSlots]
+    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += THREADS) {
         float v;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
@@ -334,23 +340,29 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         }
         gb[i] = v;
     }
-    __syncthreads();
-    char* wb = smem + LDS::shared + (size_t)w * LDS::wave;
-    u4* zb = (u4*)wb;                    // [L][NB][CH][64]
-    float* lg = (float*)(wb + LDS::z);   // [32][33]
-    const int tile = blockIdx.x * (blockDim.x >> 6) + w;
-    if (tile >= ws.ntiles) return;
-    const int64_t row = (int64_t)tile * 32 + r;
+    const int tile = blockIdx.x;
+    const int64_t row0 = (int64_t)tile * 32;
+    const int64_t row = row0 + r;
     const bool live = row < M;
-    int64_t sr = 0;
-    if (live) {
-        const int tl = (int)(row / mb);
-        const int m = (int)(row - (int64_t)tl * mb);
-        const int64_t seq = mb_seq[m];
-        const int64_t c = seq / ro.N, b = seq - c * ro.N;
-        sr = (c * ro.bptt + tl) * ro.N + b;
+    const int64_t sr = live ? store_row(ro, mb_seq, mb, row) : 0;
+    // first loss task of this thread: row tr, task tg (group, or value if tg == K)
+    const int tr = tid & 31, tg = tid >> 5;
+    const bool tlive = row0 + tr < M && tg <= K;
+    const int64_t tsr = tlive ? store_row(ro, mb_seq, mb, row0 + tr) : 0;
+    int t_act = 0;
+    float t_lp = 0.f, t_adv = 0.f, t_ret = 0.f, t_val = 0.f;
+    if (tlive) {
+        t_adv = ro.adv[tsr];
+        if (tg < K) {
+            t_act = ro.actions[tsr * K + tg];
+            t_lp = ro.logp[tsr * K + tg];
+        } else {
+            t_ret = ro.ret[tsr];
+            if (ro.values) t_val = ro.values[tsr];
+        }
     }
-    // observation fragments (natural k order), all in flight at once
+
+    // ---- forward ----
     const int nks0 = D / KS;
     frag ob[KSD];
     {
@@ -358,60 +370,56 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
 #pragma unroll
         for (int s = 0; s < KSD; ++s)
             if (s < nks0) ob[s] = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
-    }
-    // loss inputs of the first four tasks of this lane (groups h, h+2, ...)
-    int pa[4];
-    float pl[4];
+        if (w == 0) {
+            T* xrow = (T*)ws.x0 + row * D;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int g = h + 2 * i;
-        const bool ok = live && g < K;
-        pa[i] = ok ? ro.actions[sr * K + g] : 0;
-        pl[i] = ok ? ro.logp[sr * K + g] : 0.f;
+            for (int s = 0; s < KSD; ++s)
+                if (s < nks0) RT<T>::put_row(xrow, s, h, ob[s]);
+        }
     }
-    float adv = 0.f, ret = 0.f, oval = 0.f;
-    if (live) {
-        adv = ro.adv[sr];
-        ret = ro.ret[sr];
-        if (ro.values) oval = ro.values[sr];
-    }
-    STAMP(0);
-    {
-        T* xrow = (T*)ws.x0 + row * D;
-#pragma unroll
-        for (int s = 0; s < KSD; ++s)
-            if (s < nks0) RT<T>::put_row(xrow, s, h, ob[s]);
-    }
-
-    // ---- forward ----
-    f32x16 acc[NB];
-    zero_acc<NB>(acc);
-    gemm_ring<T, NB, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0], lane);
-    STAMP(1);
+    f32x16 acc[NBW];
+    zero_acc<NBW>(acc);
+    gemm_ring<T, NBW, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0] + (int64_t)w * NBW * nks0 * 64 * E,
+                              lane);
+    __syncthreads();  // LayerNorm parameters staged
     frag bf[KSH];
+    frag zr[L][NBW * SPB];  // this wave's Dense outputs (exact in the compute dtype)
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
         if (l > 0) {
-            zero_acc<NB>(acc);
-            gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.wt[l], lane);
-            STAMP(2 * l + 1);
+            zero_acc<NBW>(acc);
+            gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
+                                      (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E, lane);
         }
         float sum = 0.f, sq = 0.f;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
+        for (int i = 0; i < NBW; ++i) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const float x = rnd<T>(acc[nb][q]);  // Dense output in the compute dtype
-                acc[nb][q] = x;
+                const float x = rnd<T>(acc[i][q]);  // Dense output in the compute dtype
+                acc[i][q] = x;
                 sum += x;
                 sq += x * x;
             }
-            Z::put(zb + (l * NB + nb) * CH * 64, lane, acc[nb]);
+#pragma unroll
+            for (int t = 0; t < SPB; ++t) zr[l][i * SPB + t] = RT<T>::from_acc(acc[i], t);
         }
         sum = sum_halves(sum);
         sq = sum_halves(sq);
+        if (h == 0) {
+            red[(w * 32 + r) * 2] = sum;
+            red[(w * 32 + r) * 2 + 1] = sq;
+        }
+        __syncthreads();
+        sum = red[r * 2];
+        sq = red[r * 2 + 1];
+#pragma unroll
+        for (int v = 1; v < W; ++v) {
+            sum += red[(v * 32 + r) * 2];
+            sq += red[(v * 32 + r) * 2 + 1];
+        }
         const float mean = sum * invH;
         const float var = fmaxf(sq * invH - mean * mean, 0.f);
         const float rstd = rsqrtf(var + 1e-6f);
@@ -420,7 +428,8 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         const float* gm = gb + l * 2 * H;
         T* arow = (T*)ws.a[l] + row * H;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+        for (int i = 0; i < NBW; ++i) {
+            const int nb = w * NBW + i;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int f0 = nb * 32 + 8 * g + 4 * h;
@@ -430,63 +439,108 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
                 for (int j = 0; j < 4; ++j) {
                     const int q = 4 * g + j;
                     // LayerNorm (x - mean) * (rstd * scale) + bias, ReLU, compute dtype
-                    acc[nb][q] = rnd<T>(fmaxf((acc[nb][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
+                    acc[i][q] = rnd<T>(fmaxf((acc[i][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
                 }
-                store4(arow + f0, acc[nb][4 * g], acc[nb][4 * g + 1], acc[nb][4 * g + 2],
-                       acc[nb][4 * g + 3]);
+                store4(arow + f0, acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2],
+                       acc[i][4 * g + 3]);
             }
+        }
+        if (l + 1 < L) {
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+            for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
-        STAMP(2 * l + 2);
+                for (int t = 0; t < SPB; ++t)
+                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
+        }
     }
+    // heads over this wave's features; partials summed in wave order:
+    // lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22, models.py:154)
     {
+        frag hb[NBW * SPB];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = RT<T>::from_acc(acc[i], t);
         f32x16 ha[1];
         zero_acc<1>(ha);
-        gemm_rb<T, 1, KSH, 8>(ha, bf, (const T*)P.head_t, lane);
+        gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int j = feat(0, q, h);
-            lg[r * 33 + j] = rnd<T>(rnd<T>(ha[0][q]) + rnd<T>(hbias[j]));
-        }
+        for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * 33 + feat(0, q, h)] = ha[0][q];
     }
-    wave_lds_sync();
-    STAMP(2 * L + 1);
+    __syncthreads();
+    for (int i = tid; i < 32 * MLEARN_HEAD_COLS; i += THREADS) {
+        const int rr = i >> 5, j = i & 31;
+        float x = lgp[rr * 33 + j];
+#pragma unroll
+        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * 33 + j];
+        lg[rr * 33 + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+    }
+    __syncthreads();
 
-    // ---- loss: lane half h takes tasks h, h + 2, ... (task K = value) ----
+    // ---- loss: one (row, group | value) task per thread (ppo.py:129-262) ----
     {
-        if (hp.norm_adv) adv = (adv - adv_st[0]) * adv_st[1];
         LossAcc m;
-        float* lr = lg + r * 33;
-        if (live) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int g = h + 2 * i;
+        const float as0 = adv_st[0], as1 = adv_st[1];
+        for (int task = tid; task < 32 * (K + 1); task += THREADS) {
+            const int rr = task & 31, g = task >> 5;
+            float* lr = lg + rr * 33;
+            const int64_t f = row0 + rr;
+            if (f >= M) {  // padding row: zero its d logits
                 if (g < K)
-                    loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], pa[i], pl[i], adv,
-                               hp.ecoef[g], m);
-                else if (g == K)
-                    loss_value(hp, lr, P.A, ret, oval, m);
-            }
-            for (int g = h + 8; g <= K; g += 2) {
-                if (g < K)
-                    loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], ro.actions[sr * K + g],
-                               ro.logp[sr * K + g], adv, hp.ecoef[g], m);
+                    for (int j = P.off[g]; j < P.off[g + 1]; ++j) lr[j] = 0.f;
                 else
-                    loss_value(hp, lr, P.A, ret, oval, m);
+                    for (int j = P.A; j < MLEARN_HEAD_COLS; ++j) lr[j] = 0.f;
+                continue;
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) lr[16 * h + j] = 0.f;
+            int act;
+            float olp, adv, ret, oval;
+            if (task == tid) {
+                act = t_act, olp = t_lp, adv = t_adv, ret = t_ret, oval = t_val;
+            } else {
+                const int64_t q = store_row(ro, mb_seq, mb, f);
+                adv = ro.adv[q];
+                act = g < K ? ro.actions[q * K + g] : 0;
+                olp = g < K ? ro.logp[q * K + g] : 0.f;
+                ret = g < K ? 0.f : ro.ret[q];
+                oval = (g < K || !ro.values) ? 0.f : ro.values[q];
+            }
+            if (g < K) {
+                if (hp.norm_adv) adv = (adv - as0) * as1;
+                loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], act, olp, adv, hp.ecoef[g],
+                           m);
+            } else {
+                loss_value(hp, lr, P.A, ret, oval, m);
+            }
         }
-        store_loss_partials(m, ws.loss_part + (int64_t)tile * kLossSlots, lane);
+        const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
+                                        m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
+                                        m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < kLossSlots; ++s) {
+            const int kind = (s < 16) ? (s & 3) : 0;
+            float v = vals[s];
+            v = kind == 2 ? half_reduce<2>(v) : (kind == 3 ? half_reduce<3>(v) : half_reduce<0>(v));
+            const float u = __shfl_xor(v, 32);
+            v = kind == 2 ? fminf(v, u) : (kind == 3 ? fmaxf(v, u) : v + u);
+            if (lane == 0) lred[w * kLossSlots + s] = v;
+        }
     }
-    wave_lds_sync();
-    STAMP(2 * L + 2);
-
+    __syncthreads();
+    if (tid < kLossSlots) {
+        const int kind = (tid < 16) ? (tid & 3) : 0;
+        double v = lred[tid];
+        for (int u = 1; u < W; ++u) {
+            const double x = lred[u * kLossSlots + tid];
+            v = kind == 2 ? fmin(v, x) : (kind == 3 ? fmax(v, x) : v + x);
+        }
+        ws.loss_part[(int64_t)tile * kLossSlots + tid] = v;
+    }
     // d head: row-major store (wgrad operand) and the head-bias column partial
-    {
+    if (w == 0) {
         const float* lr = lg + r * 33 + 16 * h;
         T* drow = (T*)ws.dhead + row * MLEARN_HEAD_COLS + 16 * h;
 #pragma unroll
@@ -503,11 +557,11 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         frag db[KSHD];
 #pragma unroll
         for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * 33, s, h);
-        zero_acc<NB>(acc);
-        // dA_{L-1}^T = Head . dHead^T
-        gemm_rb<T, NB, KSHD, 2>(acc, db, (const T*)P.head, lane);
+        zero_acc<NBW>(acc);
+        // dA_{L-1}^T = Head . dHead^T  (this wave's feature blocks)
+        gemm_ring<T, NBW, KSHD, 2>(acc, db, KSHD,
+                                   (const T*)P.head + (int64_t)w * NBW * KSHD * 64 * E, lane);
     }
-    STAMP(2 * L + 3);
     const int qs = col_sum16_index(lane);
     const float thr = relu_thr<T>();
 #pragma unroll
@@ -517,9 +571,9 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
         float* cp = ws.colpart + (int64_t)tile * ws.CP + l * 2 * H;
         float su = 0.f, sv = 0.f;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-            float z[16], pg[16], pb[16];
-            Z::get(zb + (l * NB + nb) * CH * 64, lane, z);
+        for (int i = 0; i < NBW; ++i) {
+            const int nb = w * NBW + i;
+            float pg[16], pb[16];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int f0 = nb * 32 + 8 * g + 4 * h;
@@ -528,14 +582,15 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int q = 4 * g + j;
-                    const float zc = z[q] - mean;
+                    const float z = frag_elem(zr[l][i * SPB + q / E], q % E);
+                    const float zc = z - mean;
                     const float xh = zc * rstd;
                     const float y = zc * (rstd * gg[j]) + bb[j];
-                    const float da = acc[nb][q];
+                    const float da = acc[i][q];
                     const bool on = (y > thr) & live;  // ReLU'
                     const float dy = on ? da : 0.f;
                     const float u = dy * gg[j];
-                    acc[nb][q] = u;
+                    acc[i][q] = u;
                     su += u;
                     sv += u * xh;
                     pg[q] = dy * xh;
@@ -543,41 +598,57 @@ __global__ __launch_bounds__(256) void ppo_step_kernel(PolicyK P, RolloutK ro,
                 }
             }
             // LayerNorm scale/bias partials: column sums over the tile's rows
-            const float tg = col_sum16(pg, lane);
-            const float tb = col_sum16(pb, lane);
+            const float tgs = col_sum16(pg, lane);
+            const float tbs = col_sum16(pb, lane);
             if ((lane & 16) == 0) {
                 const int f = feat(nb, qs, h);
-                cp[f] = tb;
-                cp[H + f] = tg;
+                cp[f] = tbs;
+                cp[H + f] = tgs;
             }
         }
         su = sum_halves(su);
         sv = sum_halves(sv);
-        // dZ = rstd * (u - mean(u) - xh * mean(u xh)) = rstd * u + (-rstd^2 mean(u xh)) zc - rstd mean(u)
+        if (h == 0) {
+            red[(w * 32 + r) * 2] = su;
+            red[(w * 32 + r) * 2 + 1] = sv;
+        }
+        __syncthreads();
+        su = red[r * 2];
+        sv = red[r * 2 + 1];
+#pragma unroll
+        for (int v = 1; v < W; ++v) {
+            su += red[(v * 32 + r) * 2];
+            sv += red[(v * 32 + r) * 2 + 1];
+        }
+        // dZ = rstd (u - mean(u) - xh mean(u xh)) = rstd u + (-rstd^2 mean(u xh)) zc - rstd mean(u)
         const float ca = -(rstd * rstd) * (sv * invH), cb = -rstd * (su * invH);
         T* dzrow = (T*)ws.dz[l] + row * H;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-            float z[16];
-            Z::get(zb + (l * NB + nb) * CH * 64, lane, z);
+        for (int i = 0; i < NBW; ++i) {
+            const int nb = w * NBW + i;
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                acc[nb][q] = rnd<T>(rstd * acc[nb][q] + (ca * (z[q] - mean) + cb));
+            for (int q = 0; q < 16; ++q) {
+                const float z = frag_elem(zr[l][i * SPB + q / E], q % E);
+                acc[i][q] = rnd<T>(rstd * acc[i][q] + (ca * (z - mean) + cb));
+            }
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-                store4(dzrow + nb * 32 + 8 * g + 4 * h, acc[nb][4 * g], acc[nb][4 * g + 1],
-                       acc[nb][4 * g + 2], acc[nb][4 * g + 3]);
+                store4(dzrow + nb * 32 + 8 * g + 4 * h, acc[i][4 * g], acc[i][4 * g + 1],
+                       acc[i][4 * g + 2], acc[i][4 * g + 3]);
         }
-        STAMP(2 * L + 4 + 2 * (L - 1 - l));
         if (l > 0) {
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
+            for (int i = 0; i < NBW; ++i)
 #pragma unroll
-                for (int t = 0; t < SPB; ++t) bf[nb * SPB + t] = RT<T>::from_acc(acc[nb], t);
-            zero_acc<NB>(acc);
-            // dA_{l-1}^T = W_l . dZ_l^T
-            gemm_rb<T, NB, KSH, 2>(acc, bf, (const T*)P.w[l], lane);
-            STAMP(2 * L + 5 + 2 * (L - 1 - l));
+                for (int t = 0; t < SPB; ++t)
+                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
+            zero_acc<NBW>(acc);
+            // dA_{l-1}^T = W_l . dZ_l^T  (this wave's feature blocks)
+            gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
+                                      (const T*)P.w[l] + (int64_t)w * NBW * KSH * 64 * E, lane);
         }
     }
 }
@@ -586,18 +657,17 @@ template <typename T, int H, int L>
 static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                         int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                         hipStream_t s) {
-    typedef StepLds<T, H, L> LDS;
     auto k = ppo_step_kernel<T, H, L>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+                                  128 * 1024);
         attr_set = true;
     }
-    const int wpb = LDS::waves();
-    const size_t lds = LDS::shared + wpb * LDS::wave;
-    hipLaunchKernelGGL(k, dim3((ws.ntiles + wpb - 1) / wpb), dim3(64 * wpb), lds, s, P, R, mb_seq,
-                       mb, M, adv_st, hp, ws);
+    const size_t lds = step_lds<T, H, L>();
+    const int threads = 64 * StepCfg<H>::W;
+    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(threads), lds, s, P, R, mb_seq, mb, M, adv_st, hp,
+                       ws);
 }
 
 // ---------------------------------------------------------------------------
