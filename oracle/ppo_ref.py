@@ -470,11 +470,15 @@ def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs,
 # rollout (rollouts.py:829-978) with the synthetic env
 # ---------------------------------------------------------------------------
 def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99,
-            env_returns=None, ad=np.float64, actions_override=None):
+            env_returns=None, ad=np.float64, actions_override=None, policy_fn=None):
     """rollout_loop restated: per step policy forward + Gumbel-max sample,
     store, env step, env-return bookkeeping; then the bootstrap critic.
     actions_override[t] (e.g. the GPU's actions) drives the env instead of
-    the oracle's own samples (used to replay a GPU trajectory exactly)."""
+    the oracle's own samples (used to replay a GPU trajectory exactly).
+    policy_fn(obs) -> (actions, log_probs, values) replaces the MLP policy
+    (integer fake-policy KAT, tests/test_rollout_kat.py)."""
+    if policy_fn is not None:
+        return _rollout_fake(policy_fn, env, T, gamma, env_returns)
     P = unflatten(flat_p, lay, ad)
     N = env.N
     A = int(sum(buckets))
@@ -504,7 +508,37 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
         store["dones"].append(done)
         er = np.where(done.astype(bool), np.float32(0), er).astype(np.float32)
     _, boot, _ = forward(P, rnd(obs, mode, ad), mode, ad)
+    return _finish_store(store, boot, trace), er
+
+
+def _finish_store(store, boot, trace):
     out = {k: np.stack(v) for k, v in store.items()}
-    out["bootstrap"] = boot.astype(np.float32)
+    out["bootstrap"] = np.asarray(boot).astype(np.float32)
     out["env_returns_trace"] = np.stack(trace)
-    return out, er
+    return out
+
+
+def _rollout_fake(policy_fn, env, T, gamma, env_returns):
+    """Same store / bookkeeping order as rollout() with a pluggable policy
+    (rollouts.py:829-978: infer -> store -> sim step -> done bookkeeping)."""
+    store = {k: [] for k in ("obs", "actions", "log_probs", "values", "rewards", "dones")}
+    er = np.zeros(env.N, np.float32) if env_returns is None else env_returns
+    trace = []
+    obs = env.obs.copy()
+    for t in range(T):
+        acts, logp, V = policy_fn(obs)
+        store["obs"].append(obs.copy())
+        store["actions"].append(acts)
+        store["log_probs"].append(logp)
+        store["values"].append(V)
+        obs, rew, done = env.step(acts)
+        er = (rew + np.float32(gamma) * er).astype(np.float32)
+        trace.append(er.copy())
+        store["rewards"].append(rew)
+        store["dones"].append(done)
+        er = np.where(done.astype(bool), np.float32(0), er).astype(np.float32)
+    _, _, boot = policy_fn(obs)
+    return _finish_store(store, boot, trace), er
+
+
+

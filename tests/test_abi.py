@@ -1,0 +1,82 @@
+"""The C-ABI library (include/mlearn.h) loads without a GPU, exports every
+function the header declares, and rejects bad arguments with MLEARN_EINVAL
+and a message before touching the device (no compute calls here)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mlearn.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(mlearn_[a-z0-9_]+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("mlearn_gae_f32", "mlearn_policy_rollout_step", "mlearn_ppo_minibatch_grad",
+                 "mlearn_optim_step", "mlearn_minibatch_perm", "mlearn_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from madrona_learn import _native as nat
+    lib = nat.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # every bound signature in the Python mirror is a declared function
+    assert set(nat._SIGNATURES) <= set(declared_functions())
+
+
+def test_abi_version():
+    from madrona_learn import _native as nat
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 2
+    hdr = open(HEADER).read()
+    assert f"#define MLEARN_ABI_VERSION {nat.ABI_VERSION}" in hdr
+
+
+def _einval(rc):
+    from madrona_learn import _native as nat
+    assert rc == -1, rc  # MLEARN_EINVAL
+    msg = nat.lib().mlearn_last_error()
+    assert msg and len(msg) > 0
+    return msg.decode()
+
+
+def test_bad_arguments_are_rejected_without_gpu():
+    from madrona_learn import _native as nat
+    L = nat.lib()
+    # GAE with a null pointer
+    msg = _einval(L.mlearn_gae_f32(None, None, None, None, None, None, 32, 64, 0.99, 0.95, None))
+    assert "null" in msg.lower() or "pointer" in msg.lower()
+    # permutation size out of range
+    _einval(L.mlearn_minibatch_perm(1, 2, None, 0, 0, 0, None, None))
+    # bad policy descriptors
+    d = nat.MlpPolicy()
+    d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_F32, 64, 96, 2
+    assert L.mlearn_param_count(ctypes.byref(d)) == -1
+    assert "hidden" in L.mlearn_last_error().decode()
+    d.hidden, d.obs_dim = 256, 20
+    assert L.mlearn_param_count(ctypes.byref(d)) == -1
+    assert "obs_dim" in L.mlearn_last_error().decode()
+
+
+def test_param_count_matches_oracle_layout():
+    from madrona_learn import _native as nat
+    from oracle import ppo_ref as ref
+    d = nat.MlpPolicy()
+    d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_F32, 64, 256, 2
+    d.actions = nat.action_layout([4, 8, 5, 5, 2, 2])
+    for l in range(2):
+        d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
+        d.w[l] = 1
+    d.head_t = d.head = d.head_bias = 1
+    n = nat.lib().mlearn_param_count(ctypes.byref(d))
+    assert n == ref.param_layout(64, 256, 2, 26)["total"] == 89883
