@@ -61,7 +61,8 @@ def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True):
 
 
 def time_call(fn, iters, stream):
-    """Average device time of fn() over iters launches, HIP events on `stream`."""
+    """Average device time of fn() over iters launches, HIP events recorded on
+    `stream` (the stream fn launches on)."""
     with torch.cuda.stream(stream):
         fn()
         start = torch.cuda.Event(enable_timing=True)
@@ -74,16 +75,92 @@ def time_call(fn, iters, stream):
     return start.elapsed_time(end) / iters * 1e-3  # seconds
 
 
+def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
+    """Algorithmic FLOPs per sample: trunk + heads forward, and
+    the backward's dX products (d head -> d A_{L-1}, dZ_l -> dA_{l-1}); the
+    weight gradients (X^T dZ) are the wgrad kernel's."""
+    fwd = 2 * (D * H + (L - 1) * H * H + H * A1)
+    bwd_dx = 2 * (A1 * H + (L - 1) * H * H)
+    wgrad = 2 * (D * H + (L - 1) * H * H + H * A1)
+    return fwd, bwd_dx, wgrad
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_r01.json, tools/pmc_traffic.py): FETCH_SIZE doubled (gfx950
+    reports half the bytes of 16-B streaming reads, MI355X_MICROARCH.md HBM)
+    + WRITE_SIZE.  None when no summary is committed."""
+    path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel_key)
+    return None if k is None else k.get("hbm_bytes_per_launch")
+
+
+def kernel_rooflines(mgr, dev, iters=20):
+    """Dominant kernel (the fused PPO minibatch fwd/loss/bwd step) plus the
+    rollout policy step and GAE, each timed live with HIP events."""
+    from madrona_learn import _native as nat
+    L = nat.lib()
+    algo = mgr.algo
+    ps = mgr.state.policy_states
+    stream = torch.cuda.Stream(device=dev)
+    seqs = algo.perm[0, :algo.mb]
+
+    def step():
+        nat.check(L.mlearn_ppo_minibatch_fwd_bwd(ps.desc, algo.view, nat.ptr(seqs), algo.mb,
+                                                 nat.ptr(algo.adv_stats[0, 0]), algo.hp,
+                                                 nat.ptr(algo.ws), nat.stream_handle(stream)))
+
+    t_step = time_call(step, iters, stream)
+    M = algo.mb * algo.bptt
+    fwd, bwd, _ = flop_per_sample()
+    step_flop = (fwd + bwd) * M
+    achieved = step_flop / t_step / 1e12
+    roof = {
+        "kernel": "ppo_step_kernel<bf16,256,2> (mlearn_ppo_minibatch_fwd_bwd)",
+        "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
+        "frac": achieved / BF16_PEAK_TFS, "traffic": pmc_traffic("ppo_step"),
+        "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
+        "units_per_launch": M, "flop_per_unit": fwd + bwd,
+    }
+
+    # rollout policy step (forward + sample), N = 8192 envs
+    s = mgr.rollout_mgr.store
+    obs = torch.randn((N_ENVS, OBS), device=dev)
+    ctr = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def pol():
+        ps.rollout_step(obs, s.obs[0], s.actions[0], s.log_probs[0], s.values[0], (1, 2),
+                        ctr[0:1], 0)
+
+    t_pol = time_call(pol, iters, torch.cuda.current_stream())
+    pol_flop = fwd * N_ENVS
+    extra = {"policy_step": {"bound": "mfma", "avg_launch_us": t_pol * 1e6,
+                             "achieved": pol_flop / t_pol / 1e12, "unit": "TFLOP/s",
+                             "frac": pol_flop / t_pol / 1e12 / BF16_PEAK_TFS}}
+    sec, rd, wr = gae_roofline(dev, N_ENVS)
+    big_sec, big_rd, big_wr = gae_roofline(dev, 1 << 22, iters=20)
+    extra["gae"] = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                    "operating_point": {"N": N_ENVS, "avg_launch_us": sec * 1e6,
+                                        "achieved": (rd + wr) / sec / 1e9},
+                    "sweep_point": {"N": 1 << 22, "avg_launch_us": big_sec * 1e6,
+                                    "achieved": (big_rd + big_wr) / big_sec / 1e9,
+                                    "frac": (big_rd + big_wr) / big_sec / 1e9 / HBM_PEAK_GBS}}
+    return roof, extra
+
+
 def gae_roofline(dev, N, iters=50):
     from madrona_learn import _native as nat
-    rng = torch.Generator(device=dev)
     r = torch.randn((T, N), device=dev)
     v = torch.randn((T, N), device=dev)
     d = (torch.rand((T, N), device=dev) < 0.05).to(torch.uint8)
     b = torch.randn(N, device=dev)
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
-    s = torch.cuda.Stream()
+    s = torch.cuda.Stream(device=dev)
     L = nat.lib()
 
     def call():
@@ -96,14 +173,15 @@ def gae_roofline(dev, N, iters=50):
     return sec, read, write
 
 
-def cpu_baseline(budget_s=25.0):
-    """Oracle restatement (NumPy fp32, host BLAS threads) on a bounded sample:
-    one full PPO iteration (rollout + GAE + 2 epochs x 4 minibatches) at a
-    reduced env count so it stays within ~10-30 s."""
+def cpu_baseline(iters=2):
+    """The oracle restatement (NumPy fp32 arithmetic, host BLAS threads) of
+    `iters` full B1 PPO iterations: 8192 envs x T=32 rollout with the
+    synthetic env, GAE, 2 epochs x 4 minibatches of 2048 sequences (~10-30 s
+    of CPU work on the GPU box's host)."""
     from oracle import native as onat
     from oracle import ppo_ref as ref
-    n_env = 1024
-    mb = MB * n_env // N_ENVS
+    n_env = N_ENVS
+    mb = MB
     lay = ref.param_layout(OBS, HID, LAYERS, sum(BUCKETS))
     rng = np.random.default_rng(0)
     p = np.zeros(lay["total"], np.float32)
@@ -115,22 +193,29 @@ def cpu_baseline(budget_s=25.0):
     p[o:o + shp[0] * shp[1]] = (rng.standard_normal(shp) * 0.01).reshape(-1)
     env = onat.Env(n_env, OBS, 1, 2)
     env.reset()
-    t0 = time.perf_counter()
-    ro, _ = ref.rollout(p, lay, env, T, BUCKETS, (3, 4), 0, mode="f32", ad=np.float32)
-    adv, ret = ref.gae_f32(ro["rewards"], ro["values"], ro["dones"], ro["bootstrap"], 0.99, 0.95)
-    store = dict(ro)
-    store["advantages"], store["returns"] = adv, ret
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01}
-    z = np.zeros(lay["total"])
     norms = np.ones(LAYERS)
-    ref.ppo_update(p.astype(np.float64), (z, z.copy(), 0), [store], hp, BUCKETS, lay, norms,
-                   num_epochs=EPOCHS, minibatch_size=mb, bptt=T, key=(5, 6), epoch_base=0,
-                   mode="f32", lr=3e-4, max_grad_norm=0.5, ad=np.float32)
+    pf = p.astype(np.float64)
+    opt = (np.zeros(lay["total"]), np.zeros(lay["total"]), 0)
+    er = None
+    t0 = time.perf_counter()
+    for it in range(iters):
+        ro, er = ref.rollout(pf.astype(np.float32), lay, env, T, BUCKETS, (3, 4), it * T,
+                             mode="f32", ad=np.float32, env_returns=er)
+        adv, ret = ref.gae_f32(ro["rewards"], ro["values"], ro["dones"], ro["bootstrap"], 0.99,
+                               0.95)
+        store = dict(ro)
+        store["advantages"], store["returns"] = adv, ret
+        pf, opt, _ = ref.ppo_update(pf, opt, [store], hp, BUCKETS, lay, norms,
+                                    num_epochs=EPOCHS, minibatch_size=mb, bptt=T, key=(5, 6),
+                                    epoch_base=it * EPOCHS, mode="f32", lr=3e-4,
+                                    max_grad_norm=0.5, ad=np.float32)
     sec = time.perf_counter() - t0
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": n_env * T / sec, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"1 PPO iteration at {n_env} envs x T={T} (2 epochs x 4 minibatches of "
-                      f"{mb} seqs), NumPy fp32 oracle restatement, {sec:.1f} s"}
+    return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{iters} full B1 PPO iterations ({n_env} envs x T={T}, 2 epochs x 4 "
+                      f"minibatches of {mb} seqs), NumPy fp32 oracle restatement, {sec:.1f} s"}
 
 
 def main():
@@ -192,18 +277,7 @@ def main():
                        "hip_graph": not args.no_graph},
         }
     if rank == 0 and not args.no_roofline:
-        # dominant-kernel roofline candidates, timed live with HIP events
-        sec, rd, wr = gae_roofline(dev, N_ENVS * 1)
-        big_sec, big_rd, big_wr = gae_roofline(dev, 1 << 22, iters=20)
-        result["roofline"] = {
-            "kernel": "gae_kernel (N=2^22 sweep point)", "bound": "hbm",
-            "achieved": big_rd / big_sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": big_rd / big_sec / 1e9 / HBM_PEAK_GBS, "traffic": None,
-            "algorithmic_read_bytes": big_rd, "algorithmic_write_bytes": big_wr,
-            "avg_launch_us": big_sec * 1e6,
-            "operating_point": {"N": N_ENVS, "avg_launch_us": sec * 1e6,
-                                "read_GBs": rd / sec / 1e9},
-        }
+        result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev)
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -246,6 +246,16 @@ int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_roll
                               const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
                               void* workspace, mlearn_stream_t stream);
 
+/* The fused forward / loss / backward stage of mlearn_ppo_minibatch_grad on
+ * its own (one launch): fills the workspace with the weight-gradient
+ * operands and the per-tile partials, no reduction into a gradient.  Used to
+ * time the dominant kernel (bench.py roofline) and by callers that schedule
+ * the reduction themselves. */
+int mlearn_ppo_minibatch_fwd_bwd(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                                 const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                                 const mlearn_ppo_hparams* hp, void* workspace,
+                                 mlearn_stream_t stream);
+
 /* Parameter layout of the flat f32 buffers (params, grads, Adam m/v):
  * per layer l: W_l [in_l][hidden], ln_scale_l [hidden], ln_bias_l [hidden];
  * then head W [hidden][A+1] (logits then critic), head bias [A+1]. */

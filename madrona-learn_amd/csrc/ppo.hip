@@ -1028,7 +1028,7 @@ template <typename T, int H>
 static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
                             const int32_t* mb_seq, int mb, const float* adv_st,
                             const mlearn_ppo_hparams& h, float* grad, float* loss_out, void* wsp,
-                            hipStream_t s) {
+                            bool step_only, hipStream_t s) {
     const int64_t M = (int64_t)mb * ro.bptt_len;
     WsK ws;
     carve(p, M, (char*)wsp, &ws);
@@ -1055,6 +1055,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
         case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
         default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
+    if (step_only) return check_launch("ppo_minibatch_fwd_bwd");
     const int L = p.num_layers;
     WgJobs jobs{};
     jobs.n = L + 1;
@@ -1116,13 +1117,14 @@ int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows
     return (int64_t)carve(*policy, rows, nullptr, nullptr);
 }
 
-int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
-                              const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
-                              const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
-                              void* workspace, mlearn_stream_t stream) {
+static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                     const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                     const mlearn_ppo_hparams* hp, float* grad, float* loss_out, void* workspace,
+                     bool step_only, mlearn_stream_t stream) {
     int rc = validate_policy(policy);
     if (rc) return rc;
-    ML_REQUIRE(ro && mb_seq && adv_stats && hp && grad && workspace, "ppo: null pointer");
+    ML_REQUIRE(ro && mb_seq && adv_stats && hp && workspace, "ppo: null pointer");
+    ML_REQUIRE(step_only || grad, "ppo: null grad");
     ML_REQUIRE(mb_size >= 1, "ppo: mb_size must be >= 1");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");
     ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
@@ -1132,11 +1134,11 @@ int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_roll
 #define ML_DISPATCH(T)                                                                           \
     switch (policy->hidden) {                                                                   \
         case 64: return launch_minibatch<T, 64>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp,  \
-                                                grad, loss_out, workspace, s);                  \
+                                                grad, loss_out, workspace, step_only, s);       \
         case 128: return launch_minibatch<T, 128>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp, \
-                                                  grad, loss_out, workspace, s);                \
+                                                  grad, loss_out, workspace, step_only, s);     \
         default: return launch_minibatch<T, 256>(*policy, *ro, mb_seq, mb_size, adv_stats, *hp, \
-                                                 grad, loss_out, workspace, s);                 \
+                                                 grad, loss_out, workspace, step_only, s);      \
     }
     if (policy->dtype == MLEARN_DTYPE_BF16) {
         ML_DISPATCH(bf16)
@@ -1144,6 +1146,22 @@ int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_roll
         ML_DISPATCH(float)
     }
 #undef ML_DISPATCH
+}
+
+int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                              const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                              const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
+                              void* workspace, mlearn_stream_t stream) {
+    return ppo_entry(policy, ro, mb_seq, mb_size, adv_stats, hp, grad, loss_out, workspace, false,
+                     stream);
+}
+
+int mlearn_ppo_minibatch_fwd_bwd(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
+                                 const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
+                                 const mlearn_ppo_hparams* hp, void* workspace,
+                                 mlearn_stream_t stream) {
+    return ppo_entry(policy, ro, mb_seq, mb_size, adv_stats, hp, nullptr, nullptr, workspace, true,
+                     stream);
 }
 
 }  // extern "C"

@@ -100,6 +100,8 @@ _SIGNATURES = {
     "mlearn_ppo_workspace_bytes": (c_int64, [POINTER(MlpPolicy), c_int64]),
     "mlearn_ppo_minibatch_grad": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
                                             c_int32, _P, POINTER(PPOHparams), _P, _P, _P, _S]),
+    "mlearn_ppo_minibatch_fwd_bwd": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
+                                               c_int32, _P, POINTER(PPOHparams), _P, _S]),
     "mlearn_param_count": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(OptimState), _P, _S]),

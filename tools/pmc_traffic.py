@@ -1,0 +1,40 @@
+"""HBM traffic per launch from rocprofv3 PMC passes (tools/gpu_pmc.sh with
+FETCH_SIZE and WRITE_SIZE passes) -> profiles/pmc_<tag>.json.
+
+Correction (MI355X_MICROARCH.md, HBM): on gfx950 FETCH_SIZE reports half the
+bytes of a wide coalesced streaming read -> doubled; WRITE_SIZE is exact for
+16-B-per-lane stores (8-B stores are uncalibrated: reported as measured).
+Both counters are in KiB."""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r01.json"
+KEYS = {"ppo_step": r"ppo_step_kernel", "wgrad": r"wgrad_kernel", "policy_step": r"policy_step_kernel",
+        "gae": r"gae_kernel", "reduce_grads": r"reduce_grads_kernel"}
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+names = {}
+for f in sorted(glob.glob(f"{root}/p*/*counter_collection.csv")):
+    for row in csv.DictReader(open(f)):
+        for key, pat in KEYS.items():
+            if re.search(pat, row["Kernel_Name"]):
+                vals[key][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                names[key] = row["Kernel_Name"]
+res = {}
+for key, cs in vals.items():
+    d = {c: sum(v) / len(v) for c, v in cs.items()}
+    fetch = d.get("FETCH_SIZE")
+    write = d.get("WRITE_SIZE")
+    ent = {"kernel_name": names[key], "counters_avg_per_launch": d, "launches": {c: len(v) for c, v in cs.items()}}
+    if fetch is not None and write is not None:
+        ent["hbm_read_bytes_per_launch"] = 2 * fetch * 1024
+        ent["hbm_write_bytes_per_launch"] = write * 1024
+        ent["hbm_bytes_per_launch"] = 2 * fetch * 1024 + write * 1024
+    res[key] = ent
+json.dump({"source": root, "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; KiB->B",
+           "kernels": res}, open(out, "w"), indent=1)
+print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items()}))
