@@ -231,10 +231,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test hooks: MLEARN_DIST_BACKEND=gloo and MLEARN_SHARE_GPU=1 run several ranks on one
+    # GPU (the driver's multi-GPU runs use the defaults: RCCL, one GPU per rank)
+    backend = os.environ.get("MLEARN_DIST_BACKEND", "nccl")
+    if os.environ.get("MLEARN_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

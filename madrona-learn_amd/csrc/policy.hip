@@ -134,38 +134,23 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
 
     // layer 0: observation fragments straight from the env output (cast to
     // the compute dtype = ObservationsCaster); wave 0 copies them to the store
-    const int nks0 = D / KS;
-    frag ob[KSD];
-    {
-        const float* orow = obs + (live ? row : 0) * D;
-#pragma unroll
-        for (int s = 0; s < KSD; ++s)
-            if (s < nks0) ob[s] = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
-        if (w == 0 && obs_store && live) {
-            T* srow = obs_store + row * D;
-#pragma unroll
-            for (int s = 0; s < KSD; ++s)
-                if (s < nks0) RT<T>::put_row(srow, s, h, ob[s]);
-        }
-    }
+    // the second layer's weights (this wave's blocks) are in flight from the start
+    frag w1[KSH][NBW];
+    if (L > 1) prefetch_img<T, NBW, KSH>(w1, (const T*)P.wt[1] + (int64_t)w * NBW * KSH * 64 * E, lane);
     f32x16 acc[NBW];
     zero_acc<NBW>(acc);
-    gemm_ring<T, NBW, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0] + (int64_t)w * NBW * nks0 * 64 * E,
-                              lane);
+    gemm_first<T, NBW>(acc, obs + (live ? row : 0) * D, live, D / KS,
+                       (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
+                       (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane);
     __syncthreads();  // LayerNorm parameters staged
-    frag bf[KSH];
+    typedef typename Pk<T>::word word;
+    word aw[NBW][8];
     for (int l = 0;; ++l) {
         // LayerNorm + ReLU (models.py:46-56); row statistics over all waves
-        float sum = 0.f, sq = 0.f;
-#pragma unroll
-        for (int i = 0; i < NBW; ++i)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float x = rnd<T>(acc[i][q]);
-                acc[i][q] = x;
-                sum += x;
-                sq += x * x;
-            }
+        f2 x2[NBW][8];
+        word zw[NBW][8];
+        float sum, sq;
+        ln_pack_stats<T, NBW>(acc, zw, x2, sum, sq);
         sum = sum_halves(sum);
         sq = sum_halves(sq);
         if (h == 0) {
@@ -183,34 +168,20 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         const float mean = sum * invH;
         const float var = fmaxf(sq * invH - mean * mean, 0.f);
         const float rstd = rsqrtf(var + 1e-6f);
-        const float* gm = gb + l * 2 * H;
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-            const int nb = w * NBW + i;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int f0 = nb * 32 + 8 * g + 4 * h;
-                const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
-                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int q = 4 * g + j;
-                    acc[i][q] = rnd<T>(fmaxf((acc[i][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
-                }
-            }
-        }
+        ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
         if (l + 1 == L) break;
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int t = 0; t < SPB; ++t)
-                fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+                fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(aw[i], t);
         __syncthreads();
-#pragma unroll
-        for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
         zero_acc<NBW>(acc);
-        gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
-                                  (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);
+        if (l == 0)
+            gemm_pre_lds<T, NBW, KSH>(acc, w1, fr, lane);
+        else
+            gemm_lds<T, NBW, KSH, 8>(acc, fr,
+                                     (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);
     }
 
     // actor + critic heads over this wave's features, partials summed in wave
@@ -220,7 +191,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = RT<T>::from_acc(acc[i], t);
+            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
         f32x16 ha[1];
         zero_acc<1>(ha);
         gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(

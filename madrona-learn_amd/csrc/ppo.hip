@@ -44,6 +44,9 @@ struct HpK {
 };
 
 constexpr int kLossSlots = 20;   // per tile doubles
+#ifndef ML_STEP_WAVES
+#define ML_STEP_WAVES 2  // waves per SIMD the fused step kernel is register-budgeted for
+#endif
 constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 constexpr int kWgChunk = 32;     // weight-gradient K chunk (rows of the minibatch)
@@ -73,7 +76,7 @@ static uint64_t* g_stamp_buf = nullptr;
     do {                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                        \
         if (ws.stamps && lane == 0)                                               \
-            ws.stamps[(int64_t)tile * 16 + (i)] = __builtin_amdgcn_s_memtime();   \
+            ws.stamps[((int64_t)tile * 4 + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
 #else
@@ -298,20 +301,20 @@ template <typename T> __device__ inline float relu_thr();
 template <> __device__ inline float relu_thr<float>() { return 0.f; }
 template <> __device__ inline float relu_thr<bf16>() { return __builtin_bit_cast(float, 0x00008000u); }
 
-__device__ inline float frag_elem(const bf16x8& f, int e) { return (float)f[e]; }
-__device__ inline float frag_elem(float f, int) { return f; }
 
-// Store row of minibatch row f.
+// Store row of minibatch row f (32-bit index math: rows, sequences and N are
+// < 2^31, checked on the host).
 __device__ inline int64_t store_row(const RolloutK& ro, const int32_t* mb_seq, int mb, int64_t f) {
-    const int tl = (int)(f / mb);
-    const int m = (int)(f - (int64_t)tl * mb);
-    const int64_t seq = mb_seq[m];
-    const int64_t c = seq / ro.N, b = seq - c * ro.N;
-    return (c * ro.bptt + tl) * ro.N + b;
+    const uint32_t fu = (uint32_t)f, mbu = (uint32_t)mb, nu = (uint32_t)ro.N;
+    const uint32_t tl = fu / mbu;
+    const uint32_t m = fu - tl * mbu;
+    const uint32_t seq = (uint32_t)mb_seq[m];
+    const uint32_t c = seq / nu, b = seq - c * nu;
+    return ((int64_t)c * ro.bptt + tl) * ro.N + b;
 }
 
 template <typename T, int H, int L>
-__global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
+__global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws) {
     typedef typename RT<T>::frag frag;
@@ -362,50 +365,31 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         }
     }
 
+    STAMP(0);
     // ---- forward ----
-    const int nks0 = D / KS;
-    frag ob[KSD];
-    {
-        const T* orow = (const T*)ro.obs + sr * D;
-#pragma unroll
-        for (int s = 0; s < KSD; ++s)
-            if (s < nks0) ob[s] = live ? RT<T>::row(orow, s, h) : RT<T>::zero();
-        if (w == 0) {
-            T* xrow = (T*)ws.x0 + row * D;
-#pragma unroll
-            for (int s = 0; s < KSD; ++s)
-                if (s < nks0) RT<T>::put_row(xrow, s, h, ob[s]);
-        }
-    }
     f32x16 acc[NBW];
     zero_acc<NBW>(acc);
-    gemm_ring<T, NBW, KSD, 2>(acc, ob, nks0, (const T*)P.wt[0] + (int64_t)w * NBW * nks0 * 64 * E,
-                              lane);
+    gemm_first<T, NBW>(acc, (const T*)ro.obs + sr * D, live, D / KS,
+                       (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
+                       w == 0 ? (T*)ws.x0 + row * D : nullptr, lane);
+    STAMP(1);
     __syncthreads();  // LayerNorm parameters staged
-    frag bf[KSH];
-    frag zr[L][NBW * SPB];  // this wave's Dense outputs (exact in the compute dtype)
+    typedef typename Pk<T>::word word;
+    word zr[L][NBW][8];  // this wave's Dense outputs (exact in the compute dtype)
+    word aw[NBW][8];     // post-activation of the current layer
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
         if (l > 0) {
             zero_acc<NBW>(acc);
-            gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
-                                      (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E, lane);
+            gemm_lds<T, NBW, KSH, 8>(acc, fr, (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E,
+                                     lane);
+            STAMP(4);
         }
-        float sum = 0.f, sq = 0.f;
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float x = rnd<T>(acc[i][q]);  // Dense output in the compute dtype
-                acc[i][q] = x;
-                sum += x;
-                sq += x * x;
-            }
-#pragma unroll
-            for (int t = 0; t < SPB; ++t) zr[l][i * SPB + t] = RT<T>::from_acc(acc[i], t);
-        }
+        f2 x2[NBW][8];
+        float sum, sq;
+        ln_pack_stats<T, NBW>(acc, zr[l], x2, sum, sq);
         sum = sum_halves(sum);
         sq = sum_halves(sq);
         if (h == 0) {
@@ -425,37 +409,24 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         const float rstd = rsqrtf(var + 1e-6f);
         mean_r[l] = mean;
         rstd_r[l] = rstd;
-        const float* gm = gb + l * 2 * H;
+        STAMP(2 + 3 * l);
+        ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
         T* arow = (T*)ws.a[l] + row * H;
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-            const int nb = w * NBW + i;
+        for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int f0 = nb * 32 + 8 * g + 4 * h;
-                const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
-                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int q = 4 * g + j;
-                    // LayerNorm (x - mean) * (rstd * scale) + bias, ReLU, compute dtype
-                    acc[i][q] = rnd<T>(fmaxf((acc[i][q] - mean) * (rstd * gg[j]) + bb[j], 0.f));
-                }
-                store4(arow + f0, acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2],
-                       acc[i][4 * g + 3]);
-            }
-        }
+            for (int g = 0; g < 4; ++g)
+                Pk<T>::store4(arow + (w * NBW + i) * 32 + 8 * g + 4 * h, aw[i][2 * g], aw[i][2 * g + 1]);
         if (l + 1 < L) {
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
 #pragma unroll
                 for (int t = 0; t < SPB; ++t)
-                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(aw[i], t);
             __syncthreads();
-#pragma unroll
-            for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
         }
     }
+    STAMP(6);
     // heads over this wave's features; partials summed in wave order:
     // lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22, models.py:154)
     {
@@ -463,7 +434,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = RT<T>::from_acc(acc[i], t);
+            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
         f32x16 ha[1];
         zero_acc<1>(ha);
         gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
@@ -481,6 +452,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
     }
     __syncthreads();
 
+    STAMP(7);
     // ---- loss: one (row, group | value) task per thread (ppo.py:129-262) ----
     {
         LossAcc m;
@@ -523,9 +495,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         for (int s = 0; s < kLossSlots; ++s) {
             const int kind = (s < 16) ? (s & 3) : 0;
             float v = vals[s];
-            v = kind == 2 ? half_reduce<2>(v) : (kind == 3 ? half_reduce<3>(v) : half_reduce<0>(v));
-            const float u = __shfl_xor(v, 32);
-            v = kind == 2 ? fminf(v, u) : (kind == 3 ? fmaxf(v, u) : v + u);
+            v = kind == 2 ? wave_reduce<2>(v) : (kind == 3 ? wave_reduce<3>(v) : wave_reduce<0>(v));
             if (lane == 0) lred[w * kLossSlots + s] = v;
         }
     }
@@ -539,6 +509,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         }
         ws.loss_part[(int64_t)tile * kLossSlots + tid] = v;
     }
+    STAMP(8);
     // d head: row-major store (wgrad operand) and the head-bias column partial
     if (w == 0) {
         const float* lr = lg + r * 33 + 16 * h;
@@ -552,6 +523,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         if (h == 0) ws.colpart[(int64_t)tile * ws.CP + L * 2 * H + r] = cs;
     }
 
+    STAMP(9);
     // ---- backward ----
     {
         frag db[KSHD];
@@ -567,9 +539,11 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
         const float mean = mean_r[l], rstd = rstd_r[l];
+        const f2 m2 = {mean, mean}, r2 = {rstd, rstd};
         const float* gm = gb + l * 2 * H;
         float* cp = ws.colpart + (int64_t)tile * ws.CP + l * 2 * H;
-        float su = 0.f, sv = 0.f;
+        f2 su2 = {0.f, 0.f}, sv2 = {0.f, 0.f};
+        f2 zc2[NBW][8], u2[NBW][8];
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
             const int nb = w * NBW + i;
@@ -578,23 +552,27 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
             for (int g = 0; g < 4; ++g) {
                 const int f0 = nb * 32 + 8 * g + 4 * h;
                 const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
-                const float gg[4] = {G.x, G.y, G.z, G.w}, bb[4] = {B.x, B.y, B.z, B.w};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int q = 4 * g + j;
-                    const float z = frag_elem(zr[l][i * SPB + q / E], q % E);
-                    const float zc = z - mean;
-                    const float xh = zc * rstd;
-                    const float y = zc * (rstd * gg[j]) + bb[j];
-                    const float da = acc[i][q];
-                    const bool on = (y > thr) & live;  // ReLU'
-                    const float dy = on ? da : 0.f;
-                    const float u = dy * gg[j];
-                    acc[i][q] = u;
-                    su += u;
-                    sv += u * xh;
-                    pg[q] = dy * xh;
-                    pb[q] = dy;
+                for (int p = 0; p < 2; ++p) {
+                    const int k = 2 * g + p;
+                    const f2 gg = p ? f2{G.z, G.w} : f2{G.x, G.y};
+                    const f2 bb = p ? f2{B.z, B.w} : f2{B.x, B.y};
+                    const f2 zc = Pk<T>::unpack(zr[l][i][k]) - m2;
+                    const f2 xh = zc * r2;
+                    const f2 y = zc * (r2 * gg) + bb;
+                    // ReLU' (rnd<T>(y) > 0 <=> y > thr); padding rows carry no gradient
+                    const f2 dy = {((y.x > thr) & live) ? acc[i][2 * k] : 0.f,
+                                   ((y.y > thr) & live) ? acc[i][2 * k + 1] : 0.f};
+                    const f2 u = dy * gg;
+                    const f2 pgk = dy * xh;
+                    zc2[i][k] = zc;
+                    u2[i][k] = u;
+                    su2 += u;
+                    sv2 = u * xh + sv2;
+                    pg[2 * k] = pgk.x;
+                    pg[2 * k + 1] = pgk.y;
+                    pb[2 * k] = dy.x;
+                    pb[2 * k + 1] = dy.y;
                 }
             }
             // LayerNorm scale/bias partials: column sums over the tile's rows
@@ -606,8 +584,9 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
                 cp[H + f] = tgs;
             }
         }
-        su = sum_halves(su);
-        sv = sum_halves(sv);
+        STAMP(10 + 3 * (L - 1 - l));
+        float su = sum_halves(su2.x + su2.y);
+        float sv = sum_halves(sv2.x + sv2.y);
         if (h == 0) {
             red[(w * 32 + r) * 2] = su;
             red[(w * 32 + r) * 2 + 1] = sv;
@@ -622,35 +601,37 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) void ppo_step_kernel(
         }
         // dZ = rstd (u - mean(u) - xh mean(u xh)) = rstd u + (-rstd^2 mean(u xh)) zc - rstd mean(u)
         const float ca = -(rstd * rstd) * (sv * invH), cb = -rstd * (su * invH);
+        const f2 ca2 = {ca, ca}, cb2 = {cb, cb};
+        word dzw[NBW][8];
         T* dzrow = (T*)ws.dz[l] + row * H;
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
-            const int nb = w * NBW + i;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float z = frag_elem(zr[l][i * SPB + q / E], q % E);
-                acc[i][q] = rnd<T>(rstd * acc[i][q] + (ca * (z - mean) + cb));
+            for (int k = 0; k < 8; ++k) {
+                const f2 d = r2 * u2[i][k] + (ca2 * zc2[i][k] + cb2);
+                dzw[i][k] = Pk<T>::pack(d.x, d.y);
             }
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-                store4(dzrow + nb * 32 + 8 * g + 4 * h, acc[i][4 * g], acc[i][4 * g + 1],
-                       acc[i][4 * g + 2], acc[i][4 * g + 3]);
+                Pk<T>::store4(dzrow + (w * NBW + i) * 32 + 8 * g + 4 * h, dzw[i][2 * g],
+                              dzw[i][2 * g + 1]);
         }
+        STAMP(11 + 3 * (L - 1 - l));
         if (l > 0) {
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
 #pragma unroll
                 for (int t = 0; t < SPB; ++t)
-                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = RT<T>::from_acc(acc[i], t);
+                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(dzw[i], t);
             __syncthreads();
-#pragma unroll
-            for (int s = 0; s < KSH; ++s) bf[s] = fr[s * 64 + lane];
             zero_acc<NBW>(acc);
             // dA_{l-1}^T = W_l . dZ_l^T  (this wave's feature blocks)
-            gemm_ring<T, NBW, KSH, 4>(acc, bf, KSH,
-                                      (const T*)P.w[l] + (int64_t)w * NBW * KSH * 64 * E, lane);
+            gemm_lds<T, NBW, KSH, 8>(acc, fr, (const T*)P.w[l] + (int64_t)w * NBW * KSH * 64 * E,
+                                     lane);
+            STAMP(12 + 3 * (L - 1 - l));
         }
     }
+    STAMP(15);
 }
 
 template <typename T, int H, int L>
@@ -1126,6 +1107,8 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro && mb_seq && adv_stats && hp && workspace, "ppo: null pointer");
     ML_REQUIRE(step_only || grad, "ppo: null grad");
     ML_REQUIRE(mb_size >= 1, "ppo: mb_size must be >= 1");
+    ML_REQUIRE(ro->N >= 1 && ro->N < (1ll << 31) && (int64_t)mb_size * ro->bptt_len < (1ll << 31),
+               "ppo: N and rows per minibatch must be < 2^31");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");
     ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
                "ppo: null rollout array");

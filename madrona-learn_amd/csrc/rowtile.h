@@ -167,6 +167,97 @@ __device__ inline void gemm_rb(f32x16 (&acc)[NOUT], const typename RT<T>::frag (
     gemm_ring<T, NOUT, NKS, DEPTH>(acc, b, NKS, img, lane);
 }
 
+// As gemm_rb, with the B fragments read from LDS (fr[s*64 + lane], written
+// by the workgroup's waves) one step ahead instead of held in registers.
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag* fr,
+                                const T* __restrict__ img, int lane) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    frag ra[DEPTH][NOUT];
+#pragma unroll
+    for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * NKS + s) * FB);
+    frag b = fr[lane];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int sl = s + DEPTH - 1;
+        if (sl < NKS) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb)
+                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * NKS + sl) * FB);
+        }
+        const frag bn = s + 1 < NKS ? fr[(s + 1) * 64 + lane] : b;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ra[s % DEPTH][nb], b, acc[nb]);
+        __builtin_amdgcn_sched_barrier(0);
+        b = bn;
+    }
+}
+
+// Whole-layer A-fragment prefetch: issue every load of a product up front
+// (they land while earlier work runs), then multiply with B fragments from LDS.
+template <typename T, int NOUT, int NKS>
+__device__ inline void prefetch_img(typename RT<T>::frag (&a)[NKS][NOUT], const T* __restrict__ img,
+                                    int lane) {
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) a[s][nb] = img_load<T>(rs, voff, (nb * NKS + s) * FB);
+}
+template <typename T, int NOUT, int NKS>
+__device__ inline void gemm_pre_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&a)[NKS][NOUT],
+                                    const typename RT<T>::frag* fr, int lane) {
+    typedef typename RT<T>::frag frag;
+    frag b = fr[lane];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const frag bn = s + 1 < NKS ? fr[(s + 1) * 64 + lane] : b;
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(a[s][nb], b, acc[nb]);
+        b = bn;
+    }
+}
+
+// acc[nb] += sum_s Img[block nb][step s] x row-fragment(s) for the first layer:
+// B fragments (natural k order) read from this lane's row in memory (cast to
+// the compute dtype), runtime step count, a plain loop so the accumulators
+// stay put; the next step's A fragments and row fragment are in flight while
+// the current step's MFMAs run.  copy (may be null) receives the cast row.
+template <typename T, int NOUT, typename S>
+__device__ inline void gemm_first(f32x16 (&acc)[NOUT], const S* __restrict__ row, bool live,
+                                  int nks, const T* __restrict__ img, T* copy, int lane) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    const int h = lane >> 5;
+    frag a[NOUT], an[NOUT];
+    frag b = live ? RT<T>::row(row, 0, h) : RT<T>::zero(), bn = b;
+#pragma unroll
+    for (int nb = 0; nb < NOUT; ++nb) a[nb] = img_load<T>(rs, voff, (nb * nks) * FB);
+    for (int s = 0; s < nks; ++s) {
+        if (s + 1 < nks) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb) an[nb] = img_load<T>(rs, voff, (nb * nks + s + 1) * FB);
+            bn = live ? RT<T>::row(row, s + 1, h) : RT<T>::zero();
+        }
+        if (copy) RT<T>::put_row(copy, s, h, b);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(a[nb], b, acc[nb]);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) a[nb] = an[nb];
+        b = bn;
+    }
+}
+
 // Feature index of accumulator register q of block nb for lane half h.
 __device__ inline int feat(int nb, int q, int h) { return nb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h; }
 
@@ -178,6 +269,11 @@ __device__ inline int feat(int nb, int q, int h) { return nb * 32 + (q & 3) + 8 
     __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, true))
 #define ML_SWZ(v, pat) \
     __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), pat))
+
+// Reductions over the 32 lanes of each half-wave (result in every lane).
+template <int KIND> __device__ inline float red_op(float a, float b) {
+    return KIND == 2 ? fminf(a, b) : (KIND == 3 ? fmaxf(a, b) : a + b);
+}
 
 template <int D> __device__ inline float xlane(float v) {
     if constexpr (D == 1) return ML_DPP(v, 0xB1);       // quad_perm [1,0,3,2]
@@ -201,17 +297,24 @@ __device__ inline float add_xor32(float v) {
     return a + b;
 }
 
-// Reductions over the 32 lanes of each half-wave (result in every lane).
-template <int KIND> __device__ inline float red_op(float a, float b) {
-    return KIND == 2 ? fminf(a, b) : (KIND == 3 ? fmaxf(a, b) : a + b);
+template <int KIND> __device__ inline float xor16_op(float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    return red_op<KIND>(a, b);
 }
 template <int KIND> __device__ inline float half_reduce(float v) {
     v = red_op<KIND>(v, xlane<1>(v));
     v = red_op<KIND>(v, xlane<2>(v));
     v = red_op<KIND>(v, ML_DPP(v, 0x124));  // row_ror:4
     v = red_op<KIND>(v, xlane<8>(v));
-    v = red_op<KIND>(v, xlane<16>(v));
-    return v;
+    return xor16_op<KIND>(v);
+}
+// Over all 64 lanes (result in every lane).
+template <int KIND> __device__ inline float wave_reduce(float v) {
+    v = half_reduce<KIND>(v);
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    return red_op<KIND>(a, b);
 }
 
 // Column sums: the 16 values v[q] of every lane summed over the 32 lanes
@@ -259,6 +362,87 @@ __device__ inline void store4(bf16* p, float a, float b, float c, float d) {
 }
 __device__ inline void store4(float* p, float a, float b, float c, float d) {
     *(float4*)p = make_float4(a, b, c, d);
+}
+
+// ---------------------------------------------------------------------------
+// Pair-packed blocks: the 16 accumulator values of one 32-feature block as 8
+// words of two values in the compute dtype (bf16x2 / float2).  Packing is the
+// compute-dtype rounding point; unpacked pairs feed packed f32 math
+// (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32); the words are directly the
+// next product's B fragments and the 4-feature row-major stores.
+// ---------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct Pk;
+template <> struct Pk<bf16> {
+    typedef uint32_t word;
+    __device__ static word pack(float a, float b) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const bf16x2 v = {(bf16)a, (bf16)b};
+        return __builtin_bit_cast(uint32_t, v);
+    }
+    __device__ static f2 unpack(word w) {
+        return f2{__builtin_bit_cast(float, w << 16), __builtin_bit_cast(float, w & 0xffff0000u)};
+    }
+    // k-step t (0, 1) of the block: elements 8t .. 8t+7 = words 4t .. 4t+3
+    __device__ static bf16x8 frag(const word (&w)[8], int t) {
+        typedef __attribute__((ext_vector_type(4))) uint32_t u4;
+        const u4 v = {w[4 * t], w[4 * t + 1], w[4 * t + 2], w[4 * t + 3]};
+        return __builtin_bit_cast(bf16x8, v);
+    }
+    // features 4g .. 4g+3 of the block (words 2g, 2g+1) -> 8-byte store
+    __device__ static void store4(bf16* p, word a, word b) {
+        typedef __attribute__((ext_vector_type(2))) uint32_t u2;
+        *(u2*)p = u2{a, b};
+    }
+};
+template <> struct Pk<float> {
+    typedef f2 word;
+    __device__ static word pack(float a, float b) { return f2{a, b}; }
+    __device__ static f2 unpack(word w) { return w; }
+    // k-step t (0 .. 15) of the block: element t
+    __device__ static float frag(const word (&w)[8], int t) { return w[t >> 1][t & 1]; }
+    __device__ static void store4(float* p, word a, word b) {
+        *(float4*)p = make_float4(a.x, a.y, b.x, b.y);
+    }
+};
+
+// Dense output -> compute dtype (packed) and the lane's partial row sums.
+template <typename T, int NBW>
+__device__ inline void ln_pack_stats(const f32x16 (&acc)[NBW], typename Pk<T>::word (&zw)[NBW][8],
+                                     f2 (&x2)[NBW][8], float& sum, float& sq) {
+    f2 s = {0.f, 0.f}, q = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            zw[i][k] = Pk<T>::pack(acc[i][2 * k], acc[i][2 * k + 1]);
+            x2[i][k] = Pk<T>::unpack(zw[i][k]);
+            s += x2[i][k];
+            q = x2[i][k] * x2[i][k] + q;
+        }
+    sum = s.x + s.y;
+    sq = q.x + q.y;
+}
+
+// LayerNorm (x - mean) * (rstd * scale) + bias, ReLU, rounded to the compute
+// dtype (models.py:46-56); gm = LDS [2][H] scale | bias of the layer; blocks
+// nb0 .. nb0+NBW-1.
+template <typename T, int NBW>
+__device__ inline void ln_apply(const f2 (&x2)[NBW][8], float mean, float rstd, const float* gm,
+                                int H, int nb0, int h, typename Pk<T>::word (&aw)[NBW][8]) {
+    const f2 m2 = {mean, mean}, r2 = {rstd, rstd};
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f0 = (nb0 + i) * 32 + 8 * g + 4 * h;
+            const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
+            const f2 y0 = (x2[i][2 * g] - m2) * (r2 * f2{G.x, G.y}) + f2{B.x, B.y};
+            const f2 y1 = (x2[i][2 * g + 1] - m2) * (r2 * f2{G.z, G.w}) + f2{B.z, B.w};
+            aw[i][2 * g] = Pk<T>::pack(fmaxf(y0.x, 0.f), fmaxf(y0.y, 0.f));
+            aw[i][2 * g + 1] = Pk<T>::pack(fmaxf(y1.x, 0.f), fmaxf(y1.y, 0.f));
+        }
 }
 
 // Lane-private LDS spill of one accumulator block (16 values) in the compute

@@ -98,6 +98,7 @@ class PPO(AlgoBase):  # ppo.py:49-106
         self.perm = torch.zeros((self.E, self.num_seq), dtype=torch.int32, device=dev)
         self.adv_part = torch.zeros((self.E, self.num_mb * 66), dtype=torch.float64, device=dev)
         self.adv_stats = torch.zeros((self.E, self.num_mb, 2), dtype=torch.float32, device=dev)
+        self.adv_sums = torch.zeros((self.E, 2 * self.num_mb), dtype=torch.float64, device=dev)
         rows = self.mb * self.bptt
         nbytes = nat.lib().mlearn_ppo_workspace_bytes(policy_state.desc, rows)
         self.ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
@@ -140,8 +141,12 @@ class PPO(AlgoBase):  # ppo.py:49-106
             nat.check(L.mlearn_adv_stats(self.view, nat.ptr(self.perm[e]), self.num_mb, self.mb,
                                          nat.ptr(self.adv_part[e]), strm), "adv_stats")
         if self.dp.world_size > 1:
+            # one collective for every epoch's per-minibatch advantage sums
             for e in range(self.E):
-                yield ("allreduce", self.adv_part[e, :2 * self.num_mb])
+                self.adv_sums[e].copy_(self.adv_part[e, :2 * self.num_mb])
+            yield ("allreduce", self.adv_sums)
+            for e in range(self.E):
+                self.adv_part[e, :2 * self.num_mb].copy_(self.adv_sums[e])
         for e in range(self.E):
             nat.check(L.mlearn_adv_stats_finish(nat.ptr(self.adv_part[e]), self.num_mb,
                                                 self.count, nat.ptr(self.adv_stats[e]), strm),

@@ -1,0 +1,93 @@
+"""Data-parallel PPO iteration on the GPU path: two ranks (processes) share the
+box's one GPU, collectives over gloo (the product issues the same
+all-reduces over RCCL on a multi-GPU node).  Each rank owns its own
+environment shard; after one update (eager) and two more (HIP-graph replay)
+both ranks must hold identical parameters, and the first update must equal
+the oracle's single-process update over the union of both ranks' minibatches
+(f32 mode, tolerances of test_gpu_train)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+BUCKETS = [4, 8, 5, 5, 2, 2]
+N, D, H, T = 64, 64, 64, 32
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import madrona_learn as ml
+        from madrona_learn.envs import DummyVecEnv
+        from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dtype = torch.float32
+        env = DummyVecEnv(N, D, 6, seed=2, env_offset=rank * N, device=dev)
+        cfg = ml.TrainConfig(
+            num_worlds=N, num_agents_per_world=1, num_updates=3,
+            actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
+            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16, clip_coef=0.2,
+                                       value_loss_coef=0.5, entropy_coef={"actions": 0.01},
+                                       max_grad_norm=0.5),
+            num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=5, metrics_buffer_size=4,
+            dreamer_v3_critic=False, compute_dtype=dtype)
+        policy = ml.Policy(actor_critic=ml.ActorCritic(
+            backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(H, 2, dtype))),
+            actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
+            critic=DenseLayerCritic(dtype)))
+        mgr = ml.init_training(dev, cfg, env.sim_fns(), policy, use_graph=True)
+        ps, ts = mgr.state.policy_states, mgr.state.train_states
+        p0 = ps.params.cpu().numpy()
+        mgr.update_iter()
+        torch.cuda.synchronize()
+        s = mgr.rollout_mgr.store
+        store = {k: (v.float() if v.dtype == torch.bfloat16 else v).cpu().numpy()
+                 for k, v in s.as_dict().items()}
+        p1 = ps.params.cpu().numpy()
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), p0=p0, p1=p1,
+                 init_norms=ps.init_norms.cpu().numpy(), key=np.array(ts.update_prng_key),
+                 **{f"s_{k}": v for k, v in store.items()})
+        for _ in range(2):
+            mgr.update_iter()
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, f"rank{rank}_p3.npy"), ps.params.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_one_gpu(tmp_path):
+    from oracle import ppo_ref as ref
+    mp.spawn(worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = [np.load(os.path.join(tmp_path, f"rank{i}.npz")) for i in range(2)]
+    p3 = [np.load(os.path.join(tmp_path, f"rank{i}_p3.npy")) for i in range(2)]
+    assert np.array_equal(r[0]["p0"], r[1]["p0"]), "initial params differ across ranks"
+    assert np.array_equal(r[0]["p1"], r[1]["p1"]), "ranks diverged after the eager update"
+    assert np.array_equal(p3[0], p3[1]), "ranks diverged under graph replay"
+    assert not np.array_equal(r[0]["s_obs"], r[1]["s_obs"]), "env shards must differ"
+    stores = [{k[2:]: ri[k] for k in ri.files if k.startswith("s_")} for ri in r]
+    lay = ref.param_layout(D, H, 2, sum(BUCKETS))
+    p0 = r[0]["p0"].astype(np.float64)
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    z = np.zeros_like(p0)
+    p_ref, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay,
+                                 r[0]["init_norms"].astype(np.float64), num_epochs=2,
+                                 minibatch_size=16, bptt=T, key=tuple(int(x) for x in r[0]["key"]),
+                                 epoch_base=0, mode="f32", lr=3e-4, max_grad_norm=0.5)
+    np.testing.assert_allclose(r[0]["p1"], p_ref, rtol=1e-4, atol=2e-5)

@@ -23,10 +23,13 @@ algo = mgr.algo
 ps, ts = mgr.state.policy_states, mgr.state.train_states
 M = algo.mb * algo.bptt
 ntiles = ((M + 63) // 64 * 64) // 32
-buf = torch.zeros((ntiles, 16), dtype=torch.int64, device=dev)
+buf = torch.zeros((ntiles * 4, 16), dtype=torch.int64, device=dev)
 L.mlearn_debug_set_stamp_buffer(buf.data_ptr())
-names = ["start", "L0 gemm", "L0 ln", "L1 gemm", "L1 ln", "heads", "loss", "dhead+bwd head gemm",
-         "bwd L1 ln", "bwd W1 gemm", "bwd L0 ln"]
+# stamp index -> phase ending there (L = 2)
+names = {0: "prologue", 1: "L0 gemm", 2: "L0 stats+barrier", 4: "L0 apply+xchg+L1 gemm",
+         5: "L1 stats+barrier", 6: "L1 apply", 7: "heads+reduce", 8: "loss+partials",
+         9: "dhead/hb", 10: "bwd head gemm+L1 bwd pass1", 11: "L1 su/sv xchg+dz",
+         12: "dz xchg+W1 gemm", 13: "L0 bwd pass1", 14: "L0 xchg+dz", 15: "end"}
 for it in range(3):
     seqs = algo.perm[0, :algo.mb]
     nat.check(L.mlearn_ppo_minibatch_grad(ps.desc, algo.view, nat.ptr(seqs), algo.mb,
@@ -34,11 +37,12 @@ for it in range(3):
                                           nat.ptr(ts.grads), None, nat.ptr(algo.ws),
                                           nat.stream_handle()))
     torch.cuda.synchronize()
-st = buf.cpu().numpy().astype(np.int64)[:, :len(names)]
-d = np.diff(st, axis=1)
-print("tiles", ntiles, "cycles per phase (median / mean over tiles):")
-for i in range(1, len(names)):
-    print(f"  {names[i]:22s} {np.median(d[:, i-1]):10.0f} {d[:, i-1].mean():10.0f}")
-tot = st[:, len(names) - 1] - st[:, 0]
-print("tile total median", np.median(tot), "mean", tot.mean())
-print("kernel span", st.max() - st.min())
+st = buf.cpu().numpy().astype(np.int64)
+idx = sorted(names)
+print("tiles", ntiles, "cycles per phase (median / mean over waves):")
+for a, b in zip(idx[:-1], idx[1:]):
+    d = st[:, b] - st[:, a]
+    print(f"  {names[b]:30s} {np.median(d):10.0f} {d.mean():10.0f}")
+tot = st[:, 15] - st[:, 0]
+print("wave total median", np.median(tot), "mean", tot.mean())
+print("kernel span", st[:, 15].max() - st[:, 0].min())
