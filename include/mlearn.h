@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 2
+#define MLEARN_ABI_VERSION 3
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -176,7 +176,10 @@ int mlearn_rollout_post_step(const float* rewards, const uint8_t* dones, int64_t
 /* ---------------------------------------------------------------------- */
 typedef struct mlearn_metric_job {
     const float* x;
-    int64_t n;
+    int64_t n;          /* element count */
+    int64_t cols;       /* 0: x is contiguous; else element i is x[(i / cols) * ld + i % cols] */
+    int64_t ld;         /*    (a [n/cols][cols] window of a wider array, e.g. one policy's */
+                        /*    env columns of the [T][N] store) */
     int32_t abs_value;  /* 1: metric of |x| (ppo.py:358 'Value Errors') */
     int32_t pad;
 } mlearn_metric_job;
@@ -203,9 +206,14 @@ typedef struct mlearn_rollout_view {
     const float* advantages;  /* [T][N] */
     const float* returns;     /* [T][N] */
     const float* values;      /* [T][N] */
+    const uint8_t* dones;     /* [T][N] sequence breaks (recurrent policies; may be NULL) */
     int32_t T;                /* steps per update */
     int32_t bptt_len;         /* T / num_bptt_chunks */
-    int64_t N;                /* envs (P*B) on this rank */
+    int64_t N;                /* envs B of the policy this view trains */
+    int64_t ld;               /* row stride of the [T][.] arrays in envs (0: = N).  A policy of
+                                 a population owns env columns [p*B, (p+1)*B) of a [T][P*B]
+                                 store (pbt.py:130-133 self-play split): its view points at
+                                 column p*B with N = B, ld = P*B. */
 } mlearn_rollout_view;
 
 /* Per-minibatch advantage statistics for zscore_data (algo_common.py:133-140,

@@ -54,14 +54,44 @@ __global__ void philox_kernel(const uint4* __restrict__ ctr, uint32_t k0, uint32
 
 // ---------------------------------------------------------------------------
 // GAE (algo_common.py:84-130) + returns = adv + values (rollouts.py:761-769).
-// One lane per env column, VEC envs per lane (16-B loads of rewards/values).
+// One lane per env column (measured on MI355X at N = 2^22: one column per
+// lane streams at 5.6 TB/s, four columns per lane with 16-B loads at 4.6 TB/s,
+// fewer waves in flight; tools/gae_sweep.hip).
 // The reverse recurrence per column:
 //   nv = d_t ? 0 : nv ;  na = d_t ? 0 : na
 //   A_t = (r_t + g*nv - v_t) + g*l*na ;  nv = v_t ;  na = A_t
-// Operation order mirrors the reference expression tree; contraction is off
-// so the fp32 result is reproducible against the oracle's fp32 mode.
+// The recurrence is serial in t, so the loads are what must be parallel:
+// time runs in chunks of U steps and every load of chunk c-1 is issued
+// before chunk c is computed (register double buffer), so a lane keeps
+// 2*U*3 loads in flight instead of 3.  Stores are non-temporal (the
+// advantages/returns are read again only by the next kernel, from L2 misses
+// anyway).  Operation order mirrors the reference expression tree;
+// contraction is off so the fp32 result is reproducible against the
+// oracle's fp32 mode.
 // ---------------------------------------------------------------------------
 template <int VEC>
+struct GaeChunk;
+template <>
+struct GaeChunk<1> {
+    float r, v;
+    uint32_t d;
+    __device__ void load(const float* rw, const float* vl, const uint8_t* dn, int64_t o) {
+        r = __builtin_nontemporal_load(rw + o);
+        v = __builtin_nontemporal_load(vl + o);
+        d = dn[o];
+    }
+    __device__ float rj(int) const { return r; }
+    __device__ float vj(int) const { return v; }
+    __device__ uint32_t dj(int) const { return d; }
+};
+
+template <int VEC>
+__device__ __forceinline__ void gae_store(float* p, const float* x) {
+    static_assert(VEC == 1, "one column per lane");
+    __builtin_nontemporal_store(x[0], p);
+}
+
+template <int VEC, int U>
 __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewards,
                                                   const float* __restrict__ values,
                                                   const uint8_t* __restrict__ dones,
@@ -72,51 +102,43 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewa
     int64_t n0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * VEC;
     if (n0 >= N) return;
     float nv[VEC], na[VEC];
-    if (VEC == 4) {
-        float4 b = *(const float4*)(boot + n0);
-        nv[0] = b.x; nv[1] = b.y; nv[2] = b.z; nv[3] = b.w;
-    } else {
-        for (int j = 0; j < VEC; ++j) nv[j] = boot[n0 + j];
-    }
+    for (int j = 0; j < VEC; ++j) nv[j] = boot[n0 + j];
     for (int j = 0; j < VEC; ++j) na[j] = 0.f;
 
-    for (int t = T - 1; t >= 0; --t) {
-        int64_t o = (int64_t)t * N + n0;
-        float r[VEC], v[VEC];
-        uint32_t d[VEC];
-        if (VEC == 4) {
-            float4 r4 = *(const float4*)(rewards + o);
-            float4 v4 = *(const float4*)(values + o);
-            uint32_t d4 = *(const uint32_t*)(dones + o);
-            r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
-            v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
-            for (int j = 0; j < 4; ++j) d[j] = (d4 >> (8 * j)) & 0xffu;
-        } else {
+    GaeChunk<VEC> cur[U], nxt[U];
+    int t_hi = T - 1;  // chunk = steps (t_hi-U, t_hi]
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (t_hi - u >= 0) cur[u].load(rewards, values, dones, (int64_t)(t_hi - u) * N + n0);
+    while (t_hi >= 0) {
+        int t_nx = t_hi - U;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t_nx - u >= 0) nxt[u].load(rewards, values, dones, (int64_t)(t_nx - u) * N + n0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int t = t_hi - u;
+            if (t < 0) break;
+            float a[VEC], rt[VEC];
+#pragma unroll
             for (int j = 0; j < VEC; ++j) {
-                r[j] = rewards[o + j];
-                v[j] = values[o + j];
-                d[j] = dones[o + j];
+                uint32_t d = cur[u].dj(j);
+                float v = cur[u].vj(j);
+                float nvj = d ? 0.f : nv[j];
+                float naj = d ? 0.f : na[j];
+                float td = (cur[u].rj(j) + gamma * nvj) - v;
+                a[j] = td + gl * naj;
+                rt[j] = a[j] + v;
+                nv[j] = v;
+                na[j] = a[j];
             }
+            int64_t o = (int64_t)t * N + n0;
+            gae_store<VEC>(adv + o, a);
+            gae_store<VEC>(ret + o, rt);
         }
-        float a[VEC], rt[VEC];
-        for (int j = 0; j < VEC; ++j) {
-            float nvj = d[j] ? 0.f : nv[j];
-            float naj = d[j] ? 0.f : na[j];
-            float td = (r[j] + gamma * nvj) - v[j];
-            a[j] = td + gl * naj;
-            rt[j] = a[j] + v[j];
-            nv[j] = v[j];
-            na[j] = a[j];
-        }
-        if (VEC == 4) {
-            *(float4*)(adv + o) = make_float4(a[0], a[1], a[2], a[3]);
-            *(float4*)(ret + o) = make_float4(rt[0], rt[1], rt[2], rt[3]);
-        } else {
-            for (int j = 0; j < VEC; ++j) {
-                adv[o + j] = a[j];
-                ret[o + j] = rt[j];
-            }
-        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        t_hi = t_nx;
     }
 }
 
@@ -179,7 +201,7 @@ __global__ __launch_bounds__(256) void metrics_partial_kernel(MetricJobs jobs, d
     double s = 0, q = 0;
     float mn = 3.402823466e+38f, mx = -3.402823466e+38f;
     for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * 256) {
-        float x = J.x[i];
+        float x = J.cols ? J.x[(i / J.cols) * J.ld + i % J.cols] : J.x[i];
         if (J.abs_value) x = fabsf(x);
         s += x;
         q += (double)x * x;
@@ -385,7 +407,7 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(mlearn_rollout_view ro,
         int64_t seq = seqs[j];
         int64_t c = seq / ro.N, b = seq % ro.N;
         int64_t t = c * ro.bptt_len + tl;
-        double x = ro.advantages[t * ro.N + b];
+        double x = ro.advantages[t * ro.ld + b];
         s += x;
         q += x * x;
     }
@@ -531,16 +553,18 @@ int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* don
     if (T == 0 || N == 0) return MLEARN_OK;
     ML_REQUIRE(rewards && values && dones && bootstrap && advantages && returns,
                "gae: null pointer");
+    ML_REQUIRE(N <= ((int64_t)1 << 28), "gae: N > 2^28 columns");
     float gl = gamma * gae_lambda;  // cfg.gamma * cfg.gae_lambda (algo_common.py:120)
-    bool vec = (N % 4 == 0) && ((uintptr_t)rewards % 16 == 0) && ((uintptr_t)values % 16 == 0) &&
-               ((uintptr_t)bootstrap % 16 == 0) && ((uintptr_t)advantages % 16 == 0) &&
-               ((uintptr_t)returns % 16 == 0) && ((uintptr_t)dones % 4 == 0);
-    if (vec) {
-        hipLaunchKernelGGL(gae_kernel<4>, dim3(grid_for(N / 4, 256)), dim3(256), 0, S(stream),
-                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma, gl);
+    // Blocks of 64 below 2^20 columns so more CUs share the serial T loop (the
+    // operating point N = 8192 is latency-bound), 256 above (HBM-bound).
+    if (N >= (int64_t)1 << 20) {
+        hipLaunchKernelGGL((gae_kernel<1, 8>), dim3(grid_for(N, 256)), dim3(256), 0, S(stream),
+                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma,
+                           gl);
     } else {
-        hipLaunchKernelGGL(gae_kernel<1>, dim3(grid_for(N, 256)), dim3(256), 0, S(stream),
-                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma, gl);
+        hipLaunchKernelGGL((gae_kernel<1, 16>), dim3(grid_for(N, 64)), dim3(64), 0, S(stream),
+                           rewards, values, dones, bootstrap, advantages, returns, T, N, gamma,
+                           gl);
     }
     return check_launch("gae");
 }
@@ -628,6 +652,10 @@ int mlearn_metrics_f32(const mlearn_metric_job* jobs, int32_t num_jobs, float* o
     MetricJobs J;
     for (int i = 0; i < num_jobs; ++i) {
         ML_REQUIRE(jobs[i].n >= 0 && (jobs[i].n == 0 || jobs[i].x), "metrics: bad job %d", i);
+        ML_REQUIRE(jobs[i].cols >= 0 && (jobs[i].cols == 0 || (jobs[i].ld >= jobs[i].cols &&
+                                                                jobs[i].n % jobs[i].cols == 0)),
+                   "metrics: job %d window (cols %lld, ld %lld) does not tile n", i,
+                   (long long)jobs[i].cols, (long long)jobs[i].ld);
         J.j[i] = jobs[i];
     }
     hipLaunchKernelGGL(metrics_partial_kernel, dim3(kMetricBlocks, num_jobs), dim3(256), 0,
@@ -658,7 +686,10 @@ int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t
                "adv_stats: minibatches exceed the sequences");
     // partials layout: [num_mb][kStatBlocks][2] scratch followed by [num_mb][2] sums
     double* scratch = partials + 2 * num_mb;
-    hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb, kStatBlocks), dim3(256), 0, S(stream), *ro,
+    mlearn_rollout_view v = *ro;
+    if (v.ld == 0) v.ld = v.N;
+    ML_REQUIRE(v.ld >= v.N, "adv_stats: ld %lld < N %lld", (long long)v.ld, (long long)v.N);
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb, kStatBlocks), dim3(256), 0, S(stream), v,
                        perm, mb_size, scratch);
     hipLaunchKernelGGL(adv_stats_reduce_kernel, dim3((num_mb + 63) / 64), dim3(64), 0, S(stream),
                        (const double*)scratch, num_mb, partials);

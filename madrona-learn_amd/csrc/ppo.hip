@@ -32,7 +32,7 @@ struct RolloutK {
     const float* ret;
     const float* values;
     int T, bptt;
-    int64_t N;
+    int64_t N, ld;  // envs of this policy, row stride of the store
 };
 
 struct HpK {
@@ -310,7 +310,7 @@ __device__ inline int64_t store_row(const RolloutK& ro, const int32_t* mb_seq, i
     const uint32_t m = fu - tl * mbu;
     const uint32_t seq = (uint32_t)mb_seq[m];
     const uint32_t c = seq / nu, b = seq - c * nu;
-    return ((int64_t)c * ro.bptt + tl) * ro.N + b;
+    return ((int64_t)c * ro.bptt + tl) * ro.ld + b;
 }
 
 template <typename T, int H, int L>
@@ -1018,7 +1018,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 #endif
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
-               ro.T, ro.bptt_len, ro.N};
+               ro.T, ro.bptt_len, ro.N, ro.ld ? ro.ld : ro.N};
     HpK hp{};
     hp.clip = h.clip_coef;
     hp.vcoef = h.value_loss_coef;
@@ -1110,6 +1110,8 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro->N >= 1 && ro->N < (1ll << 31) && (int64_t)mb_size * ro->bptt_len < (1ll << 31),
                "ppo: N and rows per minibatch must be < 2^31");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");
+    ML_REQUIRE(ro->ld == 0 || ro->ld >= ro->N, "ppo: ld %lld < N %lld", (long long)ro->ld,
+               (long long)ro->N);
     ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
                "ppo: null rollout array");
     ML_REQUIRE(!hp->clip_value_loss || ro->values, "ppo: clip_value_loss needs values");

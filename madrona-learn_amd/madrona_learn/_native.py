@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -40,7 +40,8 @@ class MlpPolicy(Structure):
 
 
 class MetricJob(Structure):
-    _fields_ = [("x", c_void_p), ("n", c_int64), ("abs_value", c_int32), ("pad", c_int32)]
+    _fields_ = [("x", c_void_p), ("n", c_int64), ("cols", c_int64), ("ld", c_int64),
+                ("abs_value", c_int32), ("pad", c_int32)]
 
 
 class PostStep(Structure):
@@ -52,7 +53,8 @@ class PostStep(Structure):
 class RolloutView(Structure):
     _fields_ = [("obs", c_void_p), ("actions", c_void_p), ("log_probs", c_void_p),
                 ("advantages", c_void_p), ("returns", c_void_p), ("values", c_void_p),
-                ("T", c_int32), ("bptt_len", c_int32), ("N", c_int64)]
+                ("dones", c_void_p), ("T", c_int32), ("bptt_len", c_int32), ("N", c_int64),
+                ("ld", c_int64)]
 
 
 class PPOHparams(Structure):

@@ -60,27 +60,38 @@ class Metric:
 
 
 class TrainingMetrics:
-    def __init__(self, names, buffer_size, device, per_policy=True):
+    """Latest-record buffer [P, names, 5] (P = train policies on this rank;
+    the reference keeps a leading policy axis on per-policy metrics,
+    metrics.py:110-147) plus a metrics_buffer_size ring of it."""
+
+    def __init__(self, names, buffer_size, device, per_policy=True, num_policies=1):
         self.names = list(names)
         self.index = {n: i for i, n in enumerate(self.names)}
         self.buffer_size = int(buffer_size)
         self.per_policy = per_policy
-        self.latest = torch.zeros((len(self.names), 5), dtype=torch.float32, device=device)
-        self.latest[:, 2] = FLT_MAX
-        self.latest[:, 3] = -FLT_MAX
-        self.ring = self.latest.unsqueeze(0).repeat(self.buffer_size, 1, 1)
+        self.num_policies = int(num_policies)
+        self.latest = torch.zeros((self.num_policies, len(self.names), 5), dtype=torch.float32,
+                                  device=device)
+        self.latest[..., 2] = FLT_MAX
+        self.latest[..., 3] = -FLT_MAX
+        self.ring = self.latest.unsqueeze(0).repeat(self.buffer_size, 1, 1, 1)
         self.update_idx = 0
         self.cur_buffer_offset = 0
 
-    def slot(self, name):
+    def slot(self, name, policy=0):
         """[5] device view of the latest record of `name` (kernels write here)."""
-        return self.latest[self.index[name]]
+        return self.latest[policy, self.index[name]]
 
-    def record_tensor(self, name, vec5):
-        self.latest[self.index[name]].copy_(vec5)
+    def slots(self, first, count, policy=0):
+        """[count, 5] device view of `count` consecutive metrics from `first`."""
+        i = self.index[first]
+        return self.latest[policy, i:i + count]
 
-    def record_scalar(self, name, value):
-        s = self.latest[self.index[name]]
+    def record_tensor(self, name, vec5, policy=0):
+        self.latest[policy, self.index[name]].copy_(vec5)
+
+    def record_scalar(self, name, value, policy=0):
+        s = self.latest[policy, self.index[name]]
         s[0] = value
         s[1] = 0.0
         s[2] = value
@@ -92,15 +103,18 @@ class TrainingMetrics:
         self.update_idx += 1
         self.cur_buffer_offset = (self.cur_buffer_offset + 1) % self.buffer_size
 
-    def last(self):
+    def last(self, policy=0):
         """Host dict name -> Metric of the most recently completed update."""
         idx = (self.cur_buffer_offset - 1) % self.buffer_size
-        host = self.ring[idx].cpu().numpy()
+        host = self.ring[idx, policy].cpu().numpy()
         return {n: Metric.from_vector(self.per_policy, host[i]) for i, n in enumerate(self.names)}
 
     def pretty_print(self, tab=2):
         out = []
-        for n, m in self.last().items():
-            out.append(" " * tab + f"{n}: mean {m.mean:.4e} std {np.sqrt(max(m.var, 0)):.4e} "
-                       f"min {m.min:.4e} max {m.max:.4e} count {m.count}")
+        for p in range(self.num_policies):
+            if self.num_policies > 1:
+                out.append(" " * tab + f"policy {p}:")
+            for n, m in self.last(p).items():
+                out.append(" " * tab + f"{n}: mean {m.mean:.4e} std {np.sqrt(max(m.var, 0)):.4e} "
+                           f"min {m.min:.4e} max {m.max:.4e} count {m.count}")
         print("\n".join(out))

@@ -76,8 +76,11 @@ class PPO(AlgoBase):  # ppo.py:49-106
         return list(names) + PPO_METRICS
 
     # ------------------------------------------------------------------
-    def prepare(self, cfg, policy_state, train_state, store, dp):
-        """Allocate the per-update buffers once (graph-capture safe)."""
+    def prepare(self, cfg, policy_state, train_state, view, dp, policy_idx=0):
+        """Allocate the per-update buffers once (graph-capture safe).  ``view``
+        is the rollout view of this policy's env columns; ``dp`` the data
+        parallel group that trains this policy; ``policy_idx`` its slot in the
+        rank's metrics."""
         algo = cfg.algo
         if cfg.filter_advantages or cfg.importance_sample_trajectories:
             raise NotImplementedError(
@@ -87,7 +90,7 @@ class PPO(AlgoBase):  # ppo.py:49-106
             raise NotImplementedError("value normalisation is SURVEY §8(f) row 2")
         C = cfg.num_bptt_chunks
         self.bptt = cfg.steps_per_update // C
-        self.num_seq = C * store.N                    # per rank
+        self.num_seq = C * view.N                     # per rank
         self.mb = int(algo.minibatch_size)            # per rank
         if self.num_seq % self.mb != 0:               # ppo.py:439
             raise ValueError(f"{self.num_seq} sequences not divisible by minibatch_size "
@@ -102,7 +105,8 @@ class PPO(AlgoBase):  # ppo.py:49-106
         rows = self.mb * self.bptt
         nbytes = nat.lib().mlearn_ppo_workspace_bytes(policy_state.desc, rows)
         self.ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
-        self.view = store.view(self.bptt)
+        self.view = view
+        self.policy_idx = policy_idx
         K = policy_state.arch.num_groups
         hp = nat.PPOHparams()
         hp.clip_coef = float(algo.clip_coef)
@@ -151,7 +155,7 @@ class PPO(AlgoBase):  # ppo.py:49-106
             nat.check(L.mlearn_adv_stats_finish(nat.ptr(self.adv_part[e]), self.num_mb,
                                                 self.count, nat.ptr(self.adv_stats[e]), strm),
                       "adv_stats_finish")
-        loss_out = metrics.latest[metrics.index["Loss"]:metrics.index["Loss"] + 5]
+        loss_out = metrics.slots("Loss", 5, policy=self.policy_idx)
         for e in range(self.E):
             for m in range(self.num_mb):
                 seqs = self.perm[e, m * self.mb:(m + 1) * self.mb]
@@ -164,6 +168,11 @@ class PPO(AlgoBase):  # ppo.py:49-106
                 train_state.optimizer_step(policy_state)
                 metrics = user_metrics_cb(metrics, e, {"sequence_ids": seqs}, policy_state,
                                           train_state)
-        nat.check(L.mlearn_counters_add(nat.ptr(epoch_ctr), 1, (nat.c_uint64 * 1)(self.E), strm),
-                  "epoch counter")
         return metrics
+
+    def advance_epochs(self, epoch_ctr):
+        """Move the device epoch counter past this update's epochs (once per
+        update, after every policy's update_program)."""
+        nat.check(nat.lib().mlearn_counters_add(nat.ptr(epoch_ctr), 1,
+                                                (nat.c_uint64 * 1)(self.E),
+                                                nat.stream_handle()), "epoch counter")

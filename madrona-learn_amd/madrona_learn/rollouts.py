@@ -41,12 +41,14 @@ class RolloutConfig:  # rollouts.py:28-134 (self-play / single-policy path)
               reward_dtype=torch.float32, prob_dtype=torch.float32,
               policy_chunk_size_override=0):
         complex_mm = (num_current_policies > 1 and self_play_portion != 1.0) or \
-            num_past_policies > 0 or cross_play_portion > 0 or past_play_portion > 0
-        if complex_mm or num_current_policies != 1:
+            num_past_policies > 0 or cross_play_portion > 0 or past_play_portion > 0 or \
+            static_play_portion > 0
+        if complex_mm:
             raise NotImplementedError(
-                "PBT matchmaking / multi-policy rollouts are SURVEY §8(f) row 3; the fused "
-                "path runs one policy per device (PBT = one policy per GPU)")
-        assert num_past_policies == 0
+                "cross-play / past-play matchmaking (pbt.py:135-247) is outside the fused "
+                "path; populations use the self-play split (pbt.py:130-133): policy p owns "
+                "env columns [p*B, (p+1)*B)")
+        assert sim_batch_size % num_current_policies == 0
         policy_chunk_size = sim_batch_size // num_current_policies  # rollouts.py:104-108
         if policy_chunk_size_override != 0:
             policy_chunk_size = policy_chunk_size_override
@@ -147,17 +149,25 @@ class RolloutStore:
                 "values": self.values, "rewards": self.rewards, "dones": self.dones,
                 "advantages": self.advantages, "returns": self.returns}
 
-    def view(self, bptt_len):
+    def view(self, bptt_len, col0=0, ncols=None):
+        """Rollout view of env columns [col0, col0 + ncols) (one policy of a
+        population; the whole store by default)."""
+        ncols = self.N - col0 if ncols is None else ncols
+        assert 0 <= col0 and col0 + ncols <= self.N
+        D = self.obs.shape[2]
+        K = self.actions.shape[2]
         v = nat.RolloutView()
-        v.obs = self.obs.data_ptr()
-        v.actions = self.actions.data_ptr()
-        v.log_probs = self.log_probs.data_ptr()
-        v.advantages = self.advantages.data_ptr()
-        v.returns = self.returns.data_ptr()
-        v.values = self.values.data_ptr()
+        v.obs = self.obs.data_ptr() + col0 * D * self.obs.element_size()
+        v.actions = self.actions.data_ptr() + col0 * K * 4
+        v.log_probs = self.log_probs.data_ptr() + col0 * K * 4
+        v.advantages = self.advantages.data_ptr() + col0 * 4
+        v.returns = self.returns.data_ptr() + col0 * 4
+        v.values = self.values.data_ptr() + col0 * 4
+        v.dones = self.dones.data_ptr() + col0
         v.T = self.T
         v.bptt_len = bptt_len
-        v.N = self.N
+        v.N = ncols
+        v.ld = self.N
         return v
 
 
@@ -179,7 +189,14 @@ def obs_to_matrix(obs, N):
 
 
 class RolloutManager:  # rollouts.py:373-826
-    def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_state, env_offset=0):
+    """Runs the rollout of every train policy on this rank.  ``policy_states``
+    is one PolicyState, or a list of them for a population: policy p owns the
+    contiguous env columns [p*B, (p+1)*B) of the rank's N envs (the self-play
+    split of pbt_init_matchmaking, pbt.py:130-133) and writes those columns
+    of the shared [T][N] store, so the sim steps all N envs at once and GAE
+    runs over the whole store in one launch."""
+
+    def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_states, env_offset=0):
         self.train_cfg = train_cfg
         self._cfg = init_rollout_state.cfg
         assert train_cfg.steps_per_update % train_cfg.num_bptt_chunks == 0  # rollouts.py:387
@@ -187,29 +204,46 @@ class RolloutManager:  # rollouts.py:373-826
         self.C = train_cfg.num_bptt_chunks
         self.bptt = self.T // self.C
         self.N = self._cfg.sim_batch_size
-        self.policy_state = policy_state
-        self.prefix = policy_state.actor_critic.backbone.prefix
-        arch = policy_state.arch
+        self.policies = list(policy_states) if isinstance(policy_states, (list, tuple)) \
+            else [policy_states]
+        self.P = len(self.policies)
+        if self.N % self.P != 0:
+            raise ValueError(f"{self.N} envs do not split over {self.P} policies")
+        self.B = self.N // self.P
+        self.policy_state = self.policies[0]
+        self.prefix = self.policy_state.actor_critic.backbone.prefix
+        arch = self.policy_state.arch
+        for ps in self.policies[1:]:
+            assert ps.arch == arch, "population policies must share one architecture"
         self.store = RolloutStore(self.T, self.N, arch.obs_dim, arch.num_groups, arch.dtype,
-                                  policy_state.device)
+                                  self.policy_state.device)
         self.env_offset = int(env_offset)
         self.use_advantages = train_cfg.compute_advantages
-        dev = policy_state.device
+        dev = self.policy_state.device
         self._resets = torch.zeros((self._cfg.num_worlds, 1), dtype=torch.int32, device=dev)
         self._metrics_ws = torch.zeros(int(nat.lib().mlearn_metrics_workspace_bytes(6)),
                                        dtype=torch.uint8, device=dev)
         s = self.store
-        jobs = (nat.MetricJob * 6)()
-        for i, (x, n, a) in enumerate([(s.rewards, self.T * self.N, 0),
-                                       (s.values, self.T * self.N, 0),
-                                       (s.returns, self.T * self.N, 0),
-                                       (s.env_returns_trace, self.T * self.N, 0),
-                                       (s.advantages, self.T * self.N, 0),
-                                       (s.bootstrap, self.N, 0)]):
-            jobs[i].x = x.data_ptr()
-            jobs[i].n = n
-            jobs[i].abs_value = a
-        self._jobs = jobs
+        TN = self.T * self.B
+        self._jobs = []
+        for p in range(self.P):
+            c0 = p * self.B
+            jobs = (nat.MetricJob * 6)()
+            for i, (x, n, cols) in enumerate([(s.rewards, TN, self.B), (s.values, TN, self.B),
+                                              (s.returns, TN, self.B),
+                                              (s.env_returns_trace, TN, self.B),
+                                              (s.advantages, TN, self.B),
+                                              (s.bootstrap, self.B, 0)]):
+                jobs[i].x = x.data_ptr() + c0 * 4
+                jobs[i].n = n
+                jobs[i].cols = cols if self.P > 1 else 0
+                jobs[i].ld = self.N
+                jobs[i].abs_value = 0
+            self._jobs.append(jobs)
+
+    def view(self, p=0):
+        """Rollout view of policy p's env columns."""
+        return self.store.view(self.bptt, p * self.B, self.B)
 
     def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
         return list(names) + ROLLOUT_METRICS
@@ -218,25 +252,26 @@ class RolloutManager:  # rollouts.py:373-826
         x = self.prefix(obs, train=False)
         return obs_to_matrix(x, self.N)
 
-    def _post_desc(self, t, rew, dn, rollout_state, gamma):
-        """Post-step descriptor of env step t (rollouts.py:933-973); the tensors it
-        points at are kept alive until the next collect."""
+    def _post_desc(self, t, p, rew, dn, rollout_state, gamma):
+        """Post-step descriptor of env step t for policy p's columns
+        (rollouts.py:933-973); the tensors it points at are kept alive until
+        the next collect."""
         s = self.store
         if not hasattr(self, "_posts"):
-            self._posts = [nat.PostStep() for _ in range(self.T)]
+            self._posts = [[nat.PostStep() for _ in range(self.P)] for _ in range(self.T)]
             self._post_keep = [None] * self.T
-        p = self._posts[t]
-        p.rewards, p.dones = nat.ptr(rew), nat.ptr(dn)
-        p.store_rewards, p.store_dones = nat.ptr(s.rewards[t]), nat.ptr(s.dones[t])
-        p.env_returns = nat.ptr(rollout_state.env_returns)
-        p.env_returns_trace = nat.ptr(s.env_returns_trace[t])
-        p.gamma = gamma
+        c = slice(p * self.B, (p + 1) * self.B)
+        d = self._posts[t][p]
+        d.rewards, d.dones = nat.ptr(rew[c]), nat.ptr(dn[c])
+        d.store_rewards, d.store_dones = nat.ptr(s.rewards[t, c]), nat.ptr(s.dones[t, c])
+        d.env_returns = nat.ptr(rollout_state.env_returns[c])
+        d.env_returns_trace = nat.ptr(s.env_returns_trace[t, c])
+        d.gamma = gamma
         self._post_keep[t] = (rew, dn)
-        return p
+        return d
 
     def collect(self, train_state_mgr, rollout_state: RolloutState, metrics, user_hooks):
         """rollouts.py:501-577 restated on the fused kernels."""
-        ps = self.policy_state
         s = self.store
         L = nat.lib()
         strm = nat.stream_handle()
@@ -245,11 +280,15 @@ class RolloutManager:  # rollouts.py:373-826
             rollout_state, train_state_mgr.user_state)
         key = rollout_state.prng_key
         step_ctr = rollout_state.counters[0:1]
-        post = None  # post-step of env step t-1, fused into the policy launch of step t
+        B = self.B
+        posts = [None] * self.P  # post-step of env step t-1, fused into the policy launches of t
         for t in range(self.T):
             obs = self.prep_obs(rollout_state.cur_obs)
-            ps.rollout_step(obs, s.obs[t], s.actions[t], s.log_probs[t], s.values[t], key,
-                            step_ctr, t, self.env_offset, sample=True, post=post)
+            for p, ps in enumerate(self.policies):
+                c = slice(p * B, (p + 1) * B)
+                ps.rollout_step(obs[c], s.obs[t, c], s.actions[t, c], s.log_probs[t, c],
+                                s.values[t, c], key, step_ctr, t, self.env_offset + p * B,
+                                sample=True, post=posts[p])
             step_input = {
                 "state": rollout_state.sim_state,
                 "actions": s.actions[t],
@@ -263,11 +302,16 @@ class RolloutManager:  # rollouts.py:373-826
                 rew = rew.float()
             dn = out["dones"].reshape(-1)
             dn = dn.view(torch.uint8) if dn.dtype == torch.bool else (dn != 0).view(torch.uint8)
-            post = self._post_desc(t, rew.contiguous(), dn.contiguous(), rollout_state, gamma)
+            rew, dn = rew.contiguous(), dn.contiguous()
+            posts = [self._post_desc(t, p, rew, dn, rollout_state, gamma)
+                     for p in range(self.P)]
             rollout_state.sim_state = out["state"]
             rollout_state.cur_obs = out["obs"]
         # bootstrap values (rollouts.py:607-635), with the last post-step
-        ps.critic_only(self.prep_obs(rollout_state.cur_obs), s.bootstrap, post=post)
+        obs = self.prep_obs(rollout_state.cur_obs)
+        for p, ps in enumerate(self.policies):
+            c = slice(p * B, (p + 1) * B)
+            ps.critic_only(obs[c], s.bootstrap[c], post=posts[p])
         rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:
@@ -275,9 +319,10 @@ class RolloutManager:  # rollouts.py:373-826
                                out_adv=s.advantages, out_ret=s.returns)
         else:
             compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s.returns)
-        i0 = metrics.index["Rewards"]
-        nat.check(L.mlearn_metrics_f32(self._jobs, 6, nat.ptr(metrics.latest[i0:i0 + 6]),
-                                       nat.ptr(self._metrics_ws), strm), "rollout metrics")
+        for p in range(self.P):
+            nat.check(L.mlearn_metrics_f32(self._jobs[p], 6,
+                                           nat.ptr(metrics.slots("Rewards", 6, policy=p)),
+                                           nat.ptr(self._metrics_ws), strm), "rollout metrics")
         nat.check(L.mlearn_counters_add(nat.ptr(rollout_state.counters), 1,
                                         (nat.c_uint64 * 1)(self.T), strm), "counters")
         data = RolloutData(s, self.C)

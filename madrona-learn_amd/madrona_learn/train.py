@@ -18,7 +18,7 @@ import torch
 
 from . import _native as nat
 from .cfg import TrainConfig
-from .dist import DataParallel
+from .dist import DataParallel, policy_placement, world
 from .metrics import TrainingMetrics
 from .policy import Policy
 from .profile import profile
@@ -56,14 +56,15 @@ def _split_seed(seed, stream):
 
 
 class TrainingManager:  # train.py:35-64
-    def __init__(self, state, rollout, metrics, cfg, rollout_mgr, algo, user_hooks, dp,
+    def __init__(self, state, rollout, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                  update_idx=0, use_graph=True, profile_port=None):
         self.state = state
         self.rollout = rollout
         self.metrics = metrics
         self.cfg = cfg
         self.rollout_mgr = rollout_mgr
-        self.algo = algo
+        self.algos = list(algos)
+        self.algo = self.algos[0]
         self.user_hooks = user_hooks
         self.dp = dp
         self.update_idx = int(update_idx)
@@ -80,9 +81,15 @@ class TrainingManager:  # train.py:35-64
                  self.metrics) = self.rollout_mgr.collect(self.state, self.rollout, self.metrics,
                                                           self.user_hooks)
             with profile("Learn"):
-                self.metrics = yield from self.algo.update_program(
-                    self.cfg, self.state.policy_states, self.state.train_states, rollout_data,
-                    self.user_hooks.optimize_metrics, self.metrics, self.rollout.counters[1:2])
+                # algo_wrapper = vmap over the train policies (train.py:165-174,
+                # 206-210): each local policy updates on its own env columns
+                epoch_ctr = self.rollout.counters[1:2]
+                for ps, ts, algo in zip(self.state.policy_list, self.state.train_list,
+                                        self.algos):
+                    self.metrics = yield from algo.update_program(
+                        self.cfg, ps, ts, rollout_data, self.user_hooks.optimize_metrics,
+                        self.metrics, epoch_ctr)
+                self.algos[0].advance_epochs(epoch_ctr)
 
     def _run_eager(self):
         gen = self._program()
@@ -160,24 +167,31 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     if device.type != "cuda":
         raise ValueError(f"device must be a GPU, got {device}")
     torch.cuda.set_device(device)
-    dp = DataParallel()
-    algo = cfg.algo.setup()
-    if cfg.pbt is not None:
-        raise NotImplementedError("PBT populations are SURVEY §8(f) row 3")
     if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
         raise NotImplementedError(
             "the fused path implements the scalar DenseLayerCritic: set "
             "TrainConfig(dreamer_v3_critic=False) (DreamerV3 two-hot is SURVEY §8(f) row 2)")
+    num_policies = 1
+    if cfg.pbt is not None:
+        pbt = cfg.pbt
+        if pbt.num_past_policies != 0 or pbt.self_play_portion != 1.0:
+            raise NotImplementedError(
+                "populations run the self-play split (pbt.py:130-133); past/cross-play "
+                "matchmaking (pbt.py:135-247) is outside the fused path")
+        num_policies = int(pbt.num_train_policies)
+    # policy placement: which train policies this rank holds, and the ranks it
+    # shares gradients with (dist.policy_placement)
+    policy_ids, dp = policy_placement(num_policies)
+    rank, _ = world()
 
     sim_batch = cfg.num_agents_per_world * cfg.num_worlds
     rollout_cfg = RolloutConfig.setup(
-        num_current_policies=1, num_past_policies=0, num_teams=1,
+        num_current_policies=len(policy_ids), num_past_policies=0, num_teams=1,
         team_size=cfg.num_agents_per_world, sim_batch_size=sim_batch, actions_cfg=cfg.actions,
         self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0,
         static_play_portion=0.0, reward_gamma=cfg.gamma,
         custom_policy_ids=cfg.custom_policy_ids, policy_dtype=cfg.compute_dtype)
     rollout_key = _split_seed(cfg.seed, 1)
-    update_key = _split_seed(cfg.seed, 2)
     rnn_states = policy.actor_critic.init_recurrent_state(sim_batch)
     rollout_state = RolloutState.create(rollout_cfg, sim_fns, rollout_key, rnn_states,
                                         init_sim_ctrl, device=device)
@@ -189,25 +203,38 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     preprocess = policy.obs_preprocess
     if preprocess is not None:
         preprocess.fused_cast_dtype(cfg.compute_dtype)
-    rng = np.random.default_rng(int(cfg.seed))
-    ps = PolicyState(policy.actor_critic, arch, preprocess, device, rng)
-    dp.broadcast_(ps.params)
-    ps.sync_weights()
-    ts = PolicyTrainState(cfg, algo.init_hyperparams(cfg), ps, update_key)
-    tsm = TrainStateManager(policy_states=ps, train_states=ts, pbt_rng=None,
+    # one PolicyState / PolicyTrainState per train policy (_make_policies,
+    # train_state.py:439-488: independent init and optimizer RNG per policy)
+    pss, tss, algos = [], [], []
+    for pid in policy_ids:
+        algo = cfg.algo.setup()
+        rng = np.random.default_rng(int(cfg.seed) if num_policies == 1
+                                    else [int(cfg.seed), int(pid)])
+        ps = PolicyState(policy.actor_critic, arch, preprocess, device, rng)
+        dp.broadcast_(ps.params)
+        ps.sync_weights()
+        ts = PolicyTrainState(cfg, algo.init_hyperparams(cfg), ps,
+                              _split_seed(cfg.seed, 2 + 16 * pid))
+        ts.policy_id = pid
+        pss.append(ps)
+        tss.append(ts)
+        algos.append(algo)
+    tsm = TrainStateManager(policy_states=pss[0] if len(pss) == 1 else pss,
+                            train_states=tss[0] if len(tss) == 1 else tss, pbt_rng=None,
                             user_state=user_hooks.init_user_state())
     start = 0
     if restore_ckpt is not None:
         tsm, start = tsm.load(restore_ckpt)
 
-    rollout_mgr = RolloutManager(cfg, rollout_state, ps, env_offset=dp.rank * sim_batch)
-    names = algo.add_metrics(cfg, [])
+    rollout_mgr = RolloutManager(cfg, rollout_state, pss, env_offset=rank * sim_batch)
+    names = algos[0].add_metrics(cfg, [])
     names = rollout_mgr.add_metrics(cfg, names)
     names = user_hooks.add_metrics(names)
-    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device)
-    algo.prepare(cfg, ps, ts, rollout_mgr.store, dp)
+    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device, num_policies=len(pss))
+    for p, (ps, ts, algo) in enumerate(zip(pss, tss, algos)):
+        algo.prepare(cfg, ps, ts, rollout_mgr.view(p), dp, policy_idx=p)
     print(cfg)
-    return TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algo, user_hooks, dp,
+    return TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                            update_idx=start, use_graph=use_graph, profile_port=profile_port)
 
 

@@ -245,18 +245,38 @@ class PolicyTrainState:
 
 @dataclass
 class TrainStateManager:  # train_state.py:139-304
-    policy_states: PolicyState
-    train_states: PolicyTrainState
+    """``policy_states`` / ``train_states`` are one PolicyState /
+    PolicyTrainState, or lists of them when the rank holds several train
+    policies of a population (the reference stacks them on a leading policy
+    axis)."""
+    policy_states: Any
+    train_states: Any
     pbt_rng: Any = None
     user_state: Any = None
 
+    @property
+    def policy_list(self):
+        ps = self.policy_states
+        return list(ps) if isinstance(ps, (list, tuple)) else [ps]
+
+    @property
+    def train_list(self):
+        ts = self.train_states
+        return list(ts) if isinstance(ts, (list, tuple)) else [ts]
+
     def save(self, update_idx, path):
         torch.save({"update_idx": int(update_idx),
-                    "policy": self.policy_states.state_dict(),
-                    "train": self.train_states.state_dict()}, path)
+                    "policies": [p.state_dict() for p in self.policy_list],
+                    "train": [t.state_dict() for t in self.train_list]}, path)
 
     def load(self, path):
         sd = torch.load(path, map_location="cpu", weights_only=True)
-        self.policy_states.load_state_dict(sd["policy"])
-        self.train_states.load_state_dict(sd["train"])
+        pol, tr = sd["policies"], sd["train"]
+        if len(pol) != len(self.policy_list):
+            raise ValueError(f"checkpoint holds {len(pol)} policies, this rank trains "
+                             f"{len(self.policy_list)}")
+        for p, d in zip(self.policy_list, pol):
+            p.load_state_dict(d)
+        for t, d in zip(self.train_list, tr):
+            t.load_state_dict(d)
         return self, sd["update_idx"]

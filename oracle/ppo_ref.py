@@ -479,8 +479,22 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
     (integer fake-policy KAT, tests/test_rollout_kat.py)."""
     if policy_fn is not None:
         return _rollout_fake(policy_fn, env, T, gamma, env_returns)
-    P = unflatten(flat_p, lay, ad)
     N = env.N
+    if isinstance(flat_p, (list, tuple)):
+        # a population: policy p acts for env columns [p*B, (p+1)*B), the
+        # self-play split of pbt_init_matchmaking (pbt.py:130-133)
+        Ps = [unflatten(fp, lay, ad) for fp in flat_p]
+        B = N // len(Ps)
+
+        def forward_all(x):
+            outs = [forward(Pp, x[p * B:(p + 1) * B], mode, ad) for p, Pp in enumerate(Ps)]
+            return (np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs]),
+                    None)
+    else:
+        P = unflatten(flat_p, lay, ad)
+
+        def forward_all(x):
+            return forward(P, x, mode, ad)
     A = int(sum(buckets))
     K = len(buckets)
     store = {k: [] for k in ("obs", "actions", "log_probs", "values", "rewards", "dones")}
@@ -490,7 +504,7 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
     obs = env.obs.copy()
     for t in range(T):
         x = rnd(obs, mode, ad)
-        logits, V, _ = forward(P, x, mode, ad)
+        logits, V, _ = forward_all(x)
         gum = native.gumbel_table(key[0], key[1], step_base + t, env.eoff, N, A)
         acts, logp = sample_actions(logits.astype(np.float32), buckets, gum)
         if actions_override is not None:
@@ -507,7 +521,7 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
         store["rewards"].append(rew)
         store["dones"].append(done)
         er = np.where(done.astype(bool), np.float32(0), er).astype(np.float32)
-    _, boot, _ = forward(P, rnd(obs, mode, ad), mode, ad)
+    _, boot, _ = forward_all(rnd(obs, mode, ad))
     return _finish_store(store, boot, trace), er
 
 

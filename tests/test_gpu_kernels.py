@@ -172,18 +172,26 @@ def test_metrics(gpu):
     rng = np.random.default_rng(8)
     xs = [rng.standard_normal(n).astype(np.float32) * 5 + 1 for n in (1, 1000, 262144)]
     ts = [torch.from_numpy(x).to(gpu) for x in xs]
-    jobs = (nat.MetricJob * 3)()
+    # a [32][48] window (columns 16..63) of a [32][80] array: one policy's env
+    # columns of a population store
+    big = rng.standard_normal((32, 80)).astype(np.float32)
+    tb = torch.from_numpy(big).to(gpu)
+    jobs = (nat.MetricJob * 4)()
     for i, t in enumerate(ts):
         jobs[i].x = t.data_ptr()
         jobs[i].n = t.numel()
         jobs[i].abs_value = 1 if i == 2 else 0
-    out = torch.zeros((3, 5), device=gpu)
-    ws = torch.zeros(int(nat.lib().mlearn_metrics_workspace_bytes(3)), dtype=torch.uint8,
+    jobs[3].x = tb.data_ptr() + 16 * 4
+    jobs[3].n = 32 * 48
+    jobs[3].cols = 48
+    jobs[3].ld = 80
+    out = torch.zeros((4, 5), device=gpu)
+    ws = torch.zeros(int(nat.lib().mlearn_metrics_workspace_bytes(4)), dtype=torch.uint8,
                      device=gpu)
-    nat.check(nat.lib().mlearn_metrics_f32(jobs, 3, nat.ptr(out), nat.ptr(ws),
+    nat.check(nat.lib().mlearn_metrics_f32(jobs, 4, nat.ptr(out), nat.ptr(ws),
                                            nat.stream_handle()))
     got = out.cpu().numpy()
-    for i, x in enumerate(xs):
+    for i, x in enumerate(xs + [big[:, 16:64].reshape(-1)]):
         x = np.abs(x) if i == 2 else x
         x = x.astype(np.float64)
         np.testing.assert_allclose(got[i, 0], x.mean(), rtol=1e-5, atol=1e-6)

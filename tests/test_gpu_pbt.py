@@ -1,0 +1,96 @@
+"""Population (PBT self-play split, config P of SURVEY §8(d)) on the GPU
+path: TrainConfig.pbt with 2 train policies on one rank.  Policy p acts for
+env columns [p*B, (p+1)*B) (pbt.py:130-133), has its own initial parameters,
+optimizer state and minibatch RNG (train_state.py:439-488), and its PPO
+update sees only its own columns (the vmap of algo_wrapper, train.py:165-174).
+Checked against the oracle: the population rollout replayed on the oracle
+env, then one oracle PPO update per policy on that policy's columns."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import native as onat
+from oracle import ppo_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+BUCKETS = [4, 8, 5, 5, 2, 2]
+N, D, H, T, P = 128, 64, 64, 32, 2
+
+
+def _setup(gpu, dtype=torch.float32, use_graph=False):
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from tests.test_gpu_train import make_policy
+    env = DummyVecEnv(N, D, 6, seed=3, device=gpu)
+    cfg = ml.TrainConfig(
+        num_worlds=N, num_agents_per_world=1, num_updates=1,
+        actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
+        lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16, clip_coef=0.2,
+                                   value_loss_coef=0.5, entropy_coef={"actions": 0.01},
+                                   max_grad_norm=0.5),
+        num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=9, metrics_buffer_size=4,
+        dreamer_v3_critic=False, compute_dtype=dtype,
+        pbt=ml.PBTConfig(num_teams=1, team_size=1, num_train_policies=P, num_past_policies=0,
+                         self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0))
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(dtype, H), use_graph=use_graph)
+    return cfg, env, mgr
+
+
+def test_population_update_matches_oracle(gpu):
+    cfg, env, mgr = _setup(gpu)
+    pss, tss = mgr.state.policy_list, mgr.state.train_list
+    assert len(pss) == P and mgr.rollout_mgr.B == N // P
+    p0 = [ps.params.cpu().numpy().astype(np.float64) for ps in pss]
+    assert not np.array_equal(p0[0], p0[1]), "population members must init independently"
+    assert tss[0].update_prng_key != tss[1].update_prng_key
+    oenv = onat.Env(env.N, env.D, env.k0, env.k1, 0)
+    oenv.reset()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    lay = ref.param_layout(D, H, 2, 26)
+    ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="f32",
+                        gamma=cfg.gamma, actions_override=s.actions.cpu().numpy())
+    assert np.array_equal(s.rewards.cpu().numpy(), ro["rewards"])
+    assert np.array_equal(s.dones.cpu().numpy(), ro["dones"])
+    np.testing.assert_allclose(s.values.cpu().numpy(), ro["values"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(s.bootstrap.cpu().numpy(), ro["bootstrap"], rtol=1e-4,
+                               atol=1e-4)
+    np.testing.assert_allclose(s.log_probs.cpu().numpy(), ro["log_probs"], rtol=1e-4, atol=1e-4)
+    adv, ret = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(),
+                           s.dones.cpu().numpy(), s.bootstrap.cpu().numpy(), cfg.gamma,
+                           cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)
+    full = {k: v.cpu().numpy() for k, v in s.as_dict().items()}
+    B = N // P
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    for p in range(P):
+        c = slice(p * B, (p + 1) * B)
+        store = {k: (v[:, c] if v.ndim >= 2 else v[c]) for k, v in full.items()}
+        z = np.zeros_like(p0[p])
+        p1, _, _ = ref.ppo_update(
+            p0[p], (z, z.copy(), 0), [store], hp, BUCKETS, lay,
+            pss[p].init_norms.cpu().numpy().astype(np.float64), num_epochs=2,
+            minibatch_size=16, bptt=T, key=tss[p].update_prng_key, epoch_base=0, mode="f32",
+            lr=3e-4, max_grad_norm=0.5)
+        np.testing.assert_allclose(pss[p].params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
+        assert int(tss[p].step.item()) == 2 * (B // 16)
+        # per-policy rollout metrics cover that policy's columns only
+        last = mgr.metrics.last(policy=p)
+        np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
+        assert last["Advantages"].count == T * B
+
+
+def test_population_graph_replay_matches_eager(gpu):
+    _, _, eager = _setup(gpu, torch.bfloat16, use_graph=False)
+    _, _, graph = _setup(gpu, torch.bfloat16, use_graph=True)
+    for _ in range(3):
+        eager.update_iter()
+        graph.update_iter()
+    torch.cuda.synchronize()
+    assert graph._segments is not None
+    for a, b in zip(eager.state.policy_list, graph.state.policy_list):
+        assert torch.equal(a.params, b.params)
