@@ -294,6 +294,93 @@ int mlearn_policy_sync_weights(const mlearn_mlp_policy* policy, const float* par
                                mlearn_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
+/* Recurrent policies: BackboneShared(RecurrentBackboneEncoder(MLP, LSTM))  */
+/* (actor_critic.py:156-199, rnn.py:10-111; cell = flax 0.8.1              */
+/* OptimizedLSTMCell).  One LSTM layer of width = the MLP hidden width.      */
+/* ---------------------------------------------------------------------- */
+/* Master parameters: the MLP layout of mlearn_param_count padded to a
+ * multiple of 64 floats (mlearn_lstm_param_offset), then Wi [H][4H] (input
+ * kernels, no bias), Wh [H][4H] (hidden kernels), bias [4H]; gate blocks
+ * (i, f, g, o) concatenated along the output axis.  The compute-dtype
+ * images (written by mlearn_lstm_sync_weights / mlearn_lstm_optim_step) use
+ * the fragment layout of mlearn_mlp_policy with these logical matrices:
+ *   wi_perm, wi_nat, wh_nat: [4H gate columns][H] in unit-block order
+ *       n' = (u / 32) * 128 + gate * 32 + u % 32 (u = hidden unit), k = input
+ *       unit (wi_perm in the permuted k order of accumulator-fed fragments);
+ *   w_bwd: [2H][4H], n = input unit of [x ; h], k = gate * H + u;
+ *   head_t_nat: the head [32][H] with natural k order. */
+typedef struct mlearn_lstm {
+    int32_t hidden;          /* == policy hidden (64, 128 or 256) */
+    int32_t num_layers;      /* 1 */
+    const void* wi_perm;
+    const void* wi_nat;
+    const void* wh_nat;
+    const void* w_bwd;
+    const void* head_t_nat;
+    const float* bias;       /* [4H] f32 master bias */
+} mlearn_lstm;
+
+/* Carry of the rollout: h, c [N][H] in the compute dtype, in the env order.
+ * They hold the cell outputs of the last step; the launch clears them where
+ * post->dones (the previous env step) is set before using them
+ * (rnn_reset_fn, rollouts.py:942).  start_h / start_c (may be NULL) receive
+ * the cleared input carry: the rnn_start_states of a BPTT chunk
+ * (rollouts.py:528-537).  commit == 0 (bootstrap critic, rollouts.py:607-635)
+ * writes back the cleared carry instead of advancing it. */
+typedef struct mlearn_lstm_carry {
+    void* h;
+    void* c;
+    void* start_h;
+    void* start_c;
+    int32_t commit;
+    int32_t pad;
+} mlearn_lstm_carry;
+
+int64_t mlearn_lstm_param_offset(const mlearn_mlp_policy* policy);
+int64_t mlearn_lstm_param_count(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm);
+
+/* mlearn_policy_rollout_step with the LSTM between the trunk and the heads
+ * (ActorCritic.rollout with RecurrentBackboneEncoder, actor_critic.py:74-96,
+ * 173-177). */
+int mlearn_lstm_policy_rollout_step(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                    const mlearn_lstm_carry* carry, const float* obs, int64_t N,
+                                    void* obs_store, int32_t* actions, float* log_probs,
+                                    float* values, uint32_t k0, uint32_t k1,
+                                    const uint64_t* step_ctr, uint64_t step,
+                                    uint32_t env_offset, int32_t sample,
+                                    const mlearn_post_step* post, mlearn_stream_t stream);
+
+/* Minibatch gradient of the recurrent policy (ActorCritic.update with
+ * RecurrentBackboneEncoder.sequence, actor_critic.py:98-128, 179-199;
+ * LSTM.sequence rnn.py:81-111; PPO loss ppo.py:129-262 under
+ * jax.value_and_grad): trunk forward over the minibatch rows, the LSTM scan
+ * from the sequences' start states clearing the carry after done steps
+ * (ro->dones), heads + loss, the reverse (BPTT) scan, trunk backward, weight
+ * gradients, reduction into grad[mlearn_lstm_param_count].  start_h /
+ * start_c are [C][ld][H] compute-dtype rnn_start_states (ld, C from ro).
+ * mb_size and mb_size * bptt_len must be multiples of 32 and 64. */
+int64_t mlearn_lstm_ppo_workspace_bytes(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                        int64_t rows, int32_t mb_size);
+int mlearn_lstm_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                   const mlearn_rollout_view* ro, const void* start_h,
+                                   const void* start_c, const int32_t* mb_seq, int32_t mb_size,
+                                   const float* adv_stats, const mlearn_ppo_hparams* hp,
+                                   float* grad, float* loss_out, void* workspace,
+                                   mlearn_stream_t stream);
+
+/* mlearn_optim_step over the whole recurrent parameter vector: global-norm
+ * clip and Adam over every parameter, weight-norm projection of the trunk
+ * kernels and of each of the 8 LSTM gate kernels (init_norms = [L + 8]:
+ * trunk W_l, Wi gates i f g o, Wh gates i f g o; ppo.py:303-310), LayerNorm
+ * renorm, then the compute images of policy and lstm are refreshed. */
+int64_t mlearn_lstm_optim_workspace_bytes(const mlearn_mlp_policy* policy,
+                                          const mlearn_lstm* lstm);
+int mlearn_lstm_optim_step(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                           const mlearn_optim_state* st, void* workspace, mlearn_stream_t stream);
+int mlearn_lstm_sync_weights(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                             const float* params, mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
 /* Synthetic dummy vec-env (test/bench sim plugin, not part of the         */
 /* reference: stands in for the Madrona sim_fns['step'] custom call,       */
 /* rollouts.py:905-936).                                                   */

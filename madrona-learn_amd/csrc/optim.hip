@@ -22,10 +22,16 @@ struct CopiesK {
     void* head_t;
     void* head;
     float* head_b;
+    // recurrent policies (null otherwise); see mlearn_lstm in include/mlearn.h
+    void* wi_perm;
+    void* wi_nat;
+    void* wh_nat;
+    void* w_bwd;
+    void* head_t_nat;
 };
 
-static CopiesK make_copies(const mlearn_mlp_policy& p) {
-    CopiesK c;
+static CopiesK make_copies(const mlearn_mlp_policy& p, const mlearn_lstm* r = nullptr) {
+    CopiesK c{};
     for (int l = 0; l < MLEARN_MAX_LAYERS; ++l) {
         c.wt[l] = (void*)p.w_t[l];
         c.w[l] = (void*)p.w[l];
@@ -33,6 +39,13 @@ static CopiesK make_copies(const mlearn_mlp_policy& p) {
     c.head_t = (void*)p.head_t;
     c.head = (void*)p.head;
     c.head_b = (float*)p.head_bias;
+    if (r) {
+        c.wi_perm = (void*)r->wi_perm;
+        c.wi_nat = (void*)r->wi_nat;
+        c.wh_nat = (void*)r->wh_nat;
+        c.w_bwd = (void*)r->w_bwd;
+        c.head_t_nat = (void*)r->head_t_nat;
+    }
     return c;
 }
 
@@ -51,8 +64,16 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
 }
 
 
-// tensor id of parameter p for the projection partials: 2*l = W_l, 2*l+1 = LN_l, -1 = head
+// tensor id of parameter p for the projection partials: 2*l = W_l, 2*l+1 =
+// LN_l, 2L + 4*which + gate = LSTM gate kernel, -1 = not projected
 __device__ inline int proj_slot(const LayoutK& k, int64_t p) {
+    if (k.lstm_H && p >= k.lstm_off) {
+        const int64_t q = p - k.lstm_off, H = k.lstm_H;
+        if (q >= 8 * H * H) return -1;  // LSTM bias
+        const int which = (int)(q / (4 * H * H));
+        const int gate = (int)((q % (4 * H)) / H);
+        return 2 * k.L + 4 * which + gate;
+    }
     if (p >= k.hw_off) return -1;
     int l = k.L - 1;
     while (l > 0 && p < k.w_off[l]) --l;
@@ -78,9 +99,9 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
                                                    const int32_t* step, const double* gpart,
                                                    float lr, float b1, float b2, float eps,
                                                    float max_norm, double* proj_part) {
-    __shared__ float sh[4][2 * MLEARN_MAX_LAYERS];
+    __shared__ float sh[4][kMaxSlots];
     const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
-    const int nslot = 2 * Lk.L;
+    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     float contrib = 0.f;
     int slot = -2;
     const float gn = global_norm(gpart);
@@ -118,6 +139,25 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
 template <typename T>
 __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t p, float val) {
     const int H = Lk.H;
+    if (Lk.lstm_H && p >= Lk.mlp_total) {
+        if (p < Lk.lstm_off) return;  // alignment padding
+        const int64_t q = p - Lk.lstm_off, HH = Lk.lstm_H;
+        if (q >= 8 * HH * HH) return;  // bias: read in f32 from the master params
+        const int which = (int)(q / (4 * HH * HH));
+        const int64_t r = q - which * 4 * HH * HH;
+        const int k = (int)(r / (4 * HH)), n = (int)(r % (4 * HH));  // input unit, gate column
+        const int gate = n / (int)HH, u = n % (int)HH;
+        const int nu = (u >> 5) * 128 + gate * 32 + (u & 31);       // unit-block gate order
+        const T v = cvt<T>(val);
+        if (which == 0) {
+            ((T*)C.wi_perm)[img_index<T>(nu, k, (int)HH, true)] = v;
+            ((T*)C.wi_nat)[img_index<T>(nu, k, (int)HH, false)] = v;
+        } else {
+            ((T*)C.wh_nat)[img_index<T>(nu, k, (int)HH, false)] = v;
+        }
+        ((T*)C.w_bwd)[img_index<T>(which * (int)HH + k, n, 4 * (int)HH, false)] = v;
+        return;
+    }
     if (p >= Lk.hb_off) {
         C.head_b[p - Lk.hb_off] = val;
     } else if (p >= Lk.hw_off) {
@@ -125,6 +165,7 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
         int c = (int)(q / Lk.A1), k = (int)(q % Lk.A1);
         ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(val);
         ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(val);
+        if (C.head_t_nat) ((T*)C.head_t_nat)[img_index<T>(k, c, H, false)] = cvt<T>(val);
     } else {
         int l = Lk.L - 1;
         while (l > 0 && p < Lk.w_off[l]) --l;
@@ -146,9 +187,9 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
                                                       int32_t* step) {
     // per-slot sums of squares of the updated tensors (ppo.py:303-338), the
     // same fixed-order tree in every block
-    __shared__ double red[4][2 * MLEARN_MAX_LAYERS];
-    __shared__ float sq[2 * MLEARN_MAX_LAYERS];
-    const int nslot = 2 * Lk.L;
+    __shared__ double red[4][kMaxSlots];
+    __shared__ float sq[kMaxSlots];
+    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     for (int sl = 0; sl < nslot; ++sl) {
         double t = 0;
         for (int b = threadIdx.x; b < nblk; b += 256) t += ppart[(int64_t)b * nslot + sl];
@@ -166,7 +207,10 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
     if (p >= Lk.total) return;
     float val = params[p];
     const int slot = proj_slot(Lk, p);
-    if (slot >= 0) {
+    if (slot >= 2 * Lk.L) {  // LSTM gate kernel (ppo.py:303-310 on each ii..ho kernel)
+        if (norm_params) val = (init_norms[Lk.L + slot - 2 * Lk.L] * val) / sqrtf(sq[slot]);
+        params[p] = val;
+    } else if (slot >= 0) {
         const int l = slot >> 1;
         if ((slot & 1) == 0) {
             if (norm_params) val = (init_norms[l] * val) / sqrtf(sq[slot]);  // ppo.py:307
@@ -190,6 +234,7 @@ __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const 
         int k = Lk.A1 + (int)(p / H), c = (int)(p % H);
         ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(0.f);
         ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(0.f);
+        if (C.head_t_nat) ((T*)C.head_t_nat)[img_index<T>(k, c, H, false)] = cvt<T>(0.f);
         if (c == 0) C.head_b[k] = 0.f;
     }
     if (p < Lk.total) write_copies<T>(Lk, C, p, params[p]);
@@ -197,7 +242,7 @@ __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const 
 
 static int64_t optim_ws_doubles(const LayoutK& k) {
     int64_t nblk = (k.total + 255) / 256;
-    return kNormBlocks + nblk * 2 * k.L + 8 + 2 * MLEARN_MAX_LAYERS + 8;
+    return kNormBlocks + nblk * kMaxSlots + 8 + kMaxSlots + 8;
 }
 
 }  // namespace ml
@@ -211,16 +256,12 @@ int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy) {
     return optim_ws_doubles(make_layout(*policy)) * (int64_t)sizeof(double);
 }
 
-int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state* st,
-                      void* workspace, mlearn_stream_t stream) {
-    int rc = validate_policy(policy);
-    if (rc) return rc;
+static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
+                        const mlearn_optim_state* st, void* workspace, hipStream_t s) {
     ML_REQUIRE(st && st->params && st->grads && st->adam_m && st->adam_v && st->init_norms &&
                    st->step && workspace,
                "optim_step: null pointer");
     ML_REQUIRE(st->max_grad_norm > 0 && st->lr >= 0, "optim_step: bad hyperparameters");
-    LayoutK Lk = make_layout(*policy);
-    hipStream_t s = S(stream);
     const int64_t nblk = (Lk.total + 255) / 256;
     double* gpart = (double*)workspace;
     double* ppart = gpart + kNormBlocks;
@@ -230,8 +271,7 @@ int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state*
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
                        (const double*)gpart, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
                        ppart);
-    CopiesK C = make_copies(*policy);
-    if (policy->dtype == MLEARN_DTYPE_BF16)
+    if (dtype == MLEARN_DTYPE_BF16)
         hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
                            st->params, st->init_norms, (const double*)ppart, (int)nblk,
                            st->normalize_params, st->normalize_layernorms, st->step);
@@ -242,20 +282,64 @@ int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state*
     return check_launch("optim_step");
 }
 
+static int sync_launch(const LayoutK& Lk, const CopiesK& C, int dtype, const float* params,
+                       hipStream_t s) {
+    ML_REQUIRE(params, "sync_weights: null params");
+    int64_t n = Lk.total > (int64_t)MLEARN_HEAD_COLS * Lk.H ? Lk.total : (int64_t)MLEARN_HEAD_COLS * Lk.H;
+    unsigned g = (unsigned)((n + 255) / 256);
+    if (dtype == MLEARN_DTYPE_BF16)
+        hipLaunchKernelGGL(sync_kernel<bf16>, dim3(g), dim3(256), 0, s, Lk, C, params);
+    else
+        hipLaunchKernelGGL(sync_kernel<float>, dim3(g), dim3(256), 0, s, Lk, C, params);
+    return check_launch("sync_weights");
+}
+
+int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state* st,
+                      void* workspace, mlearn_stream_t stream) {
+    int rc = validate_policy(policy);
+    if (rc) return rc;
+    return optim_launch(make_layout(*policy), make_copies(*policy), policy->dtype, st, workspace,
+                        S(stream));
+}
+
 int mlearn_policy_sync_weights(const mlearn_mlp_policy* policy, const float* params,
                                mlearn_stream_t stream) {
     int rc = validate_policy(policy);
     if (rc) return rc;
-    ML_REQUIRE(params, "sync_weights: null params");
-    LayoutK Lk = make_layout(*policy);
-    CopiesK C = make_copies(*policy);
-    int64_t n = Lk.total > (int64_t)MLEARN_HEAD_COLS * Lk.H ? Lk.total : (int64_t)MLEARN_HEAD_COLS * Lk.H;
-    unsigned g = (unsigned)((n + 255) / 256);
-    if (policy->dtype == MLEARN_DTYPE_BF16)
-        hipLaunchKernelGGL(sync_kernel<bf16>, dim3(g), dim3(256), 0, S(stream), Lk, C, params);
-    else
-        hipLaunchKernelGGL(sync_kernel<float>, dim3(g), dim3(256), 0, S(stream), Lk, C, params);
-    return check_launch("sync_weights");
+    return sync_launch(make_layout(*policy), make_copies(*policy), policy->dtype, params,
+                       S(stream));
+}
+
+int64_t mlearn_lstm_param_offset(const mlearn_mlp_policy* policy) {
+    if (validate_policy(policy)) return -1;
+    return (make_layout(*policy).mlp_total + 63) / 64 * 64;
+}
+
+int64_t mlearn_lstm_param_count(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm) {
+    if (validate_lstm(policy, lstm)) return -1;
+    return make_layout_lstm(*policy, *lstm).total;
+}
+
+int64_t mlearn_lstm_optim_workspace_bytes(const mlearn_mlp_policy* policy,
+                                          const mlearn_lstm* lstm) {
+    if (validate_lstm(policy, lstm)) return -1;
+    return optim_ws_doubles(make_layout_lstm(*policy, *lstm)) * (int64_t)sizeof(double);
+}
+
+int mlearn_lstm_optim_step(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                           const mlearn_optim_state* st, void* workspace, mlearn_stream_t stream) {
+    int rc = validate_lstm(policy, lstm);
+    if (rc) return rc;
+    return optim_launch(make_layout_lstm(*policy, *lstm), make_copies(*policy, lstm),
+                        policy->dtype, st, workspace, S(stream));
+}
+
+int mlearn_lstm_sync_weights(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                             const float* params, mlearn_stream_t stream) {
+    int rc = validate_lstm(policy, lstm);
+    if (rc) return rc;
+    return sync_launch(make_layout_lstm(*policy, *lstm), make_copies(*policy, lstm),
+                       policy->dtype, params, S(stream));
 }
 
 }  // extern "C"

@@ -95,11 +95,27 @@ template <int H> struct PolCfg {
     static constexpr int NBW = NB / W;
 };
 
-template <typename T, int H>
+// Carry of a recurrent policy (mlearn_lstm_carry).
+struct CarryK {
+    void* h;
+    void* c;
+    void* sh;
+    void* sc;
+    int commit;
+};
+
+// RNN: the LSTM cell (RecurrentBackboneEncoder, actor_critic.py:173-177)
+// sits between the trunk and the heads.  The trunk output fragments (from
+// the accumulators, permuted k order) and the carry rows (from HBM, natural k
+// order) are staged in LDS; each wave computes the 4 gates of its own 64
+// hidden units (8 accumulator blocks, weight images in unit-block gate
+// order), so the cell update is register-local and h' lands in exactly the
+// layout the heads consume.
+template <typename T, int H, bool RNN>
 __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-    uint64_t step_add, uint32_t eoff, int sample, PostK post) {
+    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy) {
     typedef typename RT<T>::frag frag;
     typedef PolCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
@@ -115,6 +131,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     float* red = hbias + MLEARN_HEAD_COLS;                // [W][32][2]
     float* lgp = red + W * 64;                            // [W][32][33] head partials
     float* lg = lgp + W * 32 * 33;                        // [32][33]
+    float* rbias = lg + 32 * 33;                          // [4H] LSTM bias (RNN)
+    frag* frh = (frag*)(rbias + (RNN ? 4 * H : 0));       // [KSH][64] carry fragments (RNN)
     for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += THREADS) {
         float v;
         if (i < L * 2 * H) {
@@ -125,6 +143,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         }
         gb[i] = v;
     }
+    if constexpr (RNN)
+        for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
     const int64_t row0 = (int64_t)blockIdx.x * 32;
     const int64_t row = row0 + r;
     const bool live = row < N;
@@ -169,12 +189,13 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         const float var = fmaxf(sq * invH - mean * mean, 0.f);
         const float rstd = rsqrtf(var + 1e-6f);
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
-        if (l + 1 == L) break;
+        if (l + 1 == L && !RNN) break;
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int t = 0; t < SPB; ++t)
                 fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(aw[i], t);
+        if (l + 1 == L) break;
         __syncthreads();
         zero_acc<NBW>(acc);
         if (l == 0)
@@ -182,6 +203,64 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         else
             gemm_lds<T, NBW, KSH, 8>(acc, fr,
                                      (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);
+    }
+
+    if constexpr (RNN) {
+        // carry rows, cleared where the previous env step was done (rollouts.py:942)
+        const bool clr = post.rew && live && post.done[row] != 0;
+        const T* hrow = (const T*)cy.h + (live ? row : 0) * H;
+        constexpr int SPW = KSH / W;  // k-steps staged per wave
+#pragma unroll
+        for (int ss = 0; ss < SPW; ++ss) {
+            const int s = w * SPW + ss;
+            frh[s * 64 + lane] = (live && !clr) ? RT<T>::row(hrow, s, h) : RT<T>::zero();
+        }
+        __syncthreads();
+        constexpr int NG = NBW * 4;
+        f32x16 g8[NG];
+        zero_acc<NG>(g8);
+        gemm_lds<T, NG, KSH, 2>(g8, fr, (const T*)R.wi_perm + (int64_t)w * NG * KSH * 64 * E, lane);
+        gemm_lds<T, NG, KSH, 2>(g8, frh, (const T*)R.wh_nat + (int64_t)w * NG * KSH * 64 * E, lane);
+        T* hs = (T*)cy.h + row * H;
+        T* cs = (T*)cy.c + row * H;
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int u0 = (w * NBW + i) * 32 + 8 * j + 4 * h;  // units of regs 4j .. 4j+3
+                float4 hin = make_float4(0.f, 0.f, 0.f, 0.f), cin = hin;
+                if (live && !clr) {
+                    hin = load4(hs + u0);
+                    cin = load4(cs + u0);
+                }
+                float hn[4], cn[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int q = 4 * j + e, u = u0 + e;
+                    const CellOut o = lstm_cell_fwd<T>(
+                        g8[i * 4 + 0][q] + rbias[u], g8[i * 4 + 1][q] + rbias[H + u],
+                        g8[i * 4 + 2][q] + rbias[2 * H + u], g8[i * 4 + 3][q] + rbias[3 * H + u],
+                        f4get(cin, e));
+                    hn[e] = o.h;
+                    cn[e] = o.c;
+                }
+                if (live) {
+                    if (cy.sh) {
+                        store4((T*)cy.sh + row * H + u0, hin.x, hin.y, hin.z, hin.w);
+                        store4((T*)cy.sc + row * H + u0, cin.x, cin.y, cin.z, cin.w);
+                    }
+                    if (cy.commit) {
+                        store4(hs + u0, hn[0], hn[1], hn[2], hn[3]);
+                        store4(cs + u0, cn[0], cn[1], cn[2], cn[3]);
+                    } else if (clr) {
+                        store4(hs + u0, 0.f, 0.f, 0.f, 0.f);
+                        store4(cs + u0, 0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+                aw[i][2 * j] = Pk<T>::pack(hn[0], hn[1]);
+                aw[i][2 * j + 1] = Pk<T>::pack(hn[2], hn[3]);
+            }
+        }
     }
 
     // actor + critic heads over this wave's features, partials summed in wave
@@ -226,19 +305,21 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     if (values && tid < 32 && row0 + tid < N) values[row0 + tid] = lg[tid * 33 + P.A];
 }
 
-template <typename T, int H> static size_t policy_step_lds(int L) {
+template <typename T, int H, bool RNN> static size_t policy_step_lds(int L) {
     typedef PolCfg<H> C;
-    return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
-           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33) * 4;
+    const size_t frags = (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
+    return frags * (RNN ? 2 : 1) +
+           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33 +
+                    (RNN ? 4 * H : 0)) * 4;
 }
 
-template <typename T, int H>
+template <typename T, int H, bool RNN>
 static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, void* obs_store,
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
-                              const PostK& post, hipStream_t s) {
-    const size_t lds = policy_step_lds<T, H>(P.L);
-    auto kern = policy_step_kernel<T, H>;
+                              const PostK& post, const LstmK& R, const CarryK& cy, hipStream_t s) {
+    const size_t lds = policy_step_lds<T, H, RNN>(P.L);
+    auto kern = policy_step_kernel<T, H, RNN>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -248,21 +329,17 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
     const int grid = (int)((N + 31) / 32);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
                        (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
-                       post);
+                       post, R, cy);
     return check_launch("policy_rollout_step");
 }
 
-}  // namespace ml
-
-using namespace ml;
-
-extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const float* obs,
-                                          int64_t N, void* obs_store, int32_t* actions,
-                                          float* log_probs, float* values, uint32_t k0,
-                                          uint32_t k1, const uint64_t* step_ctr, uint64_t step,
-                                          uint32_t env_offset, int32_t sample,
-                                          const mlearn_post_step* post, mlearn_stream_t stream) {
-    int rc = validate_policy(policy);
+static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                              const mlearn_lstm_carry* carry, const float* obs, int64_t N,
+                              void* obs_store, int32_t* actions, float* log_probs, float* values,
+                              uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint64_t step,
+                              uint32_t env_offset, int32_t sample, const mlearn_post_step* post,
+                              mlearn_stream_t stream) {
+    int rc = lstm ? validate_lstm(policy, lstm) : validate_policy(policy);
     if (rc) return rc;
     ML_REQUIRE(N >= 0, "policy_rollout_step: N < 0");
     if (N == 0) return MLEARN_OK;
@@ -280,16 +357,28 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
         pk = PostK{post->rewards, post->dones, post->store_rewards, post->store_dones,
                    post->env_returns, post->env_returns_trace, post->gamma};
     }
+    LstmK R{};
+    CarryK cy{};
+    if (lstm) {
+        ML_REQUIRE(carry && carry->h && carry->c, "lstm rollout step: null carry");
+        ML_REQUIRE(!carry->start_h == !carry->start_c, "lstm rollout step: start_h / start_c");
+        ML_REQUIRE((uintptr_t)carry->h % 16 == 0 && (uintptr_t)carry->c % 16 == 0,
+                   "lstm rollout step: carry must be 16-byte aligned");
+        R = make_lstm_k(*lstm);
+        cy = CarryK{carry->h, carry->c, carry->start_h, carry->start_c, carry->commit};
+    }
     PolicyK P = make_policy_k(*policy);
     hipStream_t s = S(stream);
-#define ML_DISPATCH(T)                                                                              \
-    switch (policy->hidden) {                                                                      \
-        case 64: return launch_policy_step<T, 64>(P, obs, N, obs_store, actions, log_probs, values, \
-                                                  k0, k1, step_ctr, step, env_offset, sample, pk, s);            \
-        case 128: return launch_policy_step<T, 128>(P, obs, N, obs_store, actions, log_probs,      \
-                                                    values, k0, k1, step_ctr, step, env_offset, sample, pk, s);  \
-        default: return launch_policy_step<T, 256>(P, obs, N, obs_store, actions, log_probs,       \
-                                                   values, k0, k1, step_ctr, step, env_offset, sample, pk, s);   \
+#define ML_LAUNCH(T, HH)                                                                          \
+    (lstm ? launch_policy_step<T, HH, true>(P, obs, N, obs_store, actions, log_probs, values, k0, \
+                                            k1, step_ctr, step, env_offset, sample, pk, R, cy, s) \
+          : launch_policy_step<T, HH, false>(P, obs, N, obs_store, actions, log_probs, values, k0, \
+                                             k1, step_ctr, step, env_offset, sample, pk, R, cy, s))
+#define ML_DISPATCH(T)                      \
+    switch (policy->hidden) {               \
+        case 64: return ML_LAUNCH(T, 64);   \
+        case 128: return ML_LAUNCH(T, 128); \
+        default: return ML_LAUNCH(T, 256);  \
     }
     if (policy->dtype == MLEARN_DTYPE_BF16) {
         ML_DISPATCH(bf16)
@@ -297,4 +386,29 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
         ML_DISPATCH(float)
     }
 #undef ML_DISPATCH
+#undef ML_LAUNCH
+}
+
+}  // namespace ml
+
+using namespace ml;
+
+extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const float* obs,
+                                          int64_t N, void* obs_store, int32_t* actions,
+                                          float* log_probs, float* values, uint32_t k0,
+                                          uint32_t k1, const uint64_t* step_ctr, uint64_t step,
+                                          uint32_t env_offset, int32_t sample,
+                                          const mlearn_post_step* post, mlearn_stream_t stream) {
+    return rollout_step_entry(policy, nullptr, nullptr, obs, N, obs_store, actions, log_probs,
+                              values, k0, k1, step_ctr, step, env_offset, sample, post, stream);
+}
+
+extern "C" int mlearn_lstm_policy_rollout_step(
+    const mlearn_mlp_policy* policy, const mlearn_lstm* lstm, const mlearn_lstm_carry* carry,
+    const float* obs, int64_t N, void* obs_store, int32_t* actions, float* log_probs,
+    float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint64_t step,
+    uint32_t env_offset, int32_t sample, const mlearn_post_step* post, mlearn_stream_t stream) {
+    ML_REQUIRE(lstm, "lstm rollout step: null lstm descriptor");
+    return rollout_step_entry(policy, lstm, carry, obs, N, obs_store, actions, log_probs, values,
+                              k0, k1, step_ctr, step, env_offset, sample, post, stream);
 }

@@ -19,6 +19,8 @@
 //   tl = f / mb, m = f % mb, seq = mb_seq[m], c = seq / N, b = seq % N,
 //   store row = (c * bptt + tl) * N + b.
 
+#include <type_traits>
+
 #include "common.h"
 #include "rowtile.h"
 
@@ -31,6 +33,7 @@ struct RolloutK {
     const float* adv;
     const float* ret;
     const float* values;
+    const uint8_t* dones;
     int T, bptt;
     int64_t N, ld;  // envs of this policy, row stride of the store
 };
@@ -51,6 +54,21 @@ constexpr int kColChunks = 32;   // first-level chunks of the per-tile column pa
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 constexpr int kWgChunk = 32;     // weight-gradient K chunk (rows of the minibatch)
 constexpr int kRowAlign = 64;    // Mp granularity
+constexpr int kMaxJobs = MLEARN_MAX_LAYERS + 3;  // weight-gradient jobs
+
+// LSTM scan buffers of the recurrent update (rows f = t * mb + m, compute
+// dtype unless noted).
+struct LstmWsK {
+    void* hout;   // [Mp][H]  cell outputs h_t (head input)
+    void* hin;    // [Mp][H]  carry into step t (cleared after done steps)
+    void* cin;    // [Mp][H]
+    void* cout;   // [Mp][H]  c_t
+    void* gates;  // [Mp][4H] i, f, g, o activations (gate-major columns)
+    void* dg;     // [Mp][4H] d loss / d gate pre-activations
+    void* dhout;  // [Mp][H]  d loss / d h_t from the heads
+    void* dfeat;  // [Mp][H]  d loss / d trunk output
+    float* dcc;   // [mb][H]  f32 cotangent of the c carry
+};
 
 struct WsK {
     void* x0;                           // [Mp][D]  gathered obs (compute dtype)
@@ -61,9 +79,9 @@ struct WsK {
     float* colpart2;                    // [kColChunks][CP]
     double* loss_part;                  // [tiles][kLossSlots]
     float* slab;                        // split-K partial weight gradients
-    int64_t slab_off[MLEARN_MAX_LAYERS + 1];
-    int splits[MLEARN_MAX_LAYERS + 1];
-    int64_t rps[MLEARN_MAX_LAYERS + 1];  // rows per split
+    int64_t slab_off[kMaxJobs];         // jobs: W_0..W_{L-1}, head, (LSTM) Wi, Wh
+    int splits[kMaxJobs];
+    int64_t rps[kMaxJobs];  // rows per split
     int64_t Mp;
     int ntiles;                         // Mp / 32
     int CP;                             // L*2*H + 32
@@ -100,7 +118,9 @@ static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
 }
 
 // Carve the workspace; returns total bytes (base may be null to size only).
-static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
+// lstm (may be null): recurrent policy; mb = sequences per minibatch.
+static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
+                    const mlearn_lstm* lstm = nullptr, int64_t mb = 0, LstmWsK* LW = nullptr) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
     const int64_t Mp = (M + kRowAlign - 1) / kRowAlign * kRowAlign;
@@ -114,7 +134,8 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     WsK w{};
     w.Mp = Mp;
     w.ntiles = (int)tiles;
-    w.CP = L * 2 * H + MLEARN_HEAD_COLS;
+    // column partials: LayerNorm [L][2][H], head bias [32], (LSTM) bias [4H]
+    w.CP = L * 2 * H + MLEARN_HEAD_COLS + (lstm ? 4 * H : 0);
     w.x0 = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
         w.a[l] = take(Mp * H * es);
@@ -125,14 +146,28 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W) {
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
     int64_t so = 0;
-    for (int l = 0; l <= L; ++l) {
-        const int I = l == L ? H : (l == 0 ? D : H);
-        const int J = l == L ? MLEARN_HEAD_COLS : H;
+    const int njobs = L + 1 + (lstm ? 2 : 0);
+    for (int l = 0; l < njobs; ++l) {
+        const int I = l >= L ? H : (l == 0 ? D : H);
+        const int J = l == L ? MLEARN_HEAD_COLS : (l > L ? 4 * H : H);
         plan_splits(I, J, Mp, &w.splits[l], &w.rps[l]);
         w.slab_off[l] = so;
         so += (int64_t)w.splits[l] * I * J;
     }
     w.slab = (float*)take(so * sizeof(float));
+    if (lstm) {
+        LstmWsK lw{};
+        lw.hout = take(Mp * H * es);
+        lw.hin = take(Mp * H * es);
+        lw.cin = take(Mp * H * es);
+        lw.cout = take(Mp * H * es);
+        lw.gates = take(Mp * 4 * H * es);
+        lw.dg = take(Mp * 4 * H * es);
+        lw.dhout = take(Mp * H * es);
+        lw.dfeat = take(Mp * H * es);
+        lw.dcc = (float*)take(mb * H * sizeof(float));
+        if (LW) *LW = lw;
+    }
     if (W) *W = w;
     return off;
 }
@@ -313,10 +348,29 @@ __device__ inline int64_t store_row(const RolloutK& ro, const int32_t* mb_seq, i
     return ((int64_t)c * ro.bptt + tl) * ro.ld + b;
 }
 
-template <typename T, int H, int L>
+// Phases of the step kernel.  kFused: the MLP policy's whole minibatch step.
+// Recurrent policies (the LSTM scan runs in between, across time):
+//   kTrunkFwd: trunk forward only (writes X_0 and the activations A_l; the
+//              last one is the LSTM input);
+//   kHeads:    heads + loss + d head from the LSTM outputs (rows of rec.hout,
+//              natural k order), writes d loss / d LSTM output rows;
+//   kTrunkBwd: trunk forward recomputed, then its backward from the rows of
+//              d loss / d trunk output (rec.dfeat).
+constexpr int kFused = 0, kTrunkFwd = 1, kHeads = 2, kTrunkBwd = 3;
+struct RecK {
+    const void* hout;        // [Mp][H] LSTM outputs (kHeads)
+    void* dhout;             // [Mp][H] d loss / d LSTM outputs (kHeads)
+    const void* dfeat;       // [Mp][H] d loss / d trunk output (kTrunkBwd)
+    const void* head_t_nat;  // head image, natural k order (kHeads)
+};
+
+template <typename T, int H, int L, int MODE = kFused>
 __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
-    const float* __restrict__ adv_st, HpK hp, WsK ws) {
+    const float* __restrict__ adv_st, HpK hp, WsK ws, RecK rec) {
+    constexpr bool kFwd = MODE != kHeads;                     // runs the trunk forward
+    constexpr bool kLoss = MODE == kFused || MODE == kHeads;  // heads + loss
+    constexpr bool kBwd = MODE == kFused || MODE == kTrunkBwd;  // trunk backward
     typedef typename RT<T>::frag frag;
     typedef StepCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
@@ -350,7 +404,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     const int64_t sr = live ? store_row(ro, mb_seq, mb, row) : 0;
     // first loss task of this thread: row tr, task tg (group, or value if tg == K)
     const int tr = tid & 31, tg = tid >> 5;
-    const bool tlive = row0 + tr < M && tg <= K;
+    const bool tlive = kLoss && row0 + tr < M && tg <= K;
     const int64_t tsr = tlive ? store_row(ro, mb_seq, mb, row0 + tr) : 0;
     int t_act = 0;
     float t_lp = 0.f, t_adv = 0.f, t_ret = 0.f, t_val = 0.f;
@@ -369,9 +423,10 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     // ---- forward ----
     f32x16 acc[NBW];
     zero_acc<NBW>(acc);
-    gemm_first<T, NBW>(acc, (const T*)ro.obs + sr * D, live, D / KS,
-                       (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
-                       w == 0 ? (T*)ws.x0 + row * D : nullptr, lane);
+    if constexpr (kFwd)
+        gemm_first<T, NBW>(acc, (const T*)ro.obs + sr * D, live, D / KS,
+                           (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
+                           (w == 0 && MODE != kTrunkBwd) ? (T*)ws.x0 + row * D : nullptr, lane);
     STAMP(1);
     __syncthreads();  // LayerNorm parameters staged
     typedef typename Pk<T>::word word;
@@ -380,7 +435,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < (kFwd ? L : 0); ++l) {
         if (l > 0) {
             zero_acc<NBW>(acc);
             gemm_lds<T, NBW, KSH, 8>(acc, fr, (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E,
@@ -411,12 +466,15 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         rstd_r[l] = rstd;
         STAMP(2 + 3 * l);
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
-        T* arow = (T*)ws.a[l] + row * H;
+        if (MODE != kTrunkBwd) {
+            T* arow = (T*)ws.a[l] + row * H;
 #pragma unroll
-        for (int i = 0; i < NBW; ++i)
+            for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                Pk<T>::store4(arow + (w * NBW + i) * 32 + 8 * g + 4 * h, aw[i][2 * g], aw[i][2 * g + 1]);
+                for (int g = 0; g < 4; ++g)
+                    Pk<T>::store4(arow + (w * NBW + i) * 32 + 8 * g + 4 * h, aw[i][2 * g],
+                                  aw[i][2 * g + 1]);
+        }
         if (l + 1 < L) {
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
@@ -427,18 +485,28 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         }
     }
     STAMP(6);
+    if constexpr (MODE == kTrunkFwd) return;
+    if constexpr (kLoss) {
     // heads over this wave's features; partials summed in wave order:
     // lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22, models.py:154)
     {
         frag hb[NBW * SPB];
+        if constexpr (MODE == kHeads) {
+            // this wave's slice of the LSTM output row (natural k order)
+            const T* hrow = (const T*)rec.hout + row * H;
 #pragma unroll
-        for (int i = 0; i < NBW; ++i)
+            for (int j = 0; j < NBW * SPB; ++j) hb[j] = RT<T>::row(hrow, w * NBW * SPB + j, h);
+        } else {
 #pragma unroll
-            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
+            for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
+        }
+        const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
         f32x16 ha[1];
         zero_acc<1>(ha);
         gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
-            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane);
+            ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane);
 #pragma unroll
         for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * 33 + feat(0, q, h)] = ha[0][q];
     }
@@ -533,6 +601,36 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         // dA_{L-1}^T = Head . dHead^T  (this wave's feature blocks)
         gemm_ring<T, NBW, KSHD, 2>(acc, db, KSHD,
                                    (const T*)P.head + (int64_t)w * NBW * KSHD * 64 * E, lane);
+    }
+    }  // kLoss
+    if constexpr (MODE == kHeads) {
+        // d loss / d LSTM output rows, rounded to the compute dtype (the
+        // cotangent of a compute-dtype tensor)
+        T* drow = (T*)rec.dhout + row * H;
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                Pk<T>::store4(drow + (w * NBW + i) * 32 + 8 * g + 4 * h,
+                              Pk<T>::pack(acc[i][4 * g], acc[i][4 * g + 1]),
+                              Pk<T>::pack(acc[i][4 * g + 2], acc[i][4 * g + 3]));
+        return;
+    }
+    if constexpr (MODE == kTrunkBwd) {
+        // d loss / d trunk output (from the LSTM's reverse scan) into the
+        // accumulator layout of this wave's feature blocks
+        const T* frow = (const T*)rec.dfeat + row * H;
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = live ? load4(frow + (w * NBW + i) * 32 + 8 * g + 4 * h)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc[i][4 * g] = v.x;
+                acc[i][4 * g + 1] = v.y;
+                acc[i][4 * g + 2] = v.z;
+                acc[i][4 * g + 3] = v.w;
+            }
     }
     const int qs = col_sum16_index(lane);
     const float thr = relu_thr<T>();
@@ -634,11 +732,11 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     STAMP(15);
 }
 
-template <typename T, int H, int L>
+template <typename T, int H, int L, int MODE = kFused>
 static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                         int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
-                        hipStream_t s) {
-    auto k = ppo_step_kernel<T, H, L>;
+                        hipStream_t s, const RecK& rec = RecK{}) {
+    auto k = ppo_step_kernel<T, H, L, MODE>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -648,7 +746,7 @@ static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_s
     const size_t lds = step_lds<T, H, L>();
     const int threads = 64 * StepCfg<H>::W;
     hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(threads), lds, s, P, R, mb_seq, mb, M, adv_st, hp,
-                       ws);
+                       ws, rec);
 }
 
 // ---------------------------------------------------------------------------
@@ -671,7 +769,7 @@ struct WgJob {
     int I, J, ti, tj, splits, wg0;
 };
 struct WgJobs {
-    WgJob job[MLEARN_MAX_LAYERS + 1];
+    WgJob job[kMaxJobs];
     int n;
     int64_t Mp;
     int nwg, ncol, ncolx;  // weight-gradient blocks, column-sum blocks (ncolx per chunk)
@@ -870,7 +968,31 @@ LayoutK make_layout(const mlearn_mlp_policy& p) {
     k.hb_off = o;
     o += k.A1;
     k.total = o;
+    k.mlp_total = o;
+    k.lstm_off = o;
+    k.lstm_H = 0;
     return k;
+}
+
+LayoutK make_layout_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& r) {
+    LayoutK k = make_layout(p);
+    const int64_t H = r.hidden;
+    k.lstm_H = (int)H;
+    k.lstm_off = (k.mlp_total + 63) / 64 * 64;
+    k.total = k.lstm_off + 8 * H * H + 4 * H;
+    return k;
+}
+
+int validate_lstm(const mlearn_mlp_policy* p, const mlearn_lstm* r) {
+    int rc = validate_policy(p);
+    if (rc) return rc;
+    ML_REQUIRE(r, "lstm: null descriptor");
+    ML_REQUIRE(r->num_layers == 1, "lstm: one LSTM layer supported (got %d)", r->num_layers);
+    ML_REQUIRE(r->hidden == p->hidden, "lstm: width %d must equal the MLP width %d", r->hidden,
+               p->hidden);
+    ML_REQUIRE(r->wi_perm && r->wi_nat && r->wh_nat && r->w_bwd && r->head_t_nat && r->bias,
+               "lstm: null weight image");
+    return MLEARN_OK;
 }
 
 // Fixed-order reduction of the split-K slabs and column partials into the
@@ -885,11 +1007,33 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
     const int64_t p0 = (int64_t)blockIdx.x * 64;
     const int H = Lk.H, L = Lk.L;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p0 >= Lk.hw_off) {  // head weight (slab [split][H][32]) and head bias
+    if (Lk.lstm_H && p0 >= Lk.lstm_off) {  // LSTM segment (64-aligned)
+        const int64_t q0 = p0 - Lk.lstm_off, HH = Lk.lstm_H, G = 4 * HH * HH;
+        if (q0 >= 2 * G) {  // bias: column partials of d gate pre-activations
+            const int col = L * 2 * H + MLEARN_HEAD_COLS + (int)(q0 - 2 * G) + 4 * c;
+            for (int k = g; k < kColChunks; k += kRgGroups) {
+                const float4 x = *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col);
+                v[0] += x.x;
+                v[1] += x.y;
+                v[2] += x.z;
+                v[3] += x.w;
+            }
+        } else {  // Wi / Wh: split-K slabs [split][H][4H]
+            const int which = (int)(q0 / G);
+            const float* sp = ws.slab + ws.slab_off[L + 1 + which] + (q0 - which * G) + 4 * c;
+            for (int k = g; k < ws.splits[L + 1 + which]; k += kRgGroups) {
+                const float4 x = *(const float4*)(sp + k * G);
+                v[0] += x.x;
+                v[1] += x.y;
+                v[2] += x.z;
+                v[3] += x.w;
+            }
+        }
+    } else if (p0 >= Lk.hw_off) {  // head weight (slab [split][H][32]) and head bias
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t p = p0 + 4 * c + e;
-            if (p >= Lk.total) break;
+            if (p >= Lk.mlp_total) break;  // (recurrent policies: alignment padding)
             if (p >= Lk.hb_off) {
                 const int col = L * 2 * H + (int)(p - Lk.hb_off);
                 for (int k = g; k < kColChunks; k += kRgGroups)
@@ -1017,7 +1161,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     ws.stamps = g_stamp_buf;
 #endif
     PolicyK P = make_policy_k(p);
-    RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values,
+    RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values, ro.dones,
                ro.T, ro.bptt_len, ro.N, ro.ld ? ro.ld : ro.N};
     HpK hp{};
     hp.clip = h.clip_coef;
@@ -1075,6 +1219,289 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
                        dim3(256), 0, s, Lk, ws, grad);
     return check_launch("ppo_minibatch_grad");
+}
+
+// ---------------------------------------------------------------------------
+// Recurrent update: the LSTM scan over the minibatch's sequences
+// (LSTM.sequence, rnn.py:81-111) and its reverse (BPTT), one launch per
+// time step.  Rows f = t * mb + m.  A workgroup owns 32 sequences; its 4
+// waves own 32-unit blocks: each wave's 4 accumulator blocks are the gates
+// (i, f, g, o) of its units (weight images in unit-block gate order), so the
+// cell arithmetic is register-local.
+// ---------------------------------------------------------------------------
+
+// Step-0 carry rows from the sequences' rnn_start_states [C][ld][H].
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_start_kernel(const T* __restrict__ sh,
+                                                         const T* __restrict__ sc, RolloutK ro,
+                                                         const int32_t* __restrict__ mb_seq,
+                                                         int mb, int H, T* hin, T* cin) {
+    const int q = H / 4;
+    const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+    if (i >= (int64_t)mb * q) return;
+    const int m = (int)(i / q), u = (int)(i % q) * 4;
+    const int64_t seq = mb_seq[m];
+    const int64_t c = seq / ro.N, b = seq % ro.N;
+    const int64_t src = (c * ro.ld + b) * H + u;
+    const float4 hv = load4(sh + src), cv = load4(sc + src);
+    store4(hin + (int64_t)m * H + u, hv.x, hv.y, hv.z, hv.w);
+    store4(cin + (int64_t)m * H + u, cv.x, cv.y, cv.z, cv.w);
+}
+
+// Forward step t: gates = F_t Wi + hin_t Wh + bias -> cell -> h_t, c_t; the
+// carry into t + 1 is cleared where dones[t] (rnn.py:92-96).
+template <typename T, int H>
+__global__ __launch_bounds__(256) void lstm_fwd_step_kernel(LstmK R, RolloutK ro,
+                                                            const int32_t* __restrict__ mb_seq,
+                                                            int mb, int t, const T* feat,
+                                                            LstmWsK lw) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frf = (frag*)smem;     // [KSH][64] trunk-output fragments
+    frag* frh = frf + KSH * 64;  // [KSH][64] carry fragments
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.x * 32;
+    const int ub = blockIdx.y * 4 + w;
+    const int64_t f0 = (int64_t)t * mb + m0;
+    for (int idx = tid; idx < 2 * KSH * 64; idx += 256) {
+        const int which = idx >= KSH * 64, rem = idx - which * KSH * 64;
+        const int s = rem >> 6, ln = rem & 63;
+        const T* rowp = (which ? (const T*)lw.hin : feat) + (f0 + (ln & 31)) * H;
+        (which ? frh : frf)[rem] = RT<T>::row(rowp, s, ln >> 5);
+    }
+    __syncthreads();
+    if (ub >= H / 32) return;  // H = 64: two unit blocks for four waves
+    f32x16 acc[4];
+    zero_acc<4>(acc);
+    gemm_lds<T, 4, KSH, 4>(acc, frf, (const T*)R.wi_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
+    gemm_lds<T, 4, KSH, 4>(acc, frh, (const T*)R.wh_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
+    const int64_t f = f0 + r;
+    const bool more = t + 1 < ro.bptt;
+    const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+    T* gts = (T*)lw.gates + f * 4 * H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int u0 = ub * 32 + 8 * j + 4 * h;
+        const float4 ci = load4((const T*)lw.cin + f * H + u0);
+        float gi[4], gf[4], gg[4], go[4], cn[4], hn[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e, u = u0 + e;
+            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + R.bias[u], acc[1][q] + R.bias[H + u],
+                                               acc[2][q] + R.bias[2 * H + u],
+                                               acc[3][q] + R.bias[3 * H + u], f4get(ci, e));
+            gi[e] = o.i;
+            gf[e] = o.f;
+            gg[e] = o.g;
+            go[e] = o.o;
+            cn[e] = o.c;
+            hn[e] = o.h;
+        }
+        store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
+        store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
+        store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
+        store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
+        store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
+        store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
+        if (more) {
+            const float k = done ? 0.f : 1.f;
+            store4((T*)lw.hin + (f + mb) * H + u0, k * hn[0], k * hn[1], k * hn[2], k * hn[3]);
+            store4((T*)lw.cin + (f + mb) * H + u0, k * cn[0], k * cn[1], k * cn[2], k * cn[3]);
+        }
+    }
+}
+
+// Reverse step: phase B(t) (t < bptt) = [dF_t ; dh_{t-1}] = dG_t [Wi ; Wh]^T,
+// one 32-output block per wave (blocks < H/32: dF_t rows; the rest: the h
+// carry cotangent, kept in registers); phase A(t-1) (t >= 1, or t - 1 =
+// bptt - 1 in the first launch, t = bptt) on the waves of the h blocks: the
+// cell backward of step t - 1 for their units, writing dG_{t-1}, the c carry
+// cotangent and the per-tile column partials of dG (bias gradient).
+template <typename T, int H>
+__global__ __launch_bounds__(256) void lstm_bwd_step_kernel(LstmK R, RolloutK ro,
+                                                            const int32_t* __restrict__ mb_seq,
+                                                            int mb, int t, LstmWsK lw,
+                                                            float* colpart, int CP, int cp0) {
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NU = H / 32;
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.x * 32;
+    const int ob = blockIdx.y * 4 + w;
+    const bool hpart = ob >= NU;
+    const bool first = t == ro.bptt;
+    const bool doB = !first && !(hpart && t == 0);
+    const bool doA = hpart && t >= 1;
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    if (doB) {
+        const int64_t f = (int64_t)t * mb + m0 + r;
+        gemm_first<T, 1>(acc, (const T*)lw.dg + f * 4 * H, true, NKS,
+                         (const T*)R.w_bwd + (int64_t)ob * NKS * 64 * E, (T*)nullptr, lane);
+        if (!hpart) {
+            T* drow = (T*)lw.dfeat + f * H + ob * 32;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                store4(drow + 8 * g + 4 * h, acc[0][4 * g], acc[0][4 * g + 1], acc[0][4 * g + 2],
+                       acc[0][4 * g + 3]);
+        }
+    }
+    if (!doA) return;
+    const int s = t - 1, ub = ob - NU, m = m0 + r;
+    const int64_t fs = (int64_t)s * mb + m;
+    const bool cut = first || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+    const T* gts = (const T*)lw.gates + fs * 4 * H;
+    T* dgs = (T*)lw.dg + fs * 4 * H;
+    float dpi[16], dpf[16], dpg[16], dpo[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int u0 = ub * 32 + 8 * j + 4 * h;
+        const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
+        const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
+        const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
+        const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
+        const float4 ci = load4((const T*)lw.cin + fs * H + u0);
+        float* dccp = lw.dcc + (int64_t)m * H + u0;
+        const float4 dcn = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)dccp;
+        float dcc_new[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e;
+            const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
+            const float dh = f4get(dho, e) + (cut ? 0.f : acc[0][q]);
+            const float tc = tanhf(f4get(c4, e));
+            const float dout = dh * tc;
+            const float dc = f4get(dcn, e) + dh * o_ * (1.f - tc * tc);
+            dpi[q] = rnd<T>((dc * g_) * i_ * (1.f - i_));
+            dpf[q] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
+            dpg[q] = rnd<T>((dc * i_) * (1.f - g_ * g_));
+            dpo[q] = rnd<T>(dout * o_ * (1.f - o_));
+            dcc_new[e] = dc * f_;
+        }
+        store4(dgs + u0, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
+        store4(dgs + H + u0, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2], dpf[4 * j + 3]);
+        store4(dgs + 2 * H + u0, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2], dpg[4 * j + 3]);
+        store4(dgs + 3 * H + u0, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2], dpo[4 * j + 3]);
+        *(float4*)dccp = make_float4(dcc_new[0], dcc_new[1], dcc_new[2], dcc_new[3]);
+    }
+    // bias gradient: column sums of dG over this tile's 32 rows
+    const int qs = col_sum16_index(lane);
+    float* cp = colpart + (int64_t)((s * (int64_t)mb + m0) / 32) * CP + cp0;
+    const int uq = ub * 32 + feat(0, qs, h);
+    const float si = col_sum16(dpi, lane), sf = col_sum16(dpf, lane);
+    const float sg = col_sum16(dpg, lane), so = col_sum16(dpo, lane);
+    if ((lane & 16) == 0) {
+        cp[uq] = si;
+        cp[H + uq] = sf;
+        cp[2 * H + uq] = sg;
+        cp[3 * H + uq] = so;
+    }
+}
+
+template <typename T, int H>
+static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& lstm,
+                                 const mlearn_rollout_view& ro, const void* start_h,
+                                 const void* start_c, const int32_t* mb_seq, int mb,
+                                 const float* adv_st, const mlearn_ppo_hparams& h, float* grad,
+                                 float* loss_out, void* wsp, hipStream_t s) {
+    const int bptt = ro.bptt_len;
+    const int64_t M = (int64_t)mb * bptt;
+    WsK ws;
+    LstmWsK lw;
+    carve(p, M, (char*)wsp, &ws, &lstm, mb, &lw);
+    PolicyK P = make_policy_k(p);
+    LstmK RK = make_lstm_k(lstm);
+    RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values, ro.dones,
+               ro.T, ro.bptt_len, ro.N, ro.ld ? ro.ld : ro.N};
+    HpK hp{};
+    hp.clip = h.clip_coef;
+    hp.vcoef = h.value_loss_coef;
+    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
+    hp.norm_adv = h.normalize_advantages;
+    hp.clip_vl = h.clip_value_loss;
+    hp.huber = h.huber_value_loss;
+    hp.loss_scale = h.loss_scale;
+    hp.inv_s = (float)(1.0 / (double)M);
+    hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
+    const int L = p.num_layers;
+    RecK rec{lw.hout, lw.dhout, lw.dfeat, lstm.head_t_nat};
+    auto step = [&](auto mode) {
+        constexpr int MODE = decltype(mode)::value;
+        switch (L) {
+            case 1: launch_step<T, H, 1, MODE>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, rec); break;
+            case 2: launch_step<T, H, 2, MODE>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, rec); break;
+            case 3: launch_step<T, H, 3, MODE>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, rec); break;
+            default: launch_step<T, H, 4, MODE>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, rec); break;
+        }
+    };
+    // trunk forward over every row (the LSTM input F = A_{L-1})
+    step(std::integral_constant<int, kTrunkFwd>{});
+    const T* feat = (const T*)ws.a[L - 1];
+    hipLaunchKernelGGL(lstm_start_kernel<T>, dim3((unsigned)((mb * (H / 4) + 255) / 256)),
+                       dim3(256), 0, s, (const T*)start_h, (const T*)start_c, R, mb_seq, mb, H,
+                       (T*)lw.hin, (T*)lw.cin);
+    {
+        constexpr int KSH = H / RT<T>::KS;
+        const size_t lds = 2 * (size_t)KSH * 64 * sizeof(typename RT<T>::frag);
+        auto k = lstm_fwd_step_kernel<T, H>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            attr_set = true;
+        }
+        for (int t = 0; t < bptt; ++t)
+            hipLaunchKernelGGL(k, dim3(mb / 32, (H / 32 + 3) / 4), dim3(256), lds, s, RK, R,
+                               mb_seq, mb, t, feat, lw);
+    }
+    // heads + loss from the LSTM outputs
+    step(std::integral_constant<int, kHeads>{});
+    // reverse scan
+    const int cp0 = L * 2 * H + MLEARN_HEAD_COLS;
+    for (int t = bptt; t >= 0; --t)
+        hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, 2 * H / 128), dim3(256), 0,
+                           s, RK, R, mb_seq, mb, t, lw, ws.colpart, ws.CP, cp0);
+    // trunk backward from d features
+    step(std::integral_constant<int, kTrunkBwd>{});
+    // weight gradients: trunk, head (from the LSTM outputs), Wi, Wh
+    WgJobs jobs{};
+    jobs.n = L + 3;
+    jobs.Mp = ws.Mp;
+    int wg = 0;
+    for (int l = 0; l < L + 3; ++l) {
+        WgJob& J = jobs.job[l];
+        J.I = l >= L ? H : (l == 0 ? p.obs_dim : H);
+        J.J = l == L ? MLEARN_HEAD_COLS : (l > L ? 4 * H : H);
+        J.X = l == 0 ? ws.x0 : (l < L ? ws.a[l - 1] : (l == L ? lw.hout : (l == L + 1 ? (const void*)feat : lw.hin)));
+        J.Y = l < L ? ws.dz[l] : (l == L ? ws.dhead : lw.dg);
+        J.out = ws.slab + ws.slab_off[l];
+        J.rps = ws.rps[l];
+        J.ti = (J.I + kWgTile - 1) / kWgTile;
+        J.tj = (J.J + kWgTile - 1) / kWgTile;
+        J.splits = ws.splits[l];
+        J.wg0 = wg;
+        wg += J.ti * J.tj * J.splits;
+    }
+    jobs.nwg = wg;
+    jobs.ncolx = (ws.CP + 255) / 256;
+    jobs.ncol = jobs.ncolx * kColChunks;
+    {
+        auto k = wgrad_kernel<T>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)WgCfg<T>::lds);
+            attr_set = true;
+        }
+        const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
+                           p.actions.num_groups, loss_out);
+    }
+    LayoutK Lk = make_layout_lstm(p, lstm);
+    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)), dim3(256), 0,
+                       s, Lk, ws, grad);
+    return check_launch("lstm_ppo_minibatch_grad");
 }
 
 }  // namespace ml
@@ -1139,6 +1566,54 @@ int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_roll
                               void* workspace, mlearn_stream_t stream) {
     return ppo_entry(policy, ro, mb_seq, mb_size, adv_stats, hp, grad, loss_out, workspace, false,
                      stream);
+}
+
+int64_t mlearn_lstm_ppo_workspace_bytes(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                        int64_t rows, int32_t mb_size) {
+    if (validate_lstm(policy, lstm) || rows < 1 || mb_size < 1) return -1;
+    return (int64_t)carve(*policy, rows, nullptr, nullptr, lstm, mb_size, nullptr);
+}
+
+int mlearn_lstm_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                   const mlearn_rollout_view* ro, const void* start_h,
+                                   const void* start_c, const int32_t* mb_seq, int32_t mb_size,
+                                   const float* adv_stats, const mlearn_ppo_hparams* hp,
+                                   float* grad, float* loss_out, void* workspace,
+                                   mlearn_stream_t stream) {
+    int rc = validate_lstm(policy, lstm);
+    if (rc) return rc;
+    ML_REQUIRE(ro && mb_seq && adv_stats && hp && workspace && grad && start_h && start_c,
+               "lstm ppo: null pointer");
+    ML_REQUIRE(ro->dones, "lstm ppo: the rollout view needs dones (sequence breaks)");
+    ML_REQUIRE(mb_size >= 32 && mb_size % 32 == 0, "lstm ppo: mb_size must be a multiple of 32");
+    ML_REQUIRE(((int64_t)mb_size * ro->bptt_len) % 64 == 0,
+               "lstm ppo: mb_size * bptt_len must be a multiple of 64");
+    ML_REQUIRE(ro->N >= 1 && ro->N < (1ll << 31) && (int64_t)mb_size * ro->bptt_len < (1ll << 31),
+               "lstm ppo: N and rows per minibatch must be < 2^31");
+    ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "lstm ppo: bad bptt_len");
+    ML_REQUIRE(ro->ld == 0 || ro->ld >= ro->N, "lstm ppo: ld < N");
+    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
+               "lstm ppo: null rollout array");
+    ML_REQUIRE(!hp->clip_value_loss || ro->values, "lstm ppo: clip_value_loss needs values");
+    hipStream_t s = S(stream);
+#define ML_DISPATCH(T)                                                                            \
+    switch (policy->hidden) {                                                                    \
+        case 64: return launch_minibatch_lstm<T, 64>(*policy, *lstm, *ro, start_h, start_c,      \
+                                                     mb_seq, mb_size, adv_stats, *hp, grad,      \
+                                                     loss_out, workspace, s);                    \
+        case 128: return launch_minibatch_lstm<T, 128>(*policy, *lstm, *ro, start_h, start_c,    \
+                                                       mb_seq, mb_size, adv_stats, *hp, grad,    \
+                                                       loss_out, workspace, s);                  \
+        default: return launch_minibatch_lstm<T, 256>(*policy, *lstm, *ro, start_h, start_c,     \
+                                                      mb_seq, mb_size, adv_stats, *hp, grad,     \
+                                                      loss_out, workspace, s);                   \
+    }
+    if (policy->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
 }
 
 int mlearn_ppo_minibatch_fwd_bwd(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,

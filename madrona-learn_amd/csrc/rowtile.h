@@ -363,6 +363,36 @@ __device__ inline void store4(bf16* p, float a, float b, float c, float d) {
 __device__ inline void store4(float* p, float a, float b, float c, float d) {
     *(float4*)p = make_float4(a, b, c, d);
 }
+// Load 4 consecutive elements as f32.
+__device__ inline float4 load4(const bf16* p) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const bf16x4 v = *(const bf16x4*)p;
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ inline float4 load4(const float* p) { return *(const float4*)p; }
+__device__ inline float f4get(const float4& v, int j) {
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+__device__ inline float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// flax OptimizedLSTMCell step (rnn.py:28-41) on one (row, unit) from the
+// f32 gate pre-activations (x.Wi + h.Wh + bias): gate activations, c' and h'
+// rounded to the compute dtype (precision contract: oracle/lstm_ref.py).
+struct CellOut {
+    float i, f, g, o, c, h;
+};
+template <typename T>
+__device__ inline CellOut lstm_cell_fwd(float pi, float pf, float pg, float po, float cin) {
+    CellOut r;
+    r.i = rnd<T>(sigmoidf(pi));
+    r.f = rnd<T>(sigmoidf(pf));
+    r.g = rnd<T>(tanhf(pg));
+    r.o = rnd<T>(sigmoidf(po));
+    r.c = rnd<T>(r.f * cin + r.i * r.g);
+    r.h = rnd<T>(r.o * tanhf(r.c));
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // Pair-packed blocks: the 16 accumulator values of one 32-feature block as 8
@@ -489,16 +519,39 @@ struct PolicyK {
 };
 
 PolicyK make_policy_k(const mlearn_mlp_policy& p);
+
+// LSTM weights of a recurrent policy (mlearn_lstm); bias is the f32 master.
+struct LstmK {
+    const void* wi_perm;
+    const void* wi_nat;
+    const void* wh_nat;
+    const void* w_bwd;
+    const void* head_t_nat;
+    const float* bias;
+};
+inline LstmK make_lstm_k(const mlearn_lstm& r) {
+    return LstmK{r.wi_perm, r.wi_nat, r.wh_nat, r.w_bwd, r.head_t_nat, r.bias};
+}
 int validate_policy(const mlearn_mlp_policy* p);
 
 // Flat f32 parameter layout (mlearn_param_count): per layer W_l [in][H],
 // LN scale [H], LN bias [H]; then head W [H][A+1], head bias [A+1].
+// Recurrent policies append, after the MLP layout padded to 64 floats, the
+// LSTM segment Wi [H][4H], Wh [H][4H], bias [4H] (lstm_H = 0: no segment).
 struct LayoutK {
     int L, D, H, A1;  // A1 = A + 1 head outputs
     int64_t w_off[MLEARN_MAX_LAYERS], s_off[MLEARN_MAX_LAYERS], b_off[MLEARN_MAX_LAYERS];
     int64_t hw_off, hb_off, total;
+    int64_t mlp_total, lstm_off;  // end of the MLP parameters, start of the LSTM segment
+    int lstm_H;
 };
 
+// Projection slots: 2l = trunk kernel W_l, 2l + 1 = LayerNorm l, then (LSTM)
+// 2L + 4 * which + gate = gate kernel (which 0: Wi, 1: Wh).
+constexpr int kMaxSlots = 2 * MLEARN_MAX_LAYERS + 8;
+
 LayoutK make_layout(const mlearn_mlp_policy& p);
+LayoutK make_layout_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& r);
+int validate_lstm(const mlearn_mlp_policy* p, const mlearn_lstm* r);
 
 }  // namespace ml

@@ -160,10 +160,9 @@ def flatten(P, lay):
 # ---------------------------------------------------------------------------
 # actor-critic forward (models.py:46-56, 99-154; actor_critic.py:74-128)
 # ---------------------------------------------------------------------------
-def forward(P, x, mode, ad=np.float64):
-    """MLP trunk (Dense no-bias -> LayerNorm -> ReLU) + actor logits + critic.
-
-    Returns (logits [M,A] f32-valued, value [M], cache)."""
+def trunk(P, x, mode, ad=np.float64):
+    """MLP trunk (models.py:99-119): Dense no-bias -> LayerNorm -> ReLU per
+    layer.  Returns (last activation [M,H], cache)."""
     h = rnd(x, mode, ad)
     cache = {"in": [], "z": [], "mean": [], "rstd": [], "a": []}
     for l in range(len(P["W"])):
@@ -180,10 +179,26 @@ def forward(P, x, mode, ad=np.float64):
         cache["rstd"].append(rstd)
         cache["a"].append(a)
         h = a
+    return h, cache
+
+
+def heads(P, h, mode, ad=np.float64):
+    """DenseLayerDiscreteActor + DenseLayerCritic (models.py:122-154) on the
+    backbone features: Dense with bias, outputs upcast to f32.  Returns
+    (logits [M,A], value [M])."""
     Wh = rnd(P["Wh"], mode, ad)
     out = rnd(rnd(h @ Wh, mode, ad) + rnd(P["bh"], mode, ad), mode, ad)  # Dense + bias
     A = Wh.shape[1] - 1
-    return out[:, :A], out[:, A], cache
+    return out[:, :A], out[:, A]
+
+
+def forward(P, x, mode, ad=np.float64):
+    """MLP trunk + actor logits + critic.
+
+    Returns (logits [M,A] f32-valued, value [M], cache)."""
+    h, cache = trunk(P, x, mode, ad)
+    logits, V = heads(P, h, mode, ad)
+    return logits, V, cache
 
 
 def log_softmax_groups(logits, buckets):
@@ -235,12 +250,11 @@ def _dmin(a, b):
     return np.where(a < b, 1.0, np.where(a == b, 0.5, 0.0))
 
 
-def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale=1.0,
+def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0,
                    ad=np.float64):
-    """Loss (ppo.py:129-262) and d loss / d params (jax.value_and_grad) by
-    hand-written backprop.  batch: obs [M,D], actions [M,K], log_probs [M,K],
-    advantages [M], returns [M], values [M] (all rows of one minibatch)."""
-    logits, V, cache = forward(P, batch["obs"], mode, ad)
+    """PPO loss (ppo.py:129-262) and d loss / d head outputs [M, A+1]
+    (logits then value), unrounded.  batch: actions [M,K], log_probs [M,K],
+    advantages [M], returns [M], values [M]."""
     M = logits.shape[0]
     K = len(buckets)
     acts = np.asarray(batch["actions"])
@@ -300,16 +314,16 @@ def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale
         dvl = e
     dV = hp["value_loss_coef"] * inv_s * dvl * dvp * loss_scale
     loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
+    metrics = {
+        "Loss": loss, "Action Obj": obj, "Value Loss": vl, "Value Errors": np.abs(V - R),
+        "Entropy": ent,
+    }
+    return loss, np.concatenate([dlog, dV[:, None]], -1), metrics
 
-    # ---- backward ----
-    A = logits.shape[1]
-    dhead = np.concatenate([dlog, dV[:, None]], -1)
-    dhead = rnd(dhead, mode, ad)                     # cotangent in the compute dtype
-    G = {"W": [None] * len(P["W"]), "s": [None] * len(P["W"]), "b": [None] * len(P["W"])}
-    aL = cache["a"][-1]
-    G["Wh"] = aL.T @ dhead
-    G["bh"] = dhead.sum(0)
-    da = dhead @ rnd(P["Wh"], mode, ad).T
+
+def trunk_backward(P, cache, da, G, mode, ad=np.float64):
+    """Backward through the MLP trunk from d loss / d (last activation):
+    ReLU, LayerNorm (flax fast variance), Dense; fills G['W'], G['s'], G['b']."""
     for l in range(len(P["W"]) - 1, -1, -1):
         z, mean, rstd = cache["z"][l], cache["mean"][l], cache["rstd"][l]
         gam, bet = P["s"][l].astype(ad), P["b"][l].astype(ad)
@@ -324,10 +338,25 @@ def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale
         G["W"][l] = cache["in"][l].T @ dz
         if l > 0:
             da = dz @ rnd(P["W"][l], mode, ad).T
-    metrics = {
-        "Loss": loss, "Action Obj": obj, "Value Loss": vl, "Value Errors": np.abs(V - R),
-        "Entropy": ent,
-    }
+    return G
+
+
+def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale=1.0,
+                   ad=np.float64):
+    """Loss (ppo.py:129-262) and d loss / d params (jax.value_and_grad) by
+    hand-written backprop.  batch: obs [M,D], actions [M,K], log_probs [M,K],
+    advantages [M], returns [M], values [M] (all rows of one minibatch)."""
+    logits, V, cache = forward(P, batch["obs"], mode, ad)
+    loss, dhead, metrics = ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats, loss_scale,
+                                          ad)
+    # ---- backward ----
+    dhead = rnd(dhead, mode, ad)                     # cotangent in the compute dtype
+    G = {"W": [None] * len(P["W"]), "s": [None] * len(P["W"]), "b": [None] * len(P["W"])}
+    aL = cache["a"][-1]
+    G["Wh"] = aL.T @ dhead
+    G["bh"] = dhead.sum(0)
+    da = dhead @ rnd(P["Wh"], mode, ad).T
+    trunk_backward(P, cache, da, G, mode, ad)
     return loss, G, metrics, {"logits": logits, "value": V}
 
 
