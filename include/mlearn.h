@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 3
+#define MLEARN_ABI_VERSION 4
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)

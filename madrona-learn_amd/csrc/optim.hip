@@ -105,7 +105,9 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     float contrib = 0.f;
     int slot = -2;
     const float gn = global_norm(gpart);
-    if (p < Lk.total) {
+    // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
+    const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
+    if (p < Lk.total && !pad) {
         float g = grads[p];
         if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
         const int count = step[0] + 1;

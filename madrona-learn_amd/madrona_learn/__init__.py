@@ -21,11 +21,12 @@ from .profile import profile
 from .train import TrainHooks, TrainingManager, init_training, stop_training, train
 from .train_state import TrainStateManager
 from . import models
+from . import rnn
 
 __all__ = [
     "init_training", "stop_training", "train", "TrainHooks", "TrainingManager",
     "DiscreteActionsConfig", "ContinuousActionsConfig", "TrainConfig", "PBTConfig",
-    "ParamExplore", "EvalConfig", "TrainStateManager", "models", "Policy",
+    "ParamExplore", "EvalConfig", "TrainStateManager", "models", "rnn", "Policy",
     "DiscreteActionDistributions", "PhiloxKey", "ObservationsEMANormalizer",
     "ObservationsCaster", "ObservationsPreprocessNoop", "ActorCritic", "BackboneEncoder",
     "RecurrentBackboneEncoder", "Backbone", "BackboneShared", "BackboneSeparate", "PPOConfig",

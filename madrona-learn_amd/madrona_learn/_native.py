@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -72,6 +72,17 @@ class OptimState(Structure):
                 ("normalize_layernorms", c_int32)]
 
 
+class Lstm(Structure):  # mlearn_lstm
+    _fields_ = [("hidden", c_int32), ("num_layers", c_int32), ("wi_perm", c_void_p),
+                ("wi_nat", c_void_p), ("wh_nat", c_void_p), ("w_bwd", c_void_p),
+                ("head_t_nat", c_void_p), ("bias", c_void_p)]
+
+
+class LstmCarry(Structure):  # mlearn_lstm_carry
+    _fields_ = [("h", c_void_p), ("c", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
+                ("commit", c_int32), ("pad", c_int32)]
+
+
 _S = c_void_p  # hipStream_t
 _P = c_void_p
 
@@ -108,6 +119,21 @@ _SIGNATURES = {
     "mlearn_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(OptimState), _P, _S]),
     "mlearn_policy_sync_weights": (c_int32, [POINTER(MlpPolicy), _P, _S]),
+    "mlearn_lstm_param_offset": (c_int64, [POINTER(MlpPolicy)]),
+    "mlearn_lstm_param_count": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm)]),
+    "mlearn_lstm_policy_rollout_step": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm),
+                                                  POINTER(LstmCarry), _P, c_int64, _P, _P, _P, _P,
+                                                  c_uint32, c_uint32, _P, c_uint64, c_uint32,
+                                                  c_int32, POINTER(PostStep), _S]),
+    "mlearn_lstm_ppo_workspace_bytes": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm), c_int64,
+                                                  c_int32]),
+    "mlearn_lstm_ppo_minibatch_grad": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm),
+                                                 POINTER(RolloutView), _P, _P, _P, c_int32, _P,
+                                                 POINTER(PPOHparams), _P, _P, _P, _S]),
+    "mlearn_lstm_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm)]),
+    "mlearn_lstm_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(OptimState),
+                                         _P, _S]),
+    "mlearn_lstm_sync_weights": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), _P, _S]),
     "mlearn_dummy_env_step": (c_int32, [_P, _P, c_int32, c_int64, c_int32, c_uint32, c_uint32,
                                         c_uint32, _P, _P, _P, _S]),
     "mlearn_dummy_env_reset": (c_int32, [_P, c_int64, c_int32, c_uint32, c_uint32, c_uint32, _P,

@@ -76,11 +76,12 @@ class PPO(AlgoBase):  # ppo.py:49-106
         return list(names) + PPO_METRICS
 
     # ------------------------------------------------------------------
-    def prepare(self, cfg, policy_state, train_state, view, dp, policy_idx=0):
+    def prepare(self, cfg, policy_state, train_state, view, dp, policy_idx=0, start_states=None):
         """Allocate the per-update buffers once (graph-capture safe).  ``view``
         is the rollout view of this policy's env columns; ``dp`` the data
         parallel group that trains this policy; ``policy_idx`` its slot in the
-        rank's metrics."""
+        rank's metrics; ``start_states`` the device pointers of this policy's
+        rnn_start_states (recurrent policies)."""
         algo = cfg.algo
         if cfg.filter_advantages or cfg.importance_sample_trajectories:
             raise NotImplementedError(
@@ -103,7 +104,19 @@ class PPO(AlgoBase):  # ppo.py:49-106
         self.adv_stats = torch.zeros((self.E, self.num_mb, 2), dtype=torch.float32, device=dev)
         self.adv_sums = torch.zeros((self.E, 2 * self.num_mb), dtype=torch.float64, device=dev)
         rows = self.mb * self.bptt
-        nbytes = nat.lib().mlearn_ppo_workspace_bytes(policy_state.desc, rows)
+        self.lstm = policy_state.lstm_desc
+        if self.lstm is not None:
+            if start_states is None:
+                raise ValueError("a recurrent policy needs the rollout's rnn_start_states")
+            if self.mb % 32 != 0 or rows % 64 != 0:
+                raise NotImplementedError(
+                    "recurrent fused path: minibatch_size must be a multiple of 32 sequences "
+                    "and minibatch_size * bptt_len a multiple of 64")
+            self.start_h, self.start_c = (nat.c_void_p(x) for x in start_states)
+            nbytes = nat.lib().mlearn_lstm_ppo_workspace_bytes(policy_state.desc, self.lstm,
+                                                               rows, self.mb)
+        else:
+            nbytes = nat.lib().mlearn_ppo_workspace_bytes(policy_state.desc, rows)
         self.ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
         self.view = view
         self.policy_idx = policy_idx
@@ -159,10 +172,17 @@ class PPO(AlgoBase):  # ppo.py:49-106
         for e in range(self.E):
             for m in range(self.num_mb):
                 seqs = self.perm[e, m * self.mb:(m + 1) * self.mb]
-                nat.check(L.mlearn_ppo_minibatch_grad(
-                    policy_state.desc, self.view, nat.ptr(seqs), self.mb,
-                    nat.ptr(self.adv_stats[e, m]), self.hp, nat.ptr(train_state.grads),
-                    nat.ptr(loss_out), nat.ptr(self.ws), strm), "ppo_minibatch_grad")
+                if self.lstm is not None:
+                    nat.check(L.mlearn_lstm_ppo_minibatch_grad(
+                        policy_state.desc, self.lstm, self.view, self.start_h, self.start_c,
+                        nat.ptr(seqs), self.mb, nat.ptr(self.adv_stats[e, m]), self.hp,
+                        nat.ptr(train_state.grads), nat.ptr(loss_out), nat.ptr(self.ws), strm),
+                        "lstm_ppo_minibatch_grad")
+                else:
+                    nat.check(L.mlearn_ppo_minibatch_grad(
+                        policy_state.desc, self.view, nat.ptr(seqs), self.mb,
+                        nat.ptr(self.adv_stats[e, m]), self.hp, nat.ptr(train_state.grads),
+                        nat.ptr(loss_out), nat.ptr(self.ws), strm), "ppo_minibatch_grad")
                 if self.dp.world_size > 1:
                     yield ("allreduce", train_state.grads)
                 train_state.optimizer_step(policy_state)

@@ -130,7 +130,7 @@ class RolloutData:  # rollouts.py:311-334
 
 
 class RolloutStore:
-    def __init__(self, T, N, obs_dim, K, compute_dtype, device):
+    def __init__(self, T, N, obs_dim, K, compute_dtype, device, num_chunks=1, rnn_hidden=0):
         self.T, self.N = T, N
         f32 = torch.float32
         self.obs = torch.zeros((T, N, obs_dim), dtype=compute_dtype, device=device)
@@ -143,6 +143,13 @@ class RolloutStore:
         self.returns = torch.zeros((T, N), dtype=f32, device=device)
         self.env_returns_trace = torch.zeros((T, N), dtype=f32, device=device)
         self.bootstrap = torch.zeros((N,), dtype=f32, device=device)
+        # rnn_start_states (rollouts.py:528-537): the carry entering every BPTT
+        # chunk, [C][N][H] in the compute dtype (recurrent policies only)
+        self.start_h = self.start_c = None
+        if rnn_hidden:
+            self.start_h = torch.zeros((num_chunks, N, rnn_hidden), dtype=compute_dtype,
+                                       device=device)
+            self.start_c = torch.zeros_like(self.start_h)
 
     def as_dict(self):
         return {"obs": self.obs, "actions": self.actions, "log_probs": self.log_probs,
@@ -216,7 +223,21 @@ class RolloutManager:  # rollouts.py:373-826
         for ps in self.policies[1:]:
             assert ps.arch == arch, "population policies must share one architecture"
         self.store = RolloutStore(self.T, self.N, arch.obs_dim, arch.num_groups, arch.dtype,
-                                  self.policy_state.device)
+                                  self.policy_state.device, self.C, arch.lstm_hidden)
+        self.R = arch.lstm_hidden
+        if self.R:
+            # the live recurrent carry (c_states, h_states) of rollouts.py:898-901,
+            # one layer, [N][H] compute dtype, kept in the rollout state
+            rs = init_rollout_state.rnn_states
+            ok = (isinstance(rs, (tuple, list)) and len(rs) == 2 and len(rs[0]) == 1 and
+                  all(isinstance(x[0], torch.Tensor) and x[0].shape == (self.N, self.R) and
+                      x[0].dtype == arch.dtype and x[0].device == self.policy_state.device and
+                      x[0].is_contiguous() for x in rs))
+            if not ok:
+                z = lambda: torch.zeros((self.N, self.R), dtype=arch.dtype,  # noqa: E731
+                                        device=self.policy_state.device)
+                init_rollout_state.rnn_states = ([z()], [z()])
+            self._carries = {}
         self.env_offset = int(env_offset)
         self.use_advantages = train_cfg.compute_advantages
         dev = self.policy_state.device
@@ -244,6 +265,34 @@ class RolloutManager:  # rollouts.py:373-826
     def view(self, p=0):
         """Rollout view of policy p's env columns."""
         return self.store.view(self.bptt, p * self.B, self.B)
+
+    def start_states(self, p=0):
+        """Device pointers of policy p's rnn_start_states columns ([C][ld][H],
+        ld = the store's N), as the recurrent minibatch kernel reads them."""
+        s = self.store
+        off = p * self.B * self.R * s.start_h.element_size()
+        return s.start_h.data_ptr() + off, s.start_c.data_ptr() + off
+
+    def _carry(self, rollout_state, p, t):
+        """LstmCarry of policy p at env step t (t = T: the bootstrap critic,
+        which clears the carry where the last step ended an episode but does
+        not advance it)."""
+        key = (p, t)
+        d = self._carries.get(key)
+        c_states, h_states = rollout_state.rnn_states
+        h, c = h_states[0], c_states[0]
+        if d is None or d.h != h.data_ptr() + p * self.B * self.R * h.element_size():
+            d = nat.LstmCarry()
+            es = h.element_size()
+            d.h = h.data_ptr() + p * self.B * self.R * es
+            d.c = c.data_ptr() + p * self.B * self.R * es
+            if t < self.T and t % self.bptt == 0:
+                sh = self.store.start_h[t // self.bptt, p * self.B:(p + 1) * self.B]
+                sc = self.store.start_c[t // self.bptt, p * self.B:(p + 1) * self.B]
+                d.start_h, d.start_c = sh.data_ptr(), sc.data_ptr()
+            d.commit = 1 if t < self.T else 0
+            self._carries[key] = d
+        return d
 
     def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
         return list(names) + ROLLOUT_METRICS
@@ -288,7 +337,8 @@ class RolloutManager:  # rollouts.py:373-826
                 c = slice(p * B, (p + 1) * B)
                 ps.rollout_step(obs[c], s.obs[t, c], s.actions[t, c], s.log_probs[t, c],
                                 s.values[t, c], key, step_ctr, t, self.env_offset + p * B,
-                                sample=True, post=posts[p])
+                                sample=True, post=posts[p],
+                                carry=self._carry(rollout_state, p, t) if self.R else None)
             step_input = {
                 "state": rollout_state.sim_state,
                 "actions": s.actions[t],
@@ -311,7 +361,8 @@ class RolloutManager:  # rollouts.py:373-826
         obs = self.prep_obs(rollout_state.cur_obs)
         for p, ps in enumerate(self.policies):
             c = slice(p * B, (p + 1) * B)
-            ps.critic_only(obs[c], s.bootstrap[c], post=posts[p])
+            ps.critic_only(obs[c], s.bootstrap[c], post=posts[p],
+                           carry=self._carry(rollout_state, p, self.T) if self.R else None)
         rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:

@@ -232,7 +232,8 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     names = user_hooks.add_metrics(names)
     metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device, num_policies=len(pss))
     for p, (ps, ts, algo) in enumerate(zip(pss, tss, algos)):
-        algo.prepare(cfg, ps, ts, rollout_mgr.view(p), dp, policy_idx=p)
+        algo.prepare(cfg, ps, ts, rollout_mgr.view(p), dp, policy_idx=p,
+                     start_states=rollout_mgr.start_states(p) if ps.recurrent else None)
     print(cfg)
     return TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                            update_idx=start, use_graph=use_graph, profile_port=profile_port)

@@ -16,10 +16,12 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .actor_critic import ActorCritic, BackboneEncoder, BackboneShared
+from .actor_critic import (ActorCritic, BackboneEncoder, BackboneShared,
+                           RecurrentBackboneEncoder)
 from .cfg import DiscreteActionsConfig, TrainConfig
 from .models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
 from .observations import ObservationsPreprocessNoop
+from .rnn import LSTM
 
 
 @dataclass(frozen=True)
@@ -29,6 +31,7 @@ class MlpArch:
     num_layers: int
     buckets: tuple
     dtype: torch.dtype
+    lstm_hidden: int = 0  # width of the LSTM after the trunk (0: feed-forward policy)
 
     @property
     def num_logits(self):
@@ -56,6 +59,17 @@ def param_layout(arch: MlpArch):
     off += H * A1
     lay["hb"] = (off, (A1,))
     off += A1
+    if arch.lstm_hidden:
+        # mlearn_lstm_param_offset: the LSTM segment starts 64-float aligned
+        R = arch.lstm_hidden
+        off = (off + 63) // 64 * 64
+        lay["lstm_off"] = off
+        lay["wi"] = (off, (H, 4 * R))   # input kernels ii | if | ig | io
+        off += 4 * R * H
+        lay["wr"] = (off, (R, 4 * R))   # hidden kernels hi | hf | hg | ho
+        off += 4 * R * R
+        lay["bl"] = (off, (4 * R,))     # hidden-kernel biases
+        off += 4 * R
     lay["total"] = off
     return lay
 
@@ -71,11 +85,23 @@ def _actions_buckets(actor, cfg_actions):
 def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpArch:
     bb = actor_critic.backbone
     enc = bb.encoder if isinstance(bb, BackboneShared) else bb
-    if not isinstance(enc, BackboneEncoder):
+    lstm_hidden = 0
+    if isinstance(enc, RecurrentBackboneEncoder):
+        rnn = enc.rnn
+        if not isinstance(rnn, LSTM):
+            raise NotImplementedError(f"recurrent fused path needs rnn.LSTM, got "
+                                      f"{type(rnn).__name__}")
+        if rnn.num_layers != 1:
+            raise NotImplementedError("recurrent fused path: one LSTM layer (rnn.py:10-45)")
+        if rnn.num_hidden_channels != getattr(enc.net, "num_channels", None):
+            raise NotImplementedError("recurrent fused path: LSTM width must equal the MLP "
+                                      "width")
+        lstm_hidden = rnn.num_hidden_channels
+    elif not isinstance(enc, BackboneEncoder):
         raise NotImplementedError(
-            "fused path supports BackboneShared(encoder=BackboneEncoder(net=MLP)) "
-            "(actor_critic.py:131-153, 202-244); recurrent / separate backbones are the next "
-            "SURVEY §8(f) rows")
+            "fused path supports BackboneShared(encoder=BackboneEncoder(net=MLP)) and "
+            "RecurrentBackboneEncoder(net=MLP, rnn=LSTM) (actor_critic.py:131-244); "
+            "separate backbones are outside the fused path")
     net = enc.net
     if not isinstance(net, MLP):
         raise NotImplementedError(f"fused path needs an MLP trunk, got {type(net).__name__}")
@@ -85,7 +111,7 @@ def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpA
             "dreamer_v3_critic=False in TrainConfig")
     buckets = _actions_buckets(actor_critic.actor, None)
     return MlpArch(obs_dim=int(obs_dim), hidden=net.num_channels, num_layers=net.num_layers,
-                   buckets=buckets, dtype=compute_dtype)
+                   buckets=buckets, dtype=compute_dtype, lstm_hidden=lstm_hidden)
 
 
 class PolicyState:
@@ -101,8 +127,9 @@ class PolicyState:
         dt = arch.dtype
 
         host = np.zeros(self.layout["total"], dtype=np.float32)
-        net = actor_critic.backbone.encoder.net if isinstance(
-            actor_critic.backbone, BackboneShared) else actor_critic.backbone.net
+        enc = actor_critic.backbone.encoder if isinstance(
+            actor_critic.backbone, BackboneShared) else actor_critic.backbone
+        net = enc.net
         init_norms = []
         for l in range(L):
             o, shp = self.layout["w"][l]
@@ -115,6 +142,16 @@ class PolicyState:
         wa = actor_critic.actor.weight_init(rng, (H, arch.num_logits))
         wv = actor_critic.critic.weight_init(rng, (H, 1))
         host[o:o + H * A1] = np.concatenate([wa, wv], axis=1).reshape(-1)
+        if arch.lstm_hidden:
+            # OptimizedLSTMCell (rnn.py:30-36): orthogonal per gate kernel, zero bias;
+            # every gate kernel is projected to its own initial norm (ppo.py:303-310)
+            R = arch.lstm_hidden
+            for key, init in (("wi", enc.rnn.cell.kernel_init),
+                              ("wr", enc.rnn.cell.recurrent_kernel_init)):
+                o, (fin, _) = self.layout[key]
+                blocks = [init(rng, (fin, R)) for _ in range(4)]
+                host[o:o + fin * 4 * R] = np.concatenate(blocks, axis=1).reshape(-1)
+                init_norms += [float(np.linalg.norm(b.astype(np.float64))) for b in blocks]
 
         self.params = torch.from_numpy(host).to(self.device)
         self.init_norms = torch.tensor(init_norms, dtype=torch.float32, device=self.device)
@@ -143,7 +180,29 @@ class PolicyState:
         d.head = self.head.data_ptr()
         d.head_bias = self.head_b.data_ptr()
         self.desc = d
-        n = nat.lib().mlearn_param_count(d)
+        self.lstm_desc = None
+        if arch.lstm_hidden:
+            R = arch.lstm_hidden
+            self.lstm_wi_perm = torch.zeros(4 * R * H, dtype=dt, device=self.device)
+            self.lstm_wi_nat = torch.zeros(4 * R * H, dtype=dt, device=self.device)
+            self.lstm_wh_nat = torch.zeros(4 * R * R, dtype=dt, device=self.device)
+            self.lstm_w_bwd = torch.zeros((H + R) * 4 * R, dtype=dt, device=self.device)
+            self.head_t_nat = torch.zeros(nat.HEAD_COLS * R, dtype=dt, device=self.device)
+            ld = nat.Lstm()
+            ld.hidden = R
+            ld.num_layers = 1
+            ld.wi_perm = self.lstm_wi_perm.data_ptr()
+            ld.wi_nat = self.lstm_wi_nat.data_ptr()
+            ld.wh_nat = self.lstm_wh_nat.data_ptr()
+            ld.w_bwd = self.lstm_w_bwd.data_ptr()
+            ld.head_t_nat = self.head_t_nat.data_ptr()
+            ld.bias = self.params.data_ptr() + 4 * self.layout["bl"][0]
+            self.lstm_desc = ld
+            n = nat.lib().mlearn_lstm_param_count(d, ld)
+            if nat.lib().mlearn_lstm_param_offset(d) != self.layout["lstm_off"]:
+                raise RuntimeError("LSTM parameter offset mismatch")
+        else:
+            n = nat.lib().mlearn_param_count(d)
         if n != self.layout["total"]:
             raise RuntimeError(f"param layout mismatch: native {n} vs {self.layout['total']}")
         self.sync_weights()
@@ -163,31 +222,73 @@ class PolicyState:
             net[f"LayerNorm_{l}"] = {"impl": {"scale": self.view("s", l),
                                               "bias": self.view("b", l)}}
         hw, hb = self.view("hw"), self.view("hb")
+        enc = {"net": net}
+        if self.arch.lstm_hidden:
+            # flax OptimizedLSTMCell leaves ii..io (kernel), hi..ho (kernel, bias)
+            R = self.arch.lstm_hidden
+            wi, wr, bl = self.view("wi"), self.view("wr"), self.view("bl")
+            cell = {}
+            for g, name in enumerate("ifgo"):
+                cell[f"i{name}"] = {"kernel": wi[:, g * R:(g + 1) * R]}
+                cell[f"h{name}"] = {"kernel": wr[:, g * R:(g + 1) * R],
+                                    "bias": bl[g * R:(g + 1) * R]}
+            enc["rnn"] = {"cell": {"OptimizedLSTMCell_0": cell}}
         return {
-            "backbone": {"encoder": {"net": net}},
+            "backbone": {"encoder": enc},
             "actor": {"impl": {"kernel": hw[:, :A], "bias": hb[:A]}},
             "critic": {"Dense_0": {"kernel": hw[:, A:], "bias": hb[A:]}},
         }
 
     def sync_weights(self):
+        if self.lstm_desc is not None:
+            nat.check(nat.lib().mlearn_lstm_sync_weights(self.desc, self.lstm_desc,
+                                                         nat.ptr(self.params),
+                                                         nat.stream_handle()), "sync_weights")
+            return
         nat.check(nat.lib().mlearn_policy_sync_weights(self.desc, nat.ptr(self.params),
                                                        nat.stream_handle()), "sync_weights")
 
+    @property
+    def recurrent(self):
+        return self.lstm_desc is not None
+
     # -- kernels ------------------------------------------------------------
     def rollout_step(self, obs, obs_store, actions, log_probs, values, key, step_ctr, step,
-                     env_offset=0, sample=True, post=None):
+                     env_offset=0, sample=True, post=None, carry=None):
         """ActorCritic.rollout + store (actor_critic.py:74-96, rollouts.py:637-668);
-        post: optional nat.PostStep of the previous env step."""
+        post: optional nat.PostStep of the previous env step; carry: the
+        nat.LstmCarry of a recurrent policy."""
         N = obs.shape[0]
+        if self.lstm_desc is not None:
+            self._check_carry(carry)
+            nat.check(nat.lib().mlearn_lstm_policy_rollout_step(
+                self.desc, self.lstm_desc, carry, nat.ptr(obs, torch.float32, name="obs"), N,
+                nat.ptr(obs_store), nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values),
+                key[0], key[1], nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post,
+                nat.stream_handle()), "lstm_policy_rollout_step")
+            return
         nat.check(nat.lib().mlearn_policy_rollout_step(
             self.desc, nat.ptr(obs, torch.float32, name="obs"), N, nat.ptr(obs_store),
             nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values), key[0], key[1],
             nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post,
             nat.stream_handle()), "policy_rollout_step")
 
-    def critic_only(self, obs, values, post=None):
-        """ActorCritic.critic_only (actor_critic.py:65-72)."""
+    def _check_carry(self, carry):
+        if not isinstance(carry, nat.LstmCarry) or not carry.h or not carry.c:
+            raise ValueError("a recurrent policy needs its LstmCarry (rollout carry h, c)")
+
+    def critic_only(self, obs, values, post=None, carry=None):
+        """ActorCritic.critic_only (actor_critic.py:65-72).  A recurrent policy
+        runs the cell from the carry without advancing it (carry.commit = 0:
+        the carry is only cleared where post's dones are set)."""
         N = obs.shape[0]
+        if self.lstm_desc is not None:
+            self._check_carry(carry)
+            nat.check(nat.lib().mlearn_lstm_policy_rollout_step(
+                self.desc, self.lstm_desc, carry, nat.ptr(obs, torch.float32, name="obs"), N,
+                None, None, None, nat.ptr(values), 0, 0, None, 0, 0, 0, post,
+                nat.stream_handle()), "lstm_critic_only")
+            return
         nat.check(nat.lib().mlearn_policy_rollout_step(
             self.desc, nat.ptr(obs, torch.float32, name="obs"), N, None, None, None,
             nat.ptr(values), 0, 0, None, 0, 0, 0, post, nat.stream_handle()), "critic_only")
@@ -213,7 +314,11 @@ class PolicyTrainState:
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.initial_weight_norms = policy_state.init_norms
         self.update_prng_key = (int(key[0]) & 0xFFFFFFFF, int(key[1]) & 0xFFFFFFFF)
-        nbytes = nat.lib().mlearn_optim_workspace_bytes(policy_state.desc)
+        if policy_state.lstm_desc is not None:
+            nbytes = nat.lib().mlearn_lstm_optim_workspace_bytes(policy_state.desc,
+                                                                 policy_state.lstm_desc)
+        else:
+            nbytes = nat.lib().mlearn_optim_workspace_bytes(policy_state.desc)
         self.optim_ws = torch.zeros(max(nbytes, 16), dtype=torch.uint8, device=dev)
         o = nat.OptimState()
         o.params = policy_state.params.data_ptr()
@@ -230,6 +335,11 @@ class PolicyTrainState:
         self.optim_desc = o
 
     def optimizer_step(self, policy_state: PolicyState):
+        if policy_state.lstm_desc is not None:
+            nat.check(nat.lib().mlearn_lstm_optim_step(policy_state.desc, policy_state.lstm_desc,
+                                                       self.optim_desc, nat.ptr(self.optim_ws),
+                                                       nat.stream_handle()), "lstm_optim_step")
+            return
         nat.check(nat.lib().mlearn_optim_step(policy_state.desc, self.optim_desc,
                                               nat.ptr(self.optim_ws), nat.stream_handle()),
                   "optim_step")

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from madrona_learn import _native as nat
-    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 3
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 4
     hdr = open(HEADER).read()
     assert f"#define MLEARN_ABI_VERSION {nat.ABI_VERSION}" in hdr
 
@@ -80,3 +80,52 @@ def test_param_count_matches_oracle_layout():
     d.head_t = d.head = d.head_bias = 1
     n = nat.lib().mlearn_param_count(ctypes.byref(d))
     assert n == ref.param_layout(64, 256, 2, 26)["total"] == 89883
+
+
+def test_lstm_layout_matches_oracle_and_arch():
+    """LSTM parameter segment: native offsets/counts == oracle layout ==
+    the product's param_layout; RecurrentBackboneEncoder(MLP, LSTM) compiles."""
+    import madrona_learn as ml
+    from madrona_learn import _native as nat
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.rnn import LSTM
+    from madrona_learn.train_state import compile_arch, param_layout
+    from oracle import lstm_ref as lref
+    import pytest
+    import torch
+    buckets = [4, 8, 5, 5, 2, 2]
+    for H, L in ((256, 2), (64, 1), (128, 3)):
+        d = nat.MlpPolicy()
+        d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_BF16, 64, H, L
+        d.actions = nat.action_layout(buckets)
+        for l in range(L):
+            d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
+            d.w[l] = 1
+        d.head_t = d.head = d.head_bias = 1
+        r = nat.Lstm()
+        r.hidden, r.num_layers = H, 1
+        r.wi_perm = r.wi_nat = r.wh_nat = r.w_bwd = r.head_t_nat = r.bias = 1
+        lay = lref.param_layout(64, H, L, 26)
+        assert nat.lib().mlearn_lstm_param_offset(ctypes.byref(d)) == lay["lstm_off"]
+        assert nat.lib().mlearn_lstm_param_count(ctypes.byref(d), ctypes.byref(r)) == lay["total"]
+        ac = ml.ActorCritic(
+            backbone=ml.BackboneShared(encoder=ml.RecurrentBackboneEncoder(
+                net=MLP(H, L, "bf16"), rnn=LSTM(H, 1, "bf16"))),
+            actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(buckets), "bf16"),
+            critic=DenseLayerCritic("bf16"))
+        arch = compile_arch(ac, 64, torch.bfloat16)
+        assert arch.lstm_hidden == H
+        pl = param_layout(arch)
+        assert pl["total"] == lay["total"]
+        assert (pl["wi"][0], pl["wr"][0], pl["bl"][0]) == (lay["Wi"][0], lay["Wr"][0],
+                                                          lay["bl"][0])
+        # a width mismatch or a second layer is rejected, never silently run
+        r.num_layers = 2
+        assert nat.lib().mlearn_lstm_param_count(ctypes.byref(d), ctypes.byref(r)) == -1
+    bad = ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.RecurrentBackboneEncoder(
+            net=MLP(256, 2, "bf16"), rnn=LSTM(128, 1, "bf16"))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(buckets), "bf16"),
+        critic=DenseLayerCritic("bf16"))
+    with pytest.raises(NotImplementedError):
+        compile_arch(bad, 64, torch.bfloat16)
