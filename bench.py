@@ -8,6 +8,12 @@ steps + bootstrap + GAE + 8 minibatch optimizer steps), captured in HIP
 graphs.  Multi-GPU (torch.distributed.run): each rank owns 8192 envs (weak
 scaling), RCCL all-reduce of the advantage statistics and gradients.
 
+Other BASELINE.json configs (not the default line): ``--config lstm`` =
+configs[3] (the same workload with RecurrentBackboneEncoder(MLP[256,256],
+LSTM(256)), ``--bptt-chunks`` C in {1, 2}); ``--config pbt`` = configs[4]
+(8 train policies x 8192 envs, self-play split, placed over the ranks: one
+policy per GPU at 8 GPUs, all 8 on one GPU at N = 1).
+
 Prints ONE JSON line on rank 0.
 """
 
@@ -34,22 +40,45 @@ BF16_PEAK_TFS = 2500.0    # dense bf16 MFMA spec
 FWD_FLOP = 2 * (OBS * HID + HID * HID + HID * (sum(BUCKETS) + 1))  # 177,664 per sample
 
 
-def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True):
+PBT_POLICIES = 8
+
+
+def envs_per_rank(config, world):
+    if config == "pbt":
+        if PBT_POLICIES % world != 0:
+            raise SystemExit(f"--config pbt places {PBT_POLICIES} policies: world must divide it")
+        return N_ENVS * (PBT_POLICIES // world)
+    return N_ENVS
+
+
+def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True, config="b1",
+         chunks=1):
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.rnn import LSTM
     env = DummyVecEnv(N, OBS, len(BUCKETS), seed=0, env_offset=env_offset, device=dev)
+    pbt = None
+    if config == "pbt":
+        pbt = ml.PBTConfig(num_teams=1, team_size=1, num_train_policies=PBT_POLICIES,
+                           num_past_policies=0, self_play_portion=1.0, cross_play_portion=0.0,
+                           past_play_portion=0.0)
     cfg = ml.TrainConfig(
         num_worlds=N, num_agents_per_world=1, num_updates=1,
         actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T, lr=3e-4,
         algo=ml.PPOConfig(num_epochs=EPOCHS, minibatch_size=MB, clip_coef=0.2,
                           value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                           max_grad_norm=0.5),
-        num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=0, metrics_buffer_size=8,
-        dreamer_v3_critic=False, compute_dtype=dtype)
+        num_bptt_chunks=chunks, gamma=0.99, gae_lambda=0.95, seed=0, metrics_buffer_size=8,
+        dreamer_v3_critic=False, compute_dtype=dtype, pbt=pbt)
+    if config == "lstm":
+        encoder = ml.RecurrentBackboneEncoder(net=MLP(HID, LAYERS, dtype),
+                                              rnn=LSTM(HID, 1, dtype))
+    else:
+        encoder = ml.BackboneEncoder(net=MLP(HID, LAYERS, dtype))
     policy = ml.Policy(
         actor_critic=ml.ActorCritic(
-            backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(HID, LAYERS, dtype))),
+            backbone=ml.BackboneShared(encoder=encoder),
             actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
             critic=DenseLayerCritic(dtype)),
         obs_preprocess=ml.ObservationsCaster.create(dtype))
@@ -105,7 +134,7 @@ def kernel_rooflines(mgr, dev, iters=20):
     from madrona_learn import _native as nat
     L = nat.lib()
     algo = mgr.algo
-    ps = mgr.state.policy_states
+    ps = mgr.state.policy_list[0]
     stream = torch.cuda.Stream(device=dev)
     seqs = algo.perm[0, :algo.mb]
 
@@ -226,6 +255,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--config", choices=["b1", "lstm", "pbt"], default="b1")
+    ap.add_argument("--bptt-chunks", type=int, default=1)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -246,7 +277,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    mgr = make(dev, env_offset=rank * N_ENVS, use_graph=not args.no_graph)
+    n_rank = envs_per_rank(args.config, world)
+    mgr = make(dev, N=n_rank, env_offset=rank * n_rank, use_graph=not args.no_graph,
+               config=args.config, chunks=args.bptt_chunks)
     for _ in range(args.warmup):
         mgr.update_iter()
     torch.cuda.synchronize()
@@ -265,28 +298,34 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_steps = N_ENVS * world * T * args.steps
+    total_steps = n_rank * world * T * args.steps
     value = total_steps / elapsed
     ms = elapsed / args.steps * 1e3
 
     result = None
     if rank == 0:
+        workload = {
+            "b1": "B1: PPO iteration, 8192 envs/GPU, T=32, obs=64, MLP[256,256], heads "
+                  "[4,8,5,5,2,2]+critic, 2 epochs x 4 minibatches of 2048 seqs",
+            "lstm": f"L: B1 with RecurrentBackboneEncoder(MLP[256,256], LSTM(256)), "
+                    f"{args.bptt_chunks} BPTT chunk(s), minibatches of 2048 seqs",
+            "pbt": f"P: {PBT_POLICIES} train policies x 8192 envs (self-play split), "
+                   f"{PBT_POLICIES // world} per GPU, B1 policy and PPO settings",
+        }[args.config]
         result = {
             "metric": "env-steps/sec whole-node, 65536-env PPO, at 1/2/4/8 MI355X",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (dummy vec-env HIP kernel, random-init orthogonal weights)",
-            "config": {"workload": "B1: PPO iteration, 8192 envs/GPU, T=32, obs=64, "
-                                   "MLP[256,256], heads [4,8,5,5,2,2]+critic, 2 epochs x 4 "
-                                   "minibatches of 2048 seqs",
-                       "envs_per_gpu": N_ENVS, "total_envs": N_ENVS * world,
+            "config": {"workload": workload,
+                       "envs_per_gpu": n_rank, "total_envs": n_rank * world,
                        "steps_per_update": T, "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph},
         }
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and args.config != "lstm":
         result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev)
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and args.config == "b1":
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(result))

@@ -80,6 +80,8 @@ __device__ inline int proj_slot(const LayoutK& k, int64_t p) {
     return p < k.s_off[l] ? 2 * l : 2 * l + 1;
 }
 
+constexpr int kAdamBlocks = 256;
+
 // Global gradient norm from the kNormBlocks partials (every block computes it
 // the same way: wave 0, fixed butterfly order).
 __device__ inline float global_norm(const double* gpart) {
@@ -99,36 +101,43 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
                                                    const int32_t* step, const double* gpart,
                                                    float lr, float b1, float b2, float eps,
                                                    float max_norm, double* proj_part) {
+    // grid-stride over the parameters with at most kAdamBlocks blocks, so the
+    // projection reduces a short, fixed list of per-block partials
     __shared__ float sh[4][kMaxSlots];
-    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
-    float contrib = 0.f;
-    int slot = -2;
-    const float gn = global_norm(gpart);
-    // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
-    const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
-    if (p < Lk.total && !pad) {
-        float g = grads[p];
-        if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
-        const int count = step[0] + 1;
-        const float mm = (1.f - b1) * g + b1 * m[p];
-        const float vv = (1.f - b2) * (g * g) + b2 * v[p];
-        const float mhat = mm / (1.f - powf(b1, (float)count));
-        const float vhat = vv / (1.f - powf(b2, (float)count));
-        const float u = mhat / (sqrtf(vhat) + eps);
-        const float np = params[p] + (-lr) * u;
-        m[p] = mm;
-        v[p] = vv;
-        params[p] = np;
-        slot = proj_slot(Lk, p);
-        contrib = np * np;
-    }
-    // per-block partial sums of squares per projection slot
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int s = 0; s < nslot; ++s) {
-        float x = slot == s ? contrib : 0.f;
-        x = wave_sum64(x);
-        if (lane == 0) sh[w][s] = x;
+    if (threadIdx.x < 4 * kMaxSlots) sh[threadIdx.x / kMaxSlots][threadIdx.x % kMaxSlots] = 0.f;
+    const float gn = global_norm(gpart);  // (its barrier also orders the sh zeroing)
+    for (int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x; p - threadIdx.x < Lk.total;
+         p += (int64_t)gridDim.x * 256) {
+        float contrib = 0.f;
+        int slot = -2;
+        // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
+        const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
+        if (p < Lk.total && !pad) {
+            float g = grads[p];
+            if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
+            const int count = step[0] + 1;
+            const float mm = (1.f - b1) * g + b1 * m[p];
+            const float vv = (1.f - b2) * (g * g) + b2 * v[p];
+            const float mhat = mm / (1.f - powf(b1, (float)count));
+            const float vhat = vv / (1.f - powf(b2, (float)count));
+            const float u = mhat / (sqrtf(vhat) + eps);
+            const float np = params[p] + (-lr) * u;
+            m[p] = mm;
+            v[p] = vv;
+            params[p] = np;
+            slot = proj_slot(Lk, p);
+            contrib = np * np;
+        }
+        // per-block partial sums of squares per projection slot (a wave's 64
+        // parameters span at most two slots: skip the absent ones)
+        for (int s = 0; s < nslot; ++s) {
+            if (!__any(slot == s)) continue;
+            float x = slot == s ? contrib : 0.f;
+            x = wave_sum64(x);
+            if (lane == 0) sh[w][s] += x;
+        }
     }
     __syncthreads();
     if (threadIdx.x < nslot) {
@@ -265,21 +274,22 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
                "optim_step: null pointer");
     ML_REQUIRE(st->max_grad_norm > 0 && st->lr >= 0, "optim_step: bad hyperparameters");
     const int64_t nblk = (Lk.total + 255) / 256;
+    const int ablk = (int)(nblk < kAdamBlocks ? nblk : kAdamBlocks);
     double* gpart = (double*)workspace;
     double* ppart = gpart + kNormBlocks;
     hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
                        Lk.total, gpart);
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk), dim3(256), 0, s, Lk, st->params,
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
                        (const double*)gpart, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
                        ppart);
     if (dtype == MLEARN_DTYPE_BF16)
         hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const double*)ppart, (int)nblk,
+                           st->params, st->init_norms, (const double*)ppart, ablk,
                            st->normalize_params, st->normalize_layernorms, st->step);
     else
         hipLaunchKernelGGL(project_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const double*)ppart, (int)nblk,
+                           st->params, st->init_norms, (const double*)ppart, ablk,
                            st->normalize_params, st->normalize_layernorms, st->step);
     return check_launch("optim_step");
 }
