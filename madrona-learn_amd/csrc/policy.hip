@@ -89,9 +89,12 @@ __device__ inline void post_step_row(const PostK& p, int64_t n) {
 // post-activation fragments written back to LDS for the next layer.  The
 // heads split the reduction instead: each wave multiplies its own features,
 // partials are summed in wave order.
+#ifndef ML_POL_MAXW
+#define ML_POL_MAXW 4  // waves per workgroup of the rollout policy kernel (feature split)
+#endif
 template <int H> struct PolCfg {
     static constexpr int NB = H / 32;
-    static constexpr int W = NB < 4 ? NB : 4;
+    static constexpr int W = NB < ML_POL_MAXW ? NB : ML_POL_MAXW;
     static constexpr int NBW = NB / W;
 };
 

@@ -48,7 +48,7 @@ struct HpK {
 
 constexpr int kLossSlots = 20;   // per tile doubles
 #ifndef ML_STEP_WAVES
-#define ML_STEP_WAVES 2  // waves per SIMD the fused step kernel is register-budgeted for
+#define ML_STEP_WAVES 4  // waves per SIMD the fused step kernel is register-budgeted for
 #endif
 constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
@@ -317,9 +317,12 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, floa
 // statistics [W][32][2], head partials [W][32][33], logits / d logits
 // [32][33], loss partials [W][kLossSlots].
 // ---------------------------------------------------------------------------
+#ifndef ML_STEP_MAXW
+#define ML_STEP_MAXW 8  // waves per workgroup of the fused step kernel (feature split)
+#endif
 template <int H> struct StepCfg {
     static constexpr int NB = H / 32;
-    static constexpr int W = NB < 4 ? NB : 4;
+    static constexpr int W = NB < ML_STEP_MAXW ? NB : ML_STEP_MAXW;
     static constexpr int NBW = NB / W;
 };
 
