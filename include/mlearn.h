@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 4
+#define MLEARN_ABI_VERSION 5
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -42,7 +42,8 @@ extern "C" {
 
 #define MLEARN_MAX_LAYERS 4
 #define MLEARN_MAX_GROUPS 16
-#define MLEARN_HEAD_COLS 32 /* actor logits + 1 critic output, padded */
+#define MLEARN_HEAD_COLS 32     /* head width of a scalar critic: actor logits + 1, padded */
+#define MLEARN_HEAD_COLS_MAX 96 /* head width when actor logits + critic bins exceed 32 */
 
 typedef void* mlearn_stream_t; /* hipStream_t */
 
@@ -125,16 +126,24 @@ typedef struct mlearn_mlp_policy {
     int32_t obs_dim;     /* multiple of 16, <= 256 */
     int32_t hidden;      /* 64, 128 or 256 */
     int32_t num_layers;  /* 1..MLEARN_MAX_LAYERS */
+    int32_t critic_bins; /* 1: DenseLayerCritic (scalar value, models.py:142-154);
+                            odd >= 3: DreamerV3Critic two-hot logits (models.py:157-174,
+                            SymExpTwoHotDistribution dists.py:119-208; default 63) */
     mlearn_action_layout actions;
     const void* w_t[MLEARN_MAX_LAYERS];  /* hidden*in_l: Bt[n=out][k=in] = W_l[k][n] */
     const void* w[MLEARN_MAX_LAYERS];    /* hidden*in_l: Bt[n=in][k=out] = W_l[n][k];
                                             w[0] is not used */
     const float* ln_scale[MLEARN_MAX_LAYERS];  /* [hidden] f32 */
     const float* ln_bias[MLEARN_MAX_LAYERS];   /* [hidden] f32 */
-    const void* head_t;      /* 32*hidden: Bt[n=head col][k=unit]; cols 0..A-1 actor, A critic */
-    const void* head;        /* 32*hidden: Bt[n=unit][k=head col] */
-    const float* head_bias;  /* [32] f32 */
+    /* head columns: 0..A-1 actor logits, A..A+critic_bins-1 critic, zero padding up
+     * to HC = mlearn_head_cols(policy) (32, or 96 when A + critic_bins > 32) */
+    const void* head_t;      /* HC*hidden: Bt[n=head col][k=unit] */
+    const void* head;        /* HC*hidden: Bt[n=unit][k=head col] */
+    const float* head_bias;  /* [HC] f32 */
 } mlearn_mlp_policy;
+
+/* Head width HC of a policy descriptor (-1 if invalid). */
+int32_t mlearn_head_cols(const mlearn_mlp_policy* policy);
 
 /* Post-step bookkeeping of the PREVIOUS env step (rollouts.py:933-973), fused
  * into the next policy launch; same arithmetic as mlearn_rollout_post_step. */
@@ -152,7 +161,8 @@ typedef struct mlearn_post_step {
  * the post-inference store (rollouts.py:637-668): preprocess (cast to the
  * compute dtype) -> MLP trunk -> actor logits + critic -> sample -> write
  * obs_store[N][obs_dim] (may be NULL), actions[N][K] i32, log_probs[N][K] f32,
- * values[N] f32.  actions == NULL computes only the critic
+ * values[N] f32 (the scalar critic, or SymExpTwoHotDistribution.mean() of the
+ * two-hot critic, rollouts.py:601-605).  actions == NULL computes only the critic
  * (ActorCritic.critic_only, actor_critic.py:65-72, used for the bootstrap
  * values, rollouts.py:607-635).  post (may be NULL) applies the post-step of
  * the previous env step in the same launch. */
@@ -248,7 +258,10 @@ int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows
  * mb_seq = the mb_size sequence ids of this minibatch (a slice of perm).
  * adv_stats = {mean, rstd} of this minibatch.  loss_out (may be NULL) receives
  * 5 x {mean, m2, min, max, count}: 'Loss' {loss,0,loss,loss,1}, 'Action Obj',
- * 'Value Loss', 'Value Errors', 'Entropy' (ppo.py:95-106, 351-362). */
+ * 'Value Loss', 'Value Errors', 'Entropy' (ppo.py:95-106, 351-362).  With
+ * critic_bins > 1 the value loss is the two-hot cross entropy of the returns
+ * (ppo.py:169-177, dists.py:171-208); clip/huber value losses need the scalar
+ * critic (ppo.py:54-57). */
 int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
                               const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
                               const mlearn_ppo_hparams* hp, float* grad, float* loss_out,
@@ -266,7 +279,8 @@ int mlearn_ppo_minibatch_fwd_bwd(const mlearn_mlp_policy* policy, const mlearn_r
 
 /* Parameter layout of the flat f32 buffers (params, grads, Adam m/v):
  * per layer l: W_l [in_l][hidden], ln_scale_l [hidden], ln_bias_l [hidden];
- * then head W [hidden][A+1] (logits then critic), head bias [A+1]. */
+ * then head W [hidden][A+C] (logits then the C = critic_bins critic outputs),
+ * head bias [A+C]. */
 int64_t mlearn_param_count(const mlearn_mlp_policy* policy);
 
 typedef struct mlearn_optim_state {

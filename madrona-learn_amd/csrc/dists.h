@@ -41,4 +41,77 @@ __device__ inline void sample_group(const float* lg, int nb, int jbase, uint32_t
     if (logp) *logp = lg[best] - lse;
 }
 
+// ---------------------------------------------------------------------------
+// SymExpTwoHotDistribution (dists.py:119-208) over the nb critic logits of a
+// DreamerV3Critic (models.py:157-174), logits already cast to f32.
+// ---------------------------------------------------------------------------
+// Bin j (dists.py:128-141): half = symexp(linspace(-14, 0, nb/2 + 1)) in f32,
+// jnp.linspace's interpolation form start * (1 - i/div) (+ stop * i/div, stop
+// = 0); bins = [half, -half[:-1][::-1]]; symexp(x) = sign(x) expm1(|x|)
+// (utils.py:39-40).
+__device__ inline float twohot_bin(int j, int nb) {
+    const int nh = nb / 2;
+    const int i = j <= nh ? j : nb - 1 - j;
+    if (i == nh) return 0.f;
+    const float x = -14.0f * (1.0f - (float)i / (float)nh);
+    const float v = -expm1f(-x);  // symexp(x), x < 0
+    return j <= nh ? v : -v;
+}
+
+// softmax statistics of the nb logits: max and sum of exp(l - max)
+__device__ inline void twohot_softmax(const float* lg, int nb, float* mx_out, float* se_out) {
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    *mx_out = mx;
+    *se_out = se;
+}
+
+// SymExpTwoHotDistribution.mean (dists.py:143-169): p_mid * b_mid plus the
+// mirrored pairs (p_{mid-1-i} b_{mid-1-i} + p_{mid+1+i} b_{mid+1+i}) summed
+// (symmetric so that it is exactly 0 at initialisation).  bins: LDS table.
+__device__ inline float twohot_mean(const float* lg, int nb, const float* bins, float mx, float se) {
+    const int mid = (nb - 1) / 2;
+    float acc = 0.f;
+    for (int i = 0; i < mid; ++i) {
+        const int a = mid - 1 - i, b = mid + 1 + i;
+        acc += (__expf(lg[a] - mx) / se) * bins[a] + (__expf(lg[b] - mx) / se) * bins[b];
+    }
+    return (__expf(lg[mid] - mx) / se) * bins[mid] + acc;
+}
+
+// two_hot_cross_entropy_loss (dists.py:171-208) of one target: returns the
+// loss and writes d loss / d logit_j * scale in place of the logits.  The
+// bin weights are the reference's as written: lower weight = |b_lo - t| /
+// (|b_lo - t| + |b_up - t|), upper = |b_up - t| / (...), both 1/2 when the
+// clipped indices coincide.  mean_out receives mean() (metrics).
+__device__ inline float twohot_ce(float* lg, int nb, float target, const float* bins, float scale,
+                                  float* mean_out) {
+    int lo = -1, up = nb;
+    for (int j = 0; j < nb; ++j) {
+        lo += bins[j] <= target ? 1 : 0;
+        up -= bins[j] > target ? 1 : 0;
+    }
+    lo = min(max(lo, 0), nb - 1);
+    up = min(max(up, 0), nb - 1);
+    const bool same = lo == up;
+    const float dl = same ? 1.f : fabsf(bins[lo] - target);
+    const float du = same ? 1.f : fabsf(bins[up] - target);
+    const float tot = dl + du;
+    const float wl = dl / tot, wu = du / tot;
+    float mx, se;
+    twohot_softmax(lg, nb, &mx, &se);
+    *mean_out = twohot_mean(lg, nb, bins, mx, se);
+    const float lse = mx + __logf(se);
+    const float loss = -(wl * (lg[lo] - lse) + wu * (lg[up] - lse));
+    const float wsum = wl + wu;
+    for (int j = 0; j < nb; ++j) {
+        const float p = __expf(lg[j] - mx) / se;
+        const float w = (j == lo ? wl : 0.f) + (j == up ? wu : 0.f);
+        lg[j] = (wsum * p - w) * scale;
+    }
+    return loss;
+}
+
 }  // namespace ml

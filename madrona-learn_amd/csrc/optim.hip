@@ -175,7 +175,7 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
         int64_t q = p - Lk.hw_off;
         int c = (int)(q / Lk.A1), k = (int)(q % Lk.A1);
         ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(val);
-        ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(val);
+        ((T*)C.head)[img_index<T>(c, k, Lk.HC, false)] = cvt<T>(val);
         if (C.head_t_nat) ((T*)C.head_t_nat)[img_index<T>(k, c, H, false)] = cvt<T>(val);
     } else {
         int l = Lk.L - 1;
@@ -240,11 +240,11 @@ __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const 
     const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     const int H = Lk.H;
     // padding: head_t rows A1..31, head cols A1..31, head_b A1..31
-    const int64_t pad = (int64_t)(MLEARN_HEAD_COLS - Lk.A1) * H;
+    const int64_t pad = (int64_t)(Lk.HC - Lk.A1) * H;
     if (p < pad) {
         int k = Lk.A1 + (int)(p / H), c = (int)(p % H);
         ((T*)C.head_t)[img_index<T>(k, c, H, true)] = cvt<T>(0.f);
-        ((T*)C.head)[img_index<T>(c, k, MLEARN_HEAD_COLS, false)] = cvt<T>(0.f);
+        ((T*)C.head)[img_index<T>(c, k, Lk.HC, false)] = cvt<T>(0.f);
         if (C.head_t_nat) ((T*)C.head_t_nat)[img_index<T>(k, c, H, false)] = cvt<T>(0.f);
         if (c == 0) C.head_b[k] = 0.f;
     }
@@ -297,7 +297,7 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
 static int sync_launch(const LayoutK& Lk, const CopiesK& C, int dtype, const float* params,
                        hipStream_t s) {
     ML_REQUIRE(params, "sync_weights: null params");
-    int64_t n = Lk.total > (int64_t)MLEARN_HEAD_COLS * Lk.H ? Lk.total : (int64_t)MLEARN_HEAD_COLS * Lk.H;
+    int64_t n = Lk.total > (int64_t)Lk.HC * Lk.H ? Lk.total : (int64_t)Lk.HC * Lk.H;
     unsigned g = (unsigned)((n + 255) / 256);
     if (dtype == MLEARN_DTYPE_BF16)
         hipLaunchKernelGGL(sync_kernel<bf16>, dim3(g), dim3(256), 0, s, Lk, C, params);

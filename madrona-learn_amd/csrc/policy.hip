@@ -22,6 +22,8 @@ PolicyK make_policy_k(const mlearn_mlp_policy& p) {
     k.L = p.num_layers;
     k.K = p.actions.num_groups;
     k.A = p.actions.num_logits;
+    k.CB = p.critic_bins;
+    k.HC = head_cols(p);
     for (int i = 0; i <= MLEARN_MAX_GROUPS; ++i) k.off[i] = p.actions.offsets[i];
     for (int l = 0; l < MLEARN_MAX_LAYERS; ++l) {
         k.wt[l] = p.w_t[l];
@@ -45,8 +47,12 @@ int validate_policy(const mlearn_mlp_policy* p) {
     ML_REQUIRE(p->num_layers >= 1 && p->num_layers <= MLEARN_MAX_LAYERS, "policy: bad num_layers");
     const mlearn_action_layout& l = p->actions;
     ML_REQUIRE(l.num_groups >= 1 && l.num_groups <= MLEARN_MAX_GROUPS, "policy: bad num_groups");
-    ML_REQUIRE(l.num_logits >= 1 && l.num_logits + 1 <= MLEARN_HEAD_COLS,
-               "policy: at most %d logits", MLEARN_HEAD_COLS - 1);
+    ML_REQUIRE(p->critic_bins == 1 || (p->critic_bins >= 3 && p->critic_bins % 2 == 1),
+               "policy: critic_bins must be 1 (scalar critic) or odd >= 3 (two-hot), got %d",
+               p->critic_bins);
+    ML_REQUIRE(l.num_logits >= 1 && l.num_logits + p->critic_bins <= MLEARN_HEAD_COLS_MAX,
+               "policy: actor logits + critic outputs must be <= %d (got %d + %d)",
+               MLEARN_HEAD_COLS_MAX, l.num_logits, p->critic_bins);
     ML_REQUIRE(l.offsets[0] == 0 && l.offsets[l.num_groups] == l.num_logits,
                "policy: bad action offsets");
     for (int k = 0; k < l.num_groups; ++k)
@@ -114,7 +120,7 @@ struct CarryK {
 // hidden units (8 accumulator blocks, weight images in unit-block gate
 // order), so the cell update is register-local and h' lands in exactly the
 // layout the heads consume.
-template <typename T, int H, bool RNN>
+template <typename T, int H, bool RNN, int HC>
 __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
@@ -130,13 +136,15 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the buffer descriptors
     frag* fr = (frag*)smem;                               // [KSH][64] B fragments
     float* gb = (float*)(fr + KSH * 64);                  // [L][2][H]
-    float* hbias = gb + L * 2 * H;                        // [32]
-    float* red = hbias + MLEARN_HEAD_COLS;                // [W][32][2]
-    float* lgp = red + W * 64;                            // [W][32][33] head partials
-    float* lg = lgp + W * 32 * 33;                        // [32][33]
-    float* rbias = lg + 32 * 33;                          // [4H] LSTM bias (RNN)
-    frag* frh = (frag*)(rbias + (RNN ? 4 * H : 0));       // [KSH][64] carry fragments (RNN)
-    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += THREADS) {
+    constexpr int LGS = HC + 1;                           // LDS row stride of the head outputs
+    float* hbias = gb + L * 2 * H;                        // [HC]
+    float* red = hbias + HC;                              // [W][32][2]
+    float* lgp = red + W * 64;                            // [W][32][LGS] head partials
+    float* lg = lgp + W * 32 * LGS;                       // [32][LGS]
+    float* rbias = lg + 32 * LGS;                         // [4H] LSTM bias (RNN)
+    float* bins = rbias + (RNN ? 4 * H : 0);              // [HC] two-hot critic bins
+    frag* frh = (frag*)(bins + HC);                       // [KSH][64] carry fragments (RNN)
+    for (int i = tid; i < L * 2 * H + HC; i += THREADS) {
         float v;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
@@ -148,6 +156,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     }
     if constexpr (RNN)
         for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
+    if (P.CB > 1)
+        for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
     const int64_t row0 = (int64_t)blockIdx.x * 32;
     const int64_t row = row0 + r;
     const bool live = row < N;
@@ -274,20 +284,23 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
-        f32x16 ha[1];
-        zero_acc<1>(ha);
-        gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
-            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane);
+        constexpr int HB = HC / 32;
+        f32x16 ha[HB];
+        zero_acc<HB>(ha);
+        gemm_ring<T, HB, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane, KSH);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * 33 + feat(0, q, h)] = ha[0][q];
+        for (int nb = 0; nb < HB; ++nb)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(nb, q, h)] = ha[nb][q];
     }
     __syncthreads();
-    for (int i = tid; i < 32 * MLEARN_HEAD_COLS; i += THREADS) {
-        const int rr = i >> 5, j = i & 31;
-        float x = lgp[rr * 33 + j];
+    for (int i = tid; i < 32 * HC; i += THREADS) {
+        const int rr = i / HC, j = i - rr * HC;
+        float x = lgp[rr * LGS + j];
 #pragma unroll
-        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * 33 + j];
-        lg[rr * 33 + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * LGS + j];
+        lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
     }
     __syncthreads();
 
@@ -299,30 +312,39 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             if (n >= N) continue;
             int a;
             float lp;
-            sample_group(lg + rr * 33 + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
+            sample_group(lg + rr * LGS + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
                          eoff + (uint32_t)n, step, sample, &a, &lp);
             actions[n * P.K + g] = a;
             if (logp) logp[n * P.K + g] = lp;
         }
     }
-    if (values && tid < 32 && row0 + tid < N) values[row0 + tid] = lg[tid * 33 + P.A];
+    if (values && tid < 32 && row0 + tid < N) {
+        const float* cl = lg + tid * LGS + P.A;
+        float v = cl[0];
+        if (P.CB > 1) {  // SymExpTwoHotDistribution.mean() (rollouts.py:601-605)
+            float mx, se;
+            twohot_softmax(cl, P.CB, &mx, &se);
+            v = twohot_mean(cl, P.CB, bins, mx, se);
+        }
+        values[row0 + tid] = v;
+    }
 }
 
-template <typename T, int H, bool RNN> static size_t policy_step_lds(int L) {
+template <typename T, int H, bool RNN, int HC> static size_t policy_step_lds(int L) {
     typedef PolCfg<H> C;
     const size_t frags = (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
     return frags * (RNN ? 2 : 1) +
-           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33 +
-                    (RNN ? 4 * H : 0)) * 4;
+           (size_t)(L * 2 * H + HC + C::W * 64 + (C::W + 1) * 32 * (HC + 1) +
+                    (RNN ? 4 * H : 0) + HC) * 4;
 }
 
-template <typename T, int H, bool RNN>
+template <typename T, int H, bool RNN, int HC>
 static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, void* obs_store,
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
                               const PostK& post, const LstmK& R, const CarryK& cy, hipStream_t s) {
-    const size_t lds = policy_step_lds<T, H, RNN>(P.L);
-    auto kern = policy_step_kernel<T, H, RNN>;
+    const size_t lds = policy_step_lds<T, H, RNN, HC>(P.L);
+    auto kern = policy_step_kernel<T, H, RNN, HC>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -372,11 +394,15 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
     }
     PolicyK P = make_policy_k(*policy);
     hipStream_t s = S(stream);
-#define ML_LAUNCH(T, HH)                                                                          \
-    (lstm ? launch_policy_step<T, HH, true>(P, obs, N, obs_store, actions, log_probs, values, k0, \
-                                            k1, step_ctr, step, env_offset, sample, pk, R, cy, s) \
-          : launch_policy_step<T, HH, false>(P, obs, N, obs_store, actions, log_probs, values, k0, \
-                                             k1, step_ctr, step, env_offset, sample, pk, R, cy, s))
+#define ML_LAUNCH_HC(T, HH, HC)                                                                 \
+    (lstm ? launch_policy_step<T, HH, true, HC>(P, obs, N, obs_store, actions, log_probs, values, \
+                                                k0, k1, step_ctr, step, env_offset, sample, pk, R, \
+                                                cy, s)                                            \
+          : launch_policy_step<T, HH, false, HC>(P, obs, N, obs_store, actions, log_probs, values, \
+                                                 k0, k1, step_ctr, step, env_offset, sample, pk, R, \
+                                                 cy, s))
+#define ML_LAUNCH(T, HH) \
+    (P.HC == MLEARN_HEAD_COLS ? ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS) : ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS_MAX))
 #define ML_DISPATCH(T)                      \
     switch (policy->hidden) {               \
         case 64: return ML_LAUNCH(T, 64);   \
@@ -390,6 +416,7 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
     }
 #undef ML_DISPATCH
 #undef ML_LAUNCH
+#undef ML_LAUNCH_HC
 }
 
 }  // namespace ml
@@ -414,4 +441,9 @@ extern "C" int mlearn_lstm_policy_rollout_step(
     ML_REQUIRE(lstm, "lstm rollout step: null lstm descriptor");
     return rollout_step_entry(policy, lstm, carry, obs, N, obs_store, actions, log_probs, values,
                               k0, k1, step_ctr, step, env_offset, sample, post, stream);
+}
+
+extern "C" int32_t mlearn_head_cols(const mlearn_mlp_policy* policy) {
+    if (validate_policy(policy)) return -1;
+    return head_cols(*policy);
 }

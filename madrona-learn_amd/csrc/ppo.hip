@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "dists.h"
 #include "rowtile.h"
 
 namespace ml {
@@ -135,13 +136,14 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     w.Mp = Mp;
     w.ntiles = (int)tiles;
     // column partials: LayerNorm [L][2][H], head bias [32], (LSTM) bias [4H]
-    w.CP = L * 2 * H + MLEARN_HEAD_COLS + (lstm ? 4 * H : 0);
+    const int HC = head_cols(p);
+    w.CP = L * 2 * H + HC + (lstm ? 4 * H : 0);
     w.x0 = take(Mp * D * es);
     for (int l = 0; l < L; ++l) {
         w.a[l] = take(Mp * H * es);
         w.dz[l] = take(Mp * H * es);
     }
-    w.dhead = take(Mp * MLEARN_HEAD_COLS * es);
+    w.dhead = take(Mp * HC * es);
     w.colpart = (float*)take(tiles * w.CP * sizeof(float));
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
@@ -149,7 +151,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     const int njobs = L + 1 + (lstm ? 2 : 0);
     for (int l = 0; l < njobs; ++l) {
         const int I = l >= L ? H : (l == 0 ? D : H);
-        const int J = l == L ? MLEARN_HEAD_COLS : (l > L ? 4 * H : H);
+        const int J = l == L ? HC : (l > L ? 4 * H : H);
         plan_splits(I, J, Mp, &w.splits[l], &w.rps[l]);
         w.slab_off[l] = so;
         so += (int64_t)w.splits[l] * I * J;
@@ -271,8 +273,9 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
     }
 }
 
-// lg points at the row; value logit at column A; zeroes columns A+1..31.
-__device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, float ov,
+// Scalar critic (DenseLayerCritic): lg points at the row, value at column A;
+// zeroes columns A+1..HC-1.
+__device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float R, float ov,
                                   LossAcc& m) {
     const float V = lg[A];
     float vpred = V, dvp = 1.f;
@@ -294,8 +297,27 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, floa
         dvl = e;
     }
     lg[A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
-    for (int j = A + 1; j < MLEARN_HEAD_COLS; ++j) lg[j] = 0.f;
+    for (int j = A + 1; j < HC; ++j) lg[j] = 0.f;
     const float verr = fabsf(V - R);
+    m.svl += vl;
+    m.qvl += vl * vl;
+    m.mnvl = fminf(m.mnvl, vl);
+    m.mxvl = fmaxf(m.mxvl, vl);
+    m.serr += verr;
+    m.qerr += verr * verr;
+    m.mnerr = fminf(m.mnerr, verr);
+    m.mxerr = fmaxf(m.mxerr, verr);
+}
+
+// DreamerV3Critic (ppo.py:169-177): value loss = two-hot cross entropy of the
+// return against the CB bin logits at lg[A..A+CB); value error = mean() - R.
+// Writes d loss / d bin logits in place, zeroes columns A+CB..HC-1.
+__device__ inline void loss_value_twohot(const HpK& hp, float* lg, int A, int CB, int HC,
+                                         const float* bins, float R, LossAcc& m) {
+    float mean;
+    const float vl = twohot_ce(lg + A, CB, R, bins, hp.vcoef * hp.inv_s * hp.loss_scale, &mean);
+    for (int j = A + CB; j < HC; ++j) lg[j] = 0.f;
+    const float verr = fabsf(mean - R);
     m.svl += vl;
     m.qvl += vl * vl;
     m.mnvl = fminf(m.mnvl, vl);
@@ -314,8 +336,8 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, float R, floa
 // post-activation (forward) or dZ (backward) fragments through LDS.  Each
 // wave keeps its own Dense outputs in registers for the backward pass.
 // LDS: B fragments [KSH][64], LayerNorm scale/bias [L][2][H], head bias, row
-// statistics [W][32][2], head partials [W][32][33], logits / d logits
-// [32][33], loss partials [W][kLossSlots].
+// statistics [W][32][2], head partials [W][32][HC+1], logits / d logits
+// [32][HC+1], loss partials [W][kLossSlots], critic bins [HC].
 // ---------------------------------------------------------------------------
 #ifndef ML_STEP_MAXW
 #define ML_STEP_MAXW 8  // waves per workgroup of the fused step kernel (feature split)
@@ -326,11 +348,11 @@ template <int H> struct StepCfg {
     static constexpr int NBW = NB / W;
 };
 
-template <typename T, int H, int L> static size_t step_lds() {
+template <typename T, int H, int L, int HC> static size_t step_lds() {
     typedef StepCfg<H> C;
     return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
-           (size_t)(L * 2 * H + MLEARN_HEAD_COLS + C::W * 64 + (C::W + 1) * 32 * 33 +
-                    C::W * kLossSlots) * 4;
+           (size_t)(L * 2 * H + HC + C::W * 64 + (C::W + 1) * 32 * (HC + 1) +
+                    C::W * kLossSlots + HC) * 4;
 }
 
 // ReLU' threshold: rnd<T>(y) > 0  <=>  y > THR (bf16 round-to-nearest-even
@@ -367,7 +389,7 @@ struct RecK {
     const void* head_t_nat;  // head image, natural k order (kHeads)
 };
 
-template <typename T, int H, int L, int MODE = kFused>
+template <typename T, int H, int L, int MODE = kFused, int HC = MLEARN_HEAD_COLS>
 __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws, RecK rec) {
@@ -378,7 +400,8 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     typedef StepCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
     constexpr int E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB;
-    constexpr int KSH = H / KS, KSHD = MLEARN_HEAD_COLS / KS, KSD = 256 / KS;
+    constexpr int KSH = H / KS, KSHD = HC / KS, KSD = 256 / KS;
+    constexpr int LGS = HC + 1;  // LDS row stride of the head outputs
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, K = P.K;
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -386,11 +409,14 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     frag* fr = (frag*)smem;                    // [KSH][64]
     float* gb = (float*)(fr + KSH * 64);       // [L][2][H]
     float* hbias = gb + L * 2 * H;             // [32]
-    float* red = hbias + MLEARN_HEAD_COLS;     // [W][32][2]
-    float* lgp = red + W * 64;                 // [W][32][33]
-    float* lg = lgp + W * 32 * 33;             // [32][33]
-    float* lred = lg + 32 * 33;                // [W][kLossSlots]
-    for (int i = tid; i < L * 2 * H + MLEARN_HEAD_COLS; i += THREADS) {
+    float* red = hbias + HC;                   // [W][32][2]
+    float* lgp = red + W * 64;                 // [W][32][LGS]
+    float* lg = lgp + W * 32 * LGS;            // [32][LGS]
+    float* lred = lg + 32 * LGS;               // [W][kLossSlots]
+    float* bins = lred + W * kLossSlots;       // [HC] two-hot critic bins
+    if (kLoss && P.CB > 1)
+        for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
+    for (int i = tid; i < L * 2 * H + HC; i += THREADS) {
         float v;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
@@ -506,20 +532,23 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                 for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
         }
         const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
-        f32x16 ha[1];
-        zero_acc<1>(ha);
-        gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
-            ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane);
+        constexpr int HB = HC / 32;
+        f32x16 ha[HB];
+        zero_acc<HB>(ha);
+        gemm_ring<T, HB, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+            ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane, KSH);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * 33 + feat(0, q, h)] = ha[0][q];
+        for (int nb = 0; nb < HB; ++nb)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(nb, q, h)] = ha[nb][q];
     }
     __syncthreads();
-    for (int i = tid; i < 32 * MLEARN_HEAD_COLS; i += THREADS) {
-        const int rr = i >> 5, j = i & 31;
-        float x = lgp[rr * 33 + j];
+    for (int i = tid; i < 32 * HC; i += THREADS) {
+        const int rr = i / HC, j = i - rr * HC;
+        float x = lgp[rr * LGS + j];
 #pragma unroll
-        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * 33 + j];
-        lg[rr * 33 + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * LGS + j];
+        lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
     }
     __syncthreads();
 
@@ -530,13 +559,13 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         const float as0 = adv_st[0], as1 = adv_st[1];
         for (int task = tid; task < 32 * (K + 1); task += THREADS) {
             const int rr = task & 31, g = task >> 5;
-            float* lr = lg + rr * 33;
+            float* lr = lg + rr * LGS;
             const int64_t f = row0 + rr;
             if (f >= M) {  // padding row: zero its d logits
                 if (g < K)
                     for (int j = P.off[g]; j < P.off[g + 1]; ++j) lr[j] = 0.f;
                 else
-                    for (int j = P.A; j < MLEARN_HEAD_COLS; ++j) lr[j] = 0.f;
+                    for (int j = P.A; j < HC; ++j) lr[j] = 0.f;
                 continue;
             }
             int act;
@@ -555,8 +584,10 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                 if (hp.norm_adv) adv = (adv - as0) * as1;
                 loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], act, olp, adv, hp.ecoef[g],
                            m);
+            } else if (P.CB == 1) {
+                loss_value(hp, lr, P.A, HC, ret, oval, m);
             } else {
-                loss_value(hp, lr, P.A, ret, oval, m);
+                loss_value_twohot(hp, lr, P.A, P.CB, HC, bins, ret, m);
             }
         }
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
@@ -581,17 +612,20 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         ws.loss_part[(int64_t)tile * kLossSlots + tid] = v;
     }
     STAMP(8);
-    // d head: row-major store (wgrad operand) and the head-bias column partial
+    // d head: row-major store (wgrad operand) and the head-bias column
+    // partials (one 32-column block per wave)
     if (w == 0) {
-        const float* lr = lg + r * 33 + 16 * h;
-        T* drow = (T*)ws.dhead + row * MLEARN_HEAD_COLS + 16 * h;
+        const float* lr = lg + r * LGS + (HC / 2) * h;
+        T* drow = (T*)ws.dhead + row * HC + (HC / 2) * h;
 #pragma unroll
-        for (int j = 0; j < 16; j += 4) store4(drow + j, lr[j], lr[j + 1], lr[j + 2], lr[j + 3]);
+        for (int j = 0; j < HC / 2; j += 4) store4(drow + j, lr[j], lr[j + 1], lr[j + 2], lr[j + 3]);
+    }
+    for (int cb = w; cb < HC / 32; cb += W) {
         float cs = 0.f;
 #pragma unroll
-        for (int mm = 0; mm < 16; ++mm) cs += rnd<T>(lg[(16 * h + mm) * 33 + r]);
+        for (int mm = 0; mm < 16; ++mm) cs += rnd<T>(lg[(16 * h + mm) * LGS + 32 * cb + r]);
         cs = sum_halves(cs);
-        if (h == 0) ws.colpart[(int64_t)tile * ws.CP + L * 2 * H + r] = cs;
+        if (h == 0) ws.colpart[(int64_t)tile * ws.CP + L * 2 * H + 32 * cb + r] = cs;
     }
 
     STAMP(9);
@@ -599,7 +633,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     {
         frag db[KSHD];
 #pragma unroll
-        for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * 33, s, h);
+        for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * LGS, s, h);
         zero_acc<NBW>(acc);
         // dA_{L-1}^T = Head . dHead^T  (this wave's feature blocks)
         gemm_ring<T, NBW, KSHD, 2>(acc, db, KSHD,
@@ -735,21 +769,31 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     STAMP(15);
 }
 
-template <typename T, int H, int L, int MODE = kFused>
-static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
-                        int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
-                        hipStream_t s, const RecK& rec = RecK{}) {
-    auto k = ppo_step_kernel<T, H, L, MODE>;
+template <typename T, int H, int L, int MODE, int HC>
+static void launch_step_hc(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                           int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                           hipStream_t s, const RecK& rec) {
+    auto k = ppo_step_kernel<T, H, L, MODE, HC>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   128 * 1024);
         attr_set = true;
     }
-    const size_t lds = step_lds<T, H, L>();
+    const size_t lds = step_lds<T, H, L, HC>();
     const int threads = 64 * StepCfg<H>::W;
     hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(threads), lds, s, P, R, mb_seq, mb, M, adv_st, hp,
                        ws, rec);
+}
+template <typename T, int H, int L, int MODE = kFused>
+static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                        int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                        hipStream_t s, const RecK& rec = RecK{}) {
+    if (P.HC == MLEARN_HEAD_COLS)
+        launch_step_hc<T, H, L, MODE, MLEARN_HEAD_COLS>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, rec);
+    else
+        launch_step_hc<T, H, L, MODE, MLEARN_HEAD_COLS_MAX>(P, R, mb_seq, mb, M, adv_st, hp, ws, s,
+                                                            rec);
 }
 
 // ---------------------------------------------------------------------------
@@ -956,7 +1000,8 @@ LayoutK make_layout(const mlearn_mlp_policy& p) {
     k.L = p.num_layers;
     k.D = p.obs_dim;
     k.H = p.hidden;
-    k.A1 = p.actions.num_logits + 1;
+    k.A1 = p.actions.num_logits + p.critic_bins;
+    k.HC = head_cols(p);
     int64_t o = 0;
     for (int l = 0; l < k.L; ++l) {
         k.w_off[l] = o;
@@ -1013,7 +1058,7 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
     if (Lk.lstm_H && p0 >= Lk.lstm_off) {  // LSTM segment (64-aligned)
         const int64_t q0 = p0 - Lk.lstm_off, HH = Lk.lstm_H, G = 4 * HH * HH;
         if (q0 >= 2 * G) {  // bias: column partials of d gate pre-activations
-            const int col = L * 2 * H + MLEARN_HEAD_COLS + (int)(q0 - 2 * G) + 4 * c;
+            const int col = L * 2 * H + Lk.HC + (int)(q0 - 2 * G) + 4 * c;
             for (int k = g; k < kColChunks; k += kRgGroups) {
                 const float4 x = *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col);
                 v[0] += x.x;
@@ -1044,8 +1089,8 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
             } else {
                 const int64_t q = p - Lk.hw_off;
                 const int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
-                const float* sp = ws.slab + ws.slab_off[L] + (int64_t)i * MLEARN_HEAD_COLS + j;
-                const int64_t stride = (int64_t)H * MLEARN_HEAD_COLS;
+                const float* sp = ws.slab + ws.slab_off[L] + (int64_t)i * Lk.HC + j;
+                const int64_t stride = (int64_t)H * Lk.HC;
                 for (int k = g; k < ws.splits[L]; k += kRgGroups) v[e] += sp[k * stride];
             }
         }
@@ -1192,7 +1237,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     for (int l = 0; l <= L; ++l) {
         WgJob& J = jobs.job[l];
         J.I = l == L ? H : (l == 0 ? p.obs_dim : H);
-        J.J = l == L ? MLEARN_HEAD_COLS : H;
+        J.J = l == L ? head_cols(p) : H;
         J.X = l == 0 ? ws.x0 : ws.a[l - 1];
         J.Y = l == L ? ws.dhead : ws.dz[l];
         J.out = ws.slab + ws.slab_off[l];
@@ -1461,7 +1506,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});
     // reverse scan
-    const int cp0 = L * 2 * H + MLEARN_HEAD_COLS;
+    const int cp0 = L * 2 * H + head_cols(p);
     for (int t = bptt; t >= 0; --t)
         hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, 2 * H / 128), dim3(256), 0,
                            s, RK, R, mb_seq, mb, t, lw, ws.colpart, ws.CP, cp0);
@@ -1475,7 +1520,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     for (int l = 0; l < L + 3; ++l) {
         WgJob& J = jobs.job[l];
         J.I = l >= L ? H : (l == 0 ? p.obs_dim : H);
-        J.J = l == L ? MLEARN_HEAD_COLS : (l > L ? 4 * H : H);
+        J.J = l == L ? head_cols(p) : (l > L ? 4 * H : H);
         J.X = l == 0 ? ws.x0 : (l < L ? ws.a[l - 1] : (l == L ? lw.hout : (l == L + 1 ? (const void*)feat : lw.hin)));
         J.Y = l < L ? ws.dz[l] : (l == L ? ws.dhead : lw.dg);
         J.out = ws.slab + ws.slab_off[l];

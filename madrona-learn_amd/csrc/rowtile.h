@@ -130,11 +130,13 @@ template <> __device__ inline float img_load<float>(__amdgpu_buffer_rsrc_t rs, i
 // A ring of DEPTH k-steps of A fragments is in flight ahead of the MFMAs;
 // sched_barrier fences keep the compiler from sinking each load down to its
 // MFMA, which would expose a full L2 round trip per MFMA at one wave/SIMD.
-// nks (<= NKS) is the wave-uniform number of steps actually taken.
+// nks (<= NKS) is the wave-uniform number of steps actually taken; bstride
+// (default nks) the k-steps between consecutive output blocks of the image.
 template <typename T, int NOUT, int NKS, int DEPTH>
 __device__ inline void gemm_ring(f32x16 (&acc)[NOUT], const typename RT<T>::frag (&b)[NKS],
-                                 int nks, const T* __restrict__ img, int lane) {
+                                 int nks, const T* __restrict__ img, int lane, int bstride = -1) {
     typedef typename RT<T>::frag frag;
+    const int bs = bstride < 0 ? nks : bstride;
     constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);  // bytes per fragment run
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
     const int voff = lane * RT<T>::E * (int)sizeof(T);
@@ -143,7 +145,7 @@ __device__ inline void gemm_ring(f32x16 (&acc)[NOUT], const typename RT<T>::frag
     for (int s = 0; s < DEPTH - 1; ++s)
         if (s < nks)
 #pragma unroll
-            for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * nks + s) * FB);
+            for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * bs + s) * FB);
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
         if (s < nks) {
@@ -151,7 +153,7 @@ __device__ inline void gemm_ring(f32x16 (&acc)[NOUT], const typename RT<T>::frag
             if (sl < nks) {
 #pragma unroll
                 for (int nb = 0; nb < NOUT; ++nb)
-                    ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * nks + sl) * FB);
+                    ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * bs + sl) * FB);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -508,6 +510,7 @@ template <typename T> struct ZIO {
 
 struct PolicyK {
     int D, H, L, K, A;
+    int CB, HC;  // critic outputs (1: scalar, else two-hot bins); head width (32 or 96)
     int off[MLEARN_MAX_GROUPS + 1];
     const void* wt[MLEARN_MAX_LAYERS];
     const void* w[MLEARN_MAX_LAYERS];
@@ -534,12 +537,20 @@ inline LstmK make_lstm_k(const mlearn_lstm& r) {
 }
 int validate_policy(const mlearn_mlp_policy* p);
 
+// Head width of a policy: actor logits + critic outputs, padded to 32 or 96.
+inline int head_cols(const mlearn_mlp_policy& p) {
+    return p.actions.num_logits + p.critic_bins <= MLEARN_HEAD_COLS ? MLEARN_HEAD_COLS
+                                                                   : MLEARN_HEAD_COLS_MAX;
+}
+
 // Flat f32 parameter layout (mlearn_param_count): per layer W_l [in][H],
-// LN scale [H], LN bias [H]; then head W [H][A+1], head bias [A+1].
+// LN scale [H], LN bias [H]; then head W [H][A1], head bias [A1] (A1 = actor
+// logits + critic outputs).
 // Recurrent policies append, after the MLP layout padded to 64 floats, the
 // LSTM segment Wi [H][4H], Wh [H][4H], bias [4H] (lstm_H = 0: no segment).
 struct LayoutK {
-    int L, D, H, A1;  // A1 = A + 1 head outputs
+    int L, D, H, A1;  // A1 = A + critic outputs
+    int HC;           // head width (padded)
     int64_t w_off[MLEARN_MAX_LAYERS], s_off[MLEARN_MAX_LAYERS], b_off[MLEARN_MAX_LAYERS];
     int64_t hw_off, hb_off, total;
     int64_t mlp_total, lstm_off;  // end of the MLP parameters, start of the LSTM segment

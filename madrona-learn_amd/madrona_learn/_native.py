@@ -17,13 +17,14 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
 MAX_LAYERS = 4
 MAX_GROUPS = 16
-HEAD_COLS = 32
+HEAD_COLS = 32       # head width with a scalar critic
+HEAD_COLS_MAX = 96   # head width when actor logits + critic bins exceed 32
 
 
 class ActionLayout(Structure):
@@ -33,7 +34,7 @@ class ActionLayout(Structure):
 
 class MlpPolicy(Structure):
     _fields_ = [("dtype", c_int32), ("obs_dim", c_int32), ("hidden", c_int32),
-                ("num_layers", c_int32), ("actions", ActionLayout),
+                ("num_layers", c_int32), ("critic_bins", c_int32), ("actions", ActionLayout),
                 ("w_t", c_void_p * MAX_LAYERS), ("w", c_void_p * MAX_LAYERS),
                 ("ln_scale", c_void_p * MAX_LAYERS), ("ln_bias", c_void_p * MAX_LAYERS),
                 ("head_t", c_void_p), ("head", c_void_p), ("head_bias", c_void_p)]
@@ -116,6 +117,7 @@ _SIGNATURES = {
     "mlearn_ppo_minibatch_fwd_bwd": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
                                                c_int32, _P, POINTER(PPOHparams), _P, _S]),
     "mlearn_param_count": (c_int64, [POINTER(MlpPolicy)]),
+    "mlearn_head_cols": (c_int32, [POINTER(MlpPolicy)]),
     "mlearn_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(OptimState), _P, _S]),
     "mlearn_policy_sync_weights": (c_int32, [POINTER(MlpPolicy), _P, _S]),
@@ -226,9 +228,19 @@ def action_layout(buckets):
         off += b
         lay.offsets[i + 1] = off
     lay.num_logits = off
-    if off + 1 > HEAD_COLS:
-        raise ValueError(f"at most {HEAD_COLS - 1} total logits supported, got {off}")
+    if off + 1 > HEAD_COLS_MAX:
+        raise ValueError(f"at most {HEAD_COLS_MAX - 1} total logits supported, got {off}")
     return lay
+
+
+def head_cols(num_logits, critic_bins):
+    """Head width HC of mlearn_mlp_policy (include/mlearn.h)."""
+    if num_logits + critic_bins <= HEAD_COLS:
+        return HEAD_COLS
+    if num_logits + critic_bins <= HEAD_COLS_MAX:
+        return HEAD_COLS_MAX
+    raise ValueError(f"{num_logits} actor logits + {critic_bins} critic outputs exceed "
+                     f"{HEAD_COLS_MAX} head columns")
 
 
 def dtype_code(dtype):

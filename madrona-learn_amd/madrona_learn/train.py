@@ -167,10 +167,10 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     if device.type != "cuda":
         raise ValueError(f"device must be a GPU, got {device}")
     torch.cuda.set_device(device)
-    if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
+    if cfg.hlgauss_critic:
         raise NotImplementedError(
-            "the fused path implements the scalar DenseLayerCritic: set "
-            "TrainConfig(dreamer_v3_critic=False) (DreamerV3 two-hot is SURVEY §8(f) row 2)")
+            "hlgauss_critic (HLGaussDist, models.py:177-315) is outside the fused path; the "
+            "scalar DenseLayerCritic and the DreamerV3Critic two-hot critic are supported")
     num_policies = 1
     if cfg.pbt is not None:
         pbt = cfg.pbt
@@ -200,6 +200,13 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     from .rollouts import obs_to_matrix
     obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
     arch = compile_arch(policy.actor_critic, obs0.shape[1], cfg.compute_dtype)
+    # the loss follows cfg.dreamer_v3_critic (ppo.py:169-218) and the stored
+    # values the critic module (rollouts.py:383-384, 601-605): they must agree
+    if bool(cfg.dreamer_v3_critic) != (arch.critic_bins > 1):
+        raise ValueError(
+            f"TrainConfig.dreamer_v3_critic={cfg.dreamer_v3_critic} but the policy's critic is "
+            f"{type(policy.actor_critic.critic).__name__}: use DreamerV3Critic with "
+            "dreamer_v3_critic=True (the reference default) or DenseLayerCritic with False")
     preprocess = policy.obs_preprocess
     if preprocess is not None:
         preprocess.fused_cast_dtype(cfg.compute_dtype)

@@ -19,7 +19,7 @@ from . import _native as nat
 from .actor_critic import (ActorCritic, BackboneEncoder, BackboneShared,
                            RecurrentBackboneEncoder)
 from .cfg import DiscreteActionsConfig, TrainConfig
-from .models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+from .models import MLP, DenseLayerCritic, DenseLayerDiscreteActor, DreamerV3Critic
 from .observations import ObservationsPreprocessNoop
 from .rnn import LSTM
 
@@ -32,10 +32,15 @@ class MlpArch:
     buckets: tuple
     dtype: torch.dtype
     lstm_hidden: int = 0  # width of the LSTM after the trunk (0: feed-forward policy)
+    critic_bins: int = 1  # 1: DenseLayerCritic; odd > 1: DreamerV3Critic two-hot bins
 
     @property
     def num_logits(self):
         return int(sum(self.buckets))
+
+    @property
+    def head_cols(self):
+        return nat.head_cols(self.num_logits, self.critic_bins)
 
     @property
     def num_groups(self):
@@ -44,7 +49,7 @@ class MlpArch:
 
 def param_layout(arch: MlpArch):
     """Python mirror of LayoutK / mlearn_param_count (csrc/ppo.hip)."""
-    H, A1 = arch.hidden, arch.num_logits + 1
+    H, A1 = arch.hidden, arch.num_logits + arch.critic_bins
     off = 0
     lay = {"w": [], "s": [], "b": []}
     for l in range(arch.num_layers):
@@ -105,13 +110,24 @@ def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpA
     net = enc.net
     if not isinstance(net, MLP):
         raise NotImplementedError(f"fused path needs an MLP trunk, got {type(net).__name__}")
-    if not isinstance(actor_critic.critic, DenseLayerCritic):
+    critic = actor_critic.critic
+    if isinstance(critic, DenseLayerCritic):
+        critic_bins = 1
+    elif isinstance(critic, DreamerV3Critic):
+        critic_bins = int(critic.num_bins)
+        if critic_bins < 3 or critic_bins % 2 != 1:
+            raise ValueError(f"DreamerV3Critic num_bins must be odd and > 1 (dists.py:131), "
+                             f"got {critic_bins}")
+    else:
         raise NotImplementedError(
-            "fused path supports DenseLayerCritic (models.py:142-154); pass "
-            "dreamer_v3_critic=False in TrainConfig")
+            "fused path supports DenseLayerCritic (models.py:142-154) and DreamerV3Critic "
+            f"(157-174); got {type(critic).__name__}")
     buckets = _actions_buckets(actor_critic.actor, None)
-    return MlpArch(obs_dim=int(obs_dim), hidden=net.num_channels, num_layers=net.num_layers,
-                   buckets=buckets, dtype=compute_dtype, lstm_hidden=lstm_hidden)
+    arch = MlpArch(obs_dim=int(obs_dim), hidden=net.num_channels, num_layers=net.num_layers,
+                   buckets=buckets, dtype=compute_dtype, lstm_hidden=lstm_hidden,
+                   critic_bins=critic_bins)
+    arch.head_cols  # raises when the head does not fit
+    return arch
 
 
 class PolicyState:
@@ -123,7 +139,7 @@ class PolicyState:
         self.obs_preprocess = obs_preprocess or ObservationsPreprocessNoop.create()
         self.device = torch.device(device)
         self.layout = param_layout(arch)
-        H, D, L, A1 = arch.hidden, arch.obs_dim, arch.num_layers, arch.num_logits + 1
+        H, D, L, A1 = arch.hidden, arch.obs_dim, arch.num_layers, arch.num_logits + arch.critic_bins
         dt = arch.dtype
 
         host = np.zeros(self.layout["total"], dtype=np.float32)
@@ -140,7 +156,7 @@ class PolicyState:
             host[o:o + H] = 1.0
         o, _ = self.layout["hw"]
         wa = actor_critic.actor.weight_init(rng, (H, arch.num_logits))
-        wv = actor_critic.critic.weight_init(rng, (H, 1))
+        wv = actor_critic.critic.weight_init(rng, (H, arch.critic_bins))
         host[o:o + H * A1] = np.concatenate([wa, wv], axis=1).reshape(-1)
         if arch.lstm_hidden:
             # OptimizedLSTMCell (rnn.py:30-36): orthogonal per gate kernel, zero bias;
@@ -161,15 +177,17 @@ class PolicyState:
             fin = D if l == 0 else H
             self.w_t.append(torch.zeros(H * fin, dtype=dt, device=self.device))
             self.w.append(torch.zeros(fin * H if l > 0 else 0, dtype=dt, device=self.device))
-        self.head_t = torch.zeros(nat.HEAD_COLS * H, dtype=dt, device=self.device)
-        self.head = torch.zeros(H * nat.HEAD_COLS, dtype=dt, device=self.device)
-        self.head_b = torch.zeros((nat.HEAD_COLS,), dtype=torch.float32, device=self.device)
+        HC = arch.head_cols
+        self.head_t = torch.zeros(HC * H, dtype=dt, device=self.device)
+        self.head = torch.zeros(H * HC, dtype=dt, device=self.device)
+        self.head_b = torch.zeros((HC,), dtype=torch.float32, device=self.device)
 
         d = nat.MlpPolicy()
         d.dtype = nat.dtype_code(dt)
         d.obs_dim = D
         d.hidden = H
         d.num_layers = L
+        d.critic_bins = arch.critic_bins
         d.actions = nat.action_layout(arch.buckets)
         for l in range(L):
             d.w_t[l] = self.w_t[l].data_ptr()
@@ -187,7 +205,7 @@ class PolicyState:
             self.lstm_wi_nat = torch.zeros(4 * R * H, dtype=dt, device=self.device)
             self.lstm_wh_nat = torch.zeros(4 * R * R, dtype=dt, device=self.device)
             self.lstm_w_bwd = torch.zeros((H + R) * 4 * R, dtype=dt, device=self.device)
-            self.head_t_nat = torch.zeros(nat.HEAD_COLS * R, dtype=dt, device=self.device)
+            self.head_t_nat = torch.zeros(HC * R, dtype=dt, device=self.device)
             ld = nat.Lstm()
             ld.hidden = R
             ld.num_layers = 1

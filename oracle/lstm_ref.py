@@ -41,8 +41,8 @@ from .ppo_ref import rnd
 GATES = ("i", "f", "g", "o")
 
 
-def param_layout(obs_dim, hidden, num_layers, num_logits):
-    lay = ref.param_layout(obs_dim, hidden, num_layers, num_logits)
+def param_layout(obs_dim, hidden, num_layers, num_logits, critic_bins=1):
+    lay = ref.param_layout(obs_dim, hidden, num_layers, num_logits, critic_bins)
     H = hidden
     off = (lay["total"] + 63) // 64 * 64
     lay["lstm_off"] = off
@@ -223,8 +223,9 @@ def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale
         m = done[t][:, None]
         hin = np.where(m, 0.0, h2)
         cin = np.where(m, 0.0, c2)
-    logits, V = ref.heads(P, Hout, mode, ad)
-    loss, dhead, metrics = ref.ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats,
+    logits, crit = ref.head_outputs(P, Hout, mode, ad)
+    V = ref.value_estimate(crit)
+    loss, dhead, metrics = ref.ppo_loss_dhead(logits, crit, batch, hp, buckets, adv_stats,
                                               loss_scale, ad)
     dhead = rnd(dhead, mode, ad)
     G = {"W": [None] * len(P["W"]), "s": [None] * len(P["W"]), "b": [None] * len(P["W"])}

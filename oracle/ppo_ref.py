@@ -114,9 +114,10 @@ def zscore(x):
 # ---------------------------------------------------------------------------
 # parameters
 # ---------------------------------------------------------------------------
-def param_layout(obs_dim, hidden, num_layers, num_logits):
-    """Flat layout shared with the HIP library (mlearn_param_count)."""
-    H, A1 = hidden, num_logits + 1
+def param_layout(obs_dim, hidden, num_layers, num_logits, critic_bins=1):
+    """Flat layout shared with the HIP library (mlearn_param_count).
+    critic_bins = 1: DenseLayerCritic; odd > 1: DreamerV3Critic bins."""
+    H, A1 = hidden, num_logits + critic_bins
     off, lay = 0, {"W": [], "s": [], "b": []}
     for l in range(num_layers):
         fin = obs_dim if l == 0 else H
@@ -131,6 +132,7 @@ def param_layout(obs_dim, hidden, num_layers, num_logits):
     lay["bh"] = (off, (A1,))
     off += A1
     lay["total"] = off
+    lay["critic_bins"] = critic_bins
     return lay
 
 
@@ -143,6 +145,7 @@ def unflatten(flat, lay, ad=np.float64):
     for k in ("Wh", "bh"):
         o, shp = lay[k]
         P[k] = flat[o:o + int(np.prod(shp))].reshape(shp).copy()
+    P["CB"] = lay.get("critic_bins", 1)
     return P
 
 
@@ -182,23 +185,112 @@ def trunk(P, x, mode, ad=np.float64):
     return h, cache
 
 
-def heads(P, h, mode, ad=np.float64):
-    """DenseLayerDiscreteActor + DenseLayerCritic (models.py:122-154) on the
-    backbone features: Dense with bias, outputs upcast to f32.  Returns
-    (logits [M,A], value [M])."""
+def head_outputs(P, h, mode, ad=np.float64):
+    """DenseLayerDiscreteActor (models.py:122-139) + DenseLayerCritic
+    (142-154) or DreamerV3Critic (157-174) on the backbone features: Dense
+    with bias, outputs upcast to f32.  Returns (logits [M,A], critic) with
+    critic = value [M] (scalar critic) or the bin logits [M, CB]."""
     Wh = rnd(P["Wh"], mode, ad)
     out = rnd(rnd(h @ Wh, mode, ad) + rnd(P["bh"], mode, ad), mode, ad)  # Dense + bias
-    A = Wh.shape[1] - 1
-    return out[:, :A], out[:, A]
+    CB = P.get("CB", 1)
+    A = Wh.shape[1] - CB
+    return out[:, :A], (out[:, A] if CB == 1 else out[:, A:A + CB])
+
+
+def value_estimate(crit):
+    """_compute_value_estimate (rollouts.py:601-605): the scalar critic, or
+    SymExpTwoHotDistribution.mean() of the bin logits."""
+    crit = np.asarray(crit)
+    return crit if crit.ndim == 1 else twohot_mean(crit)
+
+
+def heads(P, h, mode, ad=np.float64):
+    """head_outputs with the critic reduced to its value estimate:
+    (logits [M,A], value [M])."""
+    logits, crit = head_outputs(P, h, mode, ad)
+    return logits, value_estimate(crit)
 
 
 def forward(P, x, mode, ad=np.float64):
     """MLP trunk + actor logits + critic.
 
-    Returns (logits [M,A] f32-valued, value [M], cache)."""
+    Returns (logits [M,A] f32-valued, value estimate [M], cache); the raw
+    critic output is cache['crit']."""
     h, cache = trunk(P, x, mode, ad)
-    logits, V = heads(P, h, mode, ad)
-    return logits, V, cache
+    logits, crit = head_outputs(P, h, mode, ad)
+    cache["crit"] = crit
+    return logits, value_estimate(crit), cache
+
+
+# ---------------------------------------------------------------------------
+# SymExpTwoHotDistribution (dists.py:119-208; the DreamerV3 critic)
+# ---------------------------------------------------------------------------
+def twohot_bins(nb):
+    """_compute_bins (dists.py:128-141) in f32: half = symexp(linspace(-14, 0,
+    nb//2 + 1)) with jnp.linspace's interpolation form start * (1 - i/div) +
+    stop * i/div and the endpoint set to stop (third-party jax, restated);
+    symexp = sign(x) expm1(|x|) (utils.py:39-40); bins = [half,
+    -half[:-1][::-1]]."""
+    assert nb % 2 == 1 and nb > 1
+    nh = nb // 2
+    i = np.arange(nh + 1, dtype=np.float32)
+    step = (i / np.float32(nh)).astype(np.float32)
+    x = (np.float32(-14.0) * (np.float32(1.0) - step)).astype(np.float32)
+    x[-1] = 0.0
+    half = (np.sign(x) * np.expm1(np.abs(x).astype(np.float64))).astype(np.float32)
+    return np.concatenate([half, -half[:-1][::-1]]).astype(np.float32)
+
+
+def _softmax(x):
+    e = np.exp(x - x.max(-1, keepdims=True))
+    return e / e.sum(-1, keepdims=True)
+
+
+def twohot_mean(logits):
+    """SymExpTwoHotDistribution.mean (dists.py:143-169): symmetric sum of the
+    mirrored halves so that it is exactly 0 at initialisation."""
+    logits = np.asarray(logits)
+    nb = logits.shape[-1]
+    bins = twohot_bins(nb).astype(logits.dtype)
+    probs = _softmax(logits)
+    mid = (nb - 1) // 2
+    p1, p2, p3 = probs[..., :mid], probs[..., mid:mid + 1], probs[..., mid + 1:]
+    b1, b2, b3 = bins[:mid], bins[mid:mid + 1], bins[mid + 1:]
+    return (p2 * b2).sum(-1) + ((p1 * b1)[..., ::-1] + (p3 * b3)).sum(-1)
+
+
+def twohot_weights(nb, targets, dtype=np.float64):
+    """Two-hot target weights of two_hot_cross_entropy_loss (dists.py:171-203)
+    as the reference writes them: lower index = #(bins <= t) - 1, upper =
+    nb - #(bins > t), both clipped; lower weight = |b_lo - t| / (|b_lo - t| +
+    |b_up - t|) and upper = |b_up - t| / (...) (1/2 each when the clipped
+    indices coincide).  Returns [M, nb]."""
+    bins = twohot_bins(nb).astype(dtype)
+    t = np.asarray(targets, dtype)[:, None]
+    lo = np.clip((bins[None, :] <= t).sum(-1) - 1, 0, nb - 1)
+    up = np.clip(nb - (bins[None, :] > t).sum(-1), 0, nb - 1)
+    same = lo == up
+    tt = t[:, 0]
+    dl = np.where(same, 1.0, np.abs(bins[lo] - tt))
+    du = np.where(same, 1.0, np.abs(bins[up] - tt))
+    tot = dl + du
+    W = np.zeros((t.shape[0], nb), dtype)
+    rows = np.arange(t.shape[0])
+    np.add.at(W, (rows, lo), dl / tot)
+    np.add.at(W, (rows, up), du / tot)
+    return W
+
+
+def twohot_ce(logits, targets):
+    """two_hot_cross_entropy_loss (dists.py:171-208): -sum(two_hot * log_softmax).
+    Returns (loss [M], d loss / d logits [M, nb])."""
+    logits = np.asarray(logits)
+    W = twohot_weights(logits.shape[-1], targets, logits.dtype)
+    m = logits.max(-1, keepdims=True)
+    lse = m + np.log(np.exp(logits - m).sum(-1, keepdims=True))
+    loss = -(W * (logits - lse)).sum(-1)
+    grad = W.sum(-1, keepdims=True) * _softmax(logits) - W
+    return loss, grad
 
 
 def log_softmax_groups(logits, buckets):
@@ -296,6 +388,18 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         ents.append(ent)
     obj = np.stack(objs, -1)
     ent = np.stack(ents, -1)
+    if np.asarray(V).ndim == 2:
+        # DreamerV3Critic (ppo.py:169-177): two-hot cross entropy of the
+        # returns, value errors from mean(); no clip / huber (ppo.py:54-57)
+        crit = np.asarray(V, ad)
+        vl, dcrit = twohot_ce(crit, R)
+        dV = hp["value_loss_coef"] * inv_s * dcrit * loss_scale
+        loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
+        metrics = {
+            "Loss": loss, "Action Obj": obj, "Value Loss": vl,
+            "Value Errors": np.abs(twohot_mean(crit) - R), "Entropy": ent,
+        }
+        return loss, np.concatenate([dlog, dV], -1), metrics
     vpred, dvp = V, np.ones_like(V)
     if hp.get("clip_value_loss", False):
         ov = np.asarray(batch["values"], ad)
@@ -347,7 +451,8 @@ def ppo_loss_grads(P, batch, hp, buckets, mode="f64", adv_stats=None, loss_scale
     hand-written backprop.  batch: obs [M,D], actions [M,K], log_probs [M,K],
     advantages [M], returns [M], values [M] (all rows of one minibatch)."""
     logits, V, cache = forward(P, batch["obs"], mode, ad)
-    loss, dhead, metrics = ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats, loss_scale,
+    loss, dhead, metrics = ppo_loss_dhead(logits, cache["crit"], batch, hp, buckets, adv_stats,
+                                          loss_scale,
                                           ad)
     # ---- backward ----
     dhead = rnd(dhead, mode, ad)                     # cotangent in the compute dtype

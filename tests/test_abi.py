@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from madrona_learn import _native as nat
-    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 4
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 5
     hdr = open(HEADER).read()
     assert f"#define MLEARN_ABI_VERSION {nat.ABI_VERSION}" in hdr
 
@@ -61,6 +61,7 @@ def test_bad_arguments_are_rejected_without_gpu():
     # bad policy descriptors
     d = nat.MlpPolicy()
     d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_F32, 64, 96, 2
+    d.critic_bins = 1
     assert L.mlearn_param_count(ctypes.byref(d)) == -1
     assert "hidden" in L.mlearn_last_error().decode()
     d.hidden, d.obs_dim = 256, 20
@@ -73,6 +74,7 @@ def test_param_count_matches_oracle_layout():
     from oracle import ppo_ref as ref
     d = nat.MlpPolicy()
     d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_F32, 64, 256, 2
+    d.critic_bins = 1
     d.actions = nat.action_layout([4, 8, 5, 5, 2, 2])
     for l in range(2):
         d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
@@ -97,6 +99,7 @@ def test_lstm_layout_matches_oracle_and_arch():
     for H, L in ((256, 2), (64, 1), (128, 3)):
         d = nat.MlpPolicy()
         d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_BF16, 64, H, L
+        d.critic_bins = 1
         d.actions = nat.action_layout(buckets)
         for l in range(L):
             d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
@@ -129,3 +132,38 @@ def test_lstm_layout_matches_oracle_and_arch():
         critic=DenseLayerCritic("bf16"))
     with pytest.raises(NotImplementedError):
         compile_arch(bad, 64, torch.bfloat16)
+
+
+def test_two_hot_critic_layout_and_head_width():
+    """DreamerV3Critic (models.py:157-174): the head carries A + 63 outputs,
+    padded to 96 columns; the layout agrees with the oracle; bad bin counts
+    are rejected by the library and by compile_arch."""
+    import madrona_learn as ml
+    from madrona_learn import _native as nat
+    from madrona_learn.models import MLP, DenseLayerDiscreteActor, DreamerV3Critic
+    from madrona_learn.train_state import compile_arch, param_layout
+    from oracle import ppo_ref as ref
+    import torch
+    buckets = [4, 8, 5, 5, 2, 2]
+    d = nat.MlpPolicy()
+    d.dtype, d.obs_dim, d.hidden, d.num_layers = nat.DTYPE_BF16, 64, 256, 2
+    d.actions = nat.action_layout(buckets)
+    for l in range(2):
+        d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
+        d.w[l] = 1
+    d.head_t = d.head = d.head_bias = 1
+    L = nat.lib()
+    for cb, hc in ((1, 32), (5, 32), (63, 96)):
+        d.critic_bins = cb
+        assert L.mlearn_head_cols(ctypes.byref(d)) == hc == nat.head_cols(26, cb)
+        assert L.mlearn_param_count(ctypes.byref(d)) == ref.param_layout(64, 256, 2, 26, cb)["total"]
+    for bad in (0, 2, 64, 71):
+        d.critic_bins = bad
+        assert L.mlearn_param_count(ctypes.byref(d)) == -1
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(256, 2, "bf16"))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(buckets), "bf16"),
+        critic=DreamerV3Critic("bf16"))
+    arch = compile_arch(ac, 64, torch.bfloat16)
+    assert arch.critic_bins == 63 and arch.head_cols == 96
+    assert param_layout(arch)["total"] == ref.param_layout(64, 256, 2, 26, 63)["total"]

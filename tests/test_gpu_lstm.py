@@ -25,20 +25,21 @@ pytestmark = pytest.mark.gpu
 BUCKETS = [4, 8, 5, 5, 2, 2]
 
 
-def make_actor_critic(hidden, layers, dtype):
+def make_actor_critic(hidden, layers, dtype, critic_bins=1):
     import madrona_learn as ml
-    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.models import MLP, DenseLayerDiscreteActor
     from madrona_learn.rnn import LSTM
+    from tests.test_gpu_policy import make_critic
     return ml.ActorCritic(
         backbone=ml.BackboneShared(encoder=ml.RecurrentBackboneEncoder(
             net=MLP(hidden, layers, dtype), rnn=LSTM(hidden, 1, dtype))),
         actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
-        critic=DenseLayerCritic(dtype))
+        critic=make_critic(critic_bins, dtype))
 
 
-def make_policy_state(gpu, obs_dim, hidden, layers, dtype, seed=0):
+def make_policy_state(gpu, obs_dim, hidden, layers, dtype, seed=0, critic_bins=1):
     from madrona_learn.train_state import PolicyState, compile_arch
-    ac = make_actor_critic(hidden, layers, dtype)
+    ac = make_actor_critic(hidden, layers, dtype, critic_bins)
     arch = compile_arch(ac, obs_dim, dtype)
     assert arch.lstm_hidden == hidden
     return PolicyState(ac, arch, None, gpu, np.random.default_rng(seed))
@@ -46,7 +47,7 @@ def make_policy_state(gpu, obs_dim, hidden, layers, dtype, seed=0):
 
 def oracle_layout(ps):
     a = ps.arch
-    lay = lref.param_layout(a.obs_dim, a.hidden, a.num_layers, a.num_logits)
+    lay = lref.param_layout(a.obs_dim, a.hidden, a.num_layers, a.num_logits, a.critic_bins)
     assert lay["total"] == ps.layout["total"] and lay["lstm_off"] == ps.layout["lstm_off"]
     return lay
 
@@ -62,6 +63,11 @@ def perturb(ps, seed, scale=0.05):
         o, shp = ps.layout[key]
         n = int(np.prod(shp))
         p[o:o + n] += rng.standard_normal(n).astype(np.float32) * sc
+    if ps.arch.critic_bins > 1:  # zero-initialised two-hot critic: make it non-trivial
+        o, shp = ps.layout["hw"]
+        hw = p[o:o + shp[0] * shp[1]].reshape(shp)
+        hw[:, ps.arch.num_logits:] += rng.standard_normal(
+            hw[:, ps.arch.num_logits:].shape).astype(np.float32) * 0.3
     ps.params.copy_(torch.from_numpy(p))
     ps.sync_weights()
 
@@ -98,9 +104,10 @@ CASES = [("f32", torch.float32, 64, 256, 2), ("bf16", torch.bfloat16, 64, 256, 2
          ("f32", torch.float32, 32, 64, 2), ("bf16", torch.bfloat16, 48, 128, 1)]
 
 
-@pytest.mark.parametrize("mode,dtype,D,H,L", CASES)
-def test_lstm_rollout_step(gpu, mode, dtype, D, H, L):
-    ps = make_policy_state(gpu, D, H, L, dtype, seed=D + H)
+@pytest.mark.parametrize("mode,dtype,D,H,L,CB", [c + (1,) for c in CASES] + [
+    ("f32", torch.float32, 64, 256, 2, 63), ("bf16", torch.bfloat16, 32, 64, 2, 63)])
+def test_lstm_rollout_step(gpu, mode, dtype, D, H, L, CB):
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=D + H, critic_bins=CB)
     perturb(ps, 1)
     N = 1000
     rng = np.random.default_rng(3)
@@ -132,7 +139,8 @@ def test_lstm_rollout_step(gpu, mode, dtype, D, H, L):
     assert np.array_equal(store.float().cpu().numpy(), ref.rnd(obs, mode).astype(np.float32))
     assert np.array_equal(keep["sdn"].cpu().numpy(), done.astype(np.uint8))
     tol = 1e-4 if mode == "f32" else 3e-2
-    np.testing.assert_allclose(vals.cpu().numpy(), V, rtol=tol, atol=tol)
+    vtol = tol * (1.0 if CB == 1 else max(1.0, float(np.abs(V).max())))
+    np.testing.assert_allclose(vals.cpu().numpy(), V, rtol=tol, atol=vtol)
     np.testing.assert_allclose(hd.float().cpu().numpy(), h2, rtol=tol, atol=tol)
     np.testing.assert_allclose(cd.float().cpu().numpy(), c2, rtol=tol, atol=tol)
     gum = onat.gumbel_table(5, 6, 107, 3, N, 26)
@@ -202,16 +210,19 @@ def _hp(nat):
     return hp
 
 
-@pytest.mark.parametrize("mode,dtype,D,H,L", CASES)
+@pytest.mark.parametrize("mode,dtype,D,H,L,CB", [c + (1,) for c in CASES] + [
+    ("f32", torch.float32, 64, 256, 2, 63), ("bf16", torch.bfloat16, 32, 64, 2, 63)])
 @pytest.mark.parametrize("bptt", [32, 16])
-def test_lstm_minibatch_grad(gpu, mode, dtype, D, H, L, bptt):
+def test_lstm_minibatch_grad(gpu, mode, dtype, D, H, L, CB, bptt):
     from madrona_learn import _native as nat
-    ps = make_policy_state(gpu, D, H, L, dtype, seed=H + 1)
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=H + 1, critic_bins=CB)
     perturb(ps, 9, scale=0.2)
     T, N, mb = 32, 96, 64
     C = T // bptt
     rng = np.random.default_rng(12)
     st = _random_store(rng, T, N, D, H, C, ps, mode)
+    if CB > 1:
+        st["returns"] = (st["returns"] * 20.0).astype(np.float32)
     s = _device_store(gpu, st, dtype, C)
     seqs = rng.permutation(C * N)[:mb].astype(np.int32)
     batch = lref.gather_minibatch(st, seqs, bptt)
@@ -303,7 +314,7 @@ def test_lstm_optimizer_step_and_images(gpu):
     assert torch.equal(from_image(ps.head_t_nat, 32, H, False)[:hw.shape[1]], hw.t())
 
 
-def make_cfg(dtype, N=64, T=32, chunks=1, mb=32, epochs=2, seed=5):
+def make_cfg(dtype, N=64, T=32, chunks=1, mb=32, epochs=2, seed=5, critic_bins=1):
     import madrona_learn as ml
     return ml.TrainConfig(
         num_worlds=N, num_agents_per_world=1, num_updates=1,
@@ -312,25 +323,26 @@ def make_cfg(dtype, N=64, T=32, chunks=1, mb=32, epochs=2, seed=5):
                                    value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                    max_grad_norm=0.5),
         num_bptt_chunks=chunks, gamma=0.99, gae_lambda=0.95, seed=seed, metrics_buffer_size=4,
-        dreamer_v3_critic=False, compute_dtype=dtype)
+        dreamer_v3_critic=critic_bins > 1, compute_dtype=dtype)
 
 
-def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=32, use_graph=False):
+def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=32, use_graph=False, critic_bins=1):
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     env = DummyVecEnv(N, D, 6, seed=2, device=gpu)
-    cfg = make_cfg(dtype, N=N, chunks=chunks, mb=mb)
-    pol = ml.Policy(actor_critic=make_actor_critic(H, 2, dtype),
+    cfg = make_cfg(dtype, N=N, chunks=chunks, mb=mb, critic_bins=critic_bins)
+    pol = ml.Policy(actor_critic=make_actor_critic(H, 2, dtype, critic_bins),
                     obs_preprocess=ml.ObservationsCaster.create(dtype))
     mgr = ml.init_training(gpu, cfg, env.sim_fns(), pol, use_graph=use_graph)
     return cfg, env, mgr
 
 
-@pytest.mark.parametrize("mode,dtype,chunks", [("f32", torch.float32, 1),
-                                               ("f32", torch.float32, 2),
-                                               ("bf16", torch.bfloat16, 2)])
-def test_lstm_full_update_matches_oracle(gpu, mode, dtype, chunks):
-    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks)
+@pytest.mark.parametrize("mode,dtype,chunks,CB", [("f32", torch.float32, 1, 1),
+                                                  ("f32", torch.float32, 2, 1),
+                                                  ("bf16", torch.bfloat16, 2, 1),
+                                                  ("f32", torch.float32, 2, 63)])
+def test_lstm_full_update_matches_oracle(gpu, mode, dtype, chunks, CB):
+    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks, critic_bins=CB)
     ps, ts = mgr.state.policy_states, mgr.state.train_states
     lay = oracle_layout(ps)
     p0 = ps.params.cpu().numpy().astype(np.float64)

@@ -21,20 +21,27 @@ pytestmark = pytest.mark.gpu
 BUCKETS = [4, 8, 5, 5, 2, 2]
 
 
-def make_policy_state(gpu, obs_dim, hidden, layers, dtype, seed=0):
+def make_critic(critic_bins, dtype):
+    from madrona_learn.models import DenseLayerCritic, DreamerV3Critic
+    return DenseLayerCritic(dtype) if critic_bins == 1 else DreamerV3Critic(dtype,
+                                                                            num_bins=critic_bins)
+
+
+def make_policy_state(gpu, obs_dim, hidden, layers, dtype, seed=0, critic_bins=1):
     import madrona_learn as ml
-    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.models import MLP, DenseLayerDiscreteActor
     from madrona_learn.train_state import PolicyState, compile_arch
     ac = ml.ActorCritic(
         backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(hidden, layers, dtype))),
         actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
-        critic=DenseLayerCritic(dtype))
+        critic=make_critic(critic_bins, dtype))
     arch = compile_arch(ac, obs_dim, dtype)
     return PolicyState(ac, arch, None, gpu, np.random.default_rng(seed))
 
 
-def perturb(ps, seed, scale=0.05):
-    """Non-trivial LayerNorm / bias parameters (init is scale 1, bias 0)."""
+def perturb(ps, seed, scale=0.05, critic_scale=0.3):
+    """Non-trivial LayerNorm / bias parameters (init is scale 1, bias 0) and,
+    for a two-hot critic, non-trivial (zero-initialised) bin weights."""
     rng = np.random.default_rng(seed)
     p = ps.params.cpu().numpy()
     for key in ("s", "b"):
@@ -42,6 +49,10 @@ def perturb(ps, seed, scale=0.05):
             p[o:o + shp[0]] += rng.standard_normal(shp[0]).astype(np.float32) * 0.3
     o, shp = ps.layout["hw"]
     p[o:o + shp[0] * shp[1]] += rng.standard_normal(shp[0] * shp[1]).astype(np.float32) * scale
+    if ps.arch.critic_bins > 1:
+        hw = p[o:o + shp[0] * shp[1]].reshape(shp)
+        A = ps.arch.num_logits
+        hw[:, A:] += rng.standard_normal(hw[:, A:].shape).astype(np.float32) * critic_scale
     o, shp = ps.layout["hb"]
     p[o:o + shp[0]] += rng.standard_normal(shp[0]).astype(np.float32) * 0.1
     ps.params.copy_(torch.from_numpy(p))
@@ -50,17 +61,21 @@ def perturb(ps, seed, scale=0.05):
 
 def oracle_layout(ps):
     a = ps.arch
-    return ref.param_layout(a.obs_dim, a.hidden, a.num_layers, a.num_logits)
+    return ref.param_layout(a.obs_dim, a.hidden, a.num_layers, a.num_logits, a.critic_bins)
 
 
 CASES = [("f32", torch.float32, 64, 256, 2), ("bf16", torch.bfloat16, 64, 256, 2),
          ("f32", torch.float32, 32, 64, 2), ("bf16", torch.bfloat16, 48, 128, 3),
          ("f32", torch.float32, 16, 128, 1)]
+# DreamerV3Critic (two-hot, 63 bins: head width 96) on a subset of the shapes
+CRITIC_CASES = [c + (1,) for c in CASES] + [
+    ("f32", torch.float32, 64, 256, 2, 63), ("bf16", torch.bfloat16, 64, 256, 2, 63),
+    ("f32", torch.float32, 32, 64, 2, 63), ("f32", torch.float32, 16, 128, 1, 5)]
 
 
-@pytest.mark.parametrize("mode,dtype,D,H,L", CASES)
-def test_rollout_step(gpu, mode, dtype, D, H, L):
-    ps = make_policy_state(gpu, D, H, L, dtype, seed=D + H)
+@pytest.mark.parametrize("mode,dtype,D,H,L,CB", CRITIC_CASES)
+def test_rollout_step(gpu, mode, dtype, D, H, L, CB):
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=D + H, critic_bins=CB)
     perturb(ps, 1)
     N = 1000
     rng = np.random.default_rng(2)
@@ -77,7 +92,10 @@ def test_rollout_step(gpu, mode, dtype, D, H, L):
     logits, V, _ = ref.forward(P, obs, mode)
     assert np.array_equal(store.float().cpu().numpy(), ref.rnd(obs, mode).astype(np.float32))
     tol = 1e-4 if mode == "f32" else 2e-2
-    np.testing.assert_allclose(vals.cpu().numpy(), V, rtol=tol, atol=tol)
+    vtol = tol * (1.0 if CB == 1 else max(1.0, float(np.abs(V).max())))
+    np.testing.assert_allclose(vals.cpu().numpy(), V, rtol=tol, atol=vtol)
+    if CB > 1:
+        assert np.abs(V).max() > 1e-2, "two-hot values should be non-trivial"
     gum = onat.gumbel_table(5, 6, 107, 3, N, 26)
     noisy = logits.astype(np.float32) + gum
     exp_acts, _ = ref.sample_actions(logits.astype(np.float32), BUCKETS, gum)
@@ -131,15 +149,17 @@ HP = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
       "normalize_advantages": True}
 
 
-@pytest.mark.parametrize("mode,dtype,D,H,L", CASES)
+@pytest.mark.parametrize("mode,dtype,D,H,L,CB", CRITIC_CASES)
 @pytest.mark.parametrize("bptt", [32, 16])
-def test_minibatch_grad(gpu, mode, dtype, D, H, L, bptt):
+def test_minibatch_grad(gpu, mode, dtype, D, H, L, CB, bptt):
     from madrona_learn import _native as nat
-    ps = make_policy_state(gpu, D, H, L, dtype, seed=H)
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=H, critic_bins=CB)
     perturb(ps, 9, scale=0.2)
     T, N, mb = 32, 96, 40
     rng = np.random.default_rng(11)
     st = _random_store(rng, T, N, D, ps, mode)
+    if CB > 1:  # returns spread over many bins
+        st["returns"] = (st["returns"] * 20.0).astype(np.float32)
     s = _device_store(gpu, st, dtype)
     nseq = (T // bptt) * N
     seqs = rng.permutation(nseq)[:mb].astype(np.int32)

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 BUCKETS = [4, 8, 5, 5, 2, 2]
 
 
-def make_cfg(dtype, N=64, H=64, T=32, chunks=1, mb=16, epochs=2, seed=5):
+def make_cfg(dtype, N=64, H=64, T=32, chunks=1, mb=16, epochs=2, seed=5, critic_bins=1):
     import madrona_learn as ml
     return ml.TrainConfig(
         num_worlds=N, num_agents_per_world=1, num_updates=1,
@@ -24,34 +24,38 @@ def make_cfg(dtype, N=64, H=64, T=32, chunks=1, mb=16, epochs=2, seed=5):
                                    value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                    max_grad_norm=0.5),
         num_bptt_chunks=chunks, gamma=0.99, gae_lambda=0.95, seed=seed, metrics_buffer_size=4,
-        dreamer_v3_critic=False, compute_dtype=dtype)
+        dreamer_v3_critic=critic_bins > 1, compute_dtype=dtype)
 
 
-def make_policy(dtype, H, L=2):
+def make_policy(dtype, H, L=2, critic_bins=1):
     import madrona_learn as ml
-    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor, DreamerV3Critic
+    critic = DenseLayerCritic(dtype) if critic_bins == 1 else DreamerV3Critic(dtype, num_bins=critic_bins)
     return ml.Policy(actor_critic=ml.ActorCritic(
         backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(H, L, dtype))),
         actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
-        critic=DenseLayerCritic(dtype)), obs_preprocess=ml.ObservationsCaster.create(dtype))
+        critic=critic), obs_preprocess=ml.ObservationsCaster.create(dtype))
 
 
-def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=16, use_graph=False):
+def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=16, use_graph=False, critic_bins=1):
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     env = DummyVecEnv(N, D, 6, seed=2, device=gpu)
-    cfg = make_cfg(dtype, N=N, H=H, chunks=chunks, mb=mb)
-    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(dtype, H), use_graph=use_graph)
+    cfg = make_cfg(dtype, N=N, H=H, chunks=chunks, mb=mb, critic_bins=critic_bins)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(dtype, H, critic_bins=critic_bins),
+                           use_graph=use_graph)
     return cfg, env, mgr
 
 
-@pytest.mark.parametrize("mode,dtype,chunks", [("f32", torch.float32, 1),
-                                               ("f32", torch.float32, 2),
-                                               ("bf16", torch.bfloat16, 1)])
-def test_full_update_matches_oracle(gpu, mode, dtype, chunks):
-    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks)
+@pytest.mark.parametrize("mode,dtype,chunks,CB", [("f32", torch.float32, 1, 1),
+                                                  ("f32", torch.float32, 2, 1),
+                                                  ("bf16", torch.bfloat16, 1, 1),
+                                                  ("f32", torch.float32, 1, 63),
+                                                  ("bf16", torch.bfloat16, 2, 63)])
+def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB):
+    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks, critic_bins=CB)
     ps, ts = mgr.state.policy_states, mgr.state.train_states
-    lay = ref.param_layout(64, 64, 2, 26)
+    lay = ref.param_layout(64, 64, 2, 26, CB)
     p0 = ps.params.cpu().numpy().astype(np.float64)
     oenv = onat.Env(env.N, env.D, env.k0, env.k1, 0)
     oenv.reset()
@@ -66,6 +70,8 @@ def test_full_update_matches_oracle(gpu, mode, dtype, chunks):
     assert np.array_equal(s.rewards.cpu().numpy(), ro["rewards"])
     assert np.array_equal(s.dones.cpu().numpy(), ro["dones"])
     tol = 1e-4 if mode == "f32" else 3e-2
+    if CB > 1:  # zero-initialised DreamerV3Critic: every value is exactly 0 (dists.py:151-166)
+        assert not s.values.any() and not s.bootstrap.any()
     np.testing.assert_allclose(s.values.cpu().numpy(), ro["values"], rtol=tol, atol=tol)
     np.testing.assert_allclose(s.bootstrap.cpu().numpy(), ro["bootstrap"], rtol=tol, atol=tol)
     np.testing.assert_allclose(s.log_probs.cpu().numpy(), ro["log_probs"], rtol=tol, atol=tol)

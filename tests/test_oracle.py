@@ -255,3 +255,38 @@ def test_golden_optimizer_step():
     np.testing.assert_allclose(p, g["p1"], rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(m, g["m1"], rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(v, g["v1"], rtol=1e-12, atol=1e-15)
+
+
+# ---------------------------------------------------------------------------
+# SymExpTwoHotDistribution (DreamerV3Critic, dists.py:119-208): closed-form
+# properties of the restatement (parity with executed reference output is
+# unpinned: no JAX here and no reference fixture for this distribution)
+# ---------------------------------------------------------------------------
+def test_twohot_bins_and_mean():
+    b = ref.twohot_bins(63)
+    assert b.dtype == np.float32 and b.shape == (63,)
+    assert b[31] == 0 and np.array_equal(b[32:], -b[:31][::-1])
+    assert np.all(np.diff(b) > 0)
+    np.testing.assert_allclose(b[0], -np.expm1(14.0), rtol=1e-6)
+    # the symmetric sum is exactly 0 at initialisation (zero-init critic)
+    assert ref.twohot_mean(np.zeros((3, 63), np.float32)).tolist() == [0.0, 0.0, 0.0]
+    lg = np.full((1, 63), -1e4)
+    lg[0, 40] = 0.0
+    np.testing.assert_allclose(ref.twohot_mean(lg), b[40], rtol=1e-6)
+
+
+def test_twohot_weights_follow_the_reference():
+    """two_hot_cross_entropy_loss weighs the lower bin by |b_lo - t| / gap
+    (dists.py:193-196, as written)."""
+    b = ref.twohot_bins(63).astype(np.float64)
+    t = 0.25 * b[40] + 0.75 * b[41]
+    W = ref.twohot_weights(63, [t])
+    np.testing.assert_allclose(W[0, 40], 0.75, rtol=1e-9)
+    np.testing.assert_allclose(W[0, 41], 0.25, rtol=1e-9)
+    W = ref.twohot_weights(63, [b[40]])           # on a bin: dist_to_lower = 0
+    assert W[0, 41] == 1.0 and W[0].sum() == 1.0
+    W = ref.twohot_weights(63, [1e9, -1e9])      # clipped indices coincide: 1/2 + 1/2
+    assert W[0, 62] == 1.0 and W[1, 0] == 1.0
+    loss, grad = ref.twohot_ce(np.zeros((2, 63)), np.array([1e9, 0.3]))
+    np.testing.assert_allclose(loss, np.log(63.0), rtol=1e-12)
+    np.testing.assert_allclose(grad.sum(-1), 0.0, atol=1e-15)

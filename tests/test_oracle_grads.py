@@ -21,8 +21,9 @@ def torch_loss(P, batch, hp, buckets, adv_stats):
         y = (z - mean) * (torch.rsqrt(var + ref.LN_EPS) * P["s"][l]) + P["b"][l]
         h = torch.relu(y)
     out = h @ P["Wh"] + P["bh"]
-    A = out.shape[1] - 1
-    logits, V = out[:, :A], out[:, A]
+    CB = P.get("CB", 1) if isinstance(P.get("CB", 1), int) else 1
+    A = out.shape[1] - CB
+    logits, V = out[:, :A], (out[:, A] if CB == 1 else out[:, A:])
     adv = torch.tensor(batch["advantages"], dtype=torch.float64)
     mean, var = adv_stats
     adv = (adv - mean) / np.sqrt(max(var, 1e-5))
@@ -41,16 +42,20 @@ def torch_loss(P, batch, hp, buckets, adv_stats):
         ents.append(ent)
         off += nb
     R = torch.tensor(batch["returns"], dtype=torch.float64)
-    vl = 0.5 * (V - R) ** 2
+    if CB == 1:
+        vl = 0.5 * (V - R) ** 2
+    else:  # two-hot cross entropy with constant target weights (dists.py:171-208)
+        W = torch.tensor(ref.twohot_weights(CB, batch["returns"]))
+        vl = -(W * torch.log_softmax(V, -1)).sum(-1)
     return (-torch.stack(objs, -1).mean() + hp["value_loss_coef"] * vl.mean()
             - hp["entropy_coef"] * torch.stack(ents, -1).mean())
 
 
-@pytest.mark.parametrize("H,L", [(64, 2), (32, 3), (16, 1)])
-def test_backward_matches_autograd(H, L):
+@pytest.mark.parametrize("H,L,CB", [(64, 2, 1), (32, 3, 1), (16, 1, 1), (32, 2, 63), (16, 1, 7)])
+def test_backward_matches_autograd(H, L, CB):
     rng = np.random.default_rng(H + L)
     D, M = 24, 200
-    lay = ref.param_layout(D, H, L, sum(BUCKETS))
+    lay = ref.param_layout(D, H, L, sum(BUCKETS), CB)
     flat = rng.standard_normal(lay["total"]) * 0.3
     P = ref.unflatten(flat, lay)
     for l in range(L):
@@ -58,13 +63,15 @@ def test_backward_matches_autograd(H, L):
     acts = np.stack([rng.integers(0, b, M) for b in BUCKETS], -1)
     batch = {"obs": rng.standard_normal((M, D)), "actions": acts,
              "log_probs": rng.standard_normal((M, 6)) * 0.3 - 1.5,
-             "advantages": rng.standard_normal(M) + 0.2, "returns": rng.standard_normal(M),
+             "advantages": rng.standard_normal(M) + 0.2,
+             "returns": rng.standard_normal(M) * (30.0 if CB > 1 else 1.0),
              "values": rng.standard_normal(M)}
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01}
     stats = (batch["advantages"].mean(), batch["advantages"].var())
     loss, G, _, _ = ref.ppo_loss_grads(P, batch, hp, BUCKETS, "f64", adv_stats=stats)
     TP = {k: ([torch.tensor(x, requires_grad=True) for x in v] if isinstance(v, list)
-              else torch.tensor(v, requires_grad=True)) for k, v in P.items()}
+              else torch.tensor(v, requires_grad=True)) for k, v in P.items() if k != "CB"}
+    TP["CB"] = CB
     tl = torch_loss(TP, batch, hp, BUCKETS, stats)
     tl.backward()
     np.testing.assert_allclose(loss, tl.item(), rtol=1e-12)
