@@ -52,10 +52,11 @@ def envs_per_rank(config, world):
 
 
 def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True, config="b1",
-         chunks=1):
+         chunks=1, critic="scalar"):
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
-    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.models import (MLP, DenseLayerCritic, DenseLayerDiscreteActor,
+                                      DreamerV3Critic)
     from madrona_learn.rnn import LSTM
     env = DummyVecEnv(N, OBS, len(BUCKETS), seed=0, env_offset=env_offset, device=dev)
     pbt = None
@@ -70,7 +71,7 @@ def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True, conf
                           value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                           max_grad_norm=0.5),
         num_bptt_chunks=chunks, gamma=0.99, gae_lambda=0.95, seed=0, metrics_buffer_size=8,
-        dreamer_v3_critic=False, compute_dtype=dtype, pbt=pbt)
+        dreamer_v3_critic=critic == "twohot", compute_dtype=dtype, pbt=pbt)
     if config == "lstm":
         encoder = ml.RecurrentBackboneEncoder(net=MLP(HID, LAYERS, dtype),
                                               rnn=LSTM(HID, 1, dtype))
@@ -80,7 +81,7 @@ def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True, conf
         actor_critic=ml.ActorCritic(
             backbone=ml.BackboneShared(encoder=encoder),
             actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dtype),
-            critic=DenseLayerCritic(dtype)),
+            critic=DenseLayerCritic(dtype) if critic == "scalar" else DreamerV3Critic(dtype)),
         obs_preprocess=ml.ObservationsCaster.create(dtype))
     import contextlib
     import io
@@ -145,7 +146,7 @@ def kernel_rooflines(mgr, dev, iters=20):
 
     t_step = time_call(step, iters, stream)
     M = algo.mb * algo.bptt
-    fwd, bwd, _ = flop_per_sample()
+    fwd, bwd, _ = flop_per_sample(A1=ps.arch.num_logits + ps.arch.critic_bins)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
     roof = {
@@ -257,6 +258,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--config", choices=["b1", "lstm", "pbt"], default="b1")
     ap.add_argument("--bptt-chunks", type=int, default=1)
+    ap.add_argument("--critic", choices=["scalar", "twohot"], default="scalar",
+                    help="DenseLayerCritic (SURVEY B1) or DreamerV3Critic (63-bin two-hot)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -279,7 +282,7 @@ def main():
 
     n_rank = envs_per_rank(args.config, world)
     mgr = make(dev, N=n_rank, env_offset=rank * n_rank, use_graph=not args.no_graph,
-               config=args.config, chunks=args.bptt_chunks)
+               config=args.config, chunks=args.bptt_chunks, critic=args.critic)
     for _ in range(args.warmup):
         mgr.update_iter()
     torch.cuda.synchronize()
@@ -321,6 +324,7 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": n_rank, "total_envs": n_rank * world,
                        "steps_per_update": T, "parallelism": f"dp{world}",
+                       "critic": args.critic,
                        "hip_graph": not args.no_graph},
         }
     if rank == 0 and not args.no_roofline and args.config != "lstm":

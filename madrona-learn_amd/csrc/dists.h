@@ -58,55 +58,76 @@ __device__ inline float twohot_bin(int j, int nb) {
     return j <= nh ? v : -v;
 }
 
-// softmax statistics of the nb logits: max and sum of exp(l - max)
-__device__ inline void twohot_softmax(const float* lg, int nb, float* mx_out, float* se_out) {
-    float mx = lg[0];
-    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
-    float se = 0.f;
-    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
-    *mx_out = mx;
-    *se_out = se;
+// ---------------------------------------------------------------------------
+// SymExpTwoHotDistribution statistics computed by an aligned group of G
+// lanes of one wave (lane `sub` of the group handles bins sub, sub + G, ...);
+// partial results are combined with butterfly shuffles inside the group.
+//   twohot_mean_g: mean() (dists.py:143-169): p_mid b_mid plus the mirrored
+//     pairs p_{mid-1-i} b_{mid-1-i} + p_{mid+1+i} b_{mid+1+i} (the symmetric
+//     sum that makes it exactly 0 at initialisation);
+//   twohot_ce_g: two_hot_cross_entropy_loss (dists.py:171-208); the bin
+//     weights are the reference's as written: lower = |b_lo - t| / (|b_lo - t|
+//     + |b_up - t|), upper = |b_up - t| / (...), 1/2 each when the clipped
+//     indices coincide.
+// ---------------------------------------------------------------------------
+template <int G> __device__ inline float group_max(float v) {
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+template <int G> __device__ inline float group_sum(float v) {
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
-// SymExpTwoHotDistribution.mean (dists.py:143-169): p_mid * b_mid plus the
-// mirrored pairs (p_{mid-1-i} b_{mid-1-i} + p_{mid+1+i} b_{mid+1+i}) summed
-// (symmetric so that it is exactly 0 at initialisation).  bins: LDS table.
-__device__ inline float twohot_mean(const float* lg, int nb, const float* bins, float mx, float se) {
+template <int G>
+__device__ inline float twohot_mean_g(const float* lg, int nb, const float* bins, int sub,
+                                      float* mx_out, float* se_out) {
+    float mx = -3.4e38f;
+    for (int j = sub; j < nb; j += G) mx = fmaxf(mx, lg[j]);
+    mx = group_max<G>(mx);
+    float se = 0.f;
+    for (int j = sub; j < nb; j += G) se += __expf(lg[j] - mx);
+    se = group_sum<G>(se);
     const int mid = (nb - 1) / 2;
     float acc = 0.f;
-    for (int i = 0; i < mid; ++i) {
+    for (int i = sub; i < mid; i += G) {
         const int a = mid - 1 - i, b = mid + 1 + i;
         acc += (__expf(lg[a] - mx) / se) * bins[a] + (__expf(lg[b] - mx) / se) * bins[b];
     }
+    acc = group_sum<G>(acc);
+    *mx_out = mx;
+    *se_out = se;
     return (__expf(lg[mid] - mx) / se) * bins[mid] + acc;
 }
 
-// two_hot_cross_entropy_loss (dists.py:171-208) of one target: returns the
-// loss and writes d loss / d logit_j * scale in place of the logits.  The
-// bin weights are the reference's as written: lower weight = |b_lo - t| /
-// (|b_lo - t| + |b_up - t|), upper = |b_up - t| / (...), both 1/2 when the
-// clipped indices coincide.  mean_out receives mean() (metrics).
-__device__ inline float twohot_ce(float* lg, int nb, float target, const float* bins, float scale,
-                                  float* mean_out) {
-    int lo = -1, up = nb;
-    for (int j = 0; j < nb; ++j) {
-        lo += bins[j] <= target ? 1 : 0;
-        up -= bins[j] > target ? 1 : 0;
+// Every lane returns the loss and mean(); each lane writes the scaled
+// d loss / d logit of its own bins.
+template <int G>
+__device__ inline float twohot_ce_g(float* lg, int nb, float target, const float* bins, float scale,
+                                    int sub, float* mean_out) {
+    float cle = 0.f, cgt = 0.f;
+    for (int j = sub; j < nb; j += G) {
+        cle += bins[j] <= target ? 1.f : 0.f;
+        cgt += bins[j] > target ? 1.f : 0.f;
     }
-    lo = min(max(lo, 0), nb - 1);
-    up = min(max(up, 0), nb - 1);
+    cle = group_sum<G>(cle);
+    cgt = group_sum<G>(cgt);
+    const int lo = min(max((int)cle - 1, 0), nb - 1);
+    const int up = min(max(nb - (int)cgt, 0), nb - 1);
     const bool same = lo == up;
     const float dl = same ? 1.f : fabsf(bins[lo] - target);
     const float du = same ? 1.f : fabsf(bins[up] - target);
     const float tot = dl + du;
     const float wl = dl / tot, wu = du / tot;
     float mx, se;
-    twohot_softmax(lg, nb, &mx, &se);
-    *mean_out = twohot_mean(lg, nb, bins, mx, se);
+    *mean_out = twohot_mean_g<G>(lg, nb, bins, sub, &mx, &se);
     const float lse = mx + __logf(se);
-    const float loss = -(wl * (lg[lo] - lse) + wu * (lg[up] - lse));
+    const float llo = lg[lo], lup = lg[up];  // read before any lane of the group writes
+    const float loss = -(wl * (llo - lse) + wu * (lup - lse));
     const float wsum = wl + wu;
-    for (int j = 0; j < nb; ++j) {
+    for (int j = sub; j < nb; j += G) {
         const float p = __expf(lg[j] - mx) / se;
         const float w = (j == lo ? wl : 0.f) + (j == up ? wu : 0.f);
         lg[j] = (wsum * p - w) * scale;

@@ -139,8 +139,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     constexpr int LGS = HC + 1;                           // LDS row stride of the head outputs
     float* hbias = gb + L * 2 * H;                        // [HC]
     float* red = hbias + HC;                              // [W][32][2]
-    float* lgp = red + W * 64;                            // [W][32][LGS] head partials
-    float* lg = lgp + W * 32 * LGS;                       // [32][LGS]
+    float* lgp = red + W * 64;                            // [head_parts][32][LGS] partials
+    float* lg = lgp + head_parts<HC, W>() * 32 * LGS;     // [32][LGS]
     float* rbias = lg + 32 * LGS;                         // [4H] LSTM bias (RNN)
     float* bins = rbias + (RNN ? 4 * H : 0);              // [HC] two-hot critic bins
     frag* frh = (frag*)(bins + HC);                       // [KSH][64] carry fragments (RNN)
@@ -276,33 +276,56 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         }
     }
 
-    // actor + critic heads over this wave's features, partials summed in wave
-    // order: lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22)
+    // actor + critic heads (dists.py:22, models.py:154): lg[row][j] =
+    // rnd(rnd(a . W) + rnd(b)).  Head width 32: each wave multiplies its own
+    // features (B fragments from registers), partials summed in wave order.
+    // Head width 96: the features of every wave staged in LDS, wave w computes
+    // column block w / KSPLIT over k-slice w % KSPLIT.
     {
-        frag hb[NBW * SPB];
-#pragma unroll
-        for (int i = 0; i < NBW; ++i)
-#pragma unroll
-            for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
         constexpr int HB = HC / 32;
-        f32x16 ha[HB];
-        zero_acc<HB>(ha);
-        gemm_ring<T, HB, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
-            ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane, KSH);
+        constexpr int KSPLIT = head_parts<HC, W>();
+        constexpr int KPS = KSH / KSPLIT;
+        if constexpr (HB == 1) {
+            frag hb[NBW * SPB];
 #pragma unroll
-        for (int nb = 0; nb < HB; ++nb)
+            for (int i = 0; i < NBW; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(nb, q, h)] = ha[nb][q];
+                for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
+            f32x16 ha[1];
+            zero_acc<1>(ha);
+            gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+                ha, hb, NBW * SPB, (const T*)P.head_t + (int64_t)w * NBW * SPB * 64 * E, lane);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(0, q, h)] = ha[0][q];
+        } else {
+            if constexpr (RNN) __syncthreads();  // every wave is done reading fr (Wi product)
+#pragma unroll
+            for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                for (int t = 0; t < SPB; ++t)
+                    fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(aw[i], t);
+            __syncthreads();
+            for (int u = w; u < HB * KSPLIT; u += W) {
+                const int nb = u / KSPLIT, part = u % KSPLIT;
+                f32x16 ha[1];
+                zero_acc<1>(ha);
+                gemm_lds<T, 1, KPS, 8>(ha, fr + part * KPS * 64,
+                                       (const T*)P.head_t + ((int64_t)nb * KSH + part * KPS) * 64 * E,
+                                       lane);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) lgp[(part * 32 + r) * LGS + feat(nb, q, h)] = ha[0][q];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < 32 * HC; i += THREADS) {
+            const int rr = i / HC, j = i - rr * HC;
+            float x = lgp[rr * LGS + j];
+#pragma unroll
+            for (int v = 1; v < KSPLIT; ++v) x += lgp[(v * 32 + rr) * LGS + j];
+            lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int i = tid; i < 32 * HC; i += THREADS) {
-        const int rr = i / HC, j = i - rr * HC;
-        float x = lgp[rr * LGS + j];
-#pragma unroll
-        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * LGS + j];
-        lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
-    }
-    __syncthreads();
 
     // sample + store: one (env, group) task per thread
     if (actions) {
@@ -318,15 +341,19 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             if (logp) logp[n * P.K + g] = lp;
         }
     }
-    if (values && tid < 32 && row0 + tid < N) {
-        const float* cl = lg + tid * LGS + P.A;
-        float v = cl[0];
-        if (P.CB > 1) {  // SymExpTwoHotDistribution.mean() (rollouts.py:601-605)
-            float mx, se;
-            twohot_softmax(cl, P.CB, &mx, &se);
-            v = twohot_mean(cl, P.CB, bins, mx, se);
+    if (values) {
+        if (P.CB == 1) {
+            if (tid < 32 && row0 + tid < N) values[row0 + tid] = lg[tid * LGS + P.A];
+        } else {
+            // SymExpTwoHotDistribution.mean() (rollouts.py:601-605): 8 lanes per env
+            constexpr int G = 8;
+            for (int vt = tid; vt < 32 * G; vt += THREADS) {
+                const int rr = vt / G, sub = vt % G;
+                float mx, se;
+                const float v = twohot_mean_g<G>(lg + rr * LGS + P.A, P.CB, bins, sub, &mx, &se);
+                if (sub == 0 && row0 + rr < N) values[row0 + rr] = v;
+            }
         }
-        values[row0 + tid] = v;
     }
 }
 
@@ -334,7 +361,7 @@ template <typename T, int H, bool RNN, int HC> static size_t policy_step_lds(int
     typedef PolCfg<H> C;
     const size_t frags = (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
     return frags * (RNN ? 2 : 1) +
-           (size_t)(L * 2 * H + HC + C::W * 64 + (C::W + 1) * 32 * (HC + 1) +
+           (size_t)(L * 2 * H + HC + C::W * 64 + (head_parts<HC, C::W>() + 1) * 32 * (HC + 1) +
                     (RNN ? 4 * H : 0) + HC) * 4;
 }
 

@@ -311,12 +311,17 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float
 
 // DreamerV3Critic (ppo.py:169-177): value loss = two-hot cross entropy of the
 // return against the CB bin logits at lg[A..A+CB); value error = mean() - R.
-// Writes d loss / d bin logits in place, zeroes columns A+CB..HC-1.
-__device__ inline void loss_value_twohot(const HpK& hp, float* lg, int A, int CB, int HC,
-                                         const float* bins, float R, LossAcc& m) {
+// Run by an aligned group of G lanes (lane sub); writes d loss / d bin
+// logits in place, zeroes columns A+CB..HC-1; lane 0 of the group records
+// the metrics.
+template <int G>
+__device__ inline void loss_value_twohot_g(const HpK& hp, float* lg, int A, int CB, int HC,
+                                           const float* bins, float R, int sub, LossAcc& m) {
     float mean;
-    const float vl = twohot_ce(lg + A, CB, R, bins, hp.vcoef * hp.inv_s * hp.loss_scale, &mean);
-    for (int j = A + CB; j < HC; ++j) lg[j] = 0.f;
+    const float vl =
+        twohot_ce_g<G>(lg + A, CB, R, bins, hp.vcoef * hp.inv_s * hp.loss_scale, sub, &mean);
+    for (int j = A + CB + sub; j < HC; j += G) lg[j] = 0.f;
+    if (sub != 0) return;
     const float verr = fabsf(mean - R);
     m.svl += vl;
     m.qvl += vl * vl;
@@ -336,8 +341,8 @@ __device__ inline void loss_value_twohot(const HpK& hp, float* lg, int A, int CB
 // post-activation (forward) or dZ (backward) fragments through LDS.  Each
 // wave keeps its own Dense outputs in registers for the backward pass.
 // LDS: B fragments [KSH][64], LayerNorm scale/bias [L][2][H], head bias, row
-// statistics [W][32][2], head partials [W][32][HC+1], logits / d logits
-// [32][HC+1], loss partials [W][kLossSlots], critic bins [HC].
+// statistics [W][32][2], head partials [head_parts][32][HC+1], logits /
+// d logits [32][HC+1], loss partials [W][kLossSlots], critic bins [HC].
 // ---------------------------------------------------------------------------
 #ifndef ML_STEP_MAXW
 #define ML_STEP_MAXW 8  // waves per workgroup of the fused step kernel (feature split)
@@ -351,7 +356,7 @@ template <int H> struct StepCfg {
 template <typename T, int H, int L, int HC> static size_t step_lds() {
     typedef StepCfg<H> C;
     return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
-           (size_t)(L * 2 * H + HC + C::W * 64 + (C::W + 1) * 32 * (HC + 1) +
+           (size_t)(L * 2 * H + HC + C::W * 64 + (head_parts<HC, C::W>() + 1) * 32 * (HC + 1) +
                     C::W * kLossSlots + HC) * 4;
 }
 
@@ -410,8 +415,8 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     float* gb = (float*)(fr + KSH * 64);       // [L][2][H]
     float* hbias = gb + L * 2 * H;             // [32]
     float* red = hbias + HC;                   // [W][32][2]
-    float* lgp = red + W * 64;                 // [W][32][LGS]
-    float* lg = lgp + W * 32 * LGS;            // [32][LGS]
+    float* lgp = red + W * 64;                 // [kHeadParts][32][LGS] head partials
+    float* lg = lgp + head_parts<HC, W>() * 32 * LGS;  // [32][LGS]
     float* lred = lg + 32 * LGS;               // [W][kLossSlots]
     float* bins = lred + W * kLossSlots;       // [HC] two-hot critic bins
     if (kLoss && P.CB > 1)
@@ -516,48 +521,83 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     STAMP(6);
     if constexpr (MODE == kTrunkFwd) return;
     if constexpr (kLoss) {
-    // heads over this wave's features; partials summed in wave order:
-    // lg[row][j] = rnd(rnd(a . W) + rnd(b))  (dists.py:22, models.py:154)
+    // heads (dists.py:22, models.py:154): lg[row][j] = rnd(rnd(a . W) + rnd(b)).
+    // Head width 32: each wave multiplies its own features (B fragments from
+    // its registers), partials summed in wave order.  Head width 96: the
+    // backbone output of every wave is staged in LDS and wave w computes
+    // column block w / KSPLIT over k-slice w % KSPLIT of the full K.
     {
-        frag hb[NBW * SPB];
-        if constexpr (MODE == kHeads) {
-            // this wave's slice of the LSTM output row (natural k order)
-            const T* hrow = (const T*)rec.hout + row * H;
-#pragma unroll
-            for (int j = 0; j < NBW * SPB; ++j) hb[j] = RT<T>::row(hrow, w * NBW * SPB + j, h);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NBW; ++i)
-#pragma unroll
-                for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
-        }
-        const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
         constexpr int HB = HC / 32;
-        f32x16 ha[HB];
-        zero_acc<HB>(ha);
-        gemm_ring<T, HB, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
-            ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane, KSH);
+        constexpr int KSPLIT = head_parts<HC, W>();
+        constexpr int KPS = KSH / KSPLIT;  // k-steps per slice
+        if constexpr (HB == 1) {
+            frag hb[NBW * SPB];
+            if constexpr (MODE == kHeads) {
+                // this wave's slice of the LSTM output row (natural k order)
+                const T* hrow = (const T*)rec.hout + row * H;
 #pragma unroll
-        for (int nb = 0; nb < HB; ++nb)
+                for (int j = 0; j < NBW * SPB; ++j) hb[j] = RT<T>::row(hrow, w * NBW * SPB + j, h);
+            } else {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(nb, q, h)] = ha[nb][q];
+                for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                    for (int t = 0; t < SPB; ++t) hb[i * SPB + t] = Pk<T>::frag(aw[i], t);
+            }
+            const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
+            f32x16 ha[1];
+            zero_acc<1>(ha);
+            gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
+                ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lgp[(w * 32 + r) * LGS + feat(0, q, h)] = ha[0][q];
+        } else {
+            if constexpr (MODE == kHeads) {
+                // LSTM output rows (natural k order), k-steps split over the waves
+                const T* hrow = (const T*)rec.hout + row * H;
+                for (int s = w; s < KSH; s += W) fr[s * 64 + lane] = RT<T>::row(hrow, s, h);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                    for (int t = 0; t < SPB; ++t)
+                        fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(aw[i], t);
+            }
+            __syncthreads();
+            const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
+            for (int u = w; u < HB * KSPLIT; u += W) {
+                const int nb = u / KSPLIT, part = u % KSPLIT;
+                f32x16 ha[1];
+                zero_acc<1>(ha);
+                gemm_lds<T, 1, KPS, 8>(ha, fr + part * KPS * 64,
+                                       himg + ((int64_t)nb * KSH + part * KPS) * 64 * E, lane);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) lgp[(part * 32 + r) * LGS + feat(nb, q, h)] = ha[0][q];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < 32 * HC; i += THREADS) {
+            const int rr = i / HC, j = i - rr * HC;
+            float x = lgp[rr * LGS + j];
+#pragma unroll
+            for (int v = 1; v < KSPLIT; ++v) x += lgp[(v * 32 + rr) * LGS + j];
+            lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int i = tid; i < 32 * HC; i += THREADS) {
-        const int rr = i / HC, j = i - rr * HC;
-        float x = lgp[rr * LGS + j];
-#pragma unroll
-        for (int v = 1; v < W; ++v) x += lgp[(v * 32 + rr) * LGS + j];
-        lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
-    }
-    __syncthreads();
 
     STAMP(7);
     // ---- loss: one (row, group | value) task per thread (ppo.py:129-262) ----
     {
         LossAcc m;
         const float as0 = adv_st[0], as1 = adv_st[1];
-        for (int task = tid; task < 32 * (K + 1); task += THREADS) {
+        // two-hot critic: the value rows run in groups of 8 lanes (below); with
+        // 512 threads they take the last 256 while the first ones do the groups
+        const bool th = P.CB > 1;
+        const bool split = th && THREADS >= 512;
+        const int tstride = split ? THREADS - 256 : THREADS;
+        const int ntask = 32 * (th ? K : K + 1);
+        for (int task = (split && tid >= THREADS - 256) ? ntask : tid; task < ntask;
+             task += tstride) {
             const int rr = task & 31, g = task >> 5;
             float* lr = lg + rr * LGS;
             const int64_t f = row0 + rr;
@@ -584,10 +624,24 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                 if (hp.norm_adv) adv = (adv - as0) * as1;
                 loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], act, olp, adv, hp.ecoef[g],
                            m);
-            } else if (P.CB == 1) {
-                loss_value(hp, lr, P.A, HC, ret, oval, m);
             } else {
-                loss_value_twohot(hp, lr, P.A, P.CB, HC, bins, ret, m);
+                loss_value(hp, lr, P.A, HC, ret, oval, m);
+            }
+        }
+        if (th) {
+            constexpr int G = 8;
+            const int vt0 = split ? tid - (THREADS - 256) : tid;
+            const int vstride = split ? 256 : THREADS;
+            for (int vt = vt0 < 0 ? 32 * G : vt0; vt < 32 * G; vt += vstride) {
+                const int rr = vt / G, sub = vt % G;
+                float* lr = lg + rr * LGS;
+                const int64_t f = row0 + rr;
+                if (f >= M) {  // padding row: zero its d critic logits
+                    for (int j = P.A + sub; j < HC; j += G) lr[j] = 0.f;
+                    continue;
+                }
+                const float R = ro.ret[store_row(ro, mb_seq, mb, f)];
+                loss_value_twohot_g<G>(hp, lr, P.A, P.CB, HC, bins, R, sub, m);
             }
         }
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,

@@ -537,6 +537,13 @@ inline LstmK make_lstm_k(const mlearn_lstm& r) {
 }
 int validate_policy(const mlearn_mlp_policy* p);
 
+// Partial head sums per output block of the fused kernels: with W waves and
+// head width HC, the K of each 32-column block is split over W / (HC/32)
+// waves (W for HC = 32).
+template <int HC, int W> constexpr int head_parts() {
+    return HC == 32 ? W : (W / (HC / 32) > 0 ? W / (HC / 32) : 1);
+}
+
 // Head width of a policy: actor logits + critic outputs, padded to 32 or 96.
 inline int head_cols(const mlearn_mlp_policy& p) {
     return p.actions.num_logits + p.critic_bins <= MLEARN_HEAD_COLS ? MLEARN_HEAD_COLS
