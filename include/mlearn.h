@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 5
+#define MLEARN_ABI_VERSION 6
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -140,10 +140,33 @@ typedef struct mlearn_mlp_policy {
     const void* head_t;      /* HC*hidden: Bt[n=head col][k=unit] */
     const void* head;        /* HC*hidden: Bt[n=unit][k=head col] */
     const float* head_bias;  /* [HC] f32 */
+    /* ObservationsEMANormalizer (observations.py:70-132, EMANormalizer
+     * moving_avg.py:48-196).  obs_mu == NULL: the preprocess is a cast. */
+    const float* obs_mu;         /* [obs_dim] f32: x' = (x - mu) * inv_sigma, then the cast */
+    const float* obs_inv_sigma;  /* [obs_dim] f32 */
+    float* obs_stats;            /* NULL, or [obs_stats_steps][obs_stats_tiles][obs_dim][2]:
+                                    the rollout step `step` writes, per 32-env tile, the
+                                    {mean, M2} of its raw observations (update_obs_stats,
+                                    rollouts.py:670-676) */
+    int64_t obs_stats_tiles;     /* >= ceil(N / 32) */
+    int32_t obs_stats_steps;
+    int32_t obs_pad;
 } mlearn_mlp_policy;
 
 /* Head width HC of a policy descriptor (-1 if invalid). */
 int32_t mlearn_head_cols(const mlearn_mlp_policy* policy);
+
+/* Observation statistics of one rollout -> new normaliser estimates
+ * (rollouts.py:670-678 + train.py:193-204): per step t the tile partials of
+ * obs_stats are merged (Chan) into the batch mean / population variance of
+ * the N observations, folded over t = 0..steps-1 by
+ * EMANormalizer.update_input_stats (moving_avg.py:107-130, n_a = t), then
+ * update_estimates (moving_avg.py:132-180) with decay / eps.
+ * est: [5][obs_dim] f32 = mu, inv_sigma, sigma, mu_biased, sigma_sq_biased
+ * (in/out); count: the int32 update counter N (in/out, device). */
+int mlearn_obs_norm_update(const float* obs_stats, int32_t steps, int64_t tiles, int64_t N,
+                           int32_t obs_dim, float decay, float eps, float* est, int32_t* count,
+                           mlearn_stream_t stream);
 
 /* Post-step bookkeeping of the PREVIOUS env step (rollouts.py:933-973), fused
  * into the next policy launch; same arithmetic as mlearn_rollout_post_step. */

@@ -524,6 +524,104 @@ __global__ void counters_add_kernel(uint64_t* ctr, int n, Deltas d) {
     if (i < n) ctr[i] += d.d[i];
 }
 
+
+// ---------------------------------------------------------------------------
+// ObservationsEMANormalizer statistics (moving_avg.py:48-196): one block per
+// feature.  Per step t the tile partials {mean, M2} are merged (Chan, fixed
+// order: thread j of the step's group takes tiles j, j + 8, ..., then a
+// butterfly over the 8 threads) into the batch mean and population variance;
+// thread 0 folds the steps with update_input_stats (n_a = t) and applies
+// update_estimates.  f32 arithmetic like the reference.
+// ---------------------------------------------------------------------------
+constexpr int kObsGroup = 8;
+
+__device__ inline void chan_merge(float& n, float& m, float& M2, float nb, float mb, float M2b) {
+    if (nb == 0.f) return;
+    const float nn = n + nb;
+    const float d = mb - m;
+    m = m + d * (nb / nn);
+    M2 = M2 + M2b + d * d * (n * nb / nn);
+    n = nn;
+}
+
+__global__ __launch_bounds__(256) void obs_norm_update_kernel(const float* __restrict__ st,
+                                                              int steps, int64_t tiles, int64_t N,
+                                                              int D, float decay, float eps,
+                                                              float* est, int32_t* count) {
+#pragma clang fp contract(off)
+    __shared__ float bm[256 / kObsGroup], bv[256 / kObsGroup];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int g = tid / kObsGroup, j = tid % kObsGroup;
+    constexpr int SPB = 256 / kObsGroup;  // steps per pass
+    float a_mean = 0.f, a_var = 0.f;      // init_input_stats (moving_avg.py:101-105)
+    for (int t0 = 0; t0 < steps; t0 += SPB) {
+        const int t = t0 + g;
+        float n = 0.f, m = 0.f, M2 = 0.f;
+        if (t < steps) {
+            for (int64_t tile = j; tile < tiles && tile * 32 < N; tile += kObsGroup) {
+                const float nb = (float)(N - tile * 32 < 32 ? N - tile * 32 : 32);
+                const float* p = st + (((int64_t)t * tiles + tile) * D + f) * 2;
+                chan_merge(n, m, M2, nb, p[0], p[1]);
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < kObsGroup; o <<= 1) {
+            const float n2 = __shfl_xor(n, o), m2 = __shfl_xor(m, o), M22 = __shfl_xor(M2, o);
+            // fixed operand order: the lower group index is the left operand
+            if ((j & o) == 0) {
+                chan_merge(n, m, M2, n2, m2, M22);
+            } else {
+                float nl = n2, ml = m2, Ml = M22;
+                chan_merge(nl, ml, Ml, n, m, M2);
+                n = nl, m = ml, M2 = Ml;
+            }
+        }
+        if (j == 0) {
+            bm[g] = m;
+            bv[g] = M2 / (float)N;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int u = 0; u < SPB && t0 + u < steps; ++u) {
+                // update_input_stats (moving_avg.py:107-130) with n_a = t
+                const float b_mean = bm[u], b_var = bv[u];
+                const float delta = b_mean - a_mean;
+                const float b_w = 1.0f / (float)(t0 + u + 1);
+                const float a_w = 1.0f - b_w;
+                a_mean = a_mean + delta * b_w;
+                a_var = a_w * a_var + b_w * b_var + (delta * delta) * a_w * b_w;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    // update_estimates (moving_avg.py:132-180)
+    const int32_t Nold = *count;  // bumped by obs_count_kernel after every block has run
+    float* mu = est;
+    float* inv_sigma = est + D;
+    float* sigma = est + 2 * D;
+    float* mu_b = est + 3 * D;
+    float* s2_b = est + 4 * D;
+    const float oma = decay;
+    const float alpha = 1.0f - oma;
+    const int32_t Nnew = Nold + 1;
+    const float mean_delta = a_mean - mu[f];
+    const float nmb = oma * mu_b[f] + alpha * a_mean;
+    const float ns2b = oma * s2_b[f] + alpha * a_var +
+                       ((float)Nold / (float)Nnew) * (oma * alpha) * (mean_delta * mean_delta);
+    const float bc = -1.0f / expm1f((float)Nnew * logf(oma));
+    const float nmu = nmb * bc;
+    const float ns2 = ns2b * bc;
+    const float ninv = rsqrtf(fmaxf(ns2, eps));
+    mu[f] = nmu;
+    inv_sigma[f] = ninv;
+    sigma[f] = 1.0f / ninv;
+    mu_b[f] = nmb;
+    s2_b[f] = ns2b;
+}
+
+__global__ void obs_count_kernel(int32_t* count) { *count += 1; }
+
 }  // namespace ml
 
 using namespace ml;
@@ -738,6 +836,19 @@ int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t 
     hipLaunchKernelGGL(env_reset_kernel, dim3(grid_for(N * obs_dim, 256)), dim3(256), 0,
                        S(stream), (int4*)state, N, obs_dim, k0, k1, env_offset, obs);
     return check_launch("env_reset");
+}
+
+int mlearn_obs_norm_update(const float* obs_stats, int32_t steps, int64_t tiles, int64_t N,
+                           int32_t obs_dim, float decay, float eps, float* est, int32_t* count,
+                           mlearn_stream_t stream) {
+    ML_REQUIRE(obs_stats && est && count, "obs_norm_update: null pointer");
+    ML_REQUIRE(steps >= 1 && N >= 1 && tiles >= (N + 31) / 32 && obs_dim >= 1,
+               "obs_norm_update: bad sizes");
+    ML_REQUIRE(decay > 0.f && decay < 1.f && eps > 0.f, "obs_norm_update: bad decay / eps");
+    hipLaunchKernelGGL(obs_norm_update_kernel, dim3((unsigned)obs_dim), dim3(256), 0, S(stream),
+                       obs_stats, steps, tiles, N, obs_dim, decay, eps, est, count);
+    hipLaunchKernelGGL(obs_count_kernel, dim3(1), dim3(1), 0, S(stream), count);
+    return check_launch("obs_norm_update");
 }
 
 }  // extern "C"

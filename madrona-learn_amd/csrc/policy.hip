@@ -34,6 +34,11 @@ PolicyK make_policy_k(const mlearn_mlp_policy& p) {
     k.head_t = p.head_t;
     k.head = p.head;
     k.head_b = p.head_bias;
+    k.obs_mu = p.obs_mu;
+    k.obs_inv = p.obs_inv_sigma;
+    k.obs_stats = p.obs_stats;
+    k.obs_tiles = p.obs_stats_tiles;
+    k.obs_steps = p.obs_stats_steps;
     return k;
 }
 
@@ -61,6 +66,9 @@ int validate_policy(const mlearn_mlp_policy* p) {
         ML_REQUIRE(p->w_t[i] && (i == 0 || p->w[i]) && p->ln_scale[i] && p->ln_bias[i],
                    "policy: null layer %d weights", i);
     ML_REQUIRE(p->head_t && p->head && p->head_bias, "policy: null head weights");
+    ML_REQUIRE(!p->obs_mu == !p->obs_inv_sigma, "policy: obs_mu / obs_inv_sigma");
+    ML_REQUIRE(!p->obs_stats || (p->obs_stats_steps >= 1 && p->obs_stats_tiles >= 1),
+               "policy: obs_stats needs obs_stats_steps and obs_stats_tiles");
     return MLEARN_OK;
 }
 
@@ -174,7 +182,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     zero_acc<NBW>(acc);
     gemm_first<T, NBW>(acc, obs + (live ? row : 0) * D, live, D / KS,
                        (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
-                       (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane);
+                       (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane,
+                       P.obs_mu, P.obs_inv);
     __syncthreads();  // LayerNorm parameters staged
     typedef typename Pk<T>::word word;
     word aw[NBW][8];
@@ -341,6 +350,30 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             if (logp) logp[n * P.K + g] = lp;
         }
     }
+    // observation statistics of this step (update_obs_stats, rollouts.py:670-676):
+    // the tile's {mean, M2} of the raw observations per feature, 4 lanes per
+    // feature (rows q, q + 4, ...), two passes
+    if (P.obs_stats && actions && step_add < (uint64_t)P.obs_steps) {
+        const int nrow = (int)(N - row0 < 32 ? N - row0 : 32);
+        float* out = P.obs_stats + ((int64_t)step_add * P.obs_tiles + blockIdx.x) * D * 2;
+        for (int f0 = 0; f0 < D; f0 += THREADS / 4) {
+            const int f = f0 + tid / 4, q = tid % 4;
+            const float* col = obs + row0 * D + (f < D ? f : 0);
+            float sx = 0.f;
+            for (int rr = q; rr < nrow; rr += 4) sx += col[(int64_t)rr * D];
+            const float mean = group_sum<4>(sx) / (float)nrow;
+            float m2 = 0.f;
+            for (int rr = q; rr < nrow; rr += 4) {
+                const float d = col[(int64_t)rr * D] - mean;
+                m2 += d * d;
+            }
+            m2 = group_sum<4>(m2);
+            if (q == 0 && f < D) {
+                out[f * 2] = mean;
+                out[f * 2 + 1] = m2;
+            }
+        }
+    }
     if (values) {
         if (P.CB == 1) {
             if (tid < 32 && row0 + tid < N) values[row0 + tid] = lg[tid * LGS + P.A];
@@ -398,6 +431,9 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
     ML_REQUIRE(obs, "policy_rollout_step: null obs");
     ML_REQUIRE(!actions || log_probs || !sample, "policy_rollout_step: sampling needs log_probs");
     ML_REQUIRE(actions || values, "policy_rollout_step: nothing to compute");
+    ML_REQUIRE(!policy->obs_stats || !actions || policy->obs_stats_tiles >= (N + 31) / 32,
+               "policy_rollout_step: obs_stats_tiles %lld < ceil(N / 32)",
+               (long long)policy->obs_stats_tiles);
     ML_REQUIRE((uintptr_t)obs % 16 == 0, "policy_rollout_step: obs must be 16-byte aligned");
     ML_REQUIRE(!obs_store || (uintptr_t)obs_store % 16 == 0,
                "policy_rollout_step: obs_store must be 16-byte aligned");

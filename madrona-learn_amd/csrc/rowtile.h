@@ -16,6 +16,8 @@
 // A workgroup is a set of independent waves (one tile of 32 rows each) that
 // share the LayerNorm parameters staged once in LDS.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace ml {
@@ -233,23 +235,50 @@ __device__ inline void gemm_pre_lds(f32x16 (&acc)[NOUT], const typename RT<T>::f
 // the compute dtype), runtime step count, a plain loop so the accumulators
 // stay put; the next step's A fragments and row fragment are in flight while
 // the current step's MFMAs run.  copy (may be null) receives the cast row.
+// Natural-order fragment s of an f32 observation row normalised as
+// ObservationsEMANormalizer.normalize (moving_avg.py:79-88): (x - mu) * inv_sigma
+// in f32, then the cast to the compute dtype.
+template <typename T> __device__ inline typename RT<T>::frag row_norm(const float* p, const float* mu,
+                                                                    const float* inv, int s, int h);
+template <> __device__ inline bf16x8 row_norm<bf16>(const float* p, const float* mu, const float* inv,
+                                                   int s, int h) {
+    const int k = 16 * s + 8 * h;
+    bf16x8 f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (bf16)((p[k + e] - mu[k + e]) * inv[k + e]);
+    return f;
+}
+template <> __device__ inline float row_norm<float>(const float* p, const float* mu, const float* inv,
+                                                   int s, int h) {
+    const int k = 2 * s + h;
+    return (p[k] - mu[k]) * inv[k];
+}
+template <typename T, typename S>
+__device__ inline typename RT<T>::frag row_in(const S* p, const float* mu, const float* inv, int s,
+                                              int h) {
+    if constexpr (std::is_same<S, float>::value)
+        if (mu) return row_norm<T>(p, mu, inv, s, h);
+    return RT<T>::row(p, s, h);
+}
+
 template <typename T, int NOUT, typename S>
 __device__ inline void gemm_first(f32x16 (&acc)[NOUT], const S* __restrict__ row, bool live,
-                                  int nks, const T* __restrict__ img, T* copy, int lane) {
+                                  int nks, const T* __restrict__ img, T* copy, int lane,
+                                  const float* mu = nullptr, const float* inv = nullptr) {
     typedef typename RT<T>::frag frag;
     constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
     const int voff = lane * RT<T>::E * (int)sizeof(T);
     const int h = lane >> 5;
     frag a[NOUT], an[NOUT];
-    frag b = live ? RT<T>::row(row, 0, h) : RT<T>::zero(), bn = b;
+    frag b = live ? row_in<T>(row, mu, inv, 0, h) : RT<T>::zero(), bn = b;
 #pragma unroll
     for (int nb = 0; nb < NOUT; ++nb) a[nb] = img_load<T>(rs, voff, (nb * nks) * FB);
     for (int s = 0; s < nks; ++s) {
         if (s + 1 < nks) {
 #pragma unroll
             for (int nb = 0; nb < NOUT; ++nb) an[nb] = img_load<T>(rs, voff, (nb * nks + s + 1) * FB);
-            bn = live ? RT<T>::row(row, s + 1, h) : RT<T>::zero();
+            bn = live ? row_in<T>(row, mu, inv, s + 1, h) : RT<T>::zero();
         }
         if (copy) RT<T>::put_row(copy, s, h, b);
 #pragma unroll
@@ -511,6 +540,11 @@ template <typename T> struct ZIO {
 struct PolicyK {
     int D, H, L, K, A;
     int CB, HC;  // critic outputs (1: scalar, else two-hot bins); head width (32 or 96)
+    const float* obs_mu;   // ObservationsEMANormalizer estimates (null: plain cast)
+    const float* obs_inv;
+    float* obs_stats;      // per-step per-tile {mean, M2} of the raw observations
+    int64_t obs_tiles;
+    int obs_steps;
     int off[MLEARN_MAX_GROUPS + 1];
     const void* wt[MLEARN_MAX_LAYERS];
     const void* w[MLEARN_MAX_LAYERS];

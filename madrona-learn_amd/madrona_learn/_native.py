@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -37,7 +37,10 @@ class MlpPolicy(Structure):
                 ("num_layers", c_int32), ("critic_bins", c_int32), ("actions", ActionLayout),
                 ("w_t", c_void_p * MAX_LAYERS), ("w", c_void_p * MAX_LAYERS),
                 ("ln_scale", c_void_p * MAX_LAYERS), ("ln_bias", c_void_p * MAX_LAYERS),
-                ("head_t", c_void_p), ("head", c_void_p), ("head_bias", c_void_p)]
+                ("head_t", c_void_p), ("head", c_void_p), ("head_bias", c_void_p),
+                ("obs_mu", c_void_p), ("obs_inv_sigma", c_void_p), ("obs_stats", c_void_p),
+                ("obs_stats_tiles", c_int64), ("obs_stats_steps", c_int32),
+                ("obs_pad", c_int32)]
 
 
 class MetricJob(Structure):
@@ -118,6 +121,8 @@ _SIGNATURES = {
                                                c_int32, _P, POINTER(PPOHparams), _P, _S]),
     "mlearn_param_count": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_head_cols": (c_int32, [POINTER(MlpPolicy)]),
+    "mlearn_obs_norm_update": (c_int32, [_P, c_int32, c_int64, c_int64, c_int32, c_float, c_float,
+                                         _P, _P, _S]),
     "mlearn_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy)]),
     "mlearn_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(OptimState), _P, _S]),
     "mlearn_policy_sync_weights": (c_int32, [POINTER(MlpPolicy), _P, _S]),

@@ -219,6 +219,8 @@ class RolloutManager:  # rollouts.py:373-826
         self.B = self.N // self.P
         self.policy_state = self.policies[0]
         self.prefix = self.policy_state.actor_critic.backbone.prefix
+        for ps in self.policies:
+            ps.attach_obs_stats(self.T, self.N // len(self.policies))
         arch = self.policy_state.arch
         for ps in self.policies[1:]:
             assert ps.arch == arch, "population policies must share one architecture"
@@ -299,6 +301,10 @@ class RolloutManager:  # rollouts.py:373-826
 
     def prep_obs(self, obs):
         x = self.prefix(obs, train=False)
+        pre = self.policy_state.obs_preprocess
+        if hasattr(pre, "prep_fns") and pre.prep_fns and isinstance(x, dict) and len(x) == 1:
+            k = next(iter(x))
+            x = {k: pre.prep(k, x[k])}  # ObservationsEMANormalizer prep_fns (observations.py:99-101)
         return obs_to_matrix(x, self.N)
 
     def _post_desc(self, t, p, rew, dn, rollout_state, gamma):
@@ -363,6 +369,11 @@ class RolloutManager:  # rollouts.py:373-826
             c = slice(p * B, (p + 1) * B)
             ps.critic_only(obs[c], s.bootstrap[c], post=posts[p],
                            carry=self._carry(rollout_state, p, self.T) if self.R else None)
+        # obs statistics -> normaliser estimates for the next rollout
+        # (update_state, train.py:193-204; the update trains on the stored,
+        # already normalised observations)
+        for ps in self.policies:
+            ps.update_obs_norm()
         rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:

@@ -208,8 +208,18 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
             f"{type(policy.actor_critic.critic).__name__}: use DreamerV3Critic with "
             "dreamer_v3_critic=True (the reference default) or DenseLayerCritic with False")
     preprocess = policy.obs_preprocess
+    obs_key = None
     if preprocess is not None:
         preprocess.fused_cast_dtype(cfg.compute_dtype)
+        from .observations import ObservationsEMANormalizer
+        if isinstance(preprocess, ObservationsEMANormalizer):
+            from .actor_critic import _identity_prefix
+            if prefix is not _identity_prefix:
+                raise NotImplementedError(
+                    "ObservationsEMANormalizer with a BackboneShared prefix: the fused path "
+                    "applies the prefix before the normaliser")
+            o = rollout_state.cur_obs
+            obs_key = next(iter(o)) if isinstance(o, dict) else None
     # one PolicyState / PolicyTrainState per train policy (_make_policies,
     # train_state.py:439-488: independent init and optimizer RNG per policy)
     pss, tss, algos = [], [], []
@@ -217,7 +227,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         algo = cfg.algo.setup()
         rng = np.random.default_rng(int(cfg.seed) if num_policies == 1
                                     else [int(cfg.seed), int(pid)])
-        ps = PolicyState(policy.actor_critic, arch, preprocess, device, rng)
+        ps = PolicyState(policy.actor_critic, arch, preprocess, device, rng, obs_key=obs_key)
         dp.broadcast_(ps.params)
         ps.sync_weights()
         ts = PolicyTrainState(cfg, algo.init_hyperparams(cfg), ps,

@@ -20,7 +20,7 @@ from .actor_critic import (ActorCritic, BackboneEncoder, BackboneShared,
                            RecurrentBackboneEncoder)
 from .cfg import DiscreteActionsConfig, TrainConfig
 from .models import MLP, DenseLayerCritic, DenseLayerDiscreteActor, DreamerV3Critic
-from .observations import ObservationsPreprocessNoop
+from .observations import ObservationsEMANormalizer, ObservationsPreprocessNoop
 from .rnn import LSTM
 
 
@@ -133,7 +133,7 @@ def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpA
 class PolicyState:
     """Parameters + compute images of one policy (train_state.py:34-82)."""
 
-    def __init__(self, actor_critic, arch: MlpArch, obs_preprocess, device, rng):
+    def __init__(self, actor_critic, arch: MlpArch, obs_preprocess, device, rng, obs_key=None):
         self.actor_critic = actor_critic
         self.arch = arch
         self.obs_preprocess = obs_preprocess or ObservationsPreprocessNoop.create()
@@ -197,6 +197,16 @@ class PolicyState:
         d.head_t = self.head_t.data_ptr()
         d.head = self.head.data_ptr()
         d.head_bias = self.head_b.data_ptr()
+        # ObservationsEMANormalizer estimates (init_estimates, moving_avg.py:56-76):
+        # [5][D] = mu, inv_sigma, sigma, mu_biased, sigma_sq_biased, + update count
+        self.obs_est = self.obs_count = None
+        pre = self.obs_preprocess
+        if isinstance(pre, ObservationsEMANormalizer) and pre.normalizes(obs_key):
+            self.obs_est = torch.zeros((5, D), dtype=torch.float32, device=self.device)
+            self.obs_est[1:3] = 1.0
+            self.obs_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+            d.obs_mu = self.obs_est.data_ptr()
+            d.obs_inv_sigma = self.obs_est.data_ptr() + 4 * D
         self.desc = d
         self.lstm_desc = None
         if arch.lstm_hidden:
@@ -312,11 +322,40 @@ class PolicyState:
             nat.ptr(values), 0, 0, None, 0, 0, 0, post, nat.stream_handle()), "critic_only")
 
     def state_dict(self):
-        return {"params": self.params.detach().cpu()}
+        sd = {"params": self.params.detach().cpu()}
+        if self.obs_est is not None:
+            sd["obs_est"] = self.obs_est.cpu()
+            sd["obs_count"] = self.obs_count.cpu()
+        return sd
 
     def load_state_dict(self, sd):
         self.params.copy_(sd["params"].to(self.device))
+        if self.obs_est is not None and "obs_est" in sd:
+            self.obs_est.copy_(sd["obs_est"].to(self.device))
+            self.obs_count.copy_(sd["obs_count"].to(self.device))
         self.sync_weights()
+
+    def attach_obs_stats(self, T, B):
+        """Per-step tile statistics buffer of the rollout (policy B envs)."""
+        if self.obs_est is None:
+            return
+        tiles = (B + 31) // 32
+        D = self.arch.obs_dim
+        self.obs_stats = torch.zeros((T, tiles, D, 2), dtype=torch.float32, device=self.device)
+        self.desc.obs_stats = self.obs_stats.data_ptr()
+        self.desc.obs_stats_tiles = tiles
+        self.desc.obs_stats_steps = T
+        self._obs_B = B
+
+    def update_obs_norm(self):
+        """Fold the rollout's statistics into the estimates (train.py:193-204)."""
+        if self.obs_est is None:
+            return
+        n = self.obs_preprocess.normalizer
+        nat.check(nat.lib().mlearn_obs_norm_update(
+            nat.ptr(self.obs_stats), self.obs_stats.shape[0], self.obs_stats.shape[1],
+            self._obs_B, self.arch.obs_dim, float(n.decay), float(n.eps), nat.ptr(self.obs_est),
+            nat.ptr(self.obs_count), nat.stream_handle()), "obs_norm_update")
 
 
 class PolicyTrainState:

@@ -603,14 +603,70 @@ def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs,
 # ---------------------------------------------------------------------------
 # rollout (rollouts.py:829-978) with the synthetic env
 # ---------------------------------------------------------------------------
+# ---------------------------------------------------------------------------
+# ObservationsEMANormalizer / EMANormalizer (observations.py:70-132,
+# moving_avg.py:48-196), f32 like the reference
+# ---------------------------------------------------------------------------
+def ema_init(D):
+    """init_estimates (moving_avg.py:56-76)."""
+    z = np.zeros(D, np.float32)
+    return {"mu": z.copy(), "inv_sigma": np.ones(D, np.float32), "sigma": np.ones(D, np.float32),
+            "mu_biased": z.copy(), "sigma_sq_biased": z.copy(), "N": 0}
+
+
+def ema_normalize(est, x, mode):
+    """normalize (moving_avg.py:78-86) in f32, then the cast to the compute dtype."""
+    x = np.asarray(x, np.float32)
+    y = ((x - est["mu"]) * est["inv_sigma"]).astype(np.float32)
+    return rnd(y, mode)
+
+
+def ema_update_input_stats(cur, t, x):
+    """update_input_stats (moving_avg.py:107-130) with num_prev_updates = t."""
+    a_mean, a_var = cur
+    x = np.asarray(x, np.float64)
+    b_mean = x.mean(0)
+    b_var = ((x - b_mean) ** 2).mean(0)
+    b_mean, b_var = b_mean.astype(np.float32), b_var.astype(np.float32)
+    delta = (b_mean - a_mean).astype(np.float32)
+    b_w = np.float32(1.0) / np.float32(t + 1)
+    a_w = np.float32(1.0) - b_w
+    ab_mean = (a_mean + delta * b_w).astype(np.float32)
+    ab_var = (a_w * a_var + b_w * b_var + np.square(delta) * a_w * b_w).astype(np.float32)
+    return ab_mean, ab_var
+
+
+def ema_update_estimates(est, stats, decay, eps):
+    """update_estimates (moving_avg.py:132-180)."""
+    x_mean, x_var = stats
+    f = np.float32
+    mean_delta = (x_mean - est["mu"]).astype(f)
+    oma = f(decay)
+    alpha = f(1.0) - oma
+    N, nN = est["N"], est["N"] + 1
+    mu_b = (oma * est["mu_biased"] + alpha * x_mean).astype(f)
+    s2_b = (oma * est["sigma_sq_biased"] + alpha * x_var +
+            (f(N) / f(nN)) * (oma * alpha) * np.square(mean_delta)).astype(f)
+    bc = f(-1.0) / f(np.expm1(f(nN) * f(np.log(oma))))
+    mu = (mu_b * bc).astype(f)
+    s2 = (s2_b * bc).astype(f)
+    inv = (f(1.0) / np.sqrt(np.maximum(s2, f(eps)))).astype(f)
+    return {"mu": mu, "inv_sigma": inv, "sigma": (f(1.0) / inv).astype(f), "mu_biased": mu_b,
+            "sigma_sq_biased": s2_b, "N": nN}
+
+
 def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99,
-            env_returns=None, ad=np.float64, actions_override=None, policy_fn=None):
+            env_returns=None, ad=np.float64, actions_override=None, policy_fn=None,
+            obs_norm=None):
     """rollout_loop restated: per step policy forward + Gumbel-max sample,
     store, env step, env-return bookkeeping; then the bootstrap critic.
     actions_override[t] (e.g. the GPU's actions) drives the env instead of
     the oracle's own samples (used to replay a GPU trajectory exactly).
     policy_fn(obs) -> (actions, log_probs, values) replaces the MLP policy
-    (integer fake-policy KAT, tests/test_rollout_kat.py)."""
+    (integer fake-policy KAT, tests/test_rollout_kat.py).  obs_norm = (est,
+    decay, eps) applies ObservationsEMANormalizer with the estimates est and
+    returns the updated estimates as out['obs_est'] (rollouts.py:670-678,
+    train.py:193-204)."""
     if policy_fn is not None:
         return _rollout_fake(policy_fn, env, T, gamma, env_returns)
     N = env.N
@@ -636,8 +692,13 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
     er = np.zeros(N, np.float32) if env_returns is None else env_returns
     trace = []
     obs = env.obs.copy()
+    prep = (lambda o: rnd(o, mode, ad)) if obs_norm is None else \
+        (lambda o: ema_normalize(obs_norm[0], o, mode).astype(ad))
+    ostats = (np.zeros(env.D, np.float32), np.zeros(env.D, np.float32))
     for t in range(T):
-        x = rnd(obs, mode, ad)
+        x = prep(obs)
+        if obs_norm is not None:
+            ostats = ema_update_input_stats(ostats, t, obs)
         logits, V, _ = forward_all(x)
         gum = native.gumbel_table(key[0], key[1], step_base + t, env.eoff, N, A)
         acts, logp = sample_actions(logits.astype(np.float32), buckets, gum)
@@ -655,8 +716,11 @@ def rollout(flat_p, lay, env, T, buckets, key, step_base, mode="f32", gamma=0.99
         store["rewards"].append(rew)
         store["dones"].append(done)
         er = np.where(done.astype(bool), np.float32(0), er).astype(np.float32)
-    _, boot, _ = forward_all(rnd(obs, mode, ad))
-    return _finish_store(store, boot, trace), er
+    _, boot, _ = forward_all(prep(obs))
+    out = _finish_store(store, boot, trace)
+    if obs_norm is not None:
+        out["obs_est"] = ema_update_estimates(obs_norm[0], ostats, obs_norm[1], obs_norm[2])
+    return out, er
 
 
 def _finish_store(store, boot, trace):

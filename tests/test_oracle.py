@@ -290,3 +290,30 @@ def test_twohot_weights_follow_the_reference():
     loss, grad = ref.twohot_ce(np.zeros((2, 63)), np.array([1e9, 0.3]))
     np.testing.assert_allclose(loss, np.log(63.0), rtol=1e-12)
     np.testing.assert_allclose(grad.sum(-1), 0.0, atol=1e-15)
+
+
+# ---------------------------------------------------------------------------
+# EMANormalizer (moving_avg.py:48-196): closed forms of the restatement
+# ---------------------------------------------------------------------------
+def test_ema_normalizer_closed_forms():
+    rng = np.random.default_rng(3)
+    xs = [(rng.standard_normal((50, 4)) * 2 + 1).astype(np.float32) for _ in range(6)]
+    st = (np.zeros(4, np.float32), np.zeros(4, np.float32))
+    for t, x in enumerate(xs):
+        st = ref.ema_update_input_stats(st, t, x)
+    # equal-size batches: the running fold is the pooled mean / population variance
+    allx = np.concatenate(xs).astype(np.float64)
+    np.testing.assert_allclose(st[0], allx.mean(0), rtol=1e-5)
+    np.testing.assert_allclose(st[1], allx.var(0), rtol=1e-5)
+    # first update: the bias correction makes the estimate the batch statistics
+    e = ref.ema_update_estimates(ref.ema_init(4), st, 0.999, 1e-5)
+    np.testing.assert_allclose(e["mu"], st[0], rtol=1e-3)
+    np.testing.assert_allclose(e["sigma"] ** 2, st[1], rtol=2e-3)
+    assert e["N"] == 1
+    # a constant feature: variance floored at eps (rsqrt(max(var, eps)))
+    c = ref.ema_update_input_stats((np.zeros(1, np.float32), np.zeros(1, np.float32)), 0,
+                                   np.full((8, 1), 3.0, np.float32))
+    e = ref.ema_update_estimates(ref.ema_init(1), c, 0.9, 1e-5)
+    np.testing.assert_allclose(e["inv_sigma"], 1 / np.sqrt(1e-5), rtol=1e-6)
+    y = ref.ema_normalize(e, np.full((2, 1), 3.0, np.float32), "f32")
+    np.testing.assert_allclose(y, 0.0, atol=1e-3)
