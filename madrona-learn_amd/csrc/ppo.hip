@@ -1377,8 +1377,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(LstmK R, RolloutK ro
     if (ub >= H / 32) return;  // H = 64: two unit blocks for four waves
     f32x16 acc[4];
     zero_acc<4>(acc);
-    gemm_lds<T, 4, KSH, 4>(acc, frf, (const T*)R.wi_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
-    gemm_lds<T, 4, KSH, 4>(acc, frh, (const T*)R.wh_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
+    gemm_lds2<T, 4, KSH, 6>(acc, frf, (const T*)R.wi_nat + (int64_t)ub * 4 * KSH * 64 * E, frh,
+                            (const T*)R.wh_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
     const int64_t f = f0 + r;
     const bool more = t + 1 < ro.bptt;
     const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
@@ -1426,7 +1426,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(LstmK R, RolloutK ro
                                                             const int32_t* __restrict__ mb_seq,
                                                             int mb, int t, LstmWsK lw,
                                                             float* colpart, int CP, int cp0) {
+    typedef typename RT<T>::frag frag;
     constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NU = H / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frg = (frag*)smem;  // [NKS][64] dG_t row fragments of the workgroup's 32 rows
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0 = blockIdx.x * 32;
@@ -1437,10 +1440,17 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(LstmK R, RolloutK ro
     const bool doA = hpart && t >= 1;
     f32x16 acc[1];
     zero_acc<1>(acc);
+    if (!first) {  // stage dG_t of the 32 rows once per workgroup (block-uniform)
+        const T* g0 = (const T*)lw.dg + ((int64_t)t * mb + m0) * 4 * H;
+        for (int idx = tid; idx < NKS * 64; idx += 256) {
+            const int s = idx >> 6, ln = idx & 63;
+            frg[idx] = RT<T>::row(g0 + (int64_t)(ln & 31) * 4 * H, s, ln >> 5);
+        }
+        __syncthreads();
+    }
     if (doB) {
         const int64_t f = (int64_t)t * mb + m0 + r;
-        gemm_first<T, 1>(acc, (const T*)lw.dg + f * 4 * H, true, NKS,
-                         (const T*)R.w_bwd + (int64_t)ob * NKS * 64 * E, (T*)nullptr, lane);
+        gemm_lds<T, 1, NKS, 8>(acc, frg, (const T*)R.w_bwd + (int64_t)ob * NKS * 64 * E, lane);
         if (!hpart) {
             T* drow = (T*)lw.dfeat + f * H + ob * 32;
 #pragma unroll
@@ -1561,9 +1571,19 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     step(std::integral_constant<int, kHeads>{});
     // reverse scan
     const int cp0 = L * 2 * H + head_cols(p);
-    for (int t = bptt; t >= 0; --t)
-        hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, 2 * H / 128), dim3(256), 0,
-                           s, RK, R, mb_seq, mb, t, lw, ws.colpart, ws.CP, cp0);
+    {
+        const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
+        auto k = lstm_bwd_step_kernel<T, H>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            attr_set = true;
+        }
+        for (int t = bptt; t >= 0; --t)
+            hipLaunchKernelGGL(k, dim3(mb / 32, 2 * H / 128), dim3(256), lds, s, RK, R, mb_seq, mb,
+                               t, lw, ws.colpart, ws.CP, cp0);
+    }
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});
     // weight gradients: trunk, head (from the LSTM outputs), Wi, Wh

@@ -203,6 +203,45 @@ __device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag*
     }
 }
 
+// gemm_lds over two concatenated products acc += Img1 . B1 + Img2 . B2 (each
+// NKS k-steps, B fragments from LDS) as ONE ring of 2 NKS steps, so the
+// weight prefetch does not drain between them.
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_lds2(f32x16 (&acc)[NOUT], const typename RT<T>::frag* fr1,
+                                 const T* __restrict__ img1, const typename RT<T>::frag* fr2,
+                                 const T* __restrict__ img2, int lane) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    constexpr int NS = 2 * NKS;
+    const __amdgpu_buffer_rsrc_t rs1 = img_rsrc(img1), rs2 = img_rsrc(img2);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    auto ld = [&](int s, int nb) {
+        return s < NKS ? img_load<T>(rs1, voff, (nb * NKS + s) * FB)
+                       : img_load<T>(rs2, voff, (nb * NKS + s - NKS) * FB);
+    };
+    auto bf = [&](int s) { return s < NKS ? fr1[s * 64 + lane] : fr2[(s - NKS) * 64 + lane]; };
+    frag ra[DEPTH][NOUT];
+#pragma unroll
+    for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = ld(s, nb);
+    frag b = bf(0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int sl = s + DEPTH - 1;
+        if (sl < NS) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb) ra[sl % DEPTH][nb] = ld(sl, nb);
+        }
+        const frag bn = s + 1 < NS ? bf(s + 1) : b;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ra[s % DEPTH][nb], b, acc[nb]);
+        __builtin_amdgcn_sched_barrier(0);
+        b = bn;
+    }
+}
+
 // Whole-layer A-fragment prefetch: issue every load of a product up front
 // (they land while earlier work runs), then multiply with B fragments from LDS.
 template <typename T, int NOUT, int NKS>
