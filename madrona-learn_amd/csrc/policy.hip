@@ -152,15 +152,21 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     float* rbias = lg + 32 * LGS;                         // [4H] LSTM bias (RNN)
     float* bins = rbias + (RNN ? 4 * H : 0);              // [HC] two-hot critic bins
     frag* frh = (frag*)(bins + HC);                       // [KSH][64] carry fragments (RNN)
-    for (int i = tid; i < L * 2 * H + HC; i += THREADS) {
-        float v;
+    // LayerNorm / head-bias parameters: loads issued now, written to LDS after
+    // the first product (their latency hides under the observation loads)
+    constexpr int NPAR = (MLEARN_MAX_LAYERS * 2 * H + HC + THREADS - 1) / THREADS;
+    float parv[NPAR];
+#pragma unroll
+    for (int k = 0; k < NPAR; ++k) {
+        const int i = tid + k * THREADS;
+        float v = 0.f;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
             v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
-        } else {
+        } else if (i < L * 2 * H + HC) {
             v = P.head_b[i - L * 2 * H];
         }
-        gb[i] = v;
+        parv[k] = v;
     }
     if constexpr (RNN)
         for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
@@ -184,6 +190,9 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
                        (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
                        (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane,
                        P.obs_mu, P.obs_inv);
+#pragma unroll
+    for (int k = 0; k < NPAR; ++k)
+        if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
     __syncthreads();  // LayerNorm parameters staged
     typedef typename Pk<T>::word word;
     word aw[NBW][8];

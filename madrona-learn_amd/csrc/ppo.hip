@@ -95,7 +95,7 @@ static uint64_t* g_stamp_buf = nullptr;
     do {                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                        \
         if (ws.stamps && lane == 0)                                               \
-            ws.stamps[((int64_t)tile * 4 + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+            ws.stamps[((int64_t)tile * W + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
         __builtin_amdgcn_sched_barrier(0);                                        \
     } while (0)
 #else
@@ -421,15 +421,21 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     float* bins = lred + W * kLossSlots;       // [HC] two-hot critic bins
     if (kLoss && P.CB > 1)
         for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
-    for (int i = tid; i < L * 2 * H + HC; i += THREADS) {
-        float v;
+    // LayerNorm / head-bias parameters: loads issued now, written to LDS after
+    // the first product (their latency hides under the observation gather)
+    constexpr int NPAR = (L * 2 * H + HC + THREADS - 1) / THREADS;
+    float parv[NPAR];
+#pragma unroll
+    for (int k = 0; k < NPAR; ++k) {
+        const int i = tid + k * THREADS;
+        float v = 0.f;
         if (i < L * 2 * H) {
             const int l = i / (2 * H), c = i - l * 2 * H;
             v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
-        } else {
+        } else if (i < L * 2 * H + HC) {
             v = P.head_b[i - L * 2 * H];
         }
-        gb[i] = v;
+        parv[k] = v;
     }
     const int tile = blockIdx.x;
     const int64_t row0 = (int64_t)tile * 32;
@@ -462,6 +468,9 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                            (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
                            (w == 0 && MODE != kTrunkBwd) ? (T*)ws.x0 + row * D : nullptr, lane);
     STAMP(1);
+#pragma unroll
+    for (int k = 0; k < NPAR; ++k)
+        if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
     __syncthreads();  // LayerNorm parameters staged
     typedef typename Pk<T>::word word;
     word zr[L][NBW][8];  // this wave's Dense outputs (exact in the compute dtype)
@@ -589,6 +598,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     // ---- loss: one (row, group | value) task per thread (ppo.py:129-262) ----
     {
         LossAcc m;
+        bool did = false;  // this lane ran a task (waves without any skip the reductions)
         const float as0 = adv_st[0], as1 = adv_st[1];
         // two-hot critic: the value rows run in groups of 8 lanes (below); with
         // 512 threads they take the last 256 while the first ones do the groups
@@ -599,6 +609,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         for (int task = (split && tid >= THREADS - 256) ? ntask : tid; task < ntask;
              task += tstride) {
             const int rr = task & 31, g = task >> 5;
+            did = true;
             float* lr = lg + rr * LGS;
             const int64_t f = row0 + rr;
             if (f >= M) {  // padding row: zero its d logits
@@ -634,6 +645,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
             const int vstride = split ? 256 : THREADS;
             for (int vt = vt0 < 0 ? 32 * G : vt0; vt < 32 * G; vt += vstride) {
                 const int rr = vt / G, sub = vt % G;
+                did = true;
                 float* lr = lg + rr * LGS;
                 const int64_t f = row0 + rr;
                 if (f >= M) {  // padding row: zero its d critic logits
@@ -647,12 +659,20 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
                                         m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
                                         m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
+        constexpr int kUsed = 17;  // slots 17.. are padding
+        if (__any(did)) {
 #pragma unroll
-        for (int s = 0; s < kLossSlots; ++s) {
-            const int kind = (s < 16) ? (s & 3) : 0;
-            float v = vals[s];
-            v = kind == 2 ? wave_reduce<2>(v) : (kind == 3 ? wave_reduce<3>(v) : wave_reduce<0>(v));
-            if (lane == 0) lred[w * kLossSlots + s] = v;
+            for (int s = 0; s < kUsed; ++s) {
+                const int kind = (s < 16) ? (s & 3) : 0;
+                float v = vals[s];
+                v = kind == 2 ? wave_reduce<2>(v)
+                              : (kind == 3 ? wave_reduce<3>(v) : wave_reduce<0>(v));
+                if (lane == 0) lred[w * kLossSlots + s] = v;
+            }
+            if (lane >= kUsed && lane < kLossSlots) lred[w * kLossSlots + lane] = 0.f;
+        } else if (lane < kLossSlots) {  // identities of sum / min / max
+            const int kind = (lane < 16) ? (lane & 3) : 0;
+            lred[w * kLossSlots + lane] = kind == 2 ? 3.4e38f : (kind == 3 ? -3.4e38f : 0.f);
         }
     }
     __syncthreads();

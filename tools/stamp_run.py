@@ -1,5 +1,5 @@
 """Diagnostic: per-phase cycle stamps of the fused PPO minibatch kernel (B1
-shape).  Run with MADRONA_LEARN_LIB=madrona-learn_amd/build_stamps/libmlearn_stamps.so
+shape).  Run with MADRONA_LEARN_LIB=madrona-learn_amd/madrona_learn/_lib/libmlearn_stamps.so
 (tools/build_stamps.sh)."""
 import ctypes
 import os
@@ -23,7 +23,8 @@ algo = mgr.algo
 ps, ts = mgr.state.policy_states, mgr.state.train_states
 M = algo.mb * algo.bptt
 ntiles = ((M + 63) // 64 * 64) // 32
-buf = torch.zeros((ntiles * 4, 16), dtype=torch.int64, device=dev)
+W = 8  # waves per step-kernel workgroup at H = 256 (ML_STEP_MAXW)
+buf = torch.zeros((ntiles * W, 16), dtype=torch.int64, device=dev)
 L.mlearn_debug_set_stamp_buffer(buf.data_ptr())
 # stamp index -> phase ending there (L = 2)
 names = {0: "prologue", 1: "L0 gemm", 2: "L0 stats+barrier", 4: "L0 apply+xchg+L1 gemm",
