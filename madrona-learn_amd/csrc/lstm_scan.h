@@ -1,0 +1,261 @@
+// Persistent LSTM scans of the recurrent PPO update (LSTM.sequence,
+// rnn.py:81-111, and its reverse for BPTT): ONE launch per direction per
+// minibatch instead of one per time step.  Textually included by ppo.hip
+// inside namespace ml (uses its RolloutK / LstmWsK / store_row).
+//
+// A workgroup owns 32 sequences of the minibatch for the whole chunk and has
+// H/32 waves; wave w owns unit block w (units 32w .. 32w+31), i.e. the four
+// gate blocks (i, f, g, o) of those units (weight images in unit-block gate
+// order), so the cell update is register-local:
+//   - forward: the c carry stays in the lanes' registers (accumulator order);
+//     the h carry and the next step's trunk features are exchanged between
+//     the waves as B fragments in LDS (one barrier pair per step);
+//   - backward: the c cotangent stays in registers; dG_t of the 32 rows is
+//     exchanged in LDS; each wave computes its d-feature block and its h
+//     cotangent block of [dF_{t+1} ; dh_t] = dG_{t+1} [Wi ; Wh]^T, then the
+//     cell backward of step t for its units.
+// Weights stream from L2 every step (every workgroup reads the same image).
+#pragma once
+
+// Natural-order B fragments in LDS (fr[s * 64 + lane], the layout RT<T>::row
+// reads): element k of row r; put4 writes k0 .. k0+3 (k0 % 4 == 0).
+template <typename T> struct LdsRow;
+template <> struct LdsRow<bf16> {
+    __device__ static void put4(bf16x8* fr, int k0, int r, float a, float b, float c, float d) {
+        bf16* p = (bf16*)(fr + (k0 >> 4) * 64 + r + 32 * ((k0 >> 3) & 1)) + (k0 & 7);
+        store4(p, a, b, c, d);
+    }
+};
+template <> struct LdsRow<float> {
+    __device__ static void put4(float* fr, int k0, int r, float a, float b, float c, float d) {
+        float* p = fr + (k0 >> 1) * 64 + r;  // k0: step k0/2 half 0; k0+1: half 1; ...
+        p[0] = a;
+        p[32] = b;
+        p[64] = c;
+        p[96] = d;
+    }
+};
+
+// The NKS x 64 B fragments of 32 rows, loaded cooperatively by NT threads
+// into registers (load) and written to LDS later (put).
+template <typename T, int NKS, int NT> struct RowStage {
+    static constexpr int NF = NKS * 64, N = (NF + NT - 1) / NT;
+    typename RT<T>::frag v[N];
+    template <typename RowF> __device__ void load(RowF rowp, int tid) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int idx = tid + i * NT;
+            if (NF % NT == 0 || idx < NF) v[i] = RT<T>::row(rowp(idx & 31), idx >> 6, (idx >> 5) & 1);
+        }
+    }
+    __device__ void put(typename RT<T>::frag* fr, int tid) const {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int idx = tid + i * NT;
+            if (NF % NT == 0 || idx < NF) fr[idx] = v[i];
+        }
+    }
+};
+
+template <int H> constexpr int scan_threads() { return 2 * H; }  // H/32 waves
+
+// Forward scan over the chunk: gates_t = F_t Wi + h Wh + bias -> cell ->
+// gates / c_t / h_t saved for the backward, carries into t + 1 cleared where
+// dones[t] (rnn.py:92-96); the carry-in rows (hin / cin) are written for the
+// weight gradient and the backward.  Step 0 starts from the sequences'
+// rnn_start_states [C][ld][H] (rollouts.py:533-537).
+template <typename T, int H>
+__global__ __launch_bounds__(scan_threads<H>()) void lstm_fwd_scan_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, const T* __restrict__ feat,
+    const T* __restrict__ sh, const T* __restrict__ sc, LstmWsK lw) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NT = scan_threads<H>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frf = (frag*)smem;     // [KSH][64] trunk features F_t of the 32 rows
+    frag* frh = frf + KSH * 64;  // [KSH][64] h carry into step t
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.x * 32;
+    const int bptt = ro.bptt;
+    auto start_row = [&](int i) -> int64_t {
+        const int64_t seq = mb_seq[m0 + i];
+        const int64_t c = seq / ro.N, b = seq - c * ro.N;
+        return (c * ro.ld + b) * H;
+    };
+    float cc[16];  // c carry: register q = 4j + e <-> unit 32w + 8j + 4h + e of row r
+    {
+        const int64_t src = start_row(r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u0 = w * 32 + 8 * j + 4 * h;
+            const float4 hv = load4(sh + src + u0), cv = load4(sc + src + u0);
+            store4((T*)lw.hin + (int64_t)(m0 + r) * H + u0, hv.x, hv.y, hv.z, hv.w);
+            store4((T*)lw.cin + (int64_t)(m0 + r) * H + u0, cv.x, cv.y, cv.z, cv.w);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cc[4 * j + e] = f4get(cv, e);
+        }
+        RowStage<T, KSH, NT> st;
+        st.load([&](int i) { return sh + start_row(i); }, tid);
+        st.put(frh, tid);
+        st.load([&](int i) { return feat + (int64_t)(m0 + i) * H; }, tid);
+        st.put(frf, tid);
+    }
+    __syncthreads();
+    const T* wi = (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E;
+    const T* wh = (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E;
+    for (int t = 0; t < bptt; ++t) {
+        const int64_t f = (int64_t)t * mb + m0 + r;
+        const bool more = t + 1 < bptt;
+        RowStage<T, KSH, NT> nf;  // F_{t+1}, in flight during this step's product
+        if (more) nf.load([&](int i) { return feat + ((int64_t)(t + 1) * mb + m0 + i) * H; }, tid);
+        const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+        f32x16 acc[4];
+        zero_acc<4>(acc);
+        gemm_lds2<T, 4, KSH, 6>(acc, frf, wi, frh, wh, lane);
+        T* gts = (T*)lw.gates + f * 4 * H;
+        const float keep = done ? 0.f : 1.f;
+        float hc[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u0 = w * 32 + 8 * j + 4 * h;
+            float gi[4], gf[4], gg[4], go[4], cn[4], hn[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = 4 * j + e, u = u0 + e;
+                const CellOut o = lstm_cell_fwd<T>(acc[0][q] + R.bias[u], acc[1][q] + R.bias[H + u],
+                                                   acc[2][q] + R.bias[2 * H + u],
+                                                   acc[3][q] + R.bias[3 * H + u], cc[q]);
+                gi[e] = o.i;
+                gf[e] = o.f;
+                gg[e] = o.g;
+                go[e] = o.o;
+                cn[e] = o.c;
+                hn[e] = o.h;
+                cc[q] = keep * o.c;
+                hc[q] = keep * o.h;
+            }
+            store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
+            store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
+            store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
+            store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
+            store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
+            store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
+            if (more) {
+                store4((T*)lw.hin + (f + mb) * H + u0, hc[4 * j], hc[4 * j + 1], hc[4 * j + 2],
+                       hc[4 * j + 3]);
+                store4((T*)lw.cin + (f + mb) * H + u0, cc[4 * j], cc[4 * j + 1], cc[4 * j + 2],
+                       cc[4 * j + 3]);
+            }
+        }
+        if (!more) break;
+        __syncthreads();  // every wave's product has read F_t and h_t
+        nf.put(frf, tid);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            LdsRow<T>::put4(frh, w * 32 + 8 * j + 4 * h, r, hc[4 * j], hc[4 * j + 1], hc[4 * j + 2],
+                            hc[4 * j + 3]);
+        __syncthreads();
+    }
+}
+
+// Reverse scan.  Step t (from bptt-1 down to 0): [dF_{t+1} ; dh_t] =
+// dG_{t+1} [Wi ; Wh]^T (w_bwd blocks w and H/32 + w, K = 4H from LDS), then
+// the cell backward of step t for unit block w: dh = dHout_t + dh_t and the
+// c cotangent, both cut where the carry out of step t was cleared (dones[t])
+// or at the end of the chunk; writes dG_t (rounded to the compute dtype),
+// dF_{t+1}, and the per-tile column partials of dG (the bias gradient).
+template <typename T, int H>
+__global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
+    float* colpart, int CP, int cp0) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NU = H / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frg = (frag*)smem;  // [NKS][64] dG_{t+1} of the workgroup's 32 rows
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.x * 32, m = m0 + r;
+    const int bptt = ro.bptt;
+    const T* wdf = (const T*)R.w_bwd + (int64_t)w * NKS * 64 * E;  // d-feature block w
+    auto store_df = [&](const f32x16& a, int64_t f) {
+        T* drow = (T*)lw.dfeat + f * H + w * 32;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            store4(drow + 8 * g + 4 * h, a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+    };
+    float dcc[16];  // c cotangent carried from step t + 1 into t
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dcc[q] = 0.f;
+    for (int t = bptt - 1; t >= 0; --t) {
+        const int64_t fs = (int64_t)t * mb + m;
+        const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+        f32x16 acc[2];
+        zero_acc<2>(acc);
+        if (t + 1 < bptt) {
+            gemm_lds<T, 2, NKS, 8>(acc, frg, wdf, lane, NU * NKS);
+            store_df(acc[0], fs + mb);
+        }
+        const T* gts = (const T*)lw.gates + fs * 4 * H;
+        T* dgs = (T*)lw.dg + fs * 4 * H;
+        float dpi[16], dpf[16], dpg[16], dpo[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u0 = w * 32 + 8 * j + 4 * h;
+            const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
+            const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
+            const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
+            const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
+            const float4 ci = load4((const T*)lw.cin + fs * H + u0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = 4 * j + e;
+                const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
+                const float dh = f4get(dho, e) + (cut ? 0.f : acc[1][q]);
+                const float tc = tanhf(f4get(c4, e));
+                const float dout = dh * tc;
+                const float dc = (cut ? 0.f : dcc[q]) + dh * o_ * (1.f - tc * tc);
+                dpi[q] = rnd<T>((dc * g_) * i_ * (1.f - i_));
+                dpf[q] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
+                dpg[q] = rnd<T>((dc * i_) * (1.f - g_ * g_));
+                dpo[q] = rnd<T>(dout * o_ * (1.f - o_));
+                dcc[q] = dc * f_;
+            }
+            store4(dgs + u0, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
+            store4(dgs + H + u0, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2], dpf[4 * j + 3]);
+            store4(dgs + 2 * H + u0, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2], dpg[4 * j + 3]);
+            store4(dgs + 3 * H + u0, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2], dpo[4 * j + 3]);
+        }
+        __syncthreads();  // every wave's product has read dG_{t+1}
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k0 = w * 32 + 8 * j + 4 * h;
+            LdsRow<T>::put4(frg, k0, r, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
+            LdsRow<T>::put4(frg, H + k0, r, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2],
+                            dpf[4 * j + 3]);
+            LdsRow<T>::put4(frg, 2 * H + k0, r, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2],
+                            dpg[4 * j + 3]);
+            LdsRow<T>::put4(frg, 3 * H + k0, r, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2],
+                            dpo[4 * j + 3]);
+        }
+        // bias gradient: column sums of dG over this tile's 32 rows
+        {
+            const int qs = col_sum16_index(lane);
+            float* cp = colpart + (int64_t)(((int64_t)t * mb + m0) / 32) * CP + cp0;
+            const int uq = w * 32 + feat(0, qs, h);
+            const float si = col_sum16(dpi, lane), sf = col_sum16(dpf, lane);
+            const float sg = col_sum16(dpg, lane), so = col_sum16(dpo, lane);
+            if ((lane & 16) == 0) {
+                cp[uq] = si;
+                cp[H + uq] = sf;
+                cp[2 * H + uq] = sg;
+                cp[3 * H + uq] = so;
+            }
+        }
+        __syncthreads();
+    }
+    // d features of step 0
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    gemm_lds<T, 1, NKS, 8>(acc, frg, wdf, lane);
+    store_df(acc[0], m);
+}

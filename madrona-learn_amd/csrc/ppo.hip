@@ -1345,191 +1345,10 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 
 // ---------------------------------------------------------------------------
 // Recurrent update: the LSTM scan over the minibatch's sequences
-// (LSTM.sequence, rnn.py:81-111) and its reverse (BPTT), one launch per
-// time step.  Rows f = t * mb + m.  A workgroup owns 32 sequences; its 4
-// waves own 32-unit blocks: each wave's 4 accumulator blocks are the gates
-// (i, f, g, o) of its units (weight images in unit-block gate order), so the
-// cell arithmetic is register-local.
+// (LSTM.sequence, rnn.py:81-111) and its reverse (BPTT), one persistent
+// launch per direction (lstm_scan.h).  Rows f = t * mb + m.
 // ---------------------------------------------------------------------------
-
-// Step-0 carry rows from the sequences' rnn_start_states [C][ld][H].
-template <typename T>
-__global__ __launch_bounds__(256) void lstm_start_kernel(const T* __restrict__ sh,
-                                                         const T* __restrict__ sc, RolloutK ro,
-                                                         const int32_t* __restrict__ mb_seq,
-                                                         int mb, int H, T* hin, T* cin) {
-    const int q = H / 4;
-    const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
-    if (i >= (int64_t)mb * q) return;
-    const int m = (int)(i / q), u = (int)(i % q) * 4;
-    const int64_t seq = mb_seq[m];
-    const int64_t c = seq / ro.N, b = seq % ro.N;
-    const int64_t src = (c * ro.ld + b) * H + u;
-    const float4 hv = load4(sh + src), cv = load4(sc + src);
-    store4(hin + (int64_t)m * H + u, hv.x, hv.y, hv.z, hv.w);
-    store4(cin + (int64_t)m * H + u, cv.x, cv.y, cv.z, cv.w);
-}
-
-// Forward step t: gates = F_t Wi + hin_t Wh + bias -> cell -> h_t, c_t; the
-// carry into t + 1 is cleared where dones[t] (rnn.py:92-96).
-template <typename T, int H>
-__global__ __launch_bounds__(256) void lstm_fwd_step_kernel(LstmK R, RolloutK ro,
-                                                            const int32_t* __restrict__ mb_seq,
-                                                            int mb, int t, const T* feat,
-                                                            LstmWsK lw) {
-    typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    frag* frf = (frag*)smem;     // [KSH][64] trunk-output fragments
-    frag* frh = frf + KSH * 64;  // [KSH][64] carry fragments
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int m0 = blockIdx.x * 32;
-    const int ub = blockIdx.y * 4 + w;
-    const int64_t f0 = (int64_t)t * mb + m0;
-    for (int idx = tid; idx < 2 * KSH * 64; idx += 256) {
-        const int which = idx >= KSH * 64, rem = idx - which * KSH * 64;
-        const int s = rem >> 6, ln = rem & 63;
-        const T* rowp = (which ? (const T*)lw.hin : feat) + (f0 + (ln & 31)) * H;
-        (which ? frh : frf)[rem] = RT<T>::row(rowp, s, ln >> 5);
-    }
-    __syncthreads();
-    if (ub >= H / 32) return;  // H = 64: two unit blocks for four waves
-    f32x16 acc[4];
-    zero_acc<4>(acc);
-    gemm_lds2<T, 4, KSH, 6>(acc, frf, (const T*)R.wi_nat + (int64_t)ub * 4 * KSH * 64 * E, frh,
-                            (const T*)R.wh_nat + (int64_t)ub * 4 * KSH * 64 * E, lane);
-    const int64_t f = f0 + r;
-    const bool more = t + 1 < ro.bptt;
-    const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
-    T* gts = (T*)lw.gates + f * 4 * H;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u0 = ub * 32 + 8 * j + 4 * h;
-        const float4 ci = load4((const T*)lw.cin + f * H + u0);
-        float gi[4], gf[4], gg[4], go[4], cn[4], hn[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int q = 4 * j + e, u = u0 + e;
-            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + R.bias[u], acc[1][q] + R.bias[H + u],
-                                               acc[2][q] + R.bias[2 * H + u],
-                                               acc[3][q] + R.bias[3 * H + u], f4get(ci, e));
-            gi[e] = o.i;
-            gf[e] = o.f;
-            gg[e] = o.g;
-            go[e] = o.o;
-            cn[e] = o.c;
-            hn[e] = o.h;
-        }
-        store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
-        store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
-        store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
-        store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
-        store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
-        store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
-        if (more) {
-            const float k = done ? 0.f : 1.f;
-            store4((T*)lw.hin + (f + mb) * H + u0, k * hn[0], k * hn[1], k * hn[2], k * hn[3]);
-            store4((T*)lw.cin + (f + mb) * H + u0, k * cn[0], k * cn[1], k * cn[2], k * cn[3]);
-        }
-    }
-}
-
-// Reverse step: phase B(t) (t < bptt) = [dF_t ; dh_{t-1}] = dG_t [Wi ; Wh]^T,
-// one 32-output block per wave (blocks < H/32: dF_t rows; the rest: the h
-// carry cotangent, kept in registers); phase A(t-1) (t >= 1, or t - 1 =
-// bptt - 1 in the first launch, t = bptt) on the waves of the h blocks: the
-// cell backward of step t - 1 for their units, writing dG_{t-1}, the c carry
-// cotangent and the per-tile column partials of dG (bias gradient).
-template <typename T, int H>
-__global__ __launch_bounds__(256) void lstm_bwd_step_kernel(LstmK R, RolloutK ro,
-                                                            const int32_t* __restrict__ mb_seq,
-                                                            int mb, int t, LstmWsK lw,
-                                                            float* colpart, int CP, int cp0) {
-    typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NU = H / 32;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    frag* frg = (frag*)smem;  // [NKS][64] dG_t row fragments of the workgroup's 32 rows
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int m0 = blockIdx.x * 32;
-    const int ob = blockIdx.y * 4 + w;
-    const bool hpart = ob >= NU;
-    const bool first = t == ro.bptt;
-    const bool doB = !first && !(hpart && t == 0);
-    const bool doA = hpart && t >= 1;
-    f32x16 acc[1];
-    zero_acc<1>(acc);
-    if (!first) {  // stage dG_t of the 32 rows once per workgroup (block-uniform)
-        const T* g0 = (const T*)lw.dg + ((int64_t)t * mb + m0) * 4 * H;
-        for (int idx = tid; idx < NKS * 64; idx += 256) {
-            const int s = idx >> 6, ln = idx & 63;
-            frg[idx] = RT<T>::row(g0 + (int64_t)(ln & 31) * 4 * H, s, ln >> 5);
-        }
-        __syncthreads();
-    }
-    if (doB) {
-        const int64_t f = (int64_t)t * mb + m0 + r;
-        gemm_lds<T, 1, NKS, 8>(acc, frg, (const T*)R.w_bwd + (int64_t)ob * NKS * 64 * E, lane);
-        if (!hpart) {
-            T* drow = (T*)lw.dfeat + f * H + ob * 32;
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                store4(drow + 8 * g + 4 * h, acc[0][4 * g], acc[0][4 * g + 1], acc[0][4 * g + 2],
-                       acc[0][4 * g + 3]);
-        }
-    }
-    if (!doA) return;
-    const int s = t - 1, ub = ob - NU, m = m0 + r;
-    const int64_t fs = (int64_t)s * mb + m;
-    const bool cut = first || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
-    const T* gts = (const T*)lw.gates + fs * 4 * H;
-    T* dgs = (T*)lw.dg + fs * 4 * H;
-    float dpi[16], dpf[16], dpg[16], dpo[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u0 = ub * 32 + 8 * j + 4 * h;
-        const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
-        const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
-        const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
-        const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
-        const float4 ci = load4((const T*)lw.cin + fs * H + u0);
-        float* dccp = lw.dcc + (int64_t)m * H + u0;
-        const float4 dcn = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)dccp;
-        float dcc_new[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int q = 4 * j + e;
-            const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
-            const float dh = f4get(dho, e) + (cut ? 0.f : acc[0][q]);
-            const float tc = tanhf(f4get(c4, e));
-            const float dout = dh * tc;
-            const float dc = f4get(dcn, e) + dh * o_ * (1.f - tc * tc);
-            dpi[q] = rnd<T>((dc * g_) * i_ * (1.f - i_));
-            dpf[q] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
-            dpg[q] = rnd<T>((dc * i_) * (1.f - g_ * g_));
-            dpo[q] = rnd<T>(dout * o_ * (1.f - o_));
-            dcc_new[e] = dc * f_;
-        }
-        store4(dgs + u0, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
-        store4(dgs + H + u0, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2], dpf[4 * j + 3]);
-        store4(dgs + 2 * H + u0, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2], dpg[4 * j + 3]);
-        store4(dgs + 3 * H + u0, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2], dpo[4 * j + 3]);
-        *(float4*)dccp = make_float4(dcc_new[0], dcc_new[1], dcc_new[2], dcc_new[3]);
-    }
-    // bias gradient: column sums of dG over this tile's 32 rows
-    const int qs = col_sum16_index(lane);
-    float* cp = colpart + (int64_t)((s * (int64_t)mb + m0) / 32) * CP + cp0;
-    const int uq = ub * 32 + feat(0, qs, h);
-    const float si = col_sum16(dpi, lane), sf = col_sum16(dpf, lane);
-    const float sg = col_sum16(dpg, lane), so = col_sum16(dpo, lane);
-    if ((lane & 16) == 0) {
-        cp[uq] = si;
-        cp[H + uq] = sf;
-        cp[2 * H + uq] = sg;
-        cp[3 * H + uq] = so;
-    }
-}
+#include "lstm_scan.h"
 
 template <typename T, int H>
 static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& lstm,
@@ -1570,22 +1389,18 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // trunk forward over every row (the LSTM input F = A_{L-1})
     step(std::integral_constant<int, kTrunkFwd>{});
     const T* feat = (const T*)ws.a[L - 1];
-    hipLaunchKernelGGL(lstm_start_kernel<T>, dim3((unsigned)((mb * (H / 4) + 255) / 256)),
-                       dim3(256), 0, s, (const T*)start_h, (const T*)start_c, R, mb_seq, mb, H,
-                       (T*)lw.hin, (T*)lw.cin);
     {
         constexpr int KSH = H / RT<T>::KS;
         const size_t lds = 2 * (size_t)KSH * 64 * sizeof(typename RT<T>::frag);
-        auto k = lstm_fwd_step_kernel<T, H>;
+        auto k = lstm_fwd_scan_kernel<T, H>;
         static bool attr_set = false;
         if (!attr_set) {
             (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             attr_set = true;
         }
-        for (int t = 0; t < bptt; ++t)
-            hipLaunchKernelGGL(k, dim3(mb / 32, (H / 32 + 3) / 4), dim3(256), lds, s, RK, R,
-                               mb_seq, mb, t, feat, lw);
+        hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb,
+                           feat, (const T*)start_h, (const T*)start_c, lw);
     }
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});
@@ -1593,16 +1408,15 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     const int cp0 = L * 2 * H + head_cols(p);
     {
         const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
-        auto k = lstm_bwd_step_kernel<T, H>;
+        auto k = lstm_bwd_scan_kernel<T, H>;
         static bool attr_set = false;
         if (!attr_set) {
             (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             attr_set = true;
         }
-        for (int t = bptt; t >= 0; --t)
-            hipLaunchKernelGGL(k, dim3(mb / 32, 2 * H / 128), dim3(256), lds, s, RK, R, mb_seq, mb,
-                               t, lw, ws.colpart, ws.CP, cp0);
+        hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb, lw,
+                           ws.colpart, ws.CP, cp0);
     }
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});

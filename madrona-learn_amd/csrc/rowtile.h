@@ -173,9 +173,10 @@ __device__ inline void gemm_rb(f32x16 (&acc)[NOUT], const typename RT<T>::frag (
 
 // As gemm_rb, with the B fragments read from LDS (fr[s*64 + lane], written
 // by the workgroup's waves) one step ahead instead of held in registers.
+// bstride: k-steps between consecutive output blocks of the image (default NKS).
 template <typename T, int NOUT, int NKS, int DEPTH>
 __device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag* fr,
-                                const T* __restrict__ img, int lane) {
+                                const T* __restrict__ img, int lane, int bstride = NKS) {
     typedef typename RT<T>::frag frag;
     constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
@@ -184,7 +185,7 @@ __device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag*
 #pragma unroll
     for (int s = 0; s < DEPTH - 1; ++s)
 #pragma unroll
-        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * NKS + s) * FB);
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * bstride + s) * FB);
     frag b = fr[lane];
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
@@ -192,7 +193,7 @@ __device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag*
         if (sl < NKS) {
 #pragma unroll
             for (int nb = 0; nb < NOUT; ++nb)
-                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * NKS + sl) * FB);
+                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * bstride + sl) * FB);
         }
         const frag bn = s + 1 < NKS ? fr[(s + 1) * 64 + lane] : b;
         __builtin_amdgcn_sched_barrier(0);
