@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 6
+#define MLEARN_ABI_VERSION 7
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -73,6 +73,19 @@ int mlearn_counters_add(uint64_t* ctr, int32_t n, const uint64_t* deltas /* host
 int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
                    const float* bootstrap, float* advantages, float* returns, int32_t T,
                    int64_t N, float gamma, float gae_lambda, mlearn_stream_t stream);
+
+/* mlearn_gae_f32 with a value normaliser (TrainConfig.normalize_values): the
+ * stored values and the bootstrap are critic outputs in the normalised space
+ * and are inverted first, v * sigma + mu in f32 (EMANormalizer.invert,
+ * moving_avg.py:87-95, applied in _finalize_rollouts rollouts.py:726-738);
+ * returns = advantages + inverted values (rollouts.py:769).  value_norm holds
+ * one 8-float estimate record per policy, {mu, inv_sigma, sigma, mu_biased,
+ * sigma_sq_biased, 0, 0, 0} (mlearn_value_norm_chain); column n uses record
+ * n / cols_per_norm. */
+int mlearn_gae_vnorm_f32(const float* rewards, const float* values, const uint8_t* dones,
+                         const float* bootstrap, const float* value_norm, int64_t cols_per_norm,
+                         float* advantages, float* returns, int32_t T, int64_t N, float gamma,
+                         float gae_lambda, mlearn_stream_t stream);
 
 /* Discounted returns without advantages (algo_common.py:45-81), used when
  * TrainConfig.compute_advantages is False. */
@@ -261,6 +274,25 @@ int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t
 int mlearn_adv_stats_finish(const double* partials, int32_t num_mb, double count,
                             float* stats, mlearn_stream_t stream);
 
+/* mlearn_adv_stats over the returns: per-minibatch double (sum x, sum x^2)
+ * of the value normaliser's input (ppo.py:209-211), same partials layout. */
+int mlearn_return_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
+                        int32_t mb_size, double* partials, mlearn_stream_t stream);
+
+/* Value normaliser over one epoch's minibatches in order (ppo.py:205-211,
+ * 346): minibatch m updates the estimates with its returns'
+ * (mean, population variance) = return_sums[m] / count (update_input_stats
+ * from zero, then update_estimates, moving_avg.py:103-192; decay =
+ * TrainConfig.value_normalizer_decay, eps 1e-5).  est = {mu, inv_sigma,
+ * sigma, mu_biased, sigma_sq_biased, ...} (8 floats) and *n_updates are
+ * updated in place.  records[m] (8 floats) = {adv mean, adv rstd (from
+ * adv_stats[m]), mu and inv_sigma after the update, mu and sigma before it,
+ * 0, 0}: the adv_stats argument of mlearn_ppo_minibatch_grad when
+ * hp->normalize_values. */
+int mlearn_value_norm_chain(const double* return_sums, const float* adv_stats, int32_t num_mb,
+                            double count, float decay, float eps, float* est, int32_t* n_updates,
+                            float* records, mlearn_stream_t stream);
+
 typedef struct mlearn_ppo_hparams {
     float clip_coef;
     float value_loss_coef;
@@ -269,6 +301,8 @@ typedef struct mlearn_ppo_hparams {
     int32_t clip_value_loss;               /* PPOConfig.clip_value_loss */
     int32_t huber_value_loss;              /* PPOConfig.huber_value_loss */
     float loss_scale;                      /* 1/world_size under DP (mean of means) */
+    int32_t normalize_values;              /* TrainConfig.normalize_values: adv_stats is a
+                                              mlearn_value_norm_chain record */
 } mlearn_ppo_hparams;
 
 /* Size of the minibatch workspace (activations + gradient slabs). */
@@ -279,7 +313,10 @@ int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows
  * ppo.py:276-281) and the reduction of all per-row-tile partials into
  * grad[param_count] (flat f32, layout of mlearn_param_offsets).
  * mb_seq = the mb_size sequence ids of this minibatch (a slice of perm).
- * adv_stats = {mean, rstd} of this minibatch.  loss_out (may be NULL) receives
+ * adv_stats = {mean, rstd} of this minibatch (with hp->normalize_values the
+ * 8-float record of mlearn_value_norm_chain: the value target is the return
+ * normalised with the updated estimates, the value error inverts the critic
+ * with the previous ones, ppo.py:190-218).  loss_out (may be NULL) receives
  * 5 x {mean, m2, min, max, count}: 'Loss' {loss,0,loss,loss,1}, 'Action Obj',
  * 'Value Loss', 'Value Errors', 'Entropy' (ppo.py:95-106, 351-362).  With
  * critic_bins > 1 the value loss is the two-hot cross entropy of the returns

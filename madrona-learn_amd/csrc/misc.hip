@@ -97,12 +97,21 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewa
                                                   const uint8_t* __restrict__ dones,
                                                   const float* __restrict__ boot,
                                                   float* __restrict__ adv, float* __restrict__ ret,
-                                                  int T, int64_t N, float gamma, float gl) {
+                                                  int T, int64_t N, float gamma, float gl,
+                                                  const float* __restrict__ vn, int64_t vn_cols) {
 #pragma clang fp contract(off)
     int64_t n0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * VEC;
     if (n0 >= N) return;
+    // value normaliser (normalize_values): values / bootstrap are inverted,
+    // v * sigma + mu (EMANormalizer.invert, moving_avg.py:87-95)
+    float vmu = 0.f, vsig = 1.f;
+    if (vn) {
+        const float* e = vn + (n0 / vn_cols) * 8;
+        vmu = e[0];
+        vsig = e[2];
+    }
     float nv[VEC], na[VEC];
-    for (int j = 0; j < VEC; ++j) nv[j] = boot[n0 + j];
+    for (int j = 0; j < VEC; ++j) nv[j] = vn ? boot[n0 + j] * vsig + vmu : boot[n0 + j];
     for (int j = 0; j < VEC; ++j) na[j] = 0.f;
 
     GaeChunk<VEC> cur[U], nxt[U];
@@ -124,6 +133,7 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewa
             for (int j = 0; j < VEC; ++j) {
                 uint32_t d = cur[u].dj(j);
                 float v = cur[u].vj(j);
+                if (vn) v = v * vsig + vmu;
                 float nvj = d ? 0.f : nv[j];
                 float naj = d ? 0.f : na[j];
                 float td = (cur[u].rj(j) + gamma * nvj) - v;
@@ -394,6 +404,7 @@ __global__ __launch_bounds__(256) void perm_kernel(uint32_t k0, uint32_t k1,
 constexpr int kStatBlocks = 32;
 
 __global__ __launch_bounds__(256) void adv_stats_kernel(mlearn_rollout_view ro,
+                                                        const float* __restrict__ src,
                                                         const int32_t* __restrict__ perm,
                                                         int mb_size, double* part) {
     __shared__ double sh[4];
@@ -407,7 +418,7 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(mlearn_rollout_view ro,
         int64_t seq = seqs[j];
         int64_t c = seq / ro.N, b = seq % ro.N;
         int64_t t = c * ro.bptt_len + tl;
-        double x = ro.advantages[t * ro.ld + b];
+        double x = src[t * ro.ld + b];
         s += x;
         q += x * x;
     }
@@ -440,6 +451,56 @@ __global__ void adv_stats_finish_kernel(const double* sums, int num_mb, double c
     float fm = (float)mean, fv = (float)var;
     st[2 * m] = fm;
     st[2 * m + 1] = rsqrtf(fmaxf(fv, 1e-5f));
+}
+
+// Value normaliser chain over an epoch's minibatches (mlearn_value_norm_chain):
+// one thread, the estimates carried from minibatch to minibatch as in
+// _ppo_update's train_state.value_normalizer_state (ppo.py:205-211, 346).
+// f32 arithmetic in the reference's expression order (moving_avg.py:131-181).
+__global__ void value_norm_chain_kernel(const double* sums, const float* adv_st, int num_mb,
+                                        double count, float decay, float eps, float* est,
+                                        int32_t* nupd, float* rec) {
+#pragma clang fp contract(off)
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float mu = est[0], sig = est[2], mub = est[3], s2b = est[4];
+    float inv = est[1];
+    int32_t n = *nupd;
+    const float oma = decay, alpha = 1.f - oma;
+    for (int m = 0; m < num_mb; ++m) {
+        // update_input_stats from zero with n_a = 0: the batch's own mean and
+        // population variance
+        const double mean = sums[2 * m] / count;
+        const double var = sums[2 * m + 1] / count - mean * mean;
+        const float xm = (float)mean, xv = (float)(var > 0.0 ? var : 0.0);
+        const float delta = xm - mu;
+        const int32_t nn = n + 1;
+        const float mub2 = oma * mub + alpha * xm;
+        const float s2b2 = oma * s2b + alpha * xv + ((float)n / (float)nn) * (oma * alpha) * (delta * delta);
+        const float bc = -1.f / expm1f((float)nn * logf(oma));
+        const float mu2 = mub2 * bc, s22 = s2b2 * bc;
+        const float inv2 = 1.f / sqrtf(fmaxf(s22, eps));
+        float* r = rec + 8 * (int64_t)m;
+        r[0] = adv_st[2 * m];
+        r[1] = adv_st[2 * m + 1];
+        r[2] = mu2;
+        r[3] = inv2;
+        r[4] = mu;
+        r[5] = sig;
+        r[6] = 0.f;
+        r[7] = 0.f;
+        mu = mu2;
+        inv = inv2;
+        sig = 1.f / inv2;
+        mub = mub2;
+        s2b = s2b2;
+        n = nn;
+    }
+    est[0] = mu;
+    est[1] = inv;
+    est[2] = sig;
+    est[3] = mub;
+    est[4] = s2b;
+    *nupd = n;
 }
 
 // ---------------------------------------------------------------------------
@@ -658,13 +719,31 @@ int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* don
     if (N >= (int64_t)1 << 20) {
         hipLaunchKernelGGL((gae_kernel<1, 8>), dim3(grid_for(N, 256)), dim3(256), 0, S(stream),
                            rewards, values, dones, bootstrap, advantages, returns, T, N, gamma,
-                           gl);
+                           gl, (const float*)nullptr, (int64_t)1);
     } else {
         hipLaunchKernelGGL((gae_kernel<1, 16>), dim3(grid_for(N, 64)), dim3(64), 0, S(stream),
                            rewards, values, dones, bootstrap, advantages, returns, T, N, gamma,
-                           gl);
+                           gl, (const float*)nullptr, (int64_t)1);
     }
     return check_launch("gae");
+}
+
+int mlearn_gae_vnorm_f32(const float* rewards, const float* values, const uint8_t* dones,
+                         const float* bootstrap, const float* value_norm, int64_t cols_per_norm,
+                         float* advantages, float* returns, int32_t T, int64_t N, float gamma,
+                         float gae_lambda, mlearn_stream_t stream) {
+    ML_REQUIRE(T >= 0 && N >= 0, "gae_vnorm: negative size");
+    if (T == 0 || N == 0) return MLEARN_OK;
+    ML_REQUIRE(rewards && values && dones && bootstrap && advantages && returns && value_norm,
+               "gae_vnorm: null pointer");
+    ML_REQUIRE(cols_per_norm >= 1 && N % cols_per_norm == 0,
+               "gae_vnorm: N must be a multiple of cols_per_norm");
+    ML_REQUIRE(N <= ((int64_t)1 << 28), "gae_vnorm: N > 2^28 columns");
+    const float gl = gamma * gae_lambda;
+    hipLaunchKernelGGL((gae_kernel<1, 16>), dim3(grid_for(N, 64)), dim3(64), 0, S(stream), rewards,
+                       values, dones, bootstrap, advantages, returns, T, N, gamma, gl, value_norm,
+                       cols_per_norm);
+    return check_launch("gae_vnorm");
 }
 
 int mlearn_returns_f32(const float* rewards, const uint8_t* dones, const float* bootstrap,
@@ -775,9 +854,35 @@ int mlearn_minibatch_perm(uint32_t k0, uint32_t k1, const uint64_t* epoch_ctr, u
     return check_launch("minibatch_perm");
 }
 
+static int minibatch_sums(const mlearn_rollout_view* ro, const float* src, const int32_t* perm,
+                          int32_t num_mb, int32_t mb_size, double* partials, hipStream_t stream);
+
 int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
                      int32_t mb_size, double* partials, mlearn_stream_t stream) {
     ML_REQUIRE(ro && perm && partials, "adv_stats: null pointer");
+    return minibatch_sums(ro, ro->advantages, perm, num_mb, mb_size, partials, S(stream));
+}
+
+int mlearn_return_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
+                        int32_t mb_size, double* partials, mlearn_stream_t stream) {
+    ML_REQUIRE(ro && perm && partials, "return_stats: null pointer");
+    return minibatch_sums(ro, ro->returns, perm, num_mb, mb_size, partials, S(stream));
+}
+
+int mlearn_value_norm_chain(const double* return_sums, const float* adv_stats, int32_t num_mb,
+                            double count, float decay, float eps, float* est, int32_t* n_updates,
+                            float* records, mlearn_stream_t stream) {
+    ML_REQUIRE(return_sums && adv_stats && est && n_updates && records, "value_norm: null pointer");
+    ML_REQUIRE(num_mb >= 1 && count > 0, "value_norm: bad sizes");
+    ML_REQUIRE(decay > 0.f && decay < 1.f && eps > 0.f, "value_norm: bad decay / eps");
+    hipLaunchKernelGGL(value_norm_chain_kernel, dim3(1), dim3(64), 0, S(stream), return_sums,
+                       adv_stats, num_mb, count, decay, eps, est, n_updates, records);
+    return check_launch("value_norm_chain");
+}
+
+static int minibatch_sums(const mlearn_rollout_view* ro, const float* src, const int32_t* perm,
+                          int32_t num_mb, int32_t mb_size, double* partials, hipStream_t stream) {
+    ML_REQUIRE(src, "minibatch sums: null source array");
     ML_REQUIRE(num_mb >= 1 && mb_size >= 1, "adv_stats: bad minibatch sizes");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "adv_stats: bad bptt_len");
     ML_REQUIRE((int64_t)num_mb * mb_size <= (ro->T / ro->bptt_len) * ro->N,
@@ -787,9 +892,9 @@ int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t
     mlearn_rollout_view v = *ro;
     if (v.ld == 0) v.ld = v.N;
     ML_REQUIRE(v.ld >= v.N, "adv_stats: ld %lld < N %lld", (long long)v.ld, (long long)v.N);
-    hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb, kStatBlocks), dim3(256), 0, S(stream), v,
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb, kStatBlocks), dim3(256), 0, stream, v, src,
                        perm, mb_size, scratch);
-    hipLaunchKernelGGL(adv_stats_reduce_kernel, dim3((num_mb + 63) / 64), dim3(64), 0, S(stream),
+    hipLaunchKernelGGL(adv_stats_reduce_kernel, dim3((num_mb + 63) / 64), dim3(64), 0, stream,
                        (const double*)scratch, num_mb, partials);
     return check_launch("adv_stats");
 }

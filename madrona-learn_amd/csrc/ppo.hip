@@ -42,7 +42,7 @@ struct RolloutK {
 struct HpK {
     float clip, vcoef;
     float ecoef[MLEARN_MAX_GROUPS];
-    int norm_adv, clip_vl, huber;
+    int norm_adv, clip_vl, huber, norm_vals;
     float loss_scale;
     float inv_sk, inv_s;
 };
@@ -275,9 +275,13 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
 
 // Scalar critic (DenseLayerCritic): lg points at the row, value at column A;
 // zeroes columns A+1..HC-1.
+// vn (normalize_values, may be null) = {mu', inv_sigma'} after this
+// minibatch's update and {mu, sigma} before it (mlearn_value_norm_chain).
 __device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float R, float ov,
-                                  LossAcc& m) {
+                                  LossAcc& m, const float* vn) {
     const float V = lg[A];
+    // target: the return normalised with the updated estimates (ppo.py:209-211)
+    const float tgt = vn ? (R - vn[0]) * vn[1] : R;
     float vpred = V, dvp = 1.f;
     if (hp.clip_vl) {  // ppo.py:197-203
         const float vlo = ov - hp.clip, vhi = ov + hp.clip;
@@ -285,7 +289,7 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float
         vpred = fminf(yy, vhi);
         dvp = (V > vlo ? 1.f : (V == vlo ? 0.5f : 0.f)) * (yy < vhi ? 1.f : (yy == vhi ? 0.5f : 0.f));
     }
-    const float e = vpred - R;
+    const float e = vpred - tgt;
     float vl, dvl;
     if (hp.huber) {  // optax.huber_loss, delta = 1
         const float ae = fabsf(e);
@@ -298,7 +302,8 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float
     }
     lg[A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
     for (int j = A + 1; j < HC; ++j) lg[j] = 0.f;
-    const float verr = fabsf(V - R);
+    // value error: the critic inverted with the previous estimates (ppo.py:193-195)
+    const float verr = fabsf((vn ? V * vn[3] + vn[2] : V) - R);
     m.svl += vl;
     m.qvl += vl * vl;
     m.mnvl = fminf(m.mnvl, vl);
@@ -600,6 +605,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         LossAcc m;
         bool did = false;  // this lane ran a task (waves without any skip the reductions)
         const float as0 = adv_st[0], as1 = adv_st[1];
+        const float* vn = hp.norm_vals ? adv_st + 2 : nullptr;
         // two-hot critic: the value rows run in groups of 8 lanes (below); with
         // 512 threads they take the last 256 while the first ones do the groups
         const bool th = P.CB > 1;
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                 loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], act, olp, adv, hp.ecoef[g],
                            m);
             } else {
-                loss_value(hp, lr, P.A, HC, ret, oval, m);
+                loss_value(hp, lr, P.A, HC, ret, oval, m, vn);
             }
         }
         if (th) {
@@ -1291,6 +1297,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
     hp.norm_adv = h.normalize_advantages;
     hp.clip_vl = h.clip_value_loss;
+    hp.norm_vals = h.normalize_values;
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.inv_s = (float)(1.0 / (double)M);
@@ -1371,6 +1378,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
     hp.norm_adv = h.normalize_advantages;
     hp.clip_vl = h.clip_value_loss;
+    hp.norm_vals = h.normalize_values;
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.inv_s = (float)(1.0 / (double)M);
@@ -1498,6 +1506,8 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
                "ppo: null rollout array");
     ML_REQUIRE(!hp->clip_value_loss || ro->values, "ppo: clip_value_loss needs values");
+    ML_REQUIRE(!hp->normalize_values || policy->critic_bins == 1,
+               "ppo: normalize_values needs the scalar critic (ppo.py:54-57)");
     hipStream_t s = S(stream);
 #define ML_DISPATCH(T)                                                                           \
     switch (policy->hidden) {                                                                   \
@@ -1551,6 +1561,8 @@ int mlearn_lstm_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn
     ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
                "lstm ppo: null rollout array");
     ML_REQUIRE(!hp->clip_value_loss || ro->values, "lstm ppo: clip_value_loss needs values");
+    ML_REQUIRE(!hp->normalize_values || policy->critic_bins == 1,
+               "lstm ppo: normalize_values needs the scalar critic (ppo.py:54-57)");
     hipStream_t s = S(stream);
 #define ML_DISPATCH(T)                                                                            \
     switch (policy->hidden) {                                                                    \

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -65,7 +65,7 @@ class PPOHparams(Structure):
     _fields_ = [("clip_coef", c_float), ("value_loss_coef", c_float),
                 ("entropy_coef", c_float * MAX_GROUPS), ("normalize_advantages", c_int32),
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
-                ("loss_scale", c_float)]
+                ("loss_scale", c_float), ("normalize_values", c_int32)]
 
 
 class OptimState(Structure):
@@ -97,6 +97,8 @@ _SIGNATURES = {
     "mlearn_philox4x32": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64, _S]),
     "mlearn_counters_add": (c_int32, [_P, c_int32, POINTER(c_uint64), _S]),
     "mlearn_gae_f32": (c_int32, [_P, _P, _P, _P, _P, _P, c_int32, c_int64, c_float, c_float, _S]),
+    "mlearn_gae_vnorm_f32": (c_int32, [_P, _P, _P, _P, _P, c_int64, _P, _P, c_int32, c_int64,
+                                       c_float, c_float, _S]),
     "mlearn_returns_f32": (c_int32, [_P, _P, _P, _P, c_int32, c_int64, c_float, _S]),
     "mlearn_zscore_workspace_bytes": (c_int64, [c_int64]),
     "mlearn_zscore_f32": (c_int32, [_P, c_int64, _P, _P, _S]),
@@ -114,6 +116,9 @@ _SIGNATURES = {
                                         _S]),
     "mlearn_adv_stats": (c_int32, [POINTER(RolloutView), _P, c_int32, c_int32, _P, _S]),
     "mlearn_adv_stats_finish": (c_int32, [_P, c_int32, c_double, _P, _S]),
+    "mlearn_return_stats": (c_int32, [POINTER(RolloutView), _P, c_int32, c_int32, _P, _S]),
+    "mlearn_value_norm_chain": (c_int32, [_P, _P, c_int32, c_double, c_float, c_float, _P, _P, _P,
+                                          _S]),
     "mlearn_ppo_workspace_bytes": (c_int64, [POINTER(MlpPolicy), c_int64]),
     "mlearn_ppo_minibatch_grad": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
                                             c_int32, _P, POINTER(PPOHparams), _P, _P, _P, _S]),

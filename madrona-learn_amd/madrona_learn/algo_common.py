@@ -44,8 +44,11 @@ def _tn(x, T, N, dtype):
 
 
 def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=None,
-                       out_ret=None):
+                       out_ret=None, value_norm=None, norm_cols=0):
     """algo_common.py:84-130 (+ returns = adv + values, rollouts.py:761-769).
+    ``value_norm`` ([P, 8] f32 estimates, normalize_values): values and
+    bootstrap are normalised critic outputs, inverted first (rollouts.py:726-738);
+    column n uses estimate n // norm_cols.
 
     Returns (advantages, returns), both [T, N] f32."""
     T = cfg.steps_per_update
@@ -58,6 +61,12 @@ def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=No
     adv = out_adv if out_adv is not None else torch.empty((T, N), dtype=torch.float32,
                                                           device=r.device)
     ret = out_ret if out_ret is not None else torch.empty_like(adv)
+    if value_norm is not None:
+        nat.check(nat.lib().mlearn_gae_vnorm_f32(
+            nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b), nat.ptr(value_norm),
+            int(norm_cols or N), nat.ptr(adv), nat.ptr(ret), T, N, float(cfg.gamma),
+            float(cfg.gae_lambda), nat.stream_handle()), "gae_vnorm")
+        return adv, ret
     nat.check(nat.lib().mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b),
                                        nat.ptr(adv), nat.ptr(ret), T, N, float(cfg.gamma),
                                        float(cfg.gae_lambda), nat.stream_handle()), "gae")

@@ -87,8 +87,6 @@ class PPO(AlgoBase):  # ppo.py:49-106
             raise NotImplementedError(
                 "filter_advantages / importance_sample_trajectories (ppo.py:374-435) are "
                 "non-default modes outside the fused path")
-        if cfg.normalize_values:
-            raise NotImplementedError("value normalisation is SURVEY §8(f) row 2")
         C = cfg.num_bptt_chunks
         self.bptt = cfg.steps_per_update // C
         self.num_seq = C * view.N                     # per rank
@@ -142,6 +140,18 @@ class PPO(AlgoBase):  # ppo.py:49-106
         hp.clip_value_loss = 1 if algo.clip_value_loss else 0
         hp.huber_value_loss = 1 if algo.huber_value_loss else 0
         hp.loss_scale = 1.0 / dp.world_size
+        # value normaliser (normalize_values, ppo.py:190-211): the returns'
+        # per-minibatch sums join the advantage sums' collective; one chain
+        # launch per epoch turns them into per-minibatch estimate records
+        self.vnorm = bool(cfg.normalize_values)
+        hp.normalize_values = 1 if self.vnorm else 0
+        if self.vnorm:
+            self.vn_est = train_state.value_norm_est
+            self.vn_count = train_state.value_norm_count
+            self.vn_decay = float(cfg.value_normalizer_decay)
+            self.ret_part = torch.zeros_like(self.adv_part)
+            self.vn_rec = torch.zeros((self.E, self.num_mb, 8), dtype=torch.float32, device=dev)
+            self.adv_sums = torch.zeros((self.E, 4 * self.num_mb), dtype=torch.float64, device=dev)
         self.hp = hp
         self.dp = dp
         self.count = float(self.mb * dp.world_size * self.bptt)
@@ -157,31 +167,48 @@ class PPO(AlgoBase):  # ppo.py:49-106
                                               self.num_seq, nat.ptr(self.perm[e]), strm), "perm")
             nat.check(L.mlearn_adv_stats(self.view, nat.ptr(self.perm[e]), self.num_mb, self.mb,
                                          nat.ptr(self.adv_part[e]), strm), "adv_stats")
+            if self.vnorm:
+                nat.check(L.mlearn_return_stats(self.view, nat.ptr(self.perm[e]), self.num_mb,
+                                                self.mb, nat.ptr(self.ret_part[e]), strm),
+                          "return_stats")
+        n2 = 2 * self.num_mb
         if self.dp.world_size > 1:
-            # one collective for every epoch's per-minibatch advantage sums
+            # one collective for every epoch's per-minibatch advantage (and return) sums
             for e in range(self.E):
-                self.adv_sums[e].copy_(self.adv_part[e, :2 * self.num_mb])
+                self.adv_sums[e, :n2].copy_(self.adv_part[e, :n2])
+                if self.vnorm:
+                    self.adv_sums[e, n2:].copy_(self.ret_part[e, :n2])
             yield ("allreduce", self.adv_sums)
             for e in range(self.E):
-                self.adv_part[e, :2 * self.num_mb].copy_(self.adv_sums[e])
+                self.adv_part[e, :n2].copy_(self.adv_sums[e, :n2])
+                if self.vnorm:
+                    self.ret_part[e, :n2].copy_(self.adv_sums[e, n2:])
         for e in range(self.E):
             nat.check(L.mlearn_adv_stats_finish(nat.ptr(self.adv_part[e]), self.num_mb,
                                                 self.count, nat.ptr(self.adv_stats[e]), strm),
                       "adv_stats_finish")
+        if self.vnorm:
+            # the estimates move minibatch by minibatch, epochs in order (ppo.py:346)
+            for e in range(self.E):
+                nat.check(L.mlearn_value_norm_chain(
+                    nat.ptr(self.ret_part[e]), nat.ptr(self.adv_stats[e]), self.num_mb,
+                    self.count, self.vn_decay, 1e-5, nat.ptr(self.vn_est), nat.ptr(self.vn_count),
+                    nat.ptr(self.vn_rec[e]), strm), "value_norm_chain")
         loss_out = metrics.slots("Loss", 5, policy=self.policy_idx)
         for e in range(self.E):
             for m in range(self.num_mb):
                 seqs = self.perm[e, m * self.mb:(m + 1) * self.mb]
+                stats = self.vn_rec[e, m] if self.vnorm else self.adv_stats[e, m]
                 if self.lstm is not None:
                     nat.check(L.mlearn_lstm_ppo_minibatch_grad(
                         policy_state.desc, self.lstm, self.view, self.start_h, self.start_c,
-                        nat.ptr(seqs), self.mb, nat.ptr(self.adv_stats[e, m]), self.hp,
+                        nat.ptr(seqs), self.mb, nat.ptr(stats), self.hp,
                         nat.ptr(train_state.grads), nat.ptr(loss_out), nat.ptr(self.ws), strm),
                         "lstm_ppo_minibatch_grad")
                 else:
                     nat.check(L.mlearn_ppo_minibatch_grad(
                         policy_state.desc, self.view, nat.ptr(seqs), self.mb,
-                        nat.ptr(self.adv_stats[e, m]), self.hp, nat.ptr(train_state.grads),
+                        nat.ptr(stats), self.hp, nat.ptr(train_state.grads),
                         nat.ptr(loss_out), nat.ptr(self.ws), strm), "ppo_minibatch_grad")
                 if self.dp.world_size > 1:
                     yield ("allreduce", train_state.grads)

@@ -378,7 +378,8 @@ class RolloutManager:  # rollouts.py:373-826
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:
             compute_advantages(self.train_cfg, s.rewards, s.values, s.dones, s.bootstrap,
-                               out_adv=s.advantages, out_ret=s.returns)
+                               out_adv=s.advantages, out_ret=s.returns,
+                               value_norm=train_state_mgr.value_norm, norm_cols=self.B)
         else:
             compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s.returns)
         for p in range(self.P):

@@ -236,9 +236,19 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         pss.append(ps)
         tss.append(ts)
         algos.append(algo)
+    value_norm = None
+    if cfg.normalize_values:
+        # EMANormalizer.init_estimates per train policy (moving_avg.py:56-76,
+        # train_state.py:307-316): mu 0, inv_sigma 1, sigma 1, biased sums 0, N 0
+        value_norm = torch.zeros((len(tss), 8), dtype=torch.float32, device=device)
+        value_norm[:, 1] = 1.0
+        value_norm[:, 2] = 1.0
+        vcount = torch.zeros(len(tss), dtype=torch.int32, device=device)
+        for i, ts in enumerate(tss):
+            ts.value_norm_est, ts.value_norm_count = value_norm[i], vcount[i:i + 1]
     tsm = TrainStateManager(policy_states=pss[0] if len(pss) == 1 else pss,
                             train_states=tss[0] if len(tss) == 1 else tss, pbt_rng=None,
-                            user_state=user_hooks.init_user_state())
+                            user_state=user_hooks.init_user_state(), value_norm=value_norm)
     start = 0
     if restore_ckpt is not None:
         tsm, start = tsm.load(restore_ckpt)

@@ -377,6 +377,10 @@ class PolicyTrainState:
         else:
             nbytes = nat.lib().mlearn_optim_workspace_bytes(policy_state.desc)
         self.optim_ws = torch.zeros(max(nbytes, 16), dtype=torch.uint8, device=dev)
+        # value normaliser state (normalize_values; views into the manager's
+        # [P][8] estimates, set by init_training): train_state.py:86-116, 307-316
+        self.value_norm_est = None
+        self.value_norm_count = None
         o = nat.OptimState()
         o.params = policy_state.params.data_ptr()
         o.grads = self.grads.data_ptr()
@@ -402,12 +406,19 @@ class PolicyTrainState:
                   "optim_step")
 
     def state_dict(self):
-        return {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu()}
+        sd = {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu()}
+        if self.value_norm_est is not None:
+            sd["value_norm_est"] = self.value_norm_est.cpu()
+            sd["value_norm_count"] = self.value_norm_count.cpu()
+        return sd
 
     def load_state_dict(self, sd):
         self.adam_m.copy_(sd["adam_m"])
         self.adam_v.copy_(sd["adam_v"])
         self.step.copy_(sd["step"])
+        if self.value_norm_est is not None and "value_norm_est" in sd:
+            self.value_norm_est.copy_(sd["value_norm_est"])
+            self.value_norm_count.copy_(sd["value_norm_count"])
 
 
 @dataclass
@@ -420,6 +431,7 @@ class TrainStateManager:  # train_state.py:139-304
     train_states: Any
     pbt_rng: Any = None
     user_state: Any = None
+    value_norm: Any = None  # [P][8] f32 value-normaliser estimates (normalize_values)
 
     @property
     def policy_list(self):

@@ -400,6 +400,13 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
             "Value Errors": np.abs(twohot_mean(crit) - R), "Entropy": ent,
         }
         return loss, np.concatenate([dlog, dV], -1), metrics
+    # value normaliser (normalize_values, ppo.py:190-211): hp["value_norm"] =
+    # (mu', inv_sigma' after this minibatch's update, mu, sigma before it)
+    vn = hp.get("value_norm")
+    tgt = R
+    if vn is not None:
+        f = np.float32
+        tgt = ((np.asarray(batch["returns"], f) - f(vn[0])) * f(vn[1])).astype(ad)
     vpred, dvp = V, np.ones_like(V)
     if hp.get("clip_value_loss", False):
         ov = np.asarray(batch["values"], ad)
@@ -407,7 +414,7 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         vpred = np.minimum(yy, ov + clip)
         dvp = np.where(V > ov - clip, 1.0, np.where(V == ov - clip, 0.5, 0.0)) * \
             np.where(yy < ov + clip, 1.0, np.where(yy == ov + clip, 0.5, 0.0))
-    e = vpred - R
+    e = vpred - tgt
     if hp.get("huber_value_loss", False):
         ae = np.abs(e)
         quad = np.minimum(ae, 1.0)
@@ -419,8 +426,8 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
     dV = hp["value_loss_coef"] * inv_s * dvl * dvp * loss_scale
     loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
     metrics = {
-        "Loss": loss, "Action Obj": obj, "Value Loss": vl, "Value Errors": np.abs(V - R),
-        "Entropy": ent,
+        "Loss": loss, "Action Obj": obj, "Value Loss": vl,
+        "Value Errors": np.abs((V if vn is None else V * vn[3] + vn[2]) - R), "Entropy": ent,
     }
     return loss, np.concatenate([dlog, dV[:, None]], -1), metrics
 
@@ -564,7 +571,8 @@ def gather_minibatch(store, rows):
 
 
 def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs, minibatch_size,
-               bptt, key, epoch_base, mode="f64", lr, max_grad_norm, ad=np.float64):
+               bptt, key, epoch_base, mode="f64", lr, max_grad_norm, ad=np.float64,
+               value_norm=None, value_norm_decay=0.99999):
     """_ppo (ppo.py:366-488) for the default minibatch mode, over one or more
     data-parallel ranks (stores[r] = rank r's [T][N] store).  Each optimizer
     step uses the union of the ranks' minibatches: advantage statistics of the
@@ -585,10 +593,22 @@ def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs,
                 batches.append(gather_minibatch(stores[r], minibatch_rows(ids, N, bptt)))
             alladv = np.concatenate([np.asarray(b["advantages"], np.float64) for b in batches])
             stats = (alladv.mean(), alladv.var())
+            hp_mb = hp
+            if value_norm is not None:
+                # normalize_and_update_estimates on the union minibatch's returns
+                # (ppo.py:209-211; moving_avg.py:183-192), state carried (ppo.py:346)
+                allret = np.concatenate([np.asarray(b["returns"], np.float64) for b in batches])
+                z = np.zeros(1, np.float32)
+                new = ema_update_estimates(value_norm, ema_update_input_stats(
+                    (z, z), 0, allret[:, None]), value_norm_decay, 1e-5)
+                hp_mb = dict(hp, value_norm=(float(new["mu"][0]), float(new["inv_sigma"][0]),
+                                             float(value_norm["mu"][0]),
+                                             float(value_norm["sigma"][0])))
+                value_norm.update(new)
             P = unflatten(flat_p, lay, ad)
             gsum = None
             for b in batches:
-                loss, G, met, _ = ppo_loss_grads(P, b, hp, buckets, mode, adv_stats=stats,
+                loss, G, met, _ = ppo_loss_grads(P, b, hp_mb, buckets, mode, adv_stats=stats,
                                                  loss_scale=1.0 / world, ad=ad)
                 gf = flatten(G, lay)
                 gsum = gf if gsum is None else gsum + gf
@@ -612,6 +632,12 @@ def ema_init(D):
     z = np.zeros(D, np.float32)
     return {"mu": z.copy(), "inv_sigma": np.ones(D, np.float32), "sigma": np.ones(D, np.float32),
             "mu_biased": z.copy(), "sigma_sq_biased": z.copy(), "N": 0}
+
+
+def ema_invert(est, x):
+    """EMANormalizer.invert (moving_avg.py:87-95) in f32: x * sigma + mu."""
+    f = np.float32
+    return (np.asarray(x, f) * est["sigma"].astype(f) + est["mu"].astype(f)).astype(f)
 
 
 def ema_normalize(est, x, mode):

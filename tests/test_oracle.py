@@ -317,3 +317,36 @@ def test_ema_normalizer_closed_forms():
     np.testing.assert_allclose(e["inv_sigma"], 1 / np.sqrt(1e-5), rtol=1e-6)
     y = ref.ema_normalize(e, np.full((2, 1), 3.0, np.float32), "f32")
     np.testing.assert_allclose(y, 0.0, atol=1e-3)
+
+
+# ---------------------------------------------------------------------------
+# Value normaliser (normalize_values, ppo.py:190-211): closed forms
+# ---------------------------------------------------------------------------
+def test_value_normaliser_first_update_and_loss_target():
+    """The first update's estimates are the minibatch's own mean / population
+    variance (bias correction, moving_avg.py:163-167); the value target is the
+    return normalised with the updated estimates and the value error inverts
+    the critic with the previous ones (ppo.py:190-211)."""
+    rng = np.random.default_rng(7)
+    M, buckets = 64, [4, 8, 5, 5, 2, 2]
+    R = (rng.standard_normal(M) * 3 + 2).astype(np.float32)
+    z = np.zeros(1, np.float32)
+    est = ref.ema_init(1)
+    new = ref.ema_update_estimates(est, ref.ema_update_input_stats((z, z), 0, R[:, None]),
+                                   0.99999, 1e-5)
+    np.testing.assert_allclose(new["mu"][0], R.astype(np.float64).mean(), rtol=1e-4)
+    np.testing.assert_allclose(new["sigma"][0] ** 2, R.astype(np.float64).var(), rtol=1e-3)
+    assert new["N"] == 1
+    # invert is the inverse of normalize
+    x = rng.standard_normal(5).astype(np.float32)
+    np.testing.assert_allclose(ref.ema_invert(new, ref.ema_normalize(new, x, "f32")), x,
+                               rtol=1e-5, atol=1e-5)
+    V = rng.standard_normal(M)
+    batch = {"actions": np.zeros((M, 6), np.int32), "log_probs": np.zeros((M, 6)),
+             "advantages": rng.standard_normal(M), "returns": R, "values": np.zeros(M)}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "value_norm": (new["mu"][0], new["inv_sigma"][0], 0.5, 2.0)}
+    _, dhead, met = ref.ppo_loss_dhead(np.zeros((M, 26)), V, batch, hp, buckets)
+    tgt = (R - np.float32(new["mu"][0])) * np.float32(new["inv_sigma"][0])
+    np.testing.assert_allclose(dhead[:, -1], 0.5 / M * (V - tgt), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(met["Value Errors"], np.abs(V * 2.0 + 0.5 - R), rtol=1e-12)
