@@ -1,20 +1,25 @@
-// Persistent LSTM scans of the recurrent PPO update (LSTM.sequence,
-// rnn.py:81-111, and its reverse for BPTT): ONE launch per direction per
-// minibatch instead of one per time step.  Textually included by ppo.hip
-// inside namespace ml (uses its RolloutK / LstmWsK / store_row).
+// LSTM kernels of the recurrent PPO update (LSTM.sequence, rnn.py:81-111,
+// and its reverse for BPTT).  Textually included by ppo.hip inside namespace
+// ml (uses its RolloutK / LstmWsK / store_row).
 //
-// A workgroup owns 32 sequences of the minibatch for the whole chunk and has
-// H/32 waves; wave w owns unit block w (units 32w .. 32w+31), i.e. the four
-// gate blocks (i, f, g, o) of those units (weight images in unit-block gate
-// order), so the cell update is register-local:
-//   - forward: the c carry stays in the lanes' registers (accumulator order);
-//     the h carry and the next step's trunk features are exchanged between
-//     the waves as B fragments in LDS (one barrier pair per step);
-//   - backward: the c cotangent stays in registers; dG_t of the 32 rows is
-//     exchanged in LDS; each wave computes its d-feature block and its h
-//     cotangent block of [dF_{t+1} ; dh_t] = dG_{t+1} [Wi ; Wh]^T, then the
-//     cell backward of step t for its units.
-// Weights stream from L2 every step (every workgroup reads the same image).
+// The products that do not depend on the recurrence run as full-grid
+// launches over all minibatch rows, so only the hidden-to-hidden product is
+// left inside the sequential scans:
+//   lstm_gin_kernel       Gin = F Wi for every row (f32, accumulator order)
+//   lstm_fwd_scan_kernel  gates_t = Gin_t + h Wh + bias -> cell, per step
+//   lstm_bwd_scan_kernel  dh_t = dG_{t+1} Wh^T -> cell backward, per step
+//   lstm_dfeat_kernel     dF = dG Wi^T for every row
+// The split keeps the f32 accumulation order of the fused product (the
+// F k-steps, then the h k-steps, in one accumulator), so the gates are
+// bit-identical to computing both products in the scan.
+//
+// A scan workgroup owns 32 sequences of the minibatch for the whole chunk
+// and has H/32 waves; wave w owns unit block w (units 32w .. 32w+31), i.e.
+// the four gate blocks (i, f, g, o) of those units (weight images in
+// unit-block gate order), so the cell update is register-local: the c carry
+// (forward) and its cotangent (backward) stay in the lanes' registers, the h
+// carry / dG_t rows are exchanged between the waves as B fragments in LDS
+// (one barrier pair per step).  The Wh image streams from L2 every step.
 #pragma once
 
 // Natural-order B fragments in LDS (fr[s * 64 + lane], the layout RT<T>::row
@@ -59,20 +64,57 @@ template <typename T, int NKS, int NT> struct RowStage {
 
 template <int H> constexpr int scan_threads() { return 2 * H; }  // H/32 waves
 
-// Forward scan over the chunk: gates_t = F_t Wi + h Wh + bias -> cell ->
+// Gin in accumulator order: for row tile (32 rows) and unit block w, 16
+// chunks of 64 float4 (chunk c = 4 * gate + register quad, lane-contiguous),
+// i.e. every wave-instruction moves one contiguous KiB.
+__device__ inline int64_t gin_base(int64_t tile, int nw, int w) {
+    return (tile * nw + w) * 16 * 64;
+}
+
+// Gin = F Wi over every row of the minibatch (one 32-row tile per workgroup).
+template <typename T, int H>
+__global__ __launch_bounds__(scan_threads<H>()) void lstm_gin_kernel(LstmK R,
+                                                                    const T* __restrict__ feat,
+                                                                    float4* __restrict__ gin) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NT = scan_threads<H>(), NW = H / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frf = (frag*)smem;  // [KSH][64]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tile = blockIdx.x;
+    {
+        RowStage<T, KSH, NT> st;
+        st.load([&](int i) { return feat + (tile * 32 + i) * H; }, tid);
+        st.put(frf, tid);
+    }
+    __syncthreads();
+    f32x16 acc[4];
+    zero_acc<4>(acc);
+    gemm_lds<T, 4, KSH, 6>(acc, frf, (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
+    float4* o = gin + gin_base(tile, NW, w) + lane;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            o[(4 * g + c) * 64] =
+                make_float4(acc[g][4 * c], acc[g][4 * c + 1], acc[g][4 * c + 2], acc[g][4 * c + 3]);
+}
+
+// Forward scan over the chunk: gates_t = Gin_t + h Wh + bias -> cell ->
 // gates / c_t / h_t saved for the backward, carries into t + 1 cleared where
 // dones[t] (rnn.py:92-96); the carry-in rows (hin / cin) are written for the
 // weight gradient and the backward.  Step 0 starts from the sequences'
 // rnn_start_states [C][ld][H] (rollouts.py:533-537).
 template <typename T, int H>
 __global__ __launch_bounds__(scan_threads<H>()) void lstm_fwd_scan_kernel(
-    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, const T* __restrict__ feat,
-    const T* __restrict__ sh, const T* __restrict__ sc, LstmWsK lw) {
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
+    const float4* __restrict__ gin, const T* __restrict__ sh, const T* __restrict__ sc,
+    LstmWsK lw) {
     typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NT = scan_threads<H>();
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NT = scan_threads<H>(), NW = H / 32;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    frag* frf = (frag*)smem;     // [KSH][64] trunk features F_t of the 32 rows
-    frag* frh = frf + KSH * 64;  // [KSH][64] h carry into step t
+    frag* frh = (frag*)smem;  // [KSH][64] h carry into step t
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0 = blockIdx.x * 32;
@@ -97,21 +139,28 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_fwd_scan_kernel(
         RowStage<T, KSH, NT> st;
         st.load([&](int i) { return sh + start_row(i); }, tid);
         st.put(frh, tid);
-        st.load([&](int i) { return feat + (int64_t)(m0 + i) * H; }, tid);
-        st.put(frf, tid);
     }
     __syncthreads();
-    const T* wi = (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E;
     const T* wh = (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E;
     for (int t = 0; t < bptt; ++t) {
         const int64_t f = (int64_t)t * mb + m0 + r;
         const bool more = t + 1 < bptt;
-        RowStage<T, KSH, NT> nf;  // F_{t+1}, in flight during this step's product
-        if (more) nf.load([&](int i) { return feat + ((int64_t)(t + 1) * mb + m0 + i) * H; }, tid);
         const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
         f32x16 acc[4];
-        zero_acc<4>(acc);
-        gemm_lds2<T, 4, KSH, 6>(acc, frf, wi, frh, wh, lane);
+        {
+            const float4* gi = gin + gin_base((int64_t)t * (mb / 32) + blockIdx.x, NW, w) + lane;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 x = gi[(4 * g + c) * 64];
+                    acc[g][4 * c] = x.x;
+                    acc[g][4 * c + 1] = x.y;
+                    acc[g][4 * c + 2] = x.z;
+                    acc[g][4 * c + 3] = x.w;
+                }
+        }
+        gemm_lds<T, 4, KSH, 8>(acc, frh, wh, lane);
         T* gts = (T*)lw.gates + f * 4 * H;
         const float keep = done ? 0.f : 1.f;
         float hc[16];
@@ -148,8 +197,7 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_fwd_scan_kernel(
             }
         }
         if (!more) break;
-        __syncthreads();  // every wave's product has read F_t and h_t
-        nf.put(frf, tid);
+        __syncthreads();  // every wave's product has read h_t
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             LdsRow<T>::put4(frh, w * 32 + 8 * j + 4 * h, r, hc[4 * j], hc[4 * j + 1], hc[4 * j + 2],
@@ -158,12 +206,12 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_fwd_scan_kernel(
     }
 }
 
-// Reverse scan.  Step t (from bptt-1 down to 0): [dF_{t+1} ; dh_t] =
-// dG_{t+1} [Wi ; Wh]^T (w_bwd blocks w and H/32 + w, K = 4H from LDS), then
-// the cell backward of step t for unit block w: dh = dHout_t + dh_t and the
-// c cotangent, both cut where the carry out of step t was cleared (dones[t])
-// or at the end of the chunk; writes dG_t (rounded to the compute dtype),
-// dF_{t+1}, and the per-tile column partials of dG (the bias gradient).
+// Reverse scan.  Step t (from bptt-1 down to 0): dh_t = dG_{t+1} Wh^T (w_bwd
+// block H/32 + w, K = 4H from LDS), then the cell backward of step t for unit
+// block w: dh = dHout_t + dh_t and the c cotangent, both cut where the carry
+// out of step t was cleared (dones[t]) or at the end of the chunk; writes
+// dG_t (rounded to the compute dtype) and the per-tile column partials of dG
+// (the bias gradient).  dF = dG Wi^T follows as lstm_dfeat_kernel.
 template <typename T, int H>
 __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
     LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
@@ -176,25 +224,16 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0 = blockIdx.x * 32, m = m0 + r;
     const int bptt = ro.bptt;
-    const T* wdf = (const T*)R.w_bwd + (int64_t)w * NKS * 64 * E;  // d-feature block w
-    auto store_df = [&](const f32x16& a, int64_t f) {
-        T* drow = (T*)lw.dfeat + f * H + w * 32;
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            store4(drow + 8 * g + 4 * h, a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
-    };
+    const T* wdh = (const T*)R.w_bwd + (int64_t)(NU + w) * NKS * 64 * E;  // h-cotangent block w
     float dcc[16];  // c cotangent carried from step t + 1 into t
 #pragma unroll
     for (int q = 0; q < 16; ++q) dcc[q] = 0.f;
     for (int t = bptt - 1; t >= 0; --t) {
         const int64_t fs = (int64_t)t * mb + m;
         const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
-        f32x16 acc[2];
-        zero_acc<2>(acc);
-        if (t + 1 < bptt) {
-            gemm_lds<T, 2, NKS, 8>(acc, frg, wdf, lane, NU * NKS);
-            store_df(acc[0], fs + mb);
-        }
+        f32x16 acc[1];
+        zero_acc<1>(acc);
+        if (t + 1 < bptt) gemm_lds<T, 1, NKS, 8>(acc, frg, wdh, lane);
         const T* gts = (const T*)lw.gates + fs * 4 * H;
         T* dgs = (T*)lw.dg + fs * 4 * H;
         float dpi[16], dpf[16], dpg[16], dpo[16];
@@ -210,7 +249,7 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
             for (int e = 0; e < 4; ++e) {
                 const int q = 4 * j + e;
                 const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
-                const float dh = f4get(dho, e) + (cut ? 0.f : acc[1][q]);
+                const float dh = f4get(dho, e) + (cut ? 0.f : acc[0][q]);
                 const float tc = tanhf(f4get(c4, e));
                 const float dout = dh * tc;
                 const float dc = (cut ? 0.f : dcc[q]) + dh * o_ * (1.f - tc * tc);
@@ -225,17 +264,20 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
             store4(dgs + 2 * H + u0, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2], dpg[4 * j + 3]);
             store4(dgs + 3 * H + u0, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2], dpo[4 * j + 3]);
         }
-        __syncthreads();  // every wave's product has read dG_{t+1}
+        if (t > 0) {
+            __syncthreads();  // every wave's product has read dG_{t+1}
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k0 = w * 32 + 8 * j + 4 * h;
-            LdsRow<T>::put4(frg, k0, r, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
-            LdsRow<T>::put4(frg, H + k0, r, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2],
-                            dpf[4 * j + 3]);
-            LdsRow<T>::put4(frg, 2 * H + k0, r, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2],
-                            dpg[4 * j + 3]);
-            LdsRow<T>::put4(frg, 3 * H + k0, r, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2],
-                            dpo[4 * j + 3]);
+            for (int j = 0; j < 4; ++j) {
+                const int k0 = w * 32 + 8 * j + 4 * h;
+                LdsRow<T>::put4(frg, k0, r, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2],
+                                dpi[4 * j + 3]);
+                LdsRow<T>::put4(frg, H + k0, r, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2],
+                                dpf[4 * j + 3]);
+                LdsRow<T>::put4(frg, 2 * H + k0, r, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2],
+                                dpg[4 * j + 3]);
+                LdsRow<T>::put4(frg, 3 * H + k0, r, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2],
+                                dpo[4 * j + 3]);
+            }
         }
         // bias gradient: column sums of dG over this tile's 32 rows
         {
@@ -251,11 +293,33 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
                 cp[3 * H + uq] = so;
             }
         }
-        __syncthreads();
+        if (t > 0) __syncthreads();
     }
-    // d features of step 0
+}
+
+// dF = dG Wi^T over every row of the minibatch (w_bwd blocks 0 .. H/32-1,
+// one 32-feature block per wave), rounded to the compute dtype.
+template <typename T, int H>
+__global__ __launch_bounds__(scan_threads<H>()) void lstm_dfeat_kernel(LstmK R, LstmWsK lw) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NT = scan_threads<H>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* frg = (frag*)smem;  // [NKS][64] dG rows of the tile
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tile = blockIdx.x;
+    {
+        RowStage<T, NKS, NT> st;
+        st.load([&](int i) { return (const T*)lw.dg + (tile * 32 + i) * 4 * H; }, tid);
+        st.put(frg, tid);
+    }
+    __syncthreads();
     f32x16 acc[1];
     zero_acc<1>(acc);
-    gemm_lds<T, 1, NKS, 8>(acc, frg, wdf, lane);
-    store_df(acc[0], m);
+    gemm_lds<T, 1, NKS, 8>(acc, frg, (const T*)R.w_bwd + (int64_t)w * NKS * 64 * E, lane);
+    T* drow = (T*)lw.dfeat + (tile * 32 + (lane & 31)) * H + w * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+        store4(drow + 8 * g + 4 * h, acc[0][4 * g], acc[0][4 * g + 1], acc[0][4 * g + 2],
+               acc[0][4 * g + 3]);
 }

@@ -68,7 +68,7 @@ struct LstmWsK {
     void* dg;     // [Mp][4H] d loss / d gate pre-activations
     void* dhout;  // [Mp][H]  d loss / d h_t from the heads
     void* dfeat;  // [Mp][H]  d loss / d trunk output
-    float* dcc;   // [mb][H]  f32 cotangent of the c carry
+    void* gin;    // [Mp/32][H/32][16][64] float4: F Wi in accumulator order (lstm_gin_kernel)
 };
 
 struct WsK {
@@ -167,7 +167,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         lw.dg = take(Mp * 4 * H * es);
         lw.dhout = take(Mp * H * es);
         lw.dfeat = take(Mp * H * es);
-        lw.dcc = (float*)take(mb * H * sizeof(float));
+        lw.gin = take(Mp * 4 * H * sizeof(float));
         if (LW) *LW = lw;
     }
     if (W) *W = w;
@@ -1397,9 +1397,24 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // trunk forward over every row (the LSTM input F = A_{L-1})
     step(std::integral_constant<int, kTrunkFwd>{});
     const T* feat = (const T*)ws.a[L - 1];
+    constexpr int KSH = H / RT<T>::KS, NKS = 4 * H / RT<T>::KS;
+    constexpr size_t FR = sizeof(typename RT<T>::frag);
+    // hoisted input product Gin = F Wi over every row (full grid)
     {
-        constexpr int KSH = H / RT<T>::KS;
-        const size_t lds = 2 * (size_t)KSH * 64 * sizeof(typename RT<T>::frag);
+        const size_t lds = (size_t)KSH * 64 * FR;
+        auto k = lstm_gin_kernel<T, H>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, feat,
+                           (float4*)lw.gin);
+    }
+    // forward scan: one persistent launch (a workgroup per 32 sequences)
+    {
+        const size_t lds = (size_t)KSH * 64 * FR;
         auto k = lstm_fwd_scan_kernel<T, H>;
         static bool attr_set = false;
         if (!attr_set) {
@@ -1408,7 +1423,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
             attr_set = true;
         }
         hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb,
-                           feat, (const T*)start_h, (const T*)start_c, lw);
+                           (const float4*)lw.gin, (const T*)start_h, (const T*)start_c, lw);
     }
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});
@@ -1425,6 +1440,18 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         }
         hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb, lw,
                            ws.colpart, ws.CP, cp0);
+    }
+    // hoisted d-feature product dF = dG Wi^T over every row (full grid)
+    {
+        const size_t lds = (size_t)NKS * 64 * FR;
+        auto k = lstm_dfeat_kernel<T, H>;
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, lw);
     }
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});
