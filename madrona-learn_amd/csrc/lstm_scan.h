@@ -250,7 +250,7 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_bwd_scan_kernel(
                 const int q = 4 * j + e;
                 const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
                 const float dh = f4get(dho, e) + (cut ? 0.f : acc[0][q]);
-                const float tc = tanhf(f4get(c4, e));
+                const float tc = tanh_fast(f4get(c4, e));
                 const float dout = dh * tc;
                 const float dc = (cut ? 0.f : dcc[q]) + dh * o_ * (1.f - tc * tc);
                 dpi[q] = rnd<T>((dc * g_) * i_ * (1.f - i_));

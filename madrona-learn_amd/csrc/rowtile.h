@@ -445,7 +445,19 @@ __device__ inline float f4get(const float4& v, int j) {
     return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
 
-__device__ inline float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Gate activations on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32,
+// ~1 ulp each) instead of IEEE division and libm tanhf: the cell is the
+// VALU-heaviest part of the LSTM scans (rocprofv3 PMC: 32 VALU per MFMA in
+// the forward scan with libm tanhf).  Both saturate correctly (exp -> inf
+// gives rcp -> 0).  tanh uses its odd Taylor series below |x| < 1/8, where
+// 1 - 2 / (1 + e^2x) would cancel.
+__device__ inline float sigmoidf(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ inline float tanh_fast(float x) {
+    const float x2 = x * x;
+    const float series = x * (1.0f + x2 * (-1.0f / 3 + x2 * (2.0f / 15 + x2 * (-17.0f / 315))));
+    const float big = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x));
+    return fabsf(x) < 0.125f ? series : big;
+}
 
 // flax OptimizedLSTMCell step (rnn.py:28-41) on one (row, unit) from the
 // f32 gate pre-activations (x.Wi + h.Wh + bias): gate activations, c' and h'
@@ -458,10 +470,10 @@ __device__ inline CellOut lstm_cell_fwd(float pi, float pf, float pg, float po, 
     CellOut r;
     r.i = rnd<T>(sigmoidf(pi));
     r.f = rnd<T>(sigmoidf(pf));
-    r.g = rnd<T>(tanhf(pg));
+    r.g = rnd<T>(tanh_fast(pg));
     r.o = rnd<T>(sigmoidf(po));
     r.c = rnd<T>(r.f * cin + r.i * r.g);
-    r.h = rnd<T>(r.o * tanhf(r.c));
+    r.h = rnd<T>(r.o * tanh_fast(r.c));
     return r;
 }
 
