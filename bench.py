@@ -1,18 +1,22 @@
 """Benchmark: env-steps/s of the full batched-PPO iteration on MI355X.
 
-Workload (BASELINE.json configs[1], per GPU): 8192 envs, T=32, obs 64,
+Default workload = BASELINE.json's metric: 65,536-env PPO (T=32, obs 64,
 MLP[256,256] BackboneShared + discrete head [4,8,5,5,2,2] + scalar critic,
-bf16 compute, PPO 2 epochs x 4 minibatches of 2048 sequences, synthetic
-dummy vec-env (HIP kernel).  One "step" = one full update_iter (32 rollout
-steps + bootstrap + GAE + 8 minibatch optimizer steps), captured in HIP
-graphs.  Multi-GPU (torch.distributed.run): each rank owns 8192 envs (weak
-scaling), RCCL all-reduce of the advantage statistics and gradients.
+bf16 compute), PPO 2 epochs x 32 minibatches of 2048 sequences (global
+minibatch), synthetic dummy vec-env (HIP kernel).  One
+"step" = one full update_iter (32 rollout steps + bootstrap + GAE + 64
+minibatch optimizer steps), captured in HIP graphs.  Strong scaling: the
+65,536 envs and the global minibatch are split over the ranks
+(torch.distributed.run, one process per GPU): each rank owns 65536/W envs
+and 2048/W sequences of every minibatch, RCCL all-reduce of the advantage
+statistics and of every minibatch gradient.
 
-Other BASELINE.json configs (not the default line): ``--config lstm`` =
-configs[3] (the same workload with RecurrentBackboneEncoder(MLP[256,256],
-LSTM(256)), ``--bptt-chunks`` C in {1, 2}); ``--config pbt`` = configs[4]
-(8 train policies x 8192 envs, self-play split, placed over the ranks: one
-policy per GPU at 8 GPUs, all 8 on one GPU at N = 1).
+Other BASELINE.json configs (secondary lines, ``--config``): ``b1`` =
+configs[1] (8192 envs, 4 minibatches of 2048 seqs per epoch); ``lstm`` =
+configs[3] (b1 with RecurrentBackboneEncoder(MLP[256,256], LSTM(256)),
+``--bptt-chunks`` C in {1, 2}); ``pbt`` = configs[4] (8 train policies x
+8192 envs, self-play split, placed over the ranks: one policy per GPU at 8
+GPUs, all 8 on one GPU at N = 1).
 
 Prints ONE JSON line on rank 0.
 """
@@ -33,39 +37,45 @@ import torch
 import torch.distributed as dist
 
 BUCKETS = [4, 8, 5, 5, 2, 2]
-N_ENVS, T, OBS, HID, LAYERS = 8192, 32, 64, 256, 2
-EPOCHS, MB = 2, 2048
+T, OBS, HID, LAYERS = 32, 64, 256, 2
+EPOCHS, MB = 2, 2048      # global minibatch (sequences) of every config
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFS = 2500.0    # dense bf16 MFMA spec
 FWD_FLOP = 2 * (OBS * HID + HID * HID + HID * (sum(BUCKETS) + 1))  # 177,664 per sample
-
-
 PBT_POLICIES = 8
+# total envs of the job (fixed as the GPU count grows: strong scaling)
+TOTAL_ENVS = {"headline": 65536, "b1": 8192, "lstm": 8192, "pbt": 8192 * PBT_POLICIES}
+# the CPU baseline runs the oracle on a B1-sized shard (same work per env-step)
+N_B1 = 8192
 
 
 def envs_per_rank(config, world):
-    if config == "pbt":
-        if PBT_POLICIES % world != 0:
-            raise SystemExit(f"--config pbt places {PBT_POLICIES} policies: world must divide it")
-        return N_ENVS * (PBT_POLICIES // world)
-    return N_ENVS
+    total = TOTAL_ENVS[config]
+    if config == "pbt" and PBT_POLICIES % world != 0 and world % PBT_POLICIES != 0:
+        raise SystemExit(f"--config pbt places {PBT_POLICIES} policies: world must divide it")
+    if total % world != 0:
+        raise SystemExit(f"{total} envs do not split over {world} ranks")
+    return total // world
 
 
-def make(dev, dtype=torch.bfloat16, N=N_ENVS, env_offset=0, use_graph=True, config="b1",
-         chunks=1, critic="scalar"):
+def make(dev, total_envs, env_offset, n_local, dtype=torch.bfloat16, use_graph=True,
+         config="headline", chunks=1, critic="scalar"):
+    """init_training on this rank: the config is GLOBAL (num_worlds =
+    total_envs, minibatch_size = MB sequences); the sim plugin serves this
+    rank's shard of n_local envs starting at env_offset."""
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     from madrona_learn.models import (MLP, DenseLayerCritic, DenseLayerDiscreteActor,
                                       DreamerV3Critic)
     from madrona_learn.rnn import LSTM
-    env = DummyVecEnv(N, OBS, len(BUCKETS), seed=0, env_offset=env_offset, device=dev)
+    env = DummyVecEnv(n_local, OBS, len(BUCKETS), seed=0, env_offset=env_offset, device=dev)
     pbt = None
     if config == "pbt":
         pbt = ml.PBTConfig(num_teams=1, team_size=1, num_train_policies=PBT_POLICIES,
                            num_past_policies=0, self_play_portion=1.0, cross_play_portion=0.0,
                            past_play_portion=0.0)
     cfg = ml.TrainConfig(
-        num_worlds=N, num_agents_per_world=1, num_updates=1,
+        num_worlds=total_envs, num_agents_per_world=1, num_updates=1,
         actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T, lr=3e-4,
         algo=ml.PPOConfig(num_epochs=EPOCHS, minibatch_size=MB, clip_coef=0.2,
                           value_loss_coef=0.5, entropy_coef={"actions": 0.01},
@@ -115,23 +125,29 @@ def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
     return fwd, bwd_dx, wgrad
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_r01.json, tools/pmc_traffic.py): FETCH_SIZE doubled (gfx950
-    reports half the bytes of 16-B streaming reads, MI355X_MICROARCH.md HBM)
-    + WRITE_SIZE.  None when no summary is committed."""
-    path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
+    of this round (profiles/pmc_r02.json, tools/pmc_traffic.py): FETCH_SIZE
+    doubled (gfx950 reports half the bytes of 16-B streaming reads,
+    MI355X_MICROARCH.md HBM) + WRITE_SIZE, with the profiled kernel's name.
+    (None, None) when no summary is committed."""
+    if not os.path.exists(PMC_FILE):
+        return None, None
+    with open(PMC_FILE) as f:
         d = json.load(f)
     k = d.get("kernels", {}).get(kernel_key)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+    if k is None:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), k.get("kernel_name")
 
 
-def kernel_rooflines(mgr, dev, iters=20):
+def kernel_rooflines(mgr, dev, n_local, iters=20):
     """Dominant kernel (the fused PPO minibatch fwd/loss/bwd step) plus the
-    rollout policy step and GAE, each timed live with HIP events."""
+    rollout policy step and GAE, each timed live with HIP events on the
+    stream the kernel is launched on."""
     from madrona_learn import _native as nat
     L = nat.lib()
     algo = mgr.algo
@@ -149,17 +165,21 @@ def kernel_rooflines(mgr, dev, iters=20):
     fwd, bwd, _ = flop_per_sample(A1=ps.arch.num_logits + ps.arch.critic_bins)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
+    traffic, pmc_name = pmc_traffic("ppo_step")
     roof = {
-        "kernel": "ppo_step_kernel<bf16,256,2> (mlearn_ppo_minibatch_fwd_bwd)",
+        "kernel": "ppo_step_kernel<bf16,256,2,0,32> (mlearn_ppo_minibatch_fwd_bwd)",
         "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
-        "frac": achieved / BF16_PEAK_TFS, "traffic": pmc_traffic("ppo_step"),
+        "frac": achieved / BF16_PEAK_TFS, "traffic": traffic,
+        "traffic_source": (f"profiles/pmc_r02.json ({pmc_name})" if traffic is not None
+                           else None),
         "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
         "units_per_launch": M, "flop_per_unit": fwd + bwd,
+        "algorithmic_bytes_per_launch": 184 * M,
     }
 
-    # rollout policy step (forward + sample), N = 8192 envs
+    # rollout policy step (forward + sample) over this rank's envs
     s = mgr.rollout_mgr.store
-    obs = torch.randn((N_ENVS, OBS), device=dev)
+    obs = torch.randn((n_local, OBS), device=dev)
     ctr = torch.zeros(4, dtype=torch.int64, device=dev)
 
     def pol():
@@ -167,18 +187,19 @@ def kernel_rooflines(mgr, dev, iters=20):
                         ctr[0:1], 0)
 
     t_pol = time_call(pol, iters, torch.cuda.current_stream())
-    pol_flop = fwd * N_ENVS
-    extra = {"policy_step": {"bound": "mfma", "avg_launch_us": t_pol * 1e6,
+    pol_flop = fwd * n_local
+    extra = {"policy_step": {"bound": "mfma", "envs": n_local, "avg_launch_us": t_pol * 1e6,
                              "achieved": pol_flop / t_pol / 1e12, "unit": "TFLOP/s",
                              "frac": pol_flop / t_pol / 1e12 / BF16_PEAK_TFS}}
-    sec, rd, wr = gae_roofline(dev, N_ENVS)
-    big_sec, big_rd, big_wr = gae_roofline(dev, 1 << 22, iters=20)
-    extra["gae"] = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                    "operating_point": {"N": N_ENVS, "avg_launch_us": sec * 1e6,
-                                        "achieved": (rd + wr) / sec / 1e9},
-                    "sweep_point": {"N": 1 << 22, "avg_launch_us": big_sec * 1e6,
-                                    "achieved": (big_rd + big_wr) / big_sec / 1e9,
-                                    "frac": (big_rd + big_wr) / big_sec / 1e9 / HBM_PEAK_GBS}}
+    gae = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "bytes_per_env": {"read": T * 9 + 4, "write": T * 8}}
+    for name, n in (("operating_point", n_local), ("sweep_point", 1 << 22)):
+        sec, rd, wr = gae_roofline(dev, n, iters=50 if n < (1 << 20) else 20)
+        gae[name] = {"N": n, "avg_launch_us": sec * 1e6,
+                     "achieved_read": rd / sec / 1e9, "achieved_read_write": (rd + wr) / sec / 1e9,
+                     "frac_read": rd / sec / 1e9 / HBM_PEAK_GBS,
+                     "frac_read_write": (rd + wr) / sec / 1e9 / HBM_PEAK_GBS}
+    extra["gae"] = gae
     return roof, extra
 
 
@@ -205,12 +226,15 @@ def gae_roofline(dev, N, iters=50):
 
 def cpu_baseline(iters=2):
     """The oracle restatement (NumPy fp32 arithmetic, host BLAS threads) of
-    `iters` full B1 PPO iterations: 8192 envs x T=32 rollout with the
-    synthetic env, GAE, 2 epochs x 4 minibatches of 2048 sequences (~10-30 s
-    of CPU work on the GPU box's host)."""
+    `iters` full PPO iterations on an 8192-env shard of the workload: 8192
+    envs x T=32 rollout with the synthetic env, GAE, 2 epochs over every
+    sequence in minibatches of 2048 sequences (~10-30 s of CPU work on the
+    GPU box's host).  The work per env-step (one policy forward in the
+    rollout, two forward+backward passes in the update) is the same as in
+    the 65,536-env workload, so env-steps/s compare directly."""
     from oracle import native as onat
     from oracle import ppo_ref as ref
-    n_env = N_ENVS
+    n_env = N_B1
     mb = MB
     lay = ref.param_layout(OBS, HID, LAYERS, sum(BUCKETS))
     rng = np.random.default_rng(0)
@@ -244,8 +268,10 @@ def cpu_baseline(iters=2):
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": threads,
             "kind": "port",
-            "sample": f"{iters} full B1 PPO iterations ({n_env} envs x T={T}, 2 epochs x 4 "
-                      f"minibatches of {mb} seqs), NumPy fp32 oracle restatement, {sec:.1f} s"}
+            "sample": f"{iters} full PPO iterations on a {n_env}-env shard ({n_env} envs x "
+                      f"T={T}, 2 epochs x {n_env // mb} minibatches of {mb} seqs; same work per "
+                      f"env-step as the 65536-env workload), NumPy fp32 oracle restatement, "
+                      f"{sec:.1f} s"}
 
 
 def main():
@@ -256,7 +282,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--config", choices=["b1", "lstm", "pbt"], default="b1")
+    ap.add_argument("--config", choices=["headline", "b1", "lstm", "pbt"], default="headline")
     ap.add_argument("--bptt-chunks", type=int, default=1)
     ap.add_argument("--critic", choices=["scalar", "twohot"], default="scalar",
                     help="DenseLayerCritic (SURVEY B1) or DreamerV3Critic (63-bin two-hot)")
@@ -280,8 +306,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    total = TOTAL_ENVS[args.config]
     n_rank = envs_per_rank(args.config, world)
-    mgr = make(dev, N=n_rank, env_offset=rank * n_rank, use_graph=not args.no_graph,
+    mgr = make(dev, total, rank * n_rank, n_rank, use_graph=not args.no_graph,
                config=args.config, chunks=args.bptt_chunks, critic=args.critic)
     for _ in range(args.warmup):
         mgr.update_iter()
@@ -301,35 +328,42 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_steps = n_rank * world * T * args.steps
+    total_steps = total * T * args.steps
     value = total_steps / elapsed
     ms = elapsed / args.steps * 1e3
 
     result = None
     if rank == 0:
+        npol = PBT_POLICIES if args.config == "pbt" else 1
+        nmb = total // npol // MB * args.bptt_chunks
         workload = {
-            "b1": "B1: PPO iteration, 8192 envs/GPU, T=32, obs=64, MLP[256,256], heads "
-                  "[4,8,5,5,2,2]+critic, 2 epochs x 4 minibatches of 2048 seqs",
+            "headline": f"65536-env PPO iteration (BASELINE metric; SURVEY B8 semantics): T=32, "
+                        f"obs=64, MLP[256,256], heads [4,8,5,5,2,2]+critic, 2 epochs x {nmb} "
+                        f"minibatches of {MB} seqs (global), envs and minibatches split over "
+                        f"{world} GPU(s)",
+            "b1": f"B1: PPO iteration, 8192 envs, T=32, obs=64, MLP[256,256], heads "
+                  f"[4,8,5,5,2,2]+critic, 2 epochs x {nmb} minibatches of {MB} seqs",
             "lstm": f"L: B1 with RecurrentBackboneEncoder(MLP[256,256], LSTM(256)), "
-                    f"{args.bptt_chunks} BPTT chunk(s), minibatches of 2048 seqs",
-            "pbt": f"P: {PBT_POLICIES} train policies x 8192 envs (self-play split), "
-                   f"{PBT_POLICIES // world} per GPU, B1 policy and PPO settings",
+                    f"{args.bptt_chunks} BPTT chunk(s), minibatches of {MB} seqs",
+            "pbt": f"P: {PBT_POLICIES} train policies x 8192 envs (self-play split), placed over "
+                   f"{world} GPU(s), B1 policy and PPO settings",
         }[args.config]
         result = {
             "metric": "env-steps/sec whole-node, 65536-env PPO, at 1/2/4/8 MI355X",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (dummy vec-env HIP kernel, random-init orthogonal weights)",
-            "config": {"workload": workload,
-                       "envs_per_gpu": n_rank, "total_envs": n_rank * world,
+            "config": {"workload": workload, "config": args.config,
+                       "total_envs": total, "envs_per_gpu": n_rank,
+                       "global_minibatch_seqs": MB, "minibatches_per_epoch": nmb,
                        "steps_per_update": T, "parallelism": f"dp{world}",
                        "critic": args.critic,
                        "hip_graph": not args.no_graph},
         }
     if rank == 0 and not args.no_roofline and args.config != "lstm":
-        result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev)
-    if rank == 0 and not args.no_cpu_baseline and args.config == "b1":
+        result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev, n_rank)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("headline", "b1"):
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(result))

@@ -89,11 +89,18 @@ class PPO(AlgoBase):  # ppo.py:49-106
                 "non-default modes outside the fused path")
         C = cfg.num_bptt_chunks
         self.bptt = cfg.steps_per_update // C
-        self.num_seq = C * view.N                     # per rank
-        self.mb = int(algo.minibatch_size)            # per rank
-        if self.num_seq % self.mb != 0:               # ppo.py:439
-            raise ValueError(f"{self.num_seq} sequences not divisible by minibatch_size "
-                             f"{self.mb}")
+        # minibatch_size is GLOBAL (sequences per optimizer step of this
+        # policy, ppo.py:437-443); the dp.world_size ranks that train the
+        # policy each contribute an equal slice of every global minibatch
+        self.num_seq = C * view.N                     # this rank's sequences
+        G = dp.world_size
+        if int(algo.minibatch_size) % G != 0:
+            raise ValueError(f"minibatch_size {algo.minibatch_size} does not split over the "
+                             f"{G} ranks training this policy")
+        self.mb = int(algo.minibatch_size) // G       # this rank's slice
+        if self.num_seq % self.mb != 0:               # ppo.py:439 (num_seq*G % minibatch_size)
+            raise ValueError(f"{self.num_seq * G} sequences not divisible by minibatch_size "
+                             f"{algo.minibatch_size}")
         self.num_mb = self.num_seq // self.mb
         self.E = int(algo.num_epochs)
         dev = policy_state.device

@@ -182,9 +182,16 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     # policy placement: which train policies this rank holds, and the ranks it
     # shares gradients with (dist.policy_placement)
     policy_ids, dp = policy_placement(num_policies)
-    rank, _ = world()
+    rank, W = world()
 
-    sim_batch = cfg.num_agents_per_world * cfg.num_worlds
+    # Global semantics (the reference's meaning of the config, cfg.py:68-96):
+    # num_worlds counts the worlds of the whole job; rank r simulates worlds
+    # [r*num_worlds/W, (r+1)*num_worlds/W) through ITS sim_fns, and the
+    # global minibatch_size is split evenly over the ranks that train a
+    # policy (PPO.prepare).  At W = 1 this is the single-device reference.
+    if cfg.num_worlds % W != 0:
+        raise ValueError(f"num_worlds={cfg.num_worlds} does not split over {W} ranks")
+    sim_batch = cfg.num_agents_per_world * (cfg.num_worlds // W)
     rollout_cfg = RolloutConfig.setup(
         num_current_policies=len(policy_ids), num_past_policies=0, num_teams=1,
         team_size=cfg.num_agents_per_world, sim_batch_size=sim_batch, actions_cfg=cfg.actions,

@@ -1,10 +1,12 @@
 """Data-parallel PPO iteration on the GPU path: two ranks (processes) share the
 box's one GPU, collectives over gloo (the product issues the same
-all-reduces over RCCL on a multi-GPU node).  Each rank owns its own
-environment shard; after one update (eager) and two more (HIP-graph replay)
-both ranks must hold identical parameters, and the first update must equal
-the oracle's single-process update over the union of both ranks' minibatches
-(f32 mode, tolerances of test_gpu_train)."""
+all-reduces over RCCL on a multi-GPU node).  Global semantics (SURVEY §8(d)
+B8): TrainConfig.num_worlds = 2N and minibatch_size = 32 sequences describe
+the whole job; each rank simulates its N-env shard and contributes 16
+sequences to every global minibatch.  After one update (eager) and two more
+(HIP-graph replay) both ranks must hold identical parameters, and the first
+update must equal the oracle's single-process update over the union of both
+ranks' minibatches (f32 mode, tolerances of test_gpu_train)."""
 
 import os
 import socket
@@ -40,9 +42,9 @@ def worker(rank, world, port, outdir):
         dtype = torch.float32
         env = DummyVecEnv(N, D, 6, seed=2, env_offset=rank * N, device=dev)
         cfg = ml.TrainConfig(
-            num_worlds=N, num_agents_per_world=1, num_updates=3,
+            num_worlds=world * N, num_agents_per_world=1, num_updates=3,
             actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
-            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16, clip_coef=0.2,
+            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16 * world, clip_coef=0.2,
                                        value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                        max_grad_norm=0.5),
             num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=5, metrics_buffer_size=4,
@@ -53,6 +55,7 @@ def worker(rank, world, port, outdir):
             critic=DenseLayerCritic(dtype)))
         mgr = ml.init_training(dev, cfg, env.sim_fns(), policy, use_graph=True)
         ps, ts = mgr.state.policy_states, mgr.state.train_states
+        assert mgr.rollout_mgr.N == N and mgr.algo.mb == 16, "global config must split per rank"
         p0 = ps.params.cpu().numpy()
         mgr.update_iter()
         torch.cuda.synchronize()

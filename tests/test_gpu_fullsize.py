@@ -1,0 +1,205 @@
+"""GPU parity of the PPO minibatch gradient at the sizes the benchmarks run
+(SURVEY §8(d) B1 / headline: 8192-env store, minibatch 2048 sequences x
+bptt 32 = 65,536 rows, MLP[256,256], 2048 workgroups of the step kernel)
+and of the value-loss variants of PPOConfig (clip_value_loss,
+huber_value_loss; ppo.py:197-218) including rows sitting exactly on the
+clip bounds and on the huber kink, where JAX's balanced min / max / abs
+derivatives give 0.5 (oracle ppo_ref.ppo_loss_dhead restates them).
+
+Tolerances as test_gpu_policy: f32 loss within 1e-5 relative, gradients
+within 1e-3 relative + 1e-4 x max|g|; bf16 gradients within 3e-2 x max|g|,
+cosine > 0.999."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_ref as ref
+from tests.test_gpu_policy import BUCKETS, make_policy_state, oracle_layout, perturb
+
+pytestmark = pytest.mark.gpu
+
+
+def _minibatch_store(rng, ps, T, N, D, mode, seqs, bptt):
+    """[T][N] store whose minibatch rows carry old log-probs / values from the
+    oracle forward of the current parameters (+ noise, so ratios != 1);
+    every other row is random (never read)."""
+    obs = ref.rnd(rng.standard_normal((T, N, D), dtype=np.float32), mode).astype(np.float32)
+    acts = np.stack([rng.integers(0, b, (T, N)) for b in BUCKETS], -1).astype(np.int32)
+    st = {"obs": obs, "actions": acts,
+          "log_probs": (rng.standard_normal((T, N, 6)) - 2.0).astype(np.float32),
+          "values": rng.standard_normal((T, N)).astype(np.float32),
+          "advantages": (rng.standard_normal((T, N)) * 2 + 0.3).astype(np.float32),
+          "returns": rng.standard_normal((T, N)).astype(np.float32),
+          "rewards": np.zeros((T, N), np.float32)}
+    rows = ref.minibatch_rows(seqs, N, bptt)
+    P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
+    logits, V, _ = ref.forward(P, obs.reshape(T * N, D)[rows], mode)
+    lp, _ = ref.action_stats(logits, BUCKETS, acts.reshape(T * N, 6)[rows])
+    lpf = st["log_probs"].reshape(T * N, 6)
+    # ratio noise kept clear of the clip bounds 1 -/+ 0.2 (|ratio - bound| > 1e-3):
+    # the clipped objective's derivative jumps there, and a 1-ulp difference in
+    # the new log-prob would move a row across (an O(1/M) jump per row)
+    d = rng.standard_normal(lp.shape) * 0.1
+    near = (np.abs(np.exp(d) - 0.8) < 1e-3) | (np.abs(np.exp(d) - 1.2) < 1e-3)
+    d[near] = 0.0
+    lpf[rows] = (lp - d).astype(np.float32)
+    vf = st["values"].reshape(T * N)
+    vf[rows] = V.astype(np.float32)
+    rf = st["returns"].reshape(T * N)
+    rf[rows] = (V + rng.standard_normal(V.shape)).astype(np.float32)
+    return st, rows
+
+
+def _device_store(gpu, st, dtype):
+    from madrona_learn.rollouts import RolloutStore
+    T, N, D = st["obs"].shape
+    s = RolloutStore(T, N, D, 6, dtype, gpu)
+    s.obs.copy_(torch.from_numpy(st["obs"]).to(dtype))
+    s.actions.copy_(torch.from_numpy(st["actions"]))
+    s.log_probs.copy_(torch.from_numpy(st["log_probs"]))
+    s.values.copy_(torch.from_numpy(st["values"]))
+    s.advantages.copy_(torch.from_numpy(st["advantages"]))
+    s.returns.copy_(torch.from_numpy(st["returns"]))
+    return s
+
+
+def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats):
+    from madrona_learn import _native as nat
+    hp = nat.PPOHparams()
+    hp.clip_coef, hp.value_loss_coef = hpd["clip_coef"], hpd["value_loss_coef"]
+    for k in range(6):
+        hp.entropy_coef[k] = hpd["entropy_coef"]
+    hp.normalize_advantages, hp.loss_scale = 1, 1.0
+    hp.clip_value_loss = 1 if hpd.get("clip_value_loss") else 0
+    hp.huber_value_loss = 1 if hpd.get("huber_value_loss") else 0
+    st = torch.tensor([stats[0], 1.0 / np.sqrt(max(stats[1], 1e-5))], dtype=torch.float32,
+                      device=gpu)
+    M = mb * bptt
+    ws = torch.zeros(int(nat.lib().mlearn_ppo_workspace_bytes(ps.desc, M)), dtype=torch.uint8,
+                     device=gpu)
+    grad = torch.zeros(ps.layout["total"], dtype=torch.float32, device=gpu)
+    out = torch.zeros(25, dtype=torch.float32, device=gpu)
+    sq = torch.from_numpy(np.asarray(seqs, np.int32)).to(gpu)
+    nat.check(nat.lib().mlearn_ppo_minibatch_grad(ps.desc, s.view(bptt), nat.ptr(sq), mb,
+                                                  nat.ptr(st), hp, nat.ptr(grad), nat.ptr(out),
+                                                  nat.ptr(ws), nat.stream_handle()))
+    torch.cuda.synchronize()
+    return grad.cpu().numpy(), out.cpu().numpy()
+
+
+def _check(mode, g, o, loss, gflat, met, M, full_size=False):
+    scale = np.abs(gflat).max()
+    if mode == "f32" and full_size:
+        # 65,536 rows x 512 ReLUs: tens of pre-activations sit within an f32
+        # rounding of 0, where ReLU' jumps (the oracle and the kernel round the
+        # LayerNorm in different orders), each moving O(1/M) of gradient; so
+        # the elementwise bound is taken relative to the gradient's scale and
+        # the bulk is checked in norm
+        np.testing.assert_allclose(o[0], loss, rtol=1e-5, atol=1e-7)
+        err = np.abs(g - gflat).max() / scale
+        assert err < 2e-3, err
+        rel = np.linalg.norm(g - gflat) / np.linalg.norm(gflat)
+        assert rel < 1e-3, rel
+        cos = g @ gflat / (np.linalg.norm(g) * np.linalg.norm(gflat))
+        assert cos > 0.99999, cos
+        mtol = 1e-5
+    elif mode == "f32":
+        np.testing.assert_allclose(o[0], loss, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(g, gflat, rtol=1e-3, atol=1e-4 * scale)
+        mtol = 1e-5
+    else:
+        np.testing.assert_allclose(o[0], loss, rtol=2e-2, atol=2e-3)
+        err = np.abs(g - gflat).max() / scale
+        assert err < 3e-2, err
+        cos = g @ gflat / (np.linalg.norm(g) * np.linalg.norm(gflat))
+        assert cos > 0.999, cos
+        mtol = 2e-2
+    np.testing.assert_allclose(o[10], met["Value Loss"].mean(), rtol=mtol)
+    np.testing.assert_allclose(o[15], np.abs(met["Value Errors"]).mean(), rtol=mtol)
+    np.testing.assert_allclose(o[20], met["Entropy"].mean(), rtol=mtol)
+    assert o[14] == M and o[24] == M * 6
+
+
+HP = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+      "normalize_advantages": True}
+
+
+@pytest.mark.parametrize("mode,dtype", [("f32", torch.float32), ("bf16", torch.bfloat16)])
+def test_minibatch_grad_b1_size(gpu, mode, dtype):
+    """One B1 / headline minibatch: 2048 sequences of 32 steps gathered from
+    an 8192-env store (65,536 rows, 2048 step-kernel workgroups)."""
+    T, N, D, H, L, mb, bptt = 32, 8192, 64, 256, 2, 2048, 32
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=21)
+    perturb(ps, 22, scale=0.2)
+    rng = np.random.default_rng(23)
+    seqs = rng.permutation(N)[:mb].astype(np.int32)
+    st, rows = _minibatch_store(rng, ps, T, N, D, mode, seqs, bptt)
+    s = _device_store(gpu, st, dtype)
+    batch = ref.gather_minibatch(st, rows)
+    adv = batch["advantages"].astype(np.float64)
+    stats = (adv.mean(), adv.var())
+    P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
+    loss, G, met, _ = ref.ppo_loss_grads(P, batch, HP, BUCKETS, mode, adv_stats=stats)
+    gflat = ref.flatten(G, oracle_layout(ps))
+    g, o = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
+    _check(mode, g, o, loss, gflat, met, mb * bptt, full_size=True)
+
+
+def _set_constant_critic(ps, value):
+    """Critic column of the head zeroed and its bias set so that every row's
+    value is exactly `value` in both dtypes (ties are then exact)."""
+    p = ps.params.cpu().numpy()
+    o, shp = ps.layout["hw"]
+    hw = p[o:o + shp[0] * shp[1]].reshape(shp)
+    A = ps.arch.num_logits
+    hw[:, A] = 0.0
+    o, _ = ps.layout["hb"]
+    p[o + A] = value
+    ps.params.copy_(torch.from_numpy(p))
+    ps.sync_weights()
+
+
+@pytest.mark.parametrize("mode,dtype", [("f32", torch.float32), ("bf16", torch.bfloat16)])
+@pytest.mark.parametrize("clip_vl,huber", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_value_loss_variants(gpu, mode, dtype, clip_vl, huber, ties):
+    T, N, D, H, L, mb, bptt = 32, 96, 64, 128, 2, 40, 16
+    ps = make_policy_state(gpu, D, H, L, dtype, seed=31)
+    perturb(ps, 32, scale=0.2)
+    hpd = dict(HP, clip_coef=0.25, clip_value_loss=clip_vl, huber_value_loss=huber)
+    if ties:
+        _set_constant_critic(ps, 0.5)  # V == 0.5 exactly on every row
+    rng = np.random.default_rng(33)
+    nseq = (T // bptt) * N
+    seqs = rng.permutation(nseq)[:mb].astype(np.int32)
+    st, rows = _minibatch_store(rng, ps, T, N, D, mode, seqs, bptt)
+    if ties:
+        # old values on the clip bounds (V == ov -/+ clip), inside, and
+        # clipped on either side; returns on the huber kink (|vpred - R| == 1)
+        n = len(rows)
+        vf = st["values"].reshape(-1)
+        vf[rows] = np.array([0.75, 0.25, 0.5, 2.0, -1.0], np.float32)[np.arange(n) % 5]
+        rf = st["returns"].reshape(-1)
+        rf[rows] = np.array([1.5, -0.5, 0.5, 3.0, -2.5, 0.75, 0.1], np.float32)[np.arange(n) % 7]
+    else:
+        st["values"].reshape(-1)[rows] += (rng.standard_normal(len(rows)) * 0.3).astype(
+            np.float32)
+        st["returns"].reshape(-1)[rows] *= 2.0
+    s = _device_store(gpu, st, dtype)
+    batch = ref.gather_minibatch(st, rows)
+    adv = batch["advantages"].astype(np.float64)
+    stats = (adv.mean(), adv.var())
+    P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
+    loss, G, met, aux = ref.ppo_loss_grads(P, batch, hpd, BUCKETS, mode, adv_stats=stats)
+    if ties:
+        assert np.all(aux["value"] == 0.5), "the oracle's values must sit on the ties too"
+    gflat = ref.flatten(G, oracle_layout(ps))
+    g, o = _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats)
+    _check(mode, g, o, loss, gflat, met, mb * bptt)
+    if ties:
+        # the critic bias gradient is the sum of d loss / d V: pins the 0.5 tie weights
+        A = ps.arch.num_logits
+        ob, _ = ps.layout["hb"]
+        np.testing.assert_allclose(g[ob + A], gflat[ob + A], rtol=1e-5 if mode == "f32" else 2e-2,
+                                   atol=1e-7)

@@ -19,7 +19,7 @@ BUCKETS = [4, 8, 5, 5, 2, 2]
 N, D, H, T, P = 128, 64, 64, 32, 2
 
 
-def _setup(gpu, dtype=torch.float32, use_graph=False):
+def _setup(gpu, dtype=torch.float32, use_graph=False, N=N, H=H, P=P, mb=16):
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     from tests.test_gpu_train import make_policy
@@ -27,7 +27,7 @@ def _setup(gpu, dtype=torch.float32, use_graph=False):
     cfg = ml.TrainConfig(
         num_worlds=N, num_agents_per_world=1, num_updates=1,
         actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
-        lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16, clip_coef=0.2,
+        lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=mb, clip_coef=0.2,
                                    value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                    max_grad_norm=0.5),
         num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=9, metrics_buffer_size=4,
@@ -38,8 +38,13 @@ def _setup(gpu, dtype=torch.float32, use_graph=False):
     return cfg, env, mgr
 
 
-def test_population_update_matches_oracle(gpu):
-    cfg, env, mgr = _setup(gpu)
+@pytest.mark.parametrize("mode,dtype,Np,Hp,Pp,mb", [
+    ("f32", torch.float32, 128, 64, 2, 16),
+    # config P's population shape: 8 policies, MLP[256,256], bf16 (128 envs each)
+    ("bf16", torch.bfloat16, 1024, 256, 8, 32)])
+def test_population_update_matches_oracle(gpu, mode, dtype, Np, Hp, Pp, mb):
+    N, H, P = Np, Hp, Pp
+    cfg, env, mgr = _setup(gpu, dtype, N=N, H=H, P=P, mb=mb)
     pss, tss = mgr.state.policy_list, mgr.state.train_list
     assert len(pss) == P and mgr.rollout_mgr.B == N // P
     p0 = [ps.params.cpu().numpy().astype(np.float64) for ps in pss]
@@ -51,19 +56,21 @@ def test_population_update_matches_oracle(gpu):
     torch.cuda.synchronize()
     s = mgr.rollout_mgr.store
     lay = ref.param_layout(D, H, 2, 26)
-    ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="f32",
+    ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode=mode,
                         gamma=cfg.gamma, actions_override=s.actions.cpu().numpy())
     assert np.array_equal(s.rewards.cpu().numpy(), ro["rewards"])
     assert np.array_equal(s.dones.cpu().numpy(), ro["dones"])
-    np.testing.assert_allclose(s.values.cpu().numpy(), ro["values"], rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(s.bootstrap.cpu().numpy(), ro["bootstrap"], rtol=1e-4,
-                               atol=1e-4)
-    np.testing.assert_allclose(s.log_probs.cpu().numpy(), ro["log_probs"], rtol=1e-4, atol=1e-4)
+    tol = 1e-4 if mode == "f32" else 3e-2
+    np.testing.assert_allclose(s.values.cpu().numpy(), ro["values"], rtol=tol, atol=tol)
+    np.testing.assert_allclose(s.bootstrap.cpu().numpy(), ro["bootstrap"], rtol=tol,
+                               atol=tol)
+    np.testing.assert_allclose(s.log_probs.cpu().numpy(), ro["log_probs"], rtol=tol, atol=tol)
     adv, ret = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(),
                            s.dones.cpu().numpy(), s.bootstrap.cpu().numpy(), cfg.gamma,
                            cfg.gae_lambda)
     assert np.array_equal(s.advantages.cpu().numpy(), adv)
-    full = {k: v.cpu().numpy() for k, v in s.as_dict().items()}
+    full = {k: (v.float() if v.dtype == torch.bfloat16 else v).cpu().numpy()
+            for k, v in s.as_dict().items()}
     B = N // P
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
           "normalize_advantages": True}
@@ -74,10 +81,16 @@ def test_population_update_matches_oracle(gpu):
         p1, _, _ = ref.ppo_update(
             p0[p], (z, z.copy(), 0), [store], hp, BUCKETS, lay,
             pss[p].init_norms.cpu().numpy().astype(np.float64), num_epochs=2,
-            minibatch_size=16, bptt=T, key=tss[p].update_prng_key, epoch_base=0, mode="f32",
+            minibatch_size=mb, bptt=T, key=tss[p].update_prng_key, epoch_base=0, mode=mode,
             lr=3e-4, max_grad_norm=0.5)
-        np.testing.assert_allclose(pss[p].params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
-        assert int(tss[p].step.item()) == 2 * (B // 16)
+        got = pss[p].params.cpu().numpy()
+        if mode == "f32":
+            np.testing.assert_allclose(got, p1, rtol=1e-4, atol=2e-5)
+        else:
+            dg, dr = got - p0[p], p1 - p0[p]
+            cos = dg @ dr / (np.linalg.norm(dg) * np.linalg.norm(dr))
+            assert cos > 0.97, (p, cos)
+        assert int(tss[p].step.item()) == 2 * (B // mb)
         # per-policy rollout metrics cover that policy's columns only
         last = mgr.metrics.last(policy=p)
         np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)

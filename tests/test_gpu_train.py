@@ -1,6 +1,8 @@
-"""End-to-end GPU parity of one full PPO iteration (config C0 shape:
-64 envs, MLP[64,64], T=32, 2 epochs, minibatch 16 sequences) against the
-oracle replaying the same trajectory, plus HIP-graph replay == eager.
+"""End-to-end GPU parity of one full PPO iteration against the oracle
+replaying the same trajectory (config C0 shape: 64 envs, MLP[64,64], T=32,
+2 epochs, minibatch 16 sequences; and the B1 shape scaled to 1024 envs:
+MLP[256,256], bf16 and f32, 4 minibatches of 256 sequences), plus HIP-graph
+replay == eager.
 """
 
 import numpy as np
@@ -47,15 +49,19 @@ def _setup(gpu, dtype, N=64, H=64, D=64, chunks=1, mb=16, use_graph=False, criti
     return cfg, env, mgr
 
 
-@pytest.mark.parametrize("mode,dtype,chunks,CB", [("f32", torch.float32, 1, 1),
-                                                  ("f32", torch.float32, 2, 1),
-                                                  ("bf16", torch.bfloat16, 1, 1),
-                                                  ("f32", torch.float32, 1, 63),
-                                                  ("bf16", torch.bfloat16, 2, 63)])
-def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB):
-    cfg, env, mgr = _setup(gpu, dtype, chunks=chunks, critic_bins=CB)
+@pytest.mark.parametrize("mode,dtype,chunks,CB,N,H,mb", [
+    ("f32", torch.float32, 1, 1, 64, 64, 16),
+    ("f32", torch.float32, 2, 1, 64, 64, 16),
+    ("bf16", torch.bfloat16, 1, 1, 64, 64, 16),
+    ("f32", torch.float32, 1, 63, 64, 64, 16),
+    ("bf16", torch.bfloat16, 2, 63, 64, 64, 16),
+    # B1 shape (MLP[256,256], 4 minibatches per epoch) at 1024 envs
+    ("bf16", torch.bfloat16, 1, 1, 1024, 256, 256),
+    ("f32", torch.float32, 1, 1, 1024, 256, 256)])
+def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB, N, H, mb):
+    cfg, env, mgr = _setup(gpu, dtype, N=N, H=H, chunks=chunks, mb=mb, critic_bins=CB)
     ps, ts = mgr.state.policy_states, mgr.state.train_states
-    lay = ref.param_layout(64, 64, 2, 26, CB)
+    lay = ref.param_layout(64, H, 2, 26, CB)
     p0 = ps.params.cpu().numpy().astype(np.float64)
     oenv = onat.Env(env.N, env.D, env.k0, env.k1, 0)
     oenv.reset()
@@ -102,7 +108,7 @@ def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB):
     zeros = np.zeros_like(p0)
     p1, _, met = ref.ppo_update(
         p0, (zeros, zeros.copy(), 0), [store], hp, BUCKETS, lay,
-        ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=16,
+        ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=mb,
         bptt=cfg.steps_per_update // chunks, key=ts.update_prng_key, epoch_base=0, mode=mode,
         lr=3e-4, max_grad_norm=0.5)
     got = ps.params.cpu().numpy()
@@ -114,10 +120,10 @@ def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB):
         assert cos > 0.999
     else:
         assert cos > 0.97, cos
-    assert int(ts.step.item()) == 2 * (cfg.num_worlds * chunks // 16)
+    assert int(ts.step.item()) == 2 * (cfg.num_worlds * chunks // mb)
     last = mgr.metrics.last()
     np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
-    assert last["Advantages"].count == 32 * 64
+    assert last["Advantages"].count == 32 * N
 
 
 def test_graph_replay_matches_eager(gpu):
