@@ -43,6 +43,7 @@ struct HpK {
     float clip, vcoef;
     float ecoef[MLEARN_MAX_GROUPS];
     int norm_adv, clip_vl, huber, norm_vals;
+    int metrics;  // reduce the loss metrics (only the minibatch whose metrics are recorded)
     float loss_scale;
     float inv_sk, inv_s;
 };
@@ -666,7 +667,8 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
                                         m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
                                         m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
         constexpr int kUsed = 17;  // slots 17.. are padding
-        if (__any(did)) {
+        if (!hp.metrics) {
+        } else if (__any(did)) {
 #pragma unroll
             for (int s = 0; s < kUsed; ++s) {
                 const int kind = (s < 16) ? (s & 3) : 0;
@@ -682,7 +684,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         }
     }
     __syncthreads();
-    if (tid < kLossSlots) {
+    if (hp.metrics && tid < kLossSlots) {
         const int kind = (tid < 16) ? (tid & 3) : 0;
         double v = lred[tid];
         for (int u = 1; u < W; ++u) {
@@ -960,7 +962,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp,
     const WgJob& J = jobs.job[jb];
     const int local = blockIdx.x - J.wg0;
     const int nt = J.ti * J.tj;
-    const int split = local / nt, t = local - split * nt;
+    int split, t;
+    if ((J.splits & 7) == 0 && (J.wg0 & 7) == 0) {
+        // XCD-aware: blocks are dealt round-robin over the 8 XCDs (b % 8), so
+        // the nt tiles of one split (which read the same minibatch rows of X
+        // and Y) get block ids 8 apart and share an XCD's L2: the rows come
+        // from HBM once instead of once per tile (speed only, never correctness)
+        const int x = local & 7, q = local >> 3;
+        t = q % nt;
+        split = (q / nt) * 8 + x;
+    } else {
+        split = local / nt;
+        t = local - split * nt;
+    }
     const int i0 = (t % J.ti) * kWgTile, j0 = (t / J.ti) * kWgTile;
     const int64_t m0 = split * J.rps;
     const int64_t m1 = m0 + J.rps < jobs.Mp ? m0 + J.rps : jobs.Mp;  // whole chunks
@@ -1300,6 +1314,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.norm_vals = h.normalize_values;
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
+    hp.metrics = loss_out != nullptr;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
 
@@ -1381,6 +1396,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     hp.norm_vals = h.normalize_values;
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
+    hp.metrics = loss_out != nullptr;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
     const int L = p.num_layers;

@@ -310,6 +310,29 @@ __device__ inline void gemm_first(f32x16 (&acc)[NOUT], const S* __restrict__ row
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
     const int voff = lane * RT<T>::E * (int)sizeof(T);
     const int h = lane >> 5;
+    constexpr int PRE =
+        std::is_same<T, bf16>::value && std::is_same<S, T>::value && NOUT <= 2 ? 4 : 0;  // D <= 64
+    if (PRE > 0 && nks <= PRE) {
+        // short K (the observation width): every A and B fragment of the
+        // product is issued before the first MFMA, so the gathered row costs
+        // one memory latency instead of one per k-step
+        frag ap[PRE > 0 ? PRE : 1][NOUT], bp[PRE > 0 ? PRE : 1];
+#pragma unroll
+        for (int s = 0; s < PRE; ++s)
+            if (s < nks) {
+                bp[s] = live ? row_in<T>(row, mu, inv, s, h) : RT<T>::zero();
+#pragma unroll
+                for (int nb = 0; nb < NOUT; ++nb) ap[s][nb] = img_load<T>(rs, voff, (nb * nks + s) * FB);
+            }
+#pragma unroll
+        for (int s = 0; s < PRE; ++s)
+            if (s < nks) {
+                if (copy) RT<T>::put_row(copy, s, h, bp[s]);
+#pragma unroll
+                for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ap[s][nb], bp[s], acc[nb]);
+            }
+        return;
+    }
     frag a[NOUT], an[NOUT];
     frag b = live ? row_in<T>(row, mu, inv, 0, h) : RT<T>::zero(), bn = b;
 #pragma unroll

@@ -205,18 +205,23 @@ class PPO(AlgoBase):  # ppo.py:49-106
         for e in range(self.E):
             for m in range(self.num_mb):
                 seqs = self.perm[e, m * self.mb:(m + 1) * self.mb]
+                # TrainingMetrics.record writes every minibatch's metrics into the
+                # same buffer slot (metrics.py:161-181, advanced once per update):
+                # only the last minibatch's survive, so only it reduces them
+                last = e == self.E - 1 and m == self.num_mb - 1
+                lo = nat.ptr(loss_out) if last else None
                 stats = self.vn_rec[e, m] if self.vnorm else self.adv_stats[e, m]
                 if self.lstm is not None:
                     nat.check(L.mlearn_lstm_ppo_minibatch_grad(
                         policy_state.desc, self.lstm, self.view, self.start_h, self.start_c,
                         nat.ptr(seqs), self.mb, nat.ptr(stats), self.hp,
-                        nat.ptr(train_state.grads), nat.ptr(loss_out), nat.ptr(self.ws), strm),
+                        nat.ptr(train_state.grads), lo, nat.ptr(self.ws), strm),
                         "lstm_ppo_minibatch_grad")
                 else:
                     nat.check(L.mlearn_ppo_minibatch_grad(
                         policy_state.desc, self.view, nat.ptr(seqs), self.mb,
                         nat.ptr(stats), self.hp, nat.ptr(train_state.grads),
-                        nat.ptr(loss_out), nat.ptr(self.ws), strm), "ppo_minibatch_grad")
+                        lo, nat.ptr(self.ws), strm), "ppo_minibatch_grad")
                 if self.dp.world_size > 1:
                     yield ("allreduce", train_state.grads)
                 train_state.optimizer_step(policy_state)

@@ -13,9 +13,11 @@ import re
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r01.json"
+out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/pmc_summary.json"
 KEYS = {"ppo_step": r"ppo_step_kernel", "wgrad": r"wgrad_kernel", "policy_step": r"policy_step_kernel",
-        "gae": r"gae_kernel", "reduce_grads": r"reduce_grads_kernel"}
+        "gae": r"gae_kernel", "reduce_grads": r"reduce_grads_kernel", "env_step": r"env_step_kernel",
+        "adam": r"adam_kernel", "project": r"project_kernel", "sumsq": r"sumsq_partial_kernel",
+        "optim": r"optim_fused_kernel"}
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 names = {}
 for f in sorted(glob.glob(f"{root}/p*/*counter_collection.csv")):

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase cycle stamps of the fused PPO minibatch kernel (B1
+"""Diagnostic: per-phase cycle stamps of the fused PPO minibatch kernel (headline
 shape).  Run with MADRONA_LEARN_LIB=madrona-learn_amd/madrona_learn/_lib/libmlearn_stamps.so
 (tools/build_stamps.sh)."""
 import ctypes
@@ -14,7 +14,7 @@ import bench  # noqa: E402
 from madrona_learn import _native as nat  # noqa: E402
 
 dev = torch.device("cuda:0")
-mgr = bench.make(dev, use_graph=False)
+mgr = bench.make(dev, 65536, 0, 65536, use_graph=False)
 mgr.update_iter()
 torch.cuda.synchronize()
 L = nat.lib()
