@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 7
+#define MLEARN_ABI_VERSION 8
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -303,7 +303,18 @@ typedef struct mlearn_ppo_hparams {
     float loss_scale;                      /* 1/world_size under DP (mean of means) */
     int32_t normalize_values;              /* TrainConfig.normalize_values: adv_stats is a
                                               mlearn_value_norm_chain record */
+    double* grad_sumsq_out;                /* may be NULL: per-64-parameter partial sums of
+                                              grad^2 (mlearn_grad_sumsq_parts entries),
+                                              written by the gradient reduction; the next
+                                              mlearn_optim_step may take them as
+                                              grad_sumsq_part instead of re-reading grads
+                                              (only valid when grads are not all-reduced
+                                              in between) */
 } mlearn_ppo_hparams;
+
+/* Number of partials mlearn_ppo_hparams.grad_sumsq_out receives: one per 64
+ * parameters of the flat layout (ceil(param_count / 64)). */
+int64_t mlearn_grad_sumsq_parts(int64_t param_count);
 
 /* Size of the minibatch workspace (activations + gradient slabs). */
 int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows);
@@ -353,6 +364,10 @@ typedef struct mlearn_optim_state {
     float lr, b1, b2, eps, max_grad_norm;
     int32_t normalize_params;      /* ppo.py:303-310 */
     int32_t normalize_layernorms;  /* ppo.py:312-338 */
+    const double* grad_sumsq_part; /* may be NULL: partial sums of grads^2 already produced
+                                      by the gradient reduction (grad_sumsq_out); the
+                                      clip_by_global_norm norm then comes from them */
+    int64_t grad_sumsq_nparts;
 } mlearn_optim_state;
 
 int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy);

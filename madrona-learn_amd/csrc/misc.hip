@@ -527,30 +527,45 @@ __global__ __launch_bounds__(256) void post_step_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int env_episode_len(uint32_t g) { return 16 + (int)((g * 7u) % 33u); }
 
-__device__ inline float env_obs_feature(uint32_t k0, uint32_t k1, uint32_t g, int f, uint64_t step) {
+// One Philox4x32-10 call per 4 features (counter {env, f / 4, step}):
+// feature f reads word f % 4 as four bytes b_i, s = sum (b_i + 0.5) / 256
+// (Irwin-Hall n = 4 of 8-bit uniforms, exact in f32), obs = (s - 2) sqrt(3):
+// mean 0, variance 1.  CPU twin: oracle/ref_rng.c obs_feature.
+__device__ inline float env_obs_word(uint32_t w) {
 #pragma clang fp contract(off)
-    u32x4 r = philox4x32(u32x4{g, (uint32_t)f, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
-                         k1 ^ 0x5eedu);
-    float s = ((u32_to_unit(r.x) + u32_to_unit(r.y)) + u32_to_unit(r.z)) + u32_to_unit(r.w);
-    return (s - 2.0f) * 1.73205077648162841796875f;
+    const uint32_t b = (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24) + 2u;
+    return ((float)b * 0.00390625f - 2.0f) * 1.73205077648162841796875f;
+}
+__device__ inline u32x4 env_obs_words(uint32_t k0, uint32_t k1, uint32_t g, int q, uint64_t step) {
+    return philox4x32(u32x4{g, (uint32_t)q, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
+                      k1 ^ 0x5eedu);
 }
 
 // state[n] = {episode step, env step lo, env step hi, 0}; one lane per
-// (env, feature); the f == 0 lane also advances the env and emits reward/done.
+// (env, 4 features); the first quad's lane also advances the env and emits
+// reward/done.
 __global__ __launch_bounds__(256) void env_step_kernel(int4* state, const int32_t* actions,
                                                        int K, int64_t N, int D, uint32_t k0,
                                                        uint32_t k1, uint32_t eoff, float* obs,
                                                        float* rew, uint8_t* done) {
 #pragma clang fp contract(off)
+    const int Q = (D + 3) >> 2;
     int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (task >= N * D) return;
-    int64_t n = task / D;
-    int f = (int)(task % D);
+    if (task >= N * Q) return;
+    int64_t n = task / Q;
+    int q = (int)(task - n * Q);
     uint32_t g = eoff + (uint32_t)n;
     int4 st = state[n];
     const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
-    obs[task] = env_obs_feature(k0, k1, g, f, step);
-    if (f == 0) {
+    const u32x4 w = env_obs_words(k0, k1, g, q, step);
+    float* o = obs + n * D + 4 * q;
+    if ((D & 3) == 0 && ((uintptr_t)obs & 15) == 0) {
+        *(float4*)o = make_float4(env_obs_word(w.x), env_obs_word(w.y), env_obs_word(w.z),
+                                  env_obs_word(w.w));
+    } else {
+        for (int j = 0; j < 4 && 4 * q + j < D; ++j) o[j] = env_obs_word(u32x4_get(w, j));
+    }
+    if (q == 0) {
         int s = st.x + 1;
         int L = env_episode_len(g);
         bool d = s >= L;
@@ -568,13 +583,15 @@ __global__ __launch_bounds__(256) void env_step_kernel(int4* state, const int32_
 __global__ __launch_bounds__(256) void env_reset_kernel(int4* state, int64_t N, int D,
                                                         uint32_t k0, uint32_t k1, uint32_t eoff,
                                                         float* obs) {
+    const int Q = (D + 3) >> 2;
     int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (task >= N * D) return;
-    int64_t n = task / D;
-    int f = (int)(task % D);
+    if (task >= N * Q) return;
+    int64_t n = task / Q;
+    int q = (int)(task - n * Q);
     uint32_t g = eoff + (uint32_t)n;
-    obs[task] = env_obs_feature(k0, k1, g, f, 0xffffffffffffffffull);
-    if (f == 0) state[n] = make_int4((int)(g % (uint32_t)env_episode_len(g)), 0, 0, 0);
+    const u32x4 w = env_obs_words(k0, k1, g, q, 0xffffffffffffffffull);
+    for (int j = 0; j < 4 && 4 * q + j < D; ++j) obs[n * D + 4 * q + j] = env_obs_word(u32x4_get(w, j));
+    if (q == 0) state[n] = make_int4((int)(g % (uint32_t)env_episode_len(g)), 0, 0, 0);
 }
 
 struct Deltas {
@@ -926,7 +943,8 @@ int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int
     if (N == 0) return MLEARN_OK;
     ML_REQUIRE(state && obs && rewards && dones, "env_step: null pointer");
     ML_REQUIRE((uintptr_t)state % 16 == 0, "env_step: state must be 16-byte aligned");
-    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(N * obs_dim, 256)), dim3(256), 0, S(stream),
+    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(N * ((obs_dim + 3) / 4), 256)), dim3(256), 0,
+                       S(stream),
                        (int4*)state, actions, K, N, obs_dim, k0, k1, env_offset, obs, rewards,
                        dones);
     return check_launch("env_step");
@@ -938,7 +956,7 @@ int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t 
     if (N == 0) return MLEARN_OK;
     ML_REQUIRE(state && obs, "env_reset: null pointer");
     ML_REQUIRE((uintptr_t)state % 16 == 0, "env_reset: state must be 16-byte aligned");
-    hipLaunchKernelGGL(env_reset_kernel, dim3(grid_for(N * obs_dim, 256)), dim3(256), 0,
+    hipLaunchKernelGGL(env_reset_kernel, dim3(grid_for(N * ((obs_dim + 3) / 4), 256)), dim3(256), 0,
                        S(stream), (int4*)state, N, obs_dim, k0, k1, env_offset, obs);
     return check_launch("env_reset");
 }

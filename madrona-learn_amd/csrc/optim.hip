@@ -82,15 +82,18 @@ __device__ inline int proj_slot(const LayoutK& k, int64_t p) {
 
 constexpr int kAdamBlocks = 256;
 
-// Global gradient norm from the kNormBlocks partials (every block computes it
-// the same way: wave 0, fixed butterfly order).
-__device__ inline float global_norm(const double* gpart) {
+// Global gradient norm from npart partials (every block computes it the same
+// way: thread i sums partials i, i + 256, ..., then a fixed butterfly).
+__device__ inline float global_norm(const double* gpart, int64_t npart) {
+    __shared__ double gn_red[4];
     __shared__ float gn_sh;
-    if (threadIdx.x < 64) {
-        double t = threadIdx.x < kNormBlocks ? gpart[threadIdx.x] : 0.0;
-        t = wave_sum64d(t);
-        if (threadIdx.x == 0) gn_sh = sqrtf((float)t);  // optax.global_norm in f32
-    }
+    double t = 0.0;
+    for (int64_t i = threadIdx.x; i < npart; i += 256) t += gpart[i];
+    t = wave_sum64d(t);
+    if ((threadIdx.x & 63) == 0) gn_red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        gn_sh = sqrtf((float)((gn_red[0] + gn_red[1]) + (gn_red[2] + gn_red[3])));  // f32 norm
     __syncthreads();
     return gn_sh;
 }
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
                                                    const float* __restrict__ grads,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    const int32_t* step, const double* gpart,
-                                                   float lr, float b1, float b2, float eps,
+                                                   int64_t npart, float lr, float b1, float b2, float eps,
                                                    float max_norm, double* proj_part) {
     // grid-stride over the parameters with at most kAdamBlocks blocks, so the
     // projection reduces a short, fixed list of per-block partials
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x < 4 * kMaxSlots) sh[threadIdx.x / kMaxSlots][threadIdx.x % kMaxSlots] = 0.f;
-    const float gn = global_norm(gpart);  // (its barrier also orders the sh zeroing)
+    const float gn = global_norm(gpart, npart);  // (its barriers also order the sh zeroing)
     for (int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x; p - threadIdx.x < Lk.total;
          p += (int64_t)gridDim.x * 256) {
         float contrib = 0.f;
@@ -277,12 +280,21 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
     const int ablk = (int)(nblk < kAdamBlocks ? nblk : kAdamBlocks);
     double* gpart = (double*)workspace;
     double* ppart = gpart + kNormBlocks;
-    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
-                       Lk.total, gpart);
+    const double* norm_part = gpart;
+    int64_t nparts = kNormBlocks;
+    if (st->grad_sumsq_part) {  // partials from the gradient reduction (no extra launch)
+        ML_REQUIRE(st->grad_sumsq_nparts == (Lk.total + 63) / 64,
+                   "optim_step: grad_sumsq_nparts %lld != %lld", (long long)st->grad_sumsq_nparts,
+                   (long long)((Lk.total + 63) / 64));
+        norm_part = st->grad_sumsq_part;
+        nparts = st->grad_sumsq_nparts;
+    } else {
+        hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
+                           Lk.total, gpart);
+    }
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
-                       st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
-                       (const double*)gpart, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm,
-                       ppart);
+                       st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step, norm_part,
+                       nparts, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm, ppart);
     if (dtype == MLEARN_DTYPE_BF16)
         hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
                            st->params, st->init_norms, (const double*)ppart, ablk,

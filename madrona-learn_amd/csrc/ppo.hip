@@ -1143,7 +1143,8 @@ int validate_lstm(const mlearn_mlp_policy* p, const mlearn_lstm* r) {
 // threads x 16 split groups; group g sums splits g, g + 16, ... and the
 // groups are combined in order through LDS.
 constexpr int kRgGroups = 16;
-__global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad) {
+__global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad,
+                                                           double* sumsq) {
     __shared__ float red[kRgGroups][65];
     const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
     const int64_t p0 = (int64_t)blockIdx.x * 64;
@@ -1217,12 +1218,17 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
 #pragma unroll
     for (int e = 0; e < 4; ++e) red[g][4 * c + e] = v[e];
     __syncthreads();
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < 64) {  // wave 0
         const int64_t p = p0 + threadIdx.x;
         float t = red[0][threadIdx.x];
 #pragma unroll
         for (int k = 1; k < kRgGroups; ++k) t += red[k][threadIdx.x];
         if (p < Lk.total) grad[p] = t;
+        if (sumsq) {  // this block's partial of the clip_by_global_norm sum (ppo.py:84-90)
+            const double q = p < Lk.total ? (double)t * (double)t : 0.0;
+            const double w = wave_sum64d(q);
+            if (threadIdx.x == 0) sumsq[blockIdx.x] = w;
+        }
     }
 }
 
@@ -1361,7 +1367,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     }
     LayoutK Lk = make_layout(p);
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
-                       dim3(256), 0, s, Lk, ws, grad);
+                       dim3(256), 0, s, Lk, ws, grad, h.grad_sumsq_out);
     return check_launch("ppo_minibatch_grad");
 }
 
@@ -1507,7 +1513,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     }
     LayoutK Lk = make_layout_lstm(p, lstm);
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)), dim3(256), 0,
-                       s, Lk, ws, grad);
+                       s, Lk, ws, grad, h.grad_sumsq_out);
     return check_launch("lstm_ppo_minibatch_grad");
 }
 
@@ -1521,6 +1527,10 @@ extern "C" {
 // diagnostic builds only: phase timestamps of the fused minibatch kernel
 void mlearn_debug_set_stamp_buffer(uint64_t* buf) { g_stamp_buf = buf; }
 #endif
+
+int64_t mlearn_grad_sumsq_parts(int64_t param_count) {
+    return param_count < 1 ? -1 : (param_count + 63) / 64;
+}
 
 int64_t mlearn_param_count(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -65,7 +65,8 @@ class PPOHparams(Structure):
     _fields_ = [("clip_coef", c_float), ("value_loss_coef", c_float),
                 ("entropy_coef", c_float * MAX_GROUPS), ("normalize_advantages", c_int32),
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
-                ("loss_scale", c_float), ("normalize_values", c_int32)]
+                ("loss_scale", c_float), ("normalize_values", c_int32),
+                ("grad_sumsq_out", c_void_p)]
 
 
 class OptimState(Structure):
@@ -73,7 +74,8 @@ class OptimState(Structure):
                 ("adam_v", c_void_p), ("init_norms", c_void_p), ("step", c_void_p),
                 ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float),
                 ("max_grad_norm", c_float), ("normalize_params", c_int32),
-                ("normalize_layernorms", c_int32)]
+                ("normalize_layernorms", c_int32), ("grad_sumsq_part", c_void_p),
+                ("grad_sumsq_nparts", c_int64)]
 
 
 class Lstm(Structure):  # mlearn_lstm
@@ -94,6 +96,7 @@ _P = c_void_p
 _SIGNATURES = {
     "mlearn_last_error": (c_char_p, []),
     "mlearn_abi_version": (c_int32, []),
+    "mlearn_grad_sumsq_parts": (c_int64, [c_int64]),
     "mlearn_philox4x32": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64, _S]),
     "mlearn_counters_add": (c_int32, [_P, c_int32, POINTER(c_uint64), _S]),
     "mlearn_gae_f32": (c_int32, [_P, _P, _P, _P, _P, _P, c_int32, c_int64, c_float, c_float, _S]),

@@ -147,6 +147,16 @@ class PPO(AlgoBase):  # ppo.py:49-106
         hp.clip_value_loss = 1 if algo.clip_value_loss else 0
         hp.huber_value_loss = 1 if algo.huber_value_loss else 0
         hp.loss_scale = 1.0 / dp.world_size
+        # single-rank training: the gradient reduction also emits the partial
+        # sums of squares clip_by_global_norm needs, so the optimizer step skips
+        # its own pass over the gradient (under DP the norm is of the
+        # all-reduced gradient and the optimizer computes it)
+        if dp.world_size == 1:
+            nparts = int(nat.lib().mlearn_grad_sumsq_parts(policy_state.layout["total"]))
+            self.gsq = torch.zeros(nparts, dtype=torch.float64, device=dev)
+            hp.grad_sumsq_out = self.gsq.data_ptr()
+            train_state.optim_desc.grad_sumsq_part = self.gsq.data_ptr()
+            train_state.optim_desc.grad_sumsq_nparts = nparts
         # value normaliser (normalize_values, ppo.py:190-211): the returns'
         # per-minibatch sums join the advantage sums' collective; one chain
         # launch per epoch turns them into per-minibatch estimate records

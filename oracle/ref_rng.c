@@ -133,11 +133,16 @@ void oracle_gumbel_table(uint32_t k0, uint32_t k1, uint64_t step, uint32_t env_o
 /* ---- synthetic dummy env (misc.hip env_step_kernel restated) ---- */
 static int episode_len(uint32_t g) { return 16 + (int)((g * 7u) % 33u); }
 
+/* One Philox4x32-10 call per 4 features (counter {env, f / 4, step}):
+ * feature f reads word f % 4 as four bytes b_i, s = sum (b_i + 0.5) / 256
+ * (Irwin-Hall n = 4 of 8-bit uniforms, exact in f32), obs = (s - 2) sqrt(3)
+ * (mean 0, variance 1). */
 static float obs_feature(uint32_t k0, uint32_t k1, uint32_t g, int f, uint64_t step) {
-    ctr4 c = {{g, (uint32_t)f, (uint32_t)step, (uint32_t)(step >> 32)}};
+    ctr4 c = {{g, (uint32_t)(f >> 2), (uint32_t)step, (uint32_t)(step >> 32)}};
     ctr4 r = philox(c, k0, k1 ^ 0x5eedu);
-    float s = ((unit(r.v[0]) + unit(r.v[1])) + unit(r.v[2])) + unit(r.v[3]);
-    return (s - 2.0f) * 1.73205077648162841796875f;
+    uint32_t w = r.v[f & 3];
+    uint32_t b = (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24) + 2u;
+    return ((float)b * 0.00390625f - 2.0f) * 1.73205077648162841796875f;
 }
 
 void oracle_env_reset(int32_t* state, int64_t N, int32_t D, uint32_t k0, uint32_t k1,
