@@ -423,6 +423,8 @@ typedef struct mlearn_lstm_carry {
     void* start_c;
     int32_t commit;
     int32_t pad;
+    const uint8_t* clear;    /* may be NULL: [N] extra reset mask, cleared like post->dones
+                                (the sequence breaks of ActorCritic.update, rnn.py:92-96) */
 } mlearn_lstm_carry;
 
 int64_t mlearn_lstm_param_offset(const mlearn_mlp_policy* policy);
@@ -438,6 +440,23 @@ int mlearn_lstm_policy_rollout_step(const mlearn_mlp_policy* policy, const mlear
                                     const uint64_t* step_ctr, uint64_t step,
                                     uint32_t env_offset, int32_t sample,
                                     const mlearn_post_step* post, mlearn_stream_t stream);
+
+/* ActorCritic.update's forward for a feed-forward policy on a flattened
+ * batch of N rows (actor_critic.py:98-128 with DiscreteActionDistributions.
+ * action_stats, dists.py:54-77): per sub-action the log-prob of the given
+ * action (logits - logsumexp) and the entropy -sum softmax * log_softmax,
+ * and the critic output (the scalar value, or the two-hot mean()).  obs is
+ * [N][obs_dim] f32 (cast to the compute dtype as in the rollout), actions /
+ * log_probs / entropies [N][K]. */
+int mlearn_policy_evaluate(const mlearn_mlp_policy* policy, const float* obs, int64_t N,
+                           const int32_t* actions, float* log_probs, float* entropies,
+                           float* values, mlearn_stream_t stream);
+/* One time step of the recurrent ActorCritic.update forward: the carry
+ * (cleared first where carry->clear is set) is advanced when carry->commit. */
+int mlearn_lstm_policy_evaluate(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                const mlearn_lstm_carry* carry, const float* obs, int64_t N,
+                                const int32_t* actions, float* log_probs, float* entropies,
+                                float* values, mlearn_stream_t stream);
 
 /* Minibatch gradient of the recurrent policy (ActorCritic.update with
  * RecurrentBackboneEncoder.sequence, actor_critic.py:98-128, 179-199;

@@ -41,6 +41,23 @@ __device__ inline void sample_group(const float* lg, int nb, int jbase, uint32_t
     if (logp) *logp = lg[best] - lse;
 }
 
+// DiscreteActionDistributions.action_stats (dists.py:54-77) of one group:
+// log_softmax = logits - logsumexp, log-prob of the given action a, entropy
+// -sum softmax * log_softmax.
+__device__ inline void eval_group(const float* lg, int nb, int a, float* logp, float* ent) {
+#pragma clang fp contract(off)
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    const float lse = mx + __logf(se), inv = 1.0f / se;
+    float e = 0.f;
+    for (int j = 0; j < nb; ++j) e -= (__expf(lg[j] - mx) * inv) * (lg[j] - lse);
+    a = a < 0 ? 0 : (a >= nb ? nb - 1 : a);
+    *logp = lg[a] - lse;
+    *ent = e;
+}
+
 // ---------------------------------------------------------------------------
 // SymExpTwoHotDistribution (dists.py:119-208) over the nb critic logits of a
 // DreamerV3Critic (models.py:157-174), logits already cast to f32.

@@ -119,6 +119,14 @@ struct CarryK {
     void* sh;
     void* sc;
     int commit;
+    const uint8_t* clear;  // extra reset mask (ActorCritic.update's sequence breaks)
+};
+
+// ActorCritic.update forward (evaluate mode): given actions in, per
+// sub-action entropies out (log-probs go to logp).
+struct EvalK {
+    const int32_t* actions;
+    float* entropies;
 };
 
 // RNN: the LSTM cell (RecurrentBackboneEncoder, actor_critic.py:173-177)
@@ -132,7 +140,7 @@ template <typename T, int H, bool RNN, int HC>
 __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy) {
+    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev) {
     typedef typename RT<T>::frag frag;
     typedef PolCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
@@ -238,7 +246,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
 
     if constexpr (RNN) {
         // carry rows, cleared where the previous env step was done (rollouts.py:942)
-        const bool clr = post.rew && live && post.done[row] != 0;
+        const bool clr = live && ((post.rew && post.done[row] != 0) ||
+                                  (cy.clear && cy.clear[row] != 0));
         const T* hrow = (const T*)cy.h + (live ? row : 0) * H;
         constexpr int SPW = KSH / W;  // k-steps staged per wave
 #pragma unroll
@@ -358,6 +367,17 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             actions[n * P.K + g] = a;
             if (logp) logp[n * P.K + g] = lp;
         }
+    } else if (ev.actions) {
+        for (int task = tid; task < 32 * P.K; task += THREADS) {
+            const int rr = task / P.K, g = task - rr * P.K;
+            const int64_t n = row0 + rr;
+            if (n >= N) continue;
+            float lp, ent;
+            eval_group(lg + rr * LGS + P.off[g], P.off[g + 1] - P.off[g], ev.actions[n * P.K + g],
+                       &lp, &ent);
+            logp[n * P.K + g] = lp;
+            ev.entropies[n * P.K + g] = ent;
+        }
     }
     // observation statistics of this step (update_obs_stats, rollouts.py:670-676):
     // the tile's {mean, M2} of the raw observations per feature, 4 lanes per
@@ -411,7 +431,8 @@ template <typename T, int H, bool RNN, int HC>
 static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, void* obs_store,
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
-                              const PostK& post, const LstmK& R, const CarryK& cy, hipStream_t s) {
+                              const PostK& post, const LstmK& R, const CarryK& cy, const EvalK& ev,
+                              hipStream_t s) {
     const size_t lds = policy_step_lds<T, H, RNN, HC>(P.L);
     auto kern = policy_step_kernel<T, H, RNN, HC>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
@@ -423,7 +444,7 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
     const int grid = (int)((N + 31) / 32);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
                        (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
-                       post, R, cy);
+                       post, R, cy, ev);
     return check_launch("policy_rollout_step");
 }
 
@@ -432,14 +453,16 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
                               void* obs_store, int32_t* actions, float* log_probs, float* values,
                               uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint64_t step,
                               uint32_t env_offset, int32_t sample, const mlearn_post_step* post,
-                              mlearn_stream_t stream) {
+                              mlearn_stream_t stream, EvalK ev = EvalK{}) {
     int rc = lstm ? validate_lstm(policy, lstm) : validate_policy(policy);
     if (rc) return rc;
     ML_REQUIRE(N >= 0, "policy_rollout_step: N < 0");
     if (N == 0) return MLEARN_OK;
     ML_REQUIRE(obs, "policy_rollout_step: null obs");
     ML_REQUIRE(!actions || log_probs || !sample, "policy_rollout_step: sampling needs log_probs");
-    ML_REQUIRE(actions || values, "policy_rollout_step: nothing to compute");
+    ML_REQUIRE(!ev.actions || (!actions && log_probs && ev.entropies),
+               "policy_evaluate: needs log_probs and entropies outputs");
+    ML_REQUIRE(actions || values || ev.actions, "policy_rollout_step: nothing to compute");
     ML_REQUIRE(!policy->obs_stats || !actions || policy->obs_stats_tiles >= (N + 31) / 32,
                "policy_rollout_step: obs_stats_tiles %lld < ceil(N / 32)",
                (long long)policy->obs_stats_tiles);
@@ -462,17 +485,17 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
         ML_REQUIRE((uintptr_t)carry->h % 16 == 0 && (uintptr_t)carry->c % 16 == 0,
                    "lstm rollout step: carry must be 16-byte aligned");
         R = make_lstm_k(*lstm);
-        cy = CarryK{carry->h, carry->c, carry->start_h, carry->start_c, carry->commit};
+        cy = CarryK{carry->h, carry->c, carry->start_h, carry->start_c, carry->commit, carry->clear};
     }
     PolicyK P = make_policy_k(*policy);
     hipStream_t s = S(stream);
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \
     (lstm ? launch_policy_step<T, HH, true, HC>(P, obs, N, obs_store, actions, log_probs, values, \
                                                 k0, k1, step_ctr, step, env_offset, sample, pk, R, \
-                                                cy, s)                                            \
+                                                cy, ev, s)                                        \
           : launch_policy_step<T, HH, false, HC>(P, obs, N, obs_store, actions, log_probs, values, \
                                                  k0, k1, step_ctr, step, env_offset, sample, pk, R, \
-                                                 cy, s))
+                                                 cy, ev, s))
 #define ML_LAUNCH(T, HH) \
     (P.HC == MLEARN_HEAD_COLS ? ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS) : ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS_MAX))
 #define ML_DISPATCH(T)                      \
@@ -513,6 +536,26 @@ extern "C" int mlearn_lstm_policy_rollout_step(
     ML_REQUIRE(lstm, "lstm rollout step: null lstm descriptor");
     return rollout_step_entry(policy, lstm, carry, obs, N, obs_store, actions, log_probs, values,
                               k0, k1, step_ctr, step, env_offset, sample, post, stream);
+}
+
+extern "C" int mlearn_policy_evaluate(const mlearn_mlp_policy* policy, const float* obs,
+                                      int64_t N, const int32_t* actions, float* log_probs,
+                                      float* entropies, float* values, mlearn_stream_t stream) {
+    ML_REQUIRE(actions, "policy_evaluate: null actions");
+    return rollout_step_entry(policy, nullptr, nullptr, obs, N, nullptr, nullptr, log_probs, values,
+                              0, 0, nullptr, 0, 0, 0, nullptr, stream, EvalK{actions, entropies});
+}
+
+extern "C" int mlearn_lstm_policy_evaluate(const mlearn_mlp_policy* policy,
+                                           const mlearn_lstm* lstm,
+                                           const mlearn_lstm_carry* carry, const float* obs,
+                                           int64_t N, const int32_t* actions, float* log_probs,
+                                           float* entropies, float* values,
+                                           mlearn_stream_t stream) {
+    ML_REQUIRE(lstm, "lstm policy_evaluate: null lstm descriptor");
+    ML_REQUIRE(actions, "lstm policy_evaluate: null actions");
+    return rollout_step_entry(policy, lstm, carry, obs, N, nullptr, nullptr, log_probs, values, 0,
+                              0, nullptr, 0, 0, 0, nullptr, stream, EvalK{actions, entropies});
 }
 
 extern "C" int32_t mlearn_head_cols(const mlearn_mlp_policy* policy) {

@@ -86,7 +86,7 @@ class Lstm(Structure):  # mlearn_lstm
 
 class LstmCarry(Structure):  # mlearn_lstm_carry
     _fields_ = [("h", c_void_p), ("c", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
-                ("commit", c_int32), ("pad", c_int32)]
+                ("commit", c_int32), ("pad", c_int32), ("clear", c_void_p)]
 
 
 _S = c_void_p  # hipStream_t
@@ -112,6 +112,9 @@ _SIGNATURES = {
     "mlearn_policy_rollout_step": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P,
                                              c_uint32, c_uint32, _P, c_uint64, c_uint32, c_int32,
                                              POINTER(PostStep), _S]),
+    "mlearn_policy_evaluate": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P, _S]),
+    "mlearn_lstm_policy_evaluate": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
+                                              _P, c_int64, _P, _P, _P, _P, _S]),
     "mlearn_rollout_post_step": (c_int32, [_P, _P, c_int64, _P, _P, _P, _P, c_float, _S]),
     "mlearn_metrics_workspace_bytes": (c_int64, [c_int32]),
     "mlearn_metrics_f32": (c_int32, [POINTER(MetricJob), c_int32, _P, _P, _S]),

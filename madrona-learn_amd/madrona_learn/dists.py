@@ -83,3 +83,54 @@ class DiscreteActionDistributions:
             out.append(self.all_logits[..., off:off + b].float())
             off += b
         return out
+
+
+def _symexp(x):  # utils.py:39-40
+    return torch.sign(x) * torch.expm1(torch.abs(x))
+
+
+class SymExpTwoHotDistribution:  # dists.py:119-208 (critic of DreamerV3Critic)
+    """Torch form for trees outside the fused path; the fused kernels compute
+    the same mean() / two-hot cross entropy in csrc/dists.h."""
+
+    def __init__(self, logits):
+        self.logits = logits.float()
+
+    @staticmethod
+    def create(logits):
+        return SymExpTwoHotDistribution(logits)
+
+    def _compute_bins(self):
+        nb = self.logits.shape[-1]
+        assert nb % 2 == 1 and nb > 1
+        half = _symexp(torch.linspace(-14, 0, nb // 2 + 1, dtype=torch.float32,
+                                      device=self.logits.device))
+        return torch.cat([half, -torch.flip(half[:-1], [0])])
+
+    def mean(self):
+        bins = self._compute_bins()
+        mid = (bins.shape[-1] - 1) // 2
+        p = torch.softmax(self.logits, -1)
+        lo = (p[..., :mid] * bins[:mid]).flip(-1)
+        hi = p[..., mid + 1:] * bins[mid + 1:]
+        return (p[..., mid:mid + 1] * bins[mid:mid + 1]).sum(-1, keepdim=True) + \
+            (lo + hi).sum(-1, keepdim=True)
+
+    def two_hot_cross_entropy_loss(self, targets):
+        bins = self._compute_bins()
+        nb = bins.shape[-1]
+        t = targets.float()
+        lo = ((bins <= t).int().sum(-1) - 1).clamp(0, nb - 1)
+        up = (nb - (bins > t).int().sum(-1)).clamp(0, nb - 1)
+        same = (lo == up)[..., None]
+        one = torch.ones_like(t)
+        dl = torch.where(same, one, torch.abs(bins[lo][..., None] - t))
+        du = torch.where(same, one, torch.abs(bins[up][..., None] - t))
+        tot = dl + du
+        two_hot = (torch.nn.functional.one_hot(lo, nb) * (dl / tot) +
+                   torch.nn.functional.one_hot(up, nb) * (du / tot))
+        logp = self.logits - torch.logsumexp(self.logits, -1, keepdim=True)
+        return -(two_hot * logp).sum(-1, keepdim=True)
+
+    def reshape(self, *shape):
+        return SymExpTwoHotDistribution(self.logits.reshape(*shape, self.logits.shape[-1]))

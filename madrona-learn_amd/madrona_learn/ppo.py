@@ -139,11 +139,18 @@ class PPO(AlgoBase):  # ppo.py:49-106
         ec = float(_base(ec))
         for k in range(K):
             hp.entropy_coef[k] = ec
-        hp.normalize_advantages = 1 if (cfg.normalize_advantages and cfg.compute_advantages) \
-            else 0
-        if not cfg.compute_advantages:
-            raise NotImplementedError("compute_advantages=False (returns as the objective) is "
-                                      "not on the fused path yet")
+        # ppo.py:134-143: the surrogate's "advantages" are the advantages
+        # (z-scored if normalize_advantages), or with compute_advantages=False
+        # the returns (z-scored if normalize_returns); the rollout view then
+        # points its advantage column at the returns (RolloutManager.view)
+        if cfg.compute_advantages:
+            hp.normalize_advantages = 1 if cfg.normalize_advantages else 0
+        else:
+            if cfg.normalize_values:
+                raise NotImplementedError(
+                    "compute_advantages=False with normalize_values: the returns' bootstrap "
+                    "would need the inverted critic (rollouts.py:726-738, 771-775)")
+            hp.normalize_advantages = 1 if cfg.normalize_returns else 0
         hp.clip_value_loss = 1 if algo.clip_value_loss else 0
         hp.huber_value_loss = 1 if algo.huber_value_loss else 0
         hp.loss_scale = 1.0 / dp.world_size

@@ -178,8 +178,10 @@ class RolloutStore:
         return v
 
 
-ROLLOUT_METRICS = ["Rewards", "Values", "Est Returns", "Env Returns", "Advantages",
-                   "Bootstrap Values"]
+# (order of the metric jobs below; 'Advantages' only with compute_advantages,
+# rollouts.py:482-499)
+ROLLOUT_METRICS = ["Rewards", "Values", "Est Returns", "Env Returns", "Bootstrap Values",
+                   "Advantages"]
 
 
 def obs_to_matrix(obs, N):
@@ -249,14 +251,14 @@ class RolloutManager:  # rollouts.py:373-826
         s = self.store
         TN = self.T * self.B
         self._jobs = []
+        self._nmet = len(ROLLOUT_METRICS) - (0 if self.use_advantages else 1)
         for p in range(self.P):
             c0 = p * self.B
             jobs = (nat.MetricJob * 6)()
-            for i, (x, n, cols) in enumerate([(s.rewards, TN, self.B), (s.values, TN, self.B),
-                                              (s.returns, TN, self.B),
-                                              (s.env_returns_trace, TN, self.B),
-                                              (s.advantages, TN, self.B),
-                                              (s.bootstrap, self.B, 0)]):
+            srcs = [(s.rewards, TN, self.B), (s.values, TN, self.B), (s.returns, TN, self.B),
+                    (s.env_returns_trace, TN, self.B), (s.bootstrap, self.B, 0),
+                    (s.advantages, TN, self.B)]
+            for i, (x, n, cols) in enumerate(srcs[:self._nmet]):
                 jobs[i].x = x.data_ptr() + c0 * 4
                 jobs[i].n = n
                 jobs[i].cols = cols if self.P > 1 else 0
@@ -265,8 +267,13 @@ class RolloutManager:  # rollouts.py:373-826
             self._jobs.append(jobs)
 
     def view(self, p=0):
-        """Rollout view of policy p's env columns."""
-        return self.store.view(self.bptt, p * self.B, self.B)
+        """Rollout view of policy p's env columns.  With compute_advantages=False
+        the surrogate objective reads the returns (ppo.py:139-143): the view's
+        advantage column is the returns column."""
+        v = self.store.view(self.bptt, p * self.B, self.B)
+        if not self.use_advantages:
+            v.advantages = v.returns
+        return v
 
     def start_states(self, p=0):
         """Device pointers of policy p's rnn_start_states columns ([C][ld][H],
@@ -297,7 +304,7 @@ class RolloutManager:  # rollouts.py:373-826
         return d
 
     def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
-        return list(names) + ROLLOUT_METRICS
+        return list(names) + ROLLOUT_METRICS[:self._nmet]
 
     def prep_obs(self, obs):
         x = self.prefix(obs, train=False)
@@ -383,8 +390,8 @@ class RolloutManager:  # rollouts.py:373-826
         else:
             compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s.returns)
         for p in range(self.P):
-            nat.check(L.mlearn_metrics_f32(self._jobs[p], 6,
-                                           nat.ptr(metrics.slots("Rewards", 6, policy=p)),
+            nat.check(L.mlearn_metrics_f32(self._jobs[p], self._nmet,
+                                           nat.ptr(metrics.slots("Rewards", self._nmet, policy=p)),
                                            nat.ptr(self._metrics_ws), strm), "rollout metrics")
         nat.check(L.mlearn_counters_add(nat.ptr(rollout_state.counters), 1,
                                         (nat.c_uint64 * 1)(self.T), strm), "counters")

@@ -243,6 +243,9 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         pss.append(ps)
         tss.append(ts)
         algos.append(algo)
+    # ActorCritic.rollout / update / critic_only / actor_only of the user's
+    # tree now run on the (first) training policy's parameters
+    policy.actor_critic.bind(pss[0])
     value_norm = None
     if cfg.normalize_values:
         # EMANormalizer.init_estimates per train policy (moving_avg.py:56-76,

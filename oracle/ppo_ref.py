@@ -342,6 +342,19 @@ def _dmin(a, b):
     return np.where(a < b, 1.0, np.where(a == b, 0.5, 0.0))
 
 
+def objective_key(hp):
+    """ppo.py:134-143: the surrogate uses the advantages, or with
+    compute_advantages=False the returns."""
+    return "advantages" if hp.get("compute_advantages", True) else "returns"
+
+
+def objective_normalized(hp):
+    """normalize_advantages (compute_advantages) / normalize_returns (not)."""
+    if hp.get("compute_advantages", True):
+        return hp.get("normalize_advantages", True)
+    return hp.get("normalize_returns", True)
+
+
 def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0,
                    ad=np.float64):
     """PPO loss (ppo.py:129-262) and d loss / d head outputs [M, A+1]
@@ -351,9 +364,9 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
     K = len(buckets)
     acts = np.asarray(batch["actions"])
     old = np.asarray(batch["log_probs"], ad)
-    adv = np.asarray(batch["advantages"], ad)
+    adv = np.asarray(batch[objective_key(hp)], ad)
     R = np.asarray(batch["returns"], ad)
-    if hp.get("normalize_advantages", True):
+    if objective_normalized(hp):
         if adv_stats is None:
             mean, var = adv.mean(), adv.var()
         else:
@@ -591,7 +604,8 @@ def ppo_update(flat_p, opt, stores, hp, buckets, lay, init_norms, *, num_epochs,
             for r in range(world):
                 ids = perms[r][mb_i * minibatch_size:(mb_i + 1) * minibatch_size]
                 batches.append(gather_minibatch(stores[r], minibatch_rows(ids, N, bptt)))
-            alladv = np.concatenate([np.asarray(b["advantages"], np.float64) for b in batches])
+            alladv = np.concatenate([np.asarray(b[objective_key(hp)], np.float64)
+                                     for b in batches])
             stats = (alladv.mean(), alladv.var())
             hp_mb = hp
             if value_norm is not None:

@@ -145,3 +145,41 @@ def test_graph_replay_matches_eager(gpu):
     assert graph._segments is not None
     assert torch.equal(eager.state.policy_states.params, graph.state.policy_states.params)
     assert torch.equal(eager.rollout_mgr.store.actions, graph.rollout_mgr.store.actions)
+
+
+@pytest.mark.parametrize("normalize_returns", [True, False])
+def test_returns_objective_matches_oracle(gpu, normalize_returns):
+    """compute_advantages=False (cfg.py:87-89): the rollout computes discounted
+    returns (algo_common.py:45-81, bit-exact) and the surrogate uses them as
+    its "advantages", z-scored per minibatch if normalize_returns
+    (ppo.py:139-143); no 'Advantages' metric (rollouts.py:494-495)."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    dtype, N, H, mb = torch.float32, 64, 64, 16
+    env = DummyVecEnv(N, 64, 6, seed=2, device=gpu)
+    cfg = dataclasses.replace(make_cfg(dtype, N=N, H=H, mb=mb), compute_advantages=False,
+                              normalize_returns=normalize_returns)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(dtype, H), use_graph=False)
+    assert "Advantages" not in mgr.metrics.index
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    p0 = ps.params.cpu().numpy().astype(np.float64)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    ret = ref.discounted_returns_f32(s.rewards.cpu().numpy(), s.dones.cpu().numpy(),
+                                     s.bootstrap.cpu().numpy(), cfg.gamma)
+    assert np.array_equal(s.returns.cpu().numpy(), ret)
+    store = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+             for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "compute_advantages": False, "normalize_returns": normalize_returns}
+    lay = ref.param_layout(64, H, 2, 26)
+    zeros = np.zeros_like(p0)
+    p1, _, met = ref.ppo_update(
+        p0, (zeros, zeros.copy(), 0), [store], hp, BUCKETS, lay,
+        ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=mb,
+        bptt=cfg.steps_per_update, key=ts.update_prng_key, epoch_base=0, mode="f32", lr=3e-4,
+        max_grad_norm=0.5)
+    np.testing.assert_allclose(ps.params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(mgr.metrics.last()["Loss"].mean, met["Loss"], rtol=1e-4, atol=1e-6)
