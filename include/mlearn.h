@@ -296,13 +296,21 @@ int mlearn_value_norm_chain(const double* return_sums, const float* adv_stats, i
 typedef struct mlearn_ppo_hparams {
     float clip_coef;
     float value_loss_coef;
-    float entropy_coef[MLEARN_MAX_GROUPS]; /* per sub-action (ppo.py:231-239) */
+    float entropy_coef[MLEARN_MAX_GROUPS]; /* per sub-action j (ppo.py:231-239), see obj_weight */
     int32_t normalize_advantages;          /* TrainConfig.normalize_advantages */
     int32_t clip_value_loss;               /* PPOConfig.clip_value_loss */
     int32_t huber_value_loss;              /* PPOConfig.huber_value_loss */
     float loss_scale;                      /* 1/world_size under DP (mean of means) */
     int32_t normalize_values;              /* TrainConfig.normalize_values: adv_stats is a
                                               mlearn_value_norm_chain record */
+    float obj_weight[MLEARN_MAX_GROUPS];   /* per sub-action j; 0 means 1.  The loss is
+                                              -sum_j obj_weight[j] sum_rows obj_j / (M K)
+                                              + c_v mean(vl)
+                                              - sum_j entropy_coef[j] sum_rows H_j / (M K)
+                                              (K sub-actions, M rows).  The reference's
+                                              per-action-group means (ppo.py:221-239) are
+                                              obj_weight[j] = K / K_g and entropy_coef[j] =
+                                              c_g K / K_g for the group g holding j. */
     double* grad_sumsq_out;                /* may be NULL: per-64-parameter partial sums of
                                               grad^2 (mlearn_grad_sumsq_parts entries),
                                               written by the gradient reduction; the next

@@ -42,6 +42,7 @@ struct RolloutK {
 struct HpK {
     float clip, vcoef;
     float ecoef[MLEARN_MAX_GROUPS];
+    float objw[MLEARN_MAX_GROUPS];  // per sub-action surrogate weight (K / K_key)
     int norm_adv, clip_vl, huber, norm_vals;
     int metrics;  // reduce the loss metrics (only the minibatch whose metrics are recorded)
     float loss_scale;
@@ -182,6 +183,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
 // ---------------------------------------------------------------------------
 struct LossAcc {
     float sobj = 0, qobj = 0, sent = 0, qent = 0, svl = 0, qvl = 0, serr = 0, qerr = 0, sentw = 0;
+    float sobjw = 0;  // surrogate sum weighted per action group (reduce_action_objs)
     float mnobj = 3.4e38f, mxobj = -3.4e38f, mnent = 3.4e38f, mxent = -3.4e38f;
     float mnvl = 3.4e38f, mxvl = -3.4e38f, mnerr = 3.4e38f, mxerr = -3.4e38f;
 };
@@ -189,7 +191,7 @@ struct LossAcc {
 // PPO objective terms of one action group given its log-prob of the taken
 // action and entropy; returns d loss / d logp[a] and accumulates metrics.
 __device__ inline float ppo_obj(const HpK& hp, float lpa, float old_lp, float adv, float ent,
-                                float ecoef, LossAcc& m) {
+                                float ecoef, float objw, LossAcc& m) {
     const float ratio = __expf(lpa - old_lp);
     const float lo = 1.0f - hp.clip, hi = 1.0f + hp.clip;
     const float s1 = adv * ratio;
@@ -211,14 +213,15 @@ __device__ inline float ppo_obj(const HpK& hp, float lpa, float old_lp, float ad
     m.mnent = fminf(m.mnent, ent);
     m.mxent = fmaxf(m.mxent, ent);
     m.sentw += ecoef * ent;
-    return -hp.inv_sk * dobj * ratio;
+    m.sobjw += objw * obj;
+    return -hp.inv_sk * objw * dobj * ratio;
 }
 
 // Group of at most MAXB logits held in registers (fixed width, masked): no
 // dynamically indexed register arrays.
 template <int MAXB>
 __device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a, float old_lp,
-                                        float adv, float ecoef, LossAcc& m) {
+                                        float adv, float ecoef, float objw, LossAcc& m) {
     float v[MAXB];
 #pragma unroll
     for (int j = 0; j < MAXB; ++j) v[j] = j < nb ? lg[j] : -3.4e38f;
@@ -239,7 +242,7 @@ __device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a,
         if (j < nb) ent -= (ex[j] * inv) * (v[j] - lse);  // dists.py:68-69
         lpa = j == a ? v[j] - lse : lpa;
     }
-    const float g_lp = ppo_obj(hp, lpa, old_lp, adv, ent, ecoef, m);
+    const float g_lp = ppo_obj(hp, lpa, old_lp, adv, ent, ecoef, objw, m);
     const float ce = ecoef * hp.inv_sk;  // entropy term weight
 #pragma unroll
     for (int j = 0; j < MAXB; ++j) {
@@ -251,9 +254,9 @@ __device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a,
 
 // Any group size (<= 31): three passes over the logits in LDS.
 __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float old_lp, float adv,
-                                  float ecoef, LossAcc& m) {
+                                  float ecoef, float objw, LossAcc& m) {
     if (nb <= 8) {
-        loss_group_fixed<8>(hp, lg, nb, a, old_lp, adv, ecoef, m);
+        loss_group_fixed<8>(hp, lg, nb, a, old_lp, adv, ecoef, objw, m);
         return;
     }
     float mx = lg[0];
@@ -264,7 +267,7 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
     const float lse = mx + __logf(se);
     float ent = 0.f;
     for (int j = 0; j < nb; ++j) ent -= (__expf(lg[j] - mx) * inv) * (lg[j] - lse);
-    const float g_lp = ppo_obj(hp, lg[a] - lse, old_lp, adv, ent, ecoef, m);
+    const float g_lp = ppo_obj(hp, lg[a] - lse, old_lp, adv, ent, ecoef, objw, m);
     const float ce = ecoef * hp.inv_sk;
     for (int j = 0; j < nb; ++j) {
         const float lj = lg[j];
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
             if (g < K) {
                 if (hp.norm_adv) adv = (adv - as0) * as1;
                 loss_group(hp, lr + P.off[g], P.off[g + 1] - P.off[g], act, olp, adv, hp.ecoef[g],
-                           m);
+                           hp.objw[g], m);
             } else {
                 loss_value(hp, lr, P.A, HC, ret, oval, m, vn);
             }
@@ -665,8 +668,8 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         }
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
                                         m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
-                                        m.mnent, m.mxent, m.sentw, 0.f, 0.f, 0.f};
-        constexpr int kUsed = 17;  // slots 17.. are padding
+                                        m.mnent, m.mxent, m.sentw, m.sobjw, 0.f, 0.f};
+        constexpr int kUsed = 18;  // slots 18.. are padding
         if (!hp.metrics) {
         } else if (__any(did)) {
 #pragma unroll
@@ -1276,9 +1279,10 @@ __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K
     __syncthreads();
     if (tid == 0) {
         const double nk = (double)M * K, n = (double)M;
-        const double obj_mean = tot[0] / nk, vl_mean = tot[4] / n;
-        // loss = -mean(obj) + c_v * mean(vl) - sum_k c_e[k] * mean(H_k)   (ppo.py:241-252)
-        const double loss = -obj_mean + hp.vcoef * vl_mean - tot[16] / nk;
+        const double vl_mean = tot[4] / n;
+        // loss = -sum_key mean(obj_key) + c_v * mean(vl) - sum_key c_e[key] * mean(H_key)
+        // (ppo.py:221-252); the per-sub-action weights K / K_key are in slots 16, 17
+        const double loss = -tot[17] / nk + hp.vcoef * vl_mean - tot[16] / nk;
         out[0] = (float)loss;
         out[1] = 0.f;
         out[2] = (float)loss;
@@ -1314,7 +1318,10 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     HpK hp{};
     hp.clip = h.clip_coef;
     hp.vcoef = h.value_loss_coef;
-    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
+    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) {
+        hp.ecoef[i] = h.entropy_coef[i];
+        hp.objw[i] = h.obj_weight[i] != 0.f ? h.obj_weight[i] : 1.f;
+    }
     hp.norm_adv = h.normalize_advantages;
     hp.clip_vl = h.clip_value_loss;
     hp.norm_vals = h.normalize_values;
@@ -1396,7 +1403,10 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     HpK hp{};
     hp.clip = h.clip_coef;
     hp.vcoef = h.value_loss_coef;
-    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) hp.ecoef[i] = h.entropy_coef[i];
+    for (int i = 0; i < MLEARN_MAX_GROUPS; ++i) {
+        hp.ecoef[i] = h.entropy_coef[i];
+        hp.objw[i] = h.obj_weight[i] != 0.f ? h.obj_weight[i] : 1.f;
+    }
     hp.norm_adv = h.normalize_advantages;
     hp.clip_vl = h.clip_value_loss;
     hp.norm_vals = h.normalize_values;

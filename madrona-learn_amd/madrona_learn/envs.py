@@ -36,6 +36,8 @@ class DummyVecEnv:
 
     def step(self, inp):
         acts = inp["actions"]
+        if isinstance(acts, dict):  # several action groups: the first drives the reward
+            acts = next(iter(acts.values()))
         if acts.dtype != torch.int32 or not acts.is_contiguous():
             acts = acts.to(torch.int32).contiguous()
         nat.check(nat.lib().mlearn_dummy_env_step(
@@ -45,5 +47,19 @@ class DummyVecEnv:
         return {"state": self.state, "obs": self.obs, "rewards": self.rewards,
                 "dones": self.dones}
 
+    def get_ckpts(self):
+        """Per-env checkpoints (sim_fns['get_ckpts'], rollouts.py:300-301)."""
+        return self.state.clone()
+
+    def load_ckpts(self, ckpts, load_trigger=None):
+        """Restore per-env state (sim_fns['load_ckpts'], rollouts.py:303-309)."""
+        if load_trigger is None:
+            self.state.copy_(ckpts)
+        else:
+            m = load_trigger.reshape(-1).bool()
+            self.state[m] = ckpts.to(self.state.device)[m]
+        return self.obs
+
     def sim_fns(self):
-        return {"init": self.init, "step": self.step}
+        return {"init": self.init, "step": self.step, "get_ckpts": self.get_ckpts,
+                "load_ckpts": self.load_ckpts}

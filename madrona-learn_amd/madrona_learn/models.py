@@ -112,17 +112,36 @@ class MLP(nn.Module):  # models.py:99-119: Dense(no bias) -> LayerNorm -> ReLU p
         return x
 
 
+def action_groups(cfg):
+    """[(name, buckets)] of a DiscreteActionsConfig or of a dict name ->
+    DiscreteActionsConfig (TrainConfig.actions, cfg.py:73)."""
+    if isinstance(cfg, DiscreteActionsConfig):
+        return [("actions", list(cfg.actions_num_buckets))]
+    out = []
+    for k, v in cfg.items():
+        if not isinstance(v, DiscreteActionsConfig):
+            raise NotImplementedError(f"action group {k!r}: only discrete actions are supported")
+        out.append((k, list(v.actions_num_buckets)))
+    return out
+
+
 class DenseLayerDiscreteActor(nn.Module):  # models.py:122-139
-    def __init__(self, cfg: DiscreteActionsConfig, dtype, weight_init=orthogonal(0.01)):
+    """cfg: one DiscreteActionsConfig (the reference's head), or a dict of
+    them (several action groups from one Dense head, logits concatenated in
+    dict order; the distributions are keyed like TrainConfig.actions)."""
+
+    def __init__(self, cfg, dtype, weight_init=orthogonal(0.01)):
         super().__init__()
         self.cfg = cfg
         self.dtype = canonical_dtype(dtype)
         self.weight_init = weight_init
-        self.impl = _Dense(sum(cfg.actions_num_buckets), True, self.dtype, weight_init)
+        self.groups = action_groups(cfg)
+        self.buckets = [b for _, g in self.groups for b in g]
+        self.impl = _Dense(sum(self.buckets), True, self.dtype, weight_init)
 
     def forward(self, features, train=False):
         from .dists import DiscreteActionDistributions
-        return DiscreteActionDistributions(self.cfg.actions_num_buckets, self.impl(features))
+        return DiscreteActionDistributions(self.buckets, self.impl(features))
 
 
 class DenseLayerCritic(nn.Module):  # models.py:142-154 (output cast to f32)

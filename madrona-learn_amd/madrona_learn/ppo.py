@@ -129,16 +129,25 @@ class PPO(AlgoBase):  # ppo.py:49-106
         hp = nat.PPOHparams()
         hp.clip_coef = float(algo.clip_coef)
         hp.value_loss_coef = float(algo.value_loss_coef)
+        # action groups = the keys of cfg.actions (ppo.py:221-239): each key's
+        # surrogate and entropy are means over its own sub-actions, summed over
+        # the keys, each entropy with its key's coefficient -> per sub-action
+        # weights K / K_key (mlearn_ppo_hparams.obj_weight)
+        from .models import action_groups
+        groups = action_groups(cfg.actions)
+        if sum(len(b) for _, b in groups) != K or \
+                tuple(x for _, b in groups for x in b) != tuple(policy_state.arch.buckets):
+            raise ValueError(f"TrainConfig.actions {groups} does not match the actor's head "
+                             f"{policy_state.arch.buckets}")
         ec = algo.entropy_coef
-        # entropy coefficients are per action-group name (ppo.py:231-239); the fused
-        # head is the single discrete group, so one coefficient covers its K sub-actions
-        if isinstance(ec, dict):
-            if len(ec) != 1:
-                raise NotImplementedError("one discrete action group supported")
-            ec = next(iter(ec.values()))
-        ec = float(_base(ec))
-        for k in range(K):
-            hp.entropy_coef[k] = ec
+        j = 0
+        for name, b in groups:
+            c = ec[name] if isinstance(ec, dict) else ec
+            c = float(_base(c))
+            for _ in b:
+                hp.obj_weight[j] = K / len(b)
+                hp.entropy_coef[j] = c * K / len(b)
+                j += 1
         # ppo.py:134-143: the surrogate's "advantages" are the advantages
         # (z-scored if normalize_advantages), or with compute_advantages=False
         # the returns (z-scored if normalize_returns); the rollout view then

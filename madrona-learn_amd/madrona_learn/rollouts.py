@@ -303,6 +303,22 @@ class RolloutManager:  # rollouts.py:373-826
             self._carries[key] = d
         return d
 
+    def _sim_actions(self, t):
+        """The sim's 'actions' input of step t: the [N, K] store slice, or with
+        several action groups a dict keyed like TrainConfig.actions of [N, K_g]
+        views (rollouts.py:985-1002)."""
+        from .models import action_groups
+        if not hasattr(self, "_act_groups"):
+            self._act_groups = action_groups(self.train_cfg.actions)
+        a = self.store.actions[t]
+        if len(self._act_groups) == 1:
+            return a
+        out, off = {}, 0
+        for name, b in self._act_groups:
+            out[name] = a[:, off:off + len(b)]
+            off += len(b)
+        return out
+
     def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
         return list(names) + ROLLOUT_METRICS[:self._nmet]
 
@@ -354,7 +370,7 @@ class RolloutManager:  # rollouts.py:373-826
                                 carry=self._carry(rollout_state, p, t) if self.R else None)
             step_input = {
                 "state": rollout_state.sim_state,
-                "actions": s.actions[t],
+                "actions": self._sim_actions(t),
                 "resets": self._resets,
                 "sim_ctrl": rollout_state.sim_ctrl,
                 "pbt": {"policy_assignments": rollout_state.policy_assignments},

@@ -148,12 +148,77 @@ class TrainingManager:  # train.py:35-64
         self._replay()
 
     def save_ckpt(self, path):  # train.py:44-46
+        """<path>/<update_idx>.pt: the train state (TrainStateManager.save) plus
+        the rollout state a bit-identical resume needs: the device RNG counters
+        (rollout step = action sampling, epoch = minibatch permutations), the
+        running env returns, the current observations, the recurrent carry,
+        and the sim's own checkpoint when sim_fns provides 'get_ckpts'
+        (rollouts.py:206-215, 300-309)."""
+        torch.cuda.synchronize()
         os.makedirs(path, exist_ok=True)
-        self.state.save(self.update_idx, os.path.join(path, f"{self.update_idx}.pt"))
+        self.state.save(self.update_idx, os.path.join(path, f"{self.update_idx}.pt"),
+                        extra={"rollout": self._rollout_state_dict()})
 
     def load_ckpt(self, path):  # train.py:48-49
+        """A file written by save_ckpt, or its directory (latest update)."""
+        torch.cuda.synchronize()
+        path = _ckpt_file(path)
         self.state, self.update_idx = self.state.load(path)
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if "rollout" in sd:
+            self._load_rollout_state(sd["rollout"])
+        torch.cuda.synchronize()
         return self
+
+    def _rollout_state_dict(self):
+        r = self.rollout
+        out = {"counters": r.counters.cpu(), "env_returns": r.env_returns.cpu(),
+               "cur_obs": _to_cpu(r.cur_obs), "rnn_states": _to_cpu(r.rnn_states)}
+        get = getattr(self, "_sim_get_ckpts", None)
+        if get is not None:
+            out["sim"] = _to_cpu(get())
+        return out
+
+    def _load_rollout_state(self, sd):
+        r = self.rollout
+        r.counters.copy_(sd["counters"])
+        r.env_returns.copy_(sd["env_returns"])
+        _copy_into(r.cur_obs, sd["cur_obs"])
+        _copy_into(r.rnn_states, sd["rnn_states"])
+        load = getattr(self, "_sim_load_ckpts", None)
+        if load is not None and sd.get("sim") is not None:
+            load(sd["sim"])
+
+
+def _ckpt_file(path):
+    if os.path.isdir(path):
+        ids = [int(f[:-3]) for f in os.listdir(path) if f.endswith(".pt") and f[:-3].isdigit()]
+        if not ids:
+            raise FileNotFoundError(f"no checkpoint in {path}")
+        path = os.path.join(path, f"{max(ids)}.pt")
+    return path
+
+
+def _to_cpu(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu()
+    if isinstance(x, dict):
+        return {k: _to_cpu(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_to_cpu(v) for v in x]
+    return x
+
+
+def _copy_into(dst, src):
+    """Copy a saved tree into the live device tensors (same structure)."""
+    if isinstance(dst, torch.Tensor):
+        dst.copy_(src)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _copy_into(dst[k], src[k])
+    elif isinstance(dst, (list, tuple)):
+        for d, s_ in zip(dst, src):
+            _copy_into(d, s_)
 
 
 def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: Policy,
@@ -260,8 +325,16 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
                             train_states=tss[0] if len(tss) == 1 else tss, pbt_rng=None,
                             user_state=user_hooks.init_user_state(), value_norm=value_norm)
     start = 0
+    ckpt_rollout = None
     if restore_ckpt is not None:
-        tsm, start = tsm.load(restore_ckpt)
+        # train.py:353-354: the train state; the minibatch RNG position (the
+        # epoch counter) is restored with it, like the reference's advanced
+        # update_prng_key
+        path = _ckpt_file(restore_ckpt)
+        tsm, start = tsm.load(path)
+        ckpt_rollout = torch.load(path, map_location="cpu", weights_only=True).get("rollout")
+        if ckpt_rollout is not None:
+            rollout_state.counters[1].copy_(ckpt_rollout["counters"][1])
 
     rollout_mgr = RolloutManager(cfg, rollout_state, pss, env_offset=rank * sim_batch)
     names = algos[0].add_metrics(cfg, [])
@@ -272,8 +345,11 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         algo.prepare(cfg, ps, ts, rollout_mgr.view(p), dp, policy_idx=p,
                      start_states=rollout_mgr.start_states(p) if ps.recurrent else None)
     print(cfg)
-    return TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
-                           update_idx=start, use_graph=use_graph, profile_port=profile_port)
+    mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
+                          update_idx=start, use_graph=use_graph, profile_port=profile_port)
+    mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
+    mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
+    return mgr
 
 
 def stop_training(training_mgr: TrainingManager):  # train.py:148-153

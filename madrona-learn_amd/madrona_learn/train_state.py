@@ -84,7 +84,7 @@ def _actions_buckets(actor, cfg_actions):
         raise NotImplementedError(
             "fused path supports DenseLayerDiscreteActor (models.py:122-139); got "
             f"{type(actor).__name__}")
-    return tuple(int(b) for b in actor.cfg.actions_num_buckets)
+    return tuple(int(b) for b in actor.buckets)
 
 
 def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpArch:
@@ -406,7 +406,8 @@ class PolicyTrainState:
                   "optim_step")
 
     def state_dict(self):
-        sd = {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu()}
+        sd = {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu(),
+              "update_prng_key": torch.tensor(self.update_prng_key, dtype=torch.int64)}
         if self.value_norm_est is not None:
             sd["value_norm_est"] = self.value_norm_est.cpu()
             sd["value_norm_count"] = self.value_norm_count.cpu()
@@ -416,6 +417,8 @@ class PolicyTrainState:
         self.adam_m.copy_(sd["adam_m"])
         self.adam_v.copy_(sd["adam_v"])
         self.step.copy_(sd["step"])
+        if "update_prng_key" in sd:
+            self.update_prng_key = tuple(int(x) for x in sd["update_prng_key"].tolist())
         if self.value_norm_est is not None and "value_norm_est" in sd:
             self.value_norm_est.copy_(sd["value_norm_est"])
             self.value_norm_count.copy_(sd["value_norm_count"])
@@ -443,13 +446,18 @@ class TrainStateManager:  # train_state.py:139-304
         ts = self.train_states
         return list(ts) if isinstance(ts, (list, tuple)) else [ts]
 
-    def save(self, update_idx, path):
-        torch.save({"update_idx": int(update_idx),
-                    "policies": [p.state_dict() for p in self.policy_list],
-                    "train": [t.state_dict() for t in self.train_list]}, path)
+    def state_dict(self):
+        """The reference's TrainStateManager checkpoint tree (train_state.py:
+        145-163): policy states, train states (Adam moments and count, value
+        normaliser; the minibatch RNG's position is the rollout's epoch
+        counter, saved by TrainingManager), pbt_rng, user_state."""
+        return {"policies": [p.state_dict() for p in self.policy_list],
+                "train": [t.state_dict() for t in self.train_list],
+                "pbt_rng": self.pbt_rng if isinstance(self.pbt_rng, (torch.Tensor, type(None)))
+                else None,
+                "user_state": _ckpt_safe(self.user_state)}
 
-    def load(self, path):
-        sd = torch.load(path, map_location="cpu", weights_only=True)
+    def load_state_dict(self, sd):
         pol, tr = sd["policies"], sd["train"]
         if len(pol) != len(self.policy_list):
             raise ValueError(f"checkpoint holds {len(pol)} policies, this rank trains "
@@ -458,4 +466,30 @@ class TrainStateManager:  # train_state.py:139-304
             p.load_state_dict(d)
         for t, d in zip(self.train_list, tr):
             t.load_state_dict(d)
+        if sd.get("user_state") is not None:
+            self.user_state = sd["user_state"]
+        if sd.get("pbt_rng") is not None:
+            self.pbt_rng = sd["pbt_rng"]
+        return self
+
+    def save(self, update_idx, path, extra=None):  # train_state.py:145-163
+        torch.save({"update_idx": int(update_idx), "state": self.state_dict(),
+                    **(extra or {})}, path)
+
+    def load(self, path):  # train_state.py:165-196
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state_dict(sd["state"])
         return self, sd["update_idx"]
+
+
+def _ckpt_safe(x):
+    """user_state as saved: tensors / numbers / strings and dicts, lists or
+    tuples of them (what a weights_only load restores); anything else is not
+    checkpointed."""
+    if x is None or isinstance(x, (torch.Tensor, int, float, bool, str)):
+        return x.detach().cpu() if isinstance(x, torch.Tensor) else x
+    if isinstance(x, dict):
+        return {k: _ckpt_safe(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_ckpt_safe(v) for v in x)
+    return None

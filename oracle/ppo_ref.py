@@ -374,13 +374,20 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         adv = (adv - mean) / np.sqrt(max(var, 1e-5))
     clip = hp["clip_coef"]
     lo, hi = 1.0 - clip, 1.0 + clip
-    inv_sk = 1.0 / (M * K)
     inv_s = 1.0 / M
-    ce = hp["entropy_coef"]
+    # action groups = the keys of cfg.actions (ppo.py:221-239): each key's
+    # surrogate and entropy are means over its own [M, K_key] sub-actions,
+    # summed over the keys, with the key's entropy coefficient
+    groups = hp.get("action_groups") or [(K, hp["entropy_coef"])]
+    assert sum(n for n, _ in groups) == K
+    key_of = np.repeat(np.arange(len(groups)), [n for n, _ in groups])
     dlog = np.zeros((M, logits.shape[1]), ad)
     objs, ents = [], []
+    action_loss, entropy_loss = 0.0, 0.0
     rows = np.arange(M)
     for g, (off, nb, lp, p, ent) in enumerate(log_softmax_groups(logits, buckets)):
+        n_key, ce = groups[key_of[g]]
+        inv_sk = 1.0 / (M * n_key)
         a = acts[:, g]
         ratio = np.exp(lp[rows, a] - old[:, g])
         s1 = adv * ratio
@@ -399,6 +406,8 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         dlog[:, off:off + nb] = d * loss_scale
         objs.append(obj)
         ents.append(ent)
+        action_loss -= obj.sum() * inv_sk
+        entropy_loss -= ce * ent.sum() * inv_sk
     obj = np.stack(objs, -1)
     ent = np.stack(ents, -1)
     if np.asarray(V).ndim == 2:
@@ -407,7 +416,7 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         crit = np.asarray(V, ad)
         vl, dcrit = twohot_ce(crit, R)
         dV = hp["value_loss_coef"] * inv_s * dcrit * loss_scale
-        loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
+        loss = action_loss + hp["value_loss_coef"] * vl.mean() + entropy_loss
         metrics = {
             "Loss": loss, "Action Obj": obj, "Value Loss": vl,
             "Value Errors": np.abs(twohot_mean(crit) - R), "Entropy": ent,
@@ -437,7 +446,7 @@ def ppo_loss_dhead(logits, V, batch, hp, buckets, adv_stats=None, loss_scale=1.0
         vl = 0.5 * e * e
         dvl = e
     dV = hp["value_loss_coef"] * inv_s * dvl * dvp * loss_scale
-    loss = -obj.mean() + hp["value_loss_coef"] * vl.mean() - ce * ent.mean()
+    loss = action_loss + hp["value_loss_coef"] * vl.mean() + entropy_loss
     metrics = {
         "Loss": loss, "Action Obj": obj, "Value Loss": vl,
         "Value Errors": np.abs((V if vn is None else V * vn[3] + vn[2]) - R), "Entropy": ent,

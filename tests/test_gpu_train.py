@@ -183,3 +183,43 @@ def test_returns_objective_matches_oracle(gpu, normalize_returns):
         max_grad_norm=0.5)
     np.testing.assert_allclose(ps.params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
     np.testing.assert_allclose(mgr.metrics.last()["Loss"].mean, met["Loss"], rtol=1e-4, atol=1e-6)
+
+
+def test_action_groups_match_oracle(gpu):
+    """Several action groups (TrainConfig.actions keys, cfg.py:73): per-key
+    surrogate / entropy means with per-key entropy coefficients summed over
+    the keys (ppo.py:221-239); the sim gets a dict of per-key actions."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    dtype, N, H, mb = torch.float32, 64, 64, 16
+    groups = {"move": ml.DiscreteActionsConfig([4, 8, 5]), "act": ml.DiscreteActionsConfig([5, 2, 2])}
+    coefs = {"move": 0.01, "act": 0.05}
+    env = DummyVecEnv(N, 64, 3, seed=2, device=gpu)
+    base = make_cfg(dtype, N=N, H=H, mb=mb)
+    cfg = dataclasses.replace(base, actions=groups,
+                              algo=dataclasses.replace(base.algo, entropy_coef=coefs))
+    policy = ml.Policy(actor_critic=ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(H, 2, dtype))),
+        actor=DenseLayerDiscreteActor(groups, dtype), critic=DenseLayerCritic(dtype)),
+        obs_preprocess=ml.ObservationsCaster.create(dtype))
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), policy, use_graph=False)
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    p0 = ps.params.cpu().numpy().astype(np.float64)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    store = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+             for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": None,
+          "action_groups": [(3, 0.01), (3, 0.05)], "normalize_advantages": True}
+    lay = ref.param_layout(64, H, 2, 26)
+    zeros = np.zeros_like(p0)
+    p1, _, met = ref.ppo_update(
+        p0, (zeros, zeros.copy(), 0), [store], hp, BUCKETS, lay,
+        ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=mb,
+        bptt=cfg.steps_per_update, key=ts.update_prng_key, epoch_base=0, mode="f32", lr=3e-4,
+        max_grad_norm=0.5)
+    np.testing.assert_allclose(ps.params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(mgr.metrics.last()["Loss"].mean, met["Loss"], rtol=1e-4, atol=1e-6)

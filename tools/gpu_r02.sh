@@ -20,6 +20,6 @@ step() {
 rm -f gpurun_out/steps.txt
 step bench_headline 420 python bench.py --steps 20 --warmup 3
 step prof_headline 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_headline -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-}
 step b1_bench 300 python bench.py --config b1 --steps 20 --warmup 3 --no-cpu-baseline
 exit 0
