@@ -56,6 +56,10 @@ int mlearn_abi_version(void);
 /* out[i] = philox4x32(ctr[i], {k0,k1}); ctr/out are [n][4] uint32 in HBM. */
 int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,
                       int64_t n, mlearn_stream_t stream);
+/* The same on the host (host memory, no GPU): the control-plane draws of the
+ * population ops (pbt.py:473-562 explore_param, 565-722 cull / past copy). */
+int mlearn_philox4x32_host(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,
+                           int64_t n);
 
 /* Counters.  Every RNG-consuming entry point takes (const uint64_t* ctr,
  * uint64_t add): the effective counter is (ctr ? *ctr : 0) + add, read on the

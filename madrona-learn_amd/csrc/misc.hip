@@ -722,6 +722,21 @@ int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* o
     return check_launch("philox");
 }
 
+int mlearn_philox4x32_host(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,
+                           int64_t n) {
+    ML_REQUIRE(n >= 0, "philox_host: n < 0");
+    ML_REQUIRE(n == 0 || (ctr && out), "philox_host: null pointer");
+    for (int64_t i = 0; i < n; ++i) {
+        const u32x4 r = philox4x32(u32x4{ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]},
+                                   k0, k1);
+        out[4 * i] = r.x;
+        out[4 * i + 1] = r.y;
+        out[4 * i + 2] = r.z;
+        out[4 * i + 3] = r.w;
+    }
+    return MLEARN_OK;
+}
+
 int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
                    const float* bootstrap, float* advantages, float* returns, int32_t T, int64_t N,
                    float gamma, float gae_lambda, mlearn_stream_t stream) {

@@ -1,0 +1,328 @@
+"""Population-based training ops (mirrors src/madrona_learn/pbt.py:273-722
+and the initial hyperparameter draw of train.py:320-351).
+
+* ``pbt_explore_hyperparams`` (pbt.py:473-562): per ``ParamExplore`` train
+  hyperparameter (lr, entropy_coef) and reward hyperparameter, resample it in
+  [base*min_scale, base*max_scale] (linear, log10 or ln) with probability
+  ``resample_chance``, otherwise perturb it by a uniform factor in
+  [perturb_rnd_min, perturb_rnd_max) (clipped if clip_perturb).  As in the
+  reference, the optimizer keeps the learning rate it was built with
+  (train_state.py:388-389) and the loss reads cfg.algo.entropy_coef
+  (ppo.py:231-239): exploration changes the recorded hyperparameters.
+* ``pbt_update_fitness`` (pbt.py:382-470): per policy EMA (decay 0.9999) of
+  the scores of the episodes that ended this step.
+* ``pbt_cull_update`` (pbt.py:609-682): the ``num_cull_policies`` least fit
+  train policies take the state of the most fit ones when the one-sided test
+  of _check_overwrite (pbt.py:565-600) passes, keeping their own minibatch
+  RNG key, then explore the copied hyperparameters (resample chance 0.2).
+  Policies of a population are placed over the ranks (dist.policy_placement,
+  one per GPU in config P): a copy between ranks is a point-to-point
+  transfer of the policy's tensors (RCCL send/recv over xGMI, gloo on CPU);
+  the compute weight images are rebuilt on the receiving GPU.
+* ``pbt_past_update`` (pbt.py:685-722): past-policy snapshots.  The fused
+  path trains self-play populations (num_past_policies == 0, where the
+  reference returns the state unchanged).
+
+RNG: jax.random's threefry splits are replaced by Philox4x32-10 counters
+(the C ABI's ``mlearn_philox4x32_host``): the population key is
+``TrainStateManager.pbt_rng`` = int64 [k0, k1, op counter]; op c draws for
+population slot s and stream q (0 lr, 1 entropy, 2 + i reward
+hyperparameter i) the words of counter {c, s, q, 0}: word 0 decides
+resample vs perturb, word 1 is the value's uniform; the cull's source pick
+of pbt_past_update would use stream 0x7fffffff.  Uniforms are
+``u32_to_unit`` (csrc/common.h).  oracle/pbt_ref.py restates all of it.
+"""
+
+import dataclasses
+import math
+from typing import Any, Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as nat
+from .cfg import ParamExplore
+
+EMA_DECAY = 0.9999  # pbt.py:415
+CULL_RESAMPLE_CHANCE = 0.2  # pbt.py:637-638
+
+
+# ---------------------------------------------------------------------------
+# RNG
+# ---------------------------------------------------------------------------
+def philox_host(ctrs, k0, k1):
+    c = np.ascontiguousarray(np.asarray(ctrs, dtype=np.uint32).reshape(-1, 4))
+    out = np.empty_like(c)
+    nat.check(nat.lib().mlearn_philox4x32_host(c.ctypes.data, int(k0) & 0xFFFFFFFF,
+                                               int(k1) & 0xFFFFFFFF, out.ctypes.data,
+                                               c.shape[0]), "philox_host")
+    return out
+
+
+def u32_to_unit(x):
+    """(x >> 8 | 1) * 2^-24: a float32 in (0, 1) (csrc/common.h)."""
+    return np.float32(((int(x) >> 8) | 1) * 5.9604644775390625e-08)
+
+
+def new_pbt_rng(seed):
+    """TrainStateManager.pbt_rng: int64 [k0, k1, op counter] (host tensor)."""
+    ss = np.random.SeedSequence([int(seed) & 0xFFFFFFFF, 3])
+    w = ss.generate_state(2, dtype=np.uint32)
+    return torch.tensor([int(w[0]), int(w[1]), 0], dtype=torch.int64)
+
+
+def _split(pbt_rng):
+    """The next op counter of the population key (random.split)."""
+    op = int(pbt_rng[2].item())
+    pbt_rng[2] += 1
+    return int(pbt_rng[0].item()), int(pbt_rng[1].item()), op
+
+
+def _draws(key, op, slot, stream):
+    w = philox_host([[op & 0xFFFFFFFF, slot & 0xFFFFFFFF, stream & 0xFFFFFFFF, 0]], *key)[0]
+    return u32_to_unit(w[0]), u32_to_unit(w[1])
+
+
+# ---------------------------------------------------------------------------
+# hyperparameter exploration
+# ---------------------------------------------------------------------------
+def explore_param(u_resample, u_param, param, pe: ParamExplore, resample_chance):
+    """explore_param (pbt.py:480-523) in float32 given its two uniforms."""
+    f = np.float32
+    lo = f(pe.base * pe.min_scale)
+    hi = f(pe.base * pe.max_scale)
+    if u_resample < f(resample_chance):
+        if pe.log10_scale:
+            ls, hs = f(math.log10(lo)), f(math.log10(hi))
+        elif pe.ln_scale:
+            ls, hs = f(math.log(lo)), f(math.log(hi))
+        else:
+            ls, hs = lo, hi
+        s = f(ls + (hs - ls) * f(u_param))  # random.uniform(minval, maxval)
+        if pe.log10_scale:
+            s = f(f(10.0) ** s)
+        elif pe.ln_scale:
+            s = f(np.exp(s))
+        return s
+    pmin, pmax = f(pe.perturb_rnd_min), f(pe.perturb_rnd_max)
+    v = f(f(param) * f(pmin + (pmax - pmin) * f(u_param)))
+    if pe.clip_perturb:
+        v = f(min(max(v, lo), hi))
+    return v
+
+
+def pbt_explore_hyperparams(cfg, explore_rng, policy_state, train_state, resample_chance):
+    """pbt.py:473-562.  explore_rng = (k0, k1, op, slot)."""
+    k0, k1, op, slot = explore_rng
+    key = (k0, k1)
+    rh = getattr(policy_state, "reward_hyper_params", None)
+    if rh is not None:
+        vals = rh.detach().cpu().numpy().astype(np.float32)
+        for i, (_, pe) in enumerate(cfg.pbt.reward_hyper_params_explore.items()):
+            ur, up = _draws(key, op, slot, 2 + i)
+            vals[i] = explore_param(ur, up, vals[i], pe, resample_chance)
+        rh.copy_(torch.from_numpy(vals))
+    hp = train_state.hyper_params
+    if isinstance(cfg.lr, ParamExplore):
+        ur, up = _draws(key, op, slot, 0)
+        hp = dataclasses.replace(hp, lr=float(explore_param(ur, up, hp.lr, cfg.lr,
+                                                            resample_chance)))
+    ec = cfg.algo.entropy_coef
+    if isinstance(ec, ParamExplore):
+        ur, up = _draws(key, op, slot, 1)
+        hp = dataclasses.replace(hp, entropy_coef=float(
+            explore_param(ur, up, _scalar(hp.entropy_coef), ec, resample_chance)))
+    train_state.hyper_params = hp
+    return policy_state, train_state
+
+
+def _scalar(x):
+    return x.base if isinstance(x, ParamExplore) else float(x)
+
+
+def sample_initial_hyperparams(cfg, tsm):
+    """train.py:320-351: every train policy draws its hyperparameters
+    (resample chance 1) from one split of the population key; slot = the
+    policy's global id, so every rank draws the same values for it."""
+    k0, k1, op = _split(tsm.pbt_rng)
+    for ps, ts in zip(tsm.policy_list, tsm.train_list):
+        pbt_explore_hyperparams(cfg, (k0, k1, op, ts.policy_id), ps, ts, 1.0)
+    return tsm
+
+
+# ---------------------------------------------------------------------------
+# fitness
+# ---------------------------------------------------------------------------
+class MovingEpisodeScore:  # train_state.py:24-27
+    def __init__(self, device):
+        self.mean = torch.zeros(1, dtype=torch.float32, device=device)
+        self.var = torch.zeros(1, dtype=torch.float32, device=device)
+        self.N = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def tensors(self):
+        return [self.mean, self.var, self.N]
+
+
+def pbt_update_fitness(policy_columns, episode_scores, dones):
+    """pbt.py:382-470 for the self-play split: ``policy_columns`` = [(score,
+    col0, ncols)] per local policy (its MovingEpisodeScore and env columns),
+    ``episode_scores`` [N] f32 (get_episode_scores_fn of the episode
+    results), ``dones`` [N].  Device tensor ops only (graph-capturable)."""
+    d = dones.reshape(-1).bool()
+    x = episode_scores.reshape(-1).float()
+    nmax = torch.iinfo(torch.int32).max
+    for sc, c0, n in policy_columns:
+        v = d[c0:c0 + n]
+        xs = x[c0:c0 + n]
+        xn = v.sum().to(torch.int32)
+        xnf = xn.float()
+        cnt = torch.clamp(xnf, min=1.0)
+        xm = torch.where(v, xs, 0.0).sum() / cnt
+        dev = torch.where(v, xs - xm, 0.0)
+        xv = torch.where(xn > 1, (dev * dev).sum() / torch.clamp(xnf - 1.0, min=1.0), 0.0)
+        md = xm - sc.mean
+        cw = torch.expm1(xnf * math.log(EMA_DECAY)) + 1.0
+        xw = 1.0 - cw
+        cur = sc.N
+        new_n = torch.where(xn > nmax - cur, torch.full_like(cur, nmax), cur + xn)
+        mdv = torch.where(cur > 0, (cur.float() / (new_n - 1).float().clamp(min=1.0)) *
+                          (cw * xw) * md * md, torch.zeros_like(sc.var))
+        upd = xn > 0
+        sc.mean.copy_(torch.where(upd, cw * sc.mean + xw * xm, sc.mean))
+        sc.var.copy_(torch.where(upd, cw * sc.var + xw * xv + mdv, sc.var))
+        sc.N.copy_(torch.where(upd, new_n, sc.N))
+
+
+def check_overwrite(cfg, mean, var, N, src, dst):
+    """_check_overwrite (pbt.py:565-600), episode-score form: one-sided test
+    of the score difference, overwrite when p < 0.20 (float32)."""
+    f = np.float32
+    with np.errstate(divide="ignore", invalid="ignore"):
+        s2 = f(var[src]) / f(N[src]) + f(var[dst]) / f(N[dst])
+        t = (f(mean[src]) - f(mean[dst])) / np.sqrt(f(s2))
+        p = f(1.0) - f(0.5 * (1.0 + math.erf(float(t) / math.sqrt(2.0)))) \
+            if np.isfinite(t) else f(np.nan)
+    return bool(p < f(0.20))
+
+
+# ---------------------------------------------------------------------------
+# policy copies between ranks
+# ---------------------------------------------------------------------------
+def _bundle(ps, ts):
+    """Every tensor of a population member that a cull overwrites, plus its
+    hyperparameters packed as a float64 tensor."""
+    t = [ps.params]
+    if ps.obs_est is not None:
+        t += [ps.obs_est, ps.obs_count]
+    t += ps.episode_score.tensors()
+    t += [ts.adam_m, ts.adam_v, ts.step]
+    if ts.value_norm_est is not None:
+        t += [ts.value_norm_est, ts.value_norm_count]
+    return t
+
+
+def _hp_tensor(ts, device):
+    hp = ts.hyper_params
+    ec = hp.entropy_coef
+    ec = float("nan") if isinstance(ec, dict) else _scalar(ec)  # per-key dicts are not explored
+    return torch.tensor([hp.lr, ec], dtype=torch.float64, device=device)
+
+
+def _set_hp(ts, vec):
+    lr, ec = (float(x) for x in vec.cpu().tolist())
+    rep = {"lr": lr}
+    if not math.isnan(ec):
+        rep["entropy_coef"] = ec
+    ts.hyper_params = dataclasses.replace(ts.hyper_params, **rep)
+
+
+def _holders(pid, P, W):
+    """Global ranks holding train policy pid (dist.policy_placement)."""
+    if P % W == 0:
+        return [pid // (P // W)]
+    G = W // P
+    return list(range(pid * G, (pid + 1) * G))
+
+
+def copy_policy(tsm, src_pid, dst_pid, P):
+    """dst's policy/train state := src's (its own update_prng_key kept),
+    locally or from src's first holder to every holder of dst."""
+    rank, W = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+    local = {ts.policy_id: (ps, ts) for ps, ts in zip(tsm.policy_list, tsm.train_list)}
+    root = _holders(src_pid, P, W)[0]
+    for r in _holders(dst_pid, P, W):
+        if r == root:
+            if rank == r:
+                sps, sts = local[src_pid]
+                dps, dts = local[dst_pid]
+                for a, b in zip(_bundle(dps, dts), _bundle(sps, sts)):
+                    a.copy_(b)
+                dts.hyper_params = sts.hyper_params
+                dps.sync_weights()
+        elif rank == root:
+            sps, sts = local[src_pid]
+            for t in _bundle(sps, sts) + [_hp_tensor(sts, sps.params.device)]:
+                dist.send(t.contiguous(), r)
+        elif rank == r:
+            dps, dts = local[dst_pid]
+            for t in _bundle(dps, dts):
+                dist.recv(t, root)
+            hv = _hp_tensor(dts, dps.params.device)
+            dist.recv(hv, root)
+            _set_hp(dts, hv)
+            dps.sync_weights()
+
+
+def gather_fitness(tsm, P):
+    """(mean, var, N) float64 numpy arrays over all P train policies, the same
+    on every rank (one all-reduce; a DP group's root contributes)."""
+    rank, W = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+    dev = tsm.policy_list[0].params.device
+    buf = torch.zeros((P, 3), dtype=torch.float64, device=dev)
+    for ps, ts in zip(tsm.policy_list, tsm.train_list):
+        if _holders(ts.policy_id, P, W)[0] == rank:
+            e = ps.episode_score
+            buf[ts.policy_id, 0] = e.mean[0].double()
+            buf[ts.policy_id, 1] = e.var[0].double()
+            buf[ts.policy_id, 2] = e.N[0].double()
+    if W > 1:
+        dist.all_reduce(buf)
+    h = buf.cpu().numpy()
+    return h[:, 0], h[:, 1], h[:, 2]
+
+
+def cull_plan(cfg, mean, var, N, P, num_cull):
+    """[(dst, src, overwrite)]: the num_cull least fit train policies (stable
+    argsort of the fitness, pbt.py:618-622) against the most fit ones."""
+    order = np.argsort(np.asarray(mean, np.float32)[:P], kind="stable")
+    bottom, top = order[:num_cull], order[P - num_cull:]
+    return [(int(d), int(s), check_overwrite(cfg, mean, var, N, int(s), int(d)))
+            for d, s in zip(bottom, top)]
+
+
+def pbt_cull_update(cfg, tsm, num_cull_policies: int):
+    """pbt.py:609-682.  Returns the (updated) TrainStateManager and the
+    [(dst, src, overwritten)] plan (the reference prints it)."""
+    P = int(cfg.pbt.num_train_policies)
+    assert 2 * num_cull_policies <= P
+    mean, var, N = gather_fitness(tsm, P)
+    plan = cull_plan(cfg, mean, var, N, P, num_cull_policies)
+    k0, k1, op = _split(tsm.pbt_rng)
+    # every copy reads the pre-cull state of its source (top and bottom are disjoint)
+    for i, (dst, src, ok) in enumerate(plan):
+        if not ok:
+            continue
+        copy_policy(tsm, src, dst, P)
+        for ps, ts in zip(tsm.policy_list, tsm.train_list):
+            if ts.policy_id == dst:
+                pbt_explore_hyperparams(cfg, (k0, k1, op, i), ps, ts, CULL_RESAMPLE_CHANCE)
+    return tsm, plan
+
+
+def pbt_past_update(cfg, tsm):
+    """pbt.py:685-722: no past policies on the fused path (the reference
+    returns the state unchanged when num_past_policies == 0)."""
+    if cfg.pbt.num_past_policies == 0:
+        return tsm
+    raise NotImplementedError("past-policy snapshots need past-play matchmaking (pbt.py:135-247)")

@@ -386,6 +386,14 @@ class RolloutManager:  # rollouts.py:373-826
                      for p in range(self.P)]
             rollout_state.sim_state = out["state"]
             rollout_state.cur_obs = out["obs"]
+            # population fitness from the episodes that ended (pbt_update_fitness,
+            # pbt.py:382-470; episode_results from the sim's 'pbt' output)
+            res = (out.get("pbt") or {}).get("episode_results")
+            if res is not None and getattr(self, "get_episode_scores", None) is not None:
+                from .pbt import pbt_update_fitness
+                pbt_update_fitness([(ps.episode_score, p * B, B)
+                                    for p, ps in enumerate(self.policies)],
+                                   self.get_episode_scores(res), dn)
         # bootstrap values (rollouts.py:607-635), with the last post-step
         obs = self.prep_obs(rollout_state.cur_obs)
         for p, ps in enumerate(self.policies):

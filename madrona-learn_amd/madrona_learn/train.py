@@ -324,6 +324,11 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     tsm = TrainStateManager(policy_states=pss[0] if len(pss) == 1 else pss,
                             train_states=tss[0] if len(tss) == 1 else tss, pbt_rng=None,
                             user_state=user_hooks.init_user_state(), value_norm=value_norm)
+    if cfg.pbt is not None:
+        # the population key and the initial hyperparameter draw (train.py:320-351)
+        from .pbt import new_pbt_rng, sample_initial_hyperparams
+        tsm.pbt_rng = new_pbt_rng(cfg.seed)
+        sample_initial_hyperparams(cfg, tsm)
     start = 0
     ckpt_rollout = None
     if restore_ckpt is not None:
@@ -337,6 +342,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
             rollout_state.counters[1].copy_(ckpt_rollout["counters"][1])
 
     rollout_mgr = RolloutManager(cfg, rollout_state, pss, env_offset=rank * sim_batch)
+    rollout_mgr.get_episode_scores = policy.get_episode_scores
     names = algos[0].add_metrics(cfg, [])
     names = rollout_mgr.add_metrics(cfg, names)
     names = user_hooks.add_metrics(names)

@@ -208,6 +208,9 @@ class PolicyState:
             d.obs_mu = self.obs_est.data_ptr()
             d.obs_inv_sigma = self.obs_est.data_ptr() + 4 * D
         self.desc = d
+        # population fitness (MovingEpisodeScore, train_state.py:359-366)
+        from .pbt import MovingEpisodeScore
+        self.episode_score = MovingEpisodeScore(self.device)
         self.lstm_desc = None
         if arch.lstm_hidden:
             R = arch.lstm_hidden
@@ -322,7 +325,8 @@ class PolicyState:
             nat.ptr(values), 0, 0, None, 0, 0, 0, post, nat.stream_handle()), "critic_only")
 
     def state_dict(self):
-        sd = {"params": self.params.detach().cpu()}
+        sd = {"params": self.params.detach().cpu(),
+              "episode_score": [t.cpu() for t in self.episode_score.tensors()]}
         if self.obs_est is not None:
             sd["obs_est"] = self.obs_est.cpu()
             sd["obs_count"] = self.obs_count.cpu()
@@ -330,6 +334,9 @@ class PolicyState:
 
     def load_state_dict(self, sd):
         self.params.copy_(sd["params"].to(self.device))
+        if "episode_score" in sd:
+            for a, b in zip(self.episode_score.tensors(), sd["episode_score"]):
+                a.copy_(b)
         if self.obs_est is not None and "obs_est" in sd:
             self.obs_est.copy_(sd["obs_est"].to(self.device))
             self.obs_count.copy_(sd["obs_count"].to(self.device))
@@ -408,6 +415,11 @@ class PolicyTrainState:
     def state_dict(self):
         sd = {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu(),
               "update_prng_key": torch.tensor(self.update_prng_key, dtype=torch.int64)}
+        hp = self.hyper_params
+        if not isinstance(getattr(hp, "entropy_coef", None), dict):
+            ec = hp.entropy_coef
+            sd["hyper_params"] = torch.tensor(
+                [hp.lr, ec.base if hasattr(ec, "base") else float(ec)], dtype=torch.float64)
         if self.value_norm_est is not None:
             sd["value_norm_est"] = self.value_norm_est.cpu()
             sd["value_norm_count"] = self.value_norm_count.cpu()
@@ -419,6 +431,10 @@ class PolicyTrainState:
         self.step.copy_(sd["step"])
         if "update_prng_key" in sd:
             self.update_prng_key = tuple(int(x) for x in sd["update_prng_key"].tolist())
+        if "hyper_params" in sd:
+            import dataclasses
+            lr, ec = (float(x) for x in sd["hyper_params"].tolist())
+            self.hyper_params = dataclasses.replace(self.hyper_params, lr=lr, entropy_coef=ec)
         if self.value_norm_est is not None and "value_norm_est" in sd:
             self.value_norm_est.copy_(sd["value_norm_est"])
             self.value_norm_count.copy_(sd["value_norm_count"])

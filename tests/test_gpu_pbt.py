@@ -107,3 +107,64 @@ def test_population_graph_replay_matches_eager(gpu):
     assert graph._segments is not None
     for a, b in zip(eager.state.policy_list, graph.state.policy_list):
         assert torch.equal(a.params, b.params)
+
+
+def test_cull_update_gpu(gpu):
+    """pbt_cull_update on a 4-policy population on one GPU: plan and
+    hyperparameter draws as the oracle's, the culled policies hold their
+    sources' state (weights, optimizer, fitness) and rebuilt compute images,
+    keep their own minibatch RNG key, and training continues."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn import pbt
+    from oracle import pbt_ref as oref
+    cfg, env, mgr = _setup(gpu, torch.float32, N=256, H=64, P=4, mb=16)
+    lr_kw = dict(base=3e-4, min_scale=0.1, max_scale=10.0, log10_scale=True)
+    cfg = dataclasses.replace(cfg, lr=ml.ParamExplore(**lr_kw))
+    # the initial draw (train.py:320-351), redone on this cfg
+    mgr.state.pbt_rng = pbt.new_pbt_rng(cfg.seed)
+    pbt.sample_initial_hyperparams(cfg, mgr.state)
+    k0, k1 = (int(x) for x in mgr.state.pbt_rng[:2])
+    for p, ts in enumerate(mgr.state.train_list):
+        ur, up = oref.draws(k0, k1, 0, p, 0)
+        assert np.float32(ts.hyper_params.lr) == oref.explore_param(ur, up, 3e-4, lr_kw, 1.0)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    pss, tss = mgr.state.policy_list, mgr.state.train_list
+    fit = [(0.0, 1.0, 40), (-3.0, 1.0, 40), (3.0, 1.0, 40), (0.5, 1.0, 2)]
+    for ps, (m, v, n) in zip(pss, fit):
+        ps.episode_score.mean.fill_(m)
+        ps.episode_score.var.fill_(v)
+        ps.episode_score.N.fill_(n)
+    before = [(ps.params.clone(), ts.adam_m.clone(), int(ts.step.item()), ts.update_prng_key,
+               ts.hyper_params.lr) for ps, ts in zip(pss, tss)]
+    mean = np.array([f[0] for f in fit], np.float32)
+    var = np.array([f[1] for f in fit], np.float32)
+    N = np.array([f[2] for f in fit], np.float64)
+    _, plan = pbt.pbt_cull_update(cfg, mgr.state, 2)
+    assert plan == oref.cull_plan(mean, var, N, 4, 2)
+    obs = torch.randn((64, D), device=gpu)
+    for i, (dst, src, ok) in enumerate(plan):
+        if not ok:
+            assert torch.equal(pss[dst].params, before[dst][0])
+            continue
+        assert torch.equal(pss[dst].params, before[src][0])
+        assert torch.equal(tss[dst].adam_m, before[src][1])
+        assert int(tss[dst].step.item()) == before[src][2]
+        assert tss[dst].update_prng_key == before[dst][3]
+        assert float(pss[dst].episode_score.mean) == fit[src][0]
+        ur, up = oref.draws(k0, k1, 1, i, 0)
+        assert np.float32(tss[dst].hyper_params.lr) == \
+            oref.explore_param(ur, up, before[src][4], lr_kw, 0.2)
+        outs = []
+        for q in (dst, src):  # same weights -> same rollout outputs (images rebuilt)
+            a = torch.empty((64, 6), dtype=torch.int32, device=gpu)
+            lp = torch.empty((64, 6), device=gpu)
+            v = torch.empty(64, device=gpu)
+            pss[q].rollout_step(obs, None, a, lp, v, (1, 2), None, 0)
+            outs.append((a, lp, v))
+        assert all(torch.equal(x, y) for x, y in zip(*outs))
+    assert any(ok for _, _, ok in plan)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(ps.params).all() for ps in pss)

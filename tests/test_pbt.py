@@ -1,0 +1,177 @@
+"""Population ops on the host (CPU): hyperparameter exploration with the
+Philox RNG contract, the fitness EMA and the cull plan against the oracle
+restatement (oracle/pbt_ref.py, pbt.py:382-722), and the cross-rank policy
+copy of pbt_cull_update over gloo (world 2, one policy per rank)."""
+
+import dataclasses
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import pbt_ref as oref
+
+
+def _pe(**kw):
+    import madrona_learn as ml
+    return ml.ParamExplore(**kw)
+
+
+EXPLORES = [
+    dict(base=3e-4, min_scale=0.1, max_scale=10.0, log10_scale=True),
+    dict(base=0.01, min_scale=0.5, max_scale=2.0, ln_scale=True),
+    dict(base=0.5, min_scale=0.5, max_scale=1.5),
+    dict(base=0.5, min_scale=0.9, max_scale=1.1, clip_perturb=True, perturb_rnd_min=0.5,
+         perturb_rnd_max=1.5),
+]
+
+
+@pytest.mark.parametrize("chance", [0.0, 0.2, 1.0])
+@pytest.mark.parametrize("e", range(len(EXPLORES)))
+def test_explore_param_matches_oracle(chance, e):
+    from madrona_learn import pbt
+    kw = EXPLORES[e]
+    pe = _pe(**kw)
+    for op in range(4):
+        for slot in range(3):
+            ur, up = pbt._draws((0x1234, 0x5678), op, slot, 0)
+            our, oup = oref.draws(0x1234, 0x5678, op, slot, 0)
+            assert (ur, up) == (our, oup)
+            got = pbt.explore_param(ur, up, 0.37, pe, chance)
+            want = oref.explore_param(our, oup, 0.37, kw, chance)
+            assert np.float32(got) == np.float32(want)
+            lo, hi = np.float32(kw["base"] * kw["min_scale"]), np.float32(kw["base"] * kw["max_scale"])
+            if chance == 1.0 or kw.get("clip_perturb"):
+                assert lo * 0.999 <= got <= hi * 1.001
+
+
+def test_explore_hyperparams_streams():
+    """lr, entropy and reward hyperparameters use their own streams."""
+    import madrona_learn as ml
+    from madrona_learn import pbt
+    from madrona_learn.ppo import PPOHyperParams
+    lr_pe, ec_pe = _pe(**EXPLORES[0]), _pe(**EXPLORES[2])
+    cfg = types.SimpleNamespace(lr=lr_pe, algo=types.SimpleNamespace(entropy_coef=ec_pe),
+                                pbt=types.SimpleNamespace(reward_hyper_params_explore={
+                                    "a": _pe(**EXPLORES[1]), "b": _pe(**EXPLORES[3])}))
+    ts = types.SimpleNamespace(hyper_params=PPOHyperParams(
+        lr=3e-4, gamma=0.99, gae_lambda=0.95, normalize_values=False, value_normalizer_decay=0.99,
+        max_advantage_est_decay=0.99, entropy_coef=0.5))
+    ps = types.SimpleNamespace(reward_hyper_params=torch.tensor([0.01, 0.5]))
+    pbt.pbt_explore_hyperparams(cfg, (7, 9, 3, 5), ps, ts, 0.2)
+    want = oref.explore_hyperparams((7, 9), 3, 5, {"lr": 3e-4, "entropy_coef": 0.5,
+                                                   "reward": [0.01, 0.5]},
+                                    {"lr": EXPLORES[0], "entropy_coef": EXPLORES[2],
+                                     "reward": [EXPLORES[1], EXPLORES[3]]}, 0.2)
+    assert np.float32(ts.hyper_params.lr) == np.float32(want["lr"])
+    assert np.float32(ts.hyper_params.entropy_coef) == np.float32(want["entropy_coef"])
+    assert np.array_equal(ps.reward_hyper_params.numpy(), np.array(want["reward"], np.float32))
+
+
+def test_fitness_ema_matches_oracle():
+    from madrona_learn import pbt
+    rng = np.random.default_rng(0)
+    N, B = 96, 32
+    scores = [pbt.MovingEpisodeScore("cpu") for _ in range(3)]
+    state = [(np.float32(0), np.float32(0), 0) for _ in range(3)]
+    for step in range(20):
+        res = torch.from_numpy(rng.standard_normal(N).astype(np.float32))
+        dn = torch.from_numpy(rng.random(N) < (0.0 if step == 3 else 0.15))
+        pbt.pbt_update_fitness([(scores[p], p * B, B) for p in range(3)], res, dn)
+        for p in range(3):
+            sl = slice(p * B, (p + 1) * B)
+            state[p] = oref.update_fitness(*state[p], res.numpy()[sl], dn.numpy()[sl])
+    for p in range(3):
+        np.testing.assert_allclose(scores[p].mean.item(), state[p][0], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(scores[p].var.item(), state[p][1], rtol=1e-4, atol=1e-7)
+        assert scores[p].N.item() == state[p][2]
+
+
+def test_cull_plan_matches_oracle():
+    from madrona_learn import pbt
+    rng = np.random.default_rng(1)
+    for trial in range(50):
+        P = 8
+        mean = rng.standard_normal(P).astype(np.float32) * (0.1 if trial % 2 else 2.0)
+        var = rng.random(P).astype(np.float32) + 0.1
+        N = rng.integers(0 if trial % 5 == 0 else 1, 40, P).astype(np.float64)
+        for k in (1, 2, 4):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                got = pbt.cull_plan(None, mean, var, N, P, k)
+            assert got == oref.cull_plan(mean, var, N, P, k)
+
+
+# ---------------------------------------------------------------------------
+# cross-rank copy (gloo, world 2: one policy per rank, config P's placement)
+# ---------------------------------------------------------------------------
+def _fake_member(pid, seed):
+    from madrona_learn import pbt
+    from madrona_learn.ppo import PPOHyperParams
+    g = torch.Generator().manual_seed(seed)
+    ps = types.SimpleNamespace(params=torch.randn(1000, generator=g), obs_est=None,
+                               episode_score=pbt.MovingEpisodeScore("cpu"), synced=0)
+    ps.sync_weights = lambda: setattr(ps, "synced", ps.synced + 1)
+    ts = types.SimpleNamespace(
+        adam_m=torch.randn(1000, generator=g), adam_v=torch.rand(1000, generator=g),
+        step=torch.tensor([pid + 3], dtype=torch.int32), value_norm_est=None, policy_id=pid,
+        update_prng_key=(100 + pid, 200 + pid),
+        hyper_params=PPOHyperParams(lr=1e-3 * (pid + 1), gamma=0.99, gae_lambda=0.95,
+                                    normalize_values=False, value_normalizer_decay=0.99,
+                                    max_advantage_est_decay=0.99, entropy_coef=0.01))
+    return ps, ts
+
+
+def _worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from madrona_learn import pbt
+        ps, ts = _fake_member(rank, 10 + rank)
+        # policy 1 is far better with many episodes: the one-sided test passes
+        ps.episode_score.mean.fill_(5.0 if rank == 1 else -5.0)
+        ps.episode_score.var.fill_(1.0)
+        ps.episode_score.N.fill_(50)
+        tsm = types.SimpleNamespace(policy_list=[ps], train_list=[ts],
+                                    pbt_rng=torch.tensor([1, 2, 0], dtype=torch.int64))
+        lr_pe = _pe(**EXPLORES[0])
+        cfg = types.SimpleNamespace(
+            lr=lr_pe, algo=types.SimpleNamespace(entropy_coef=0.01),
+            pbt=types.SimpleNamespace(num_train_policies=2, num_past_policies=0,
+                                      reward_hyper_params_explore={}))
+        _, plan = pbt.pbt_cull_update(cfg, tsm, 1)
+        q.put((rank, plan, ps.params.clone(), ts.adam_m.clone(), int(ts.step.item()),
+               ts.update_prng_key, ts.hyper_params.lr, ps.synced, float(ps.episode_score.mean)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cull_copies_across_ranks_gloo():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    src_ps, src_ts = _fake_member(1, 11)
+    plan0, params0, m0, step0, key0, lr0, synced0, mean0 = res[0]
+    plan1, params1, m1, step1, key1, lr1, synced1, mean1 = res[1]
+    assert plan0 == plan1 == [(0, 1, True)]
+    assert torch.equal(params0, src_ps.params) and torch.equal(params1, src_ps.params)
+    assert torch.equal(m0, src_ts.adam_m) and step0 == 4 and mean0 == 5.0
+    assert key0 == (100, 200), "the culled policy keeps its own minibatch RNG key"
+    assert synced0 == 1 and synced1 == 0
+    ur, up = oref.draws(1, 2, 0, 0, 0)
+    want = oref.explore_param(ur, up, src_ts.hyper_params.lr, EXPLORES[0], 0.2)
+    assert np.float32(lr0) == np.float32(want) and lr1 == src_ts.hyper_params.lr
