@@ -46,6 +46,8 @@ extern "C" {
 #define MLEARN_HEAD_COLS_MAX 96 /* head width when actor logits + critic bins exceed 32 */
 
 typedef void* mlearn_stream_t; /* hipStream_t */
+typedef void* mlearn_comm_t;   /* RCCL communicator (mlearn_comm_init) */
+#define MLEARN_COMM_ID_BYTES 128
 
 const char* mlearn_last_error(void);
 int mlearn_abi_version(void);
@@ -517,6 +519,22 @@ int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int
 int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t k0,
                            uint32_t k1, uint32_t env_offset, float* obs,
                            mlearn_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Data-parallel collectives on the compute stream  */
+/* ---------------------------------------------------------------------- */
+/* The reference is single-device; under data parallelism the build sums the
+ * per-minibatch gradient (ppo.py:276-286 runs on the union minibatch) and the
+ * per-epoch advantage sums (algo_common.py:133-140 over the union) across
+ * the ranks.  An RCCL communicator: rank 0 makes the unique id, the caller
+ * distributes it (MLEARN_COMM_ID_BYTES bytes), every rank calls
+ * mlearn_comm_init.  The all-reduces are in-place sums enqueued on `stream`
+ * (capturable into a HIP graph). */
+int mlearn_comm_unique_id(uint8_t* id_out);
+int mlearn_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, mlearn_comm_t* comm_out);
+int mlearn_comm_destroy(mlearn_comm_t comm);
+int mlearn_allreduce_f32(mlearn_comm_t comm, float* buf, int64_t n, mlearn_stream_t stream);
+int mlearn_allreduce_f64(mlearn_comm_t comm, double* buf, int64_t n, mlearn_stream_t stream);
 
 #ifdef __cplusplus
 }

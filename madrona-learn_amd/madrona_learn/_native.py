@@ -98,6 +98,11 @@ _SIGNATURES = {
     "mlearn_abi_version": (c_int32, []),
     "mlearn_grad_sumsq_parts": (c_int64, [c_int64]),
     "mlearn_philox4x32_host": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64]),
+    "mlearn_comm_unique_id": (c_int32, [_P]),
+    "mlearn_comm_init": (c_int32, [_P, c_int32, c_int32, POINTER(c_void_p)]),
+    "mlearn_comm_destroy": (c_int32, [c_void_p]),
+    "mlearn_allreduce_f32": (c_int32, [c_void_p, _P, c_int64, _S]),
+    "mlearn_allreduce_f64": (c_int32, [c_void_p, _P, c_int64, _S]),
     "mlearn_philox4x32": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64, _S]),
     "mlearn_counters_add": (c_int32, [_P, c_int32, POINTER(c_uint64), _S]),
     "mlearn_gae_f32": (c_int32, [_P, _P, _P, _P, _P, _P, c_int32, c_int64, c_float, c_float, _S]),

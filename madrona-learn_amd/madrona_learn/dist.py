@@ -7,9 +7,16 @@ reference's per-device configuration on its own environment shard
     uses the statistics of the global minibatch, once per epoch, and
   * the flat fp32 gradient (89,883 floats for MLP[256,256]), summed with each
     rank's loss pre-scaled by 1/world, once per minibatch,
-both via torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo"
-on CPU for tests).
+both on the compute stream through the C ABI's RCCL communicator
+(mlearn_allreduce_f32 / _f64, csrc/comm.hip) when the group runs on the
+"nccl" backend (= RCCL over xGMI on MI355X), so a HIP graph captures a whole
+update including its collectives; otherwise (the "gloo" backend of the CPU
+tests, MLEARN_NATIVE_COLLECTIVES=0, or a failed self-check at setup) via
+torch.distributed between captured graph segments.
 """
+
+import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -33,9 +40,57 @@ class DataParallel:
             self.rank = dist.get_rank(group)
             self.world_size = dist.get_world_size(group)
 
+        self.comm = None  # RCCL communicator owned by libmlearn (enable_native)
+
+    def enable_native(self, device):
+        """Bootstrap this group's RCCL communicator in the C ABI: the group's
+        first rank makes the unique id, torch.distributed broadcasts it, every
+        member calls mlearn_comm_init.  A sum of rank ids through the new
+        communicator must come out right on every rank, else the group keeps
+        the torch.distributed path."""
+        if self.world_size <= 1 or os.environ.get("MLEARN_NATIVE_COLLECTIVES", "1") == "0":
+            return False
+        if dist.get_backend(self.group) != "nccl":
+            return False
+        from . import _native as nat
+        L = nat.lib()
+        idt = torch.zeros(128, dtype=torch.uint8, device=device)
+        ok = True
+        if self.rank == 0:
+            buf = (ctypes.c_uint8 * 128)()
+            ok = L.mlearn_comm_unique_id(buf) == 0
+            idt.copy_(torch.tensor(list(buf), dtype=torch.uint8))
+        dist.broadcast(idt, src=self.root, group=self.group)
+        ids = (ctypes.c_uint8 * 128)(*idt.cpu().tolist())
+        comm = ctypes.c_void_p()
+        ok = ok and L.mlearn_comm_init(ids, self.world_size, self.rank, ctypes.byref(comm)) == 0
+        if ok:
+            t = torch.full((4,), float(self.rank + 1), dtype=torch.float32, device=device)
+            ok = L.mlearn_allreduce_f32(comm, nat.ptr(t), 4, nat.stream_handle()) == 0
+            torch.cuda.synchronize()
+            W = self.world_size
+            ok = ok and bool((t == W * (W + 1) / 2).all().item())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) != 1:
+            if comm.value:
+                L.mlearn_comm_destroy(comm)
+            return False
+        self.comm = comm
+        return True
+
     def all_reduce_sum_(self, t: torch.Tensor):
         if self.world_size > 1:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def native_all_reduce_sum_(self, t: torch.Tensor):
+        """In-place sum over the group, enqueued on the current stream by the
+        C ABI (captured into the update's HIP graph)."""
+        from . import _native as nat
+        L = nat.lib()
+        f = L.mlearn_allreduce_f64 if t.dtype == torch.float64 else L.mlearn_allreduce_f32
+        nat.check(f(self.comm, nat.ptr(t), t.numel(), nat.stream_handle()), "allreduce")
         return t
 
     def broadcast_(self, t: torch.Tensor):

@@ -211,7 +211,10 @@ class PPO(AlgoBase):  # ppo.py:49-106
                 self.adv_sums[e, :n2].copy_(self.adv_part[e, :n2])
                 if self.vnorm:
                     self.adv_sums[e, n2:].copy_(self.ret_part[e, :n2])
-            yield ("allreduce", self.adv_sums)
+            if self.dp.comm is not None:
+                self.dp.native_all_reduce_sum_(self.adv_sums)
+            else:
+                yield ("allreduce", self.adv_sums)
             for e in range(self.E):
                 self.adv_part[e, :n2].copy_(self.adv_sums[e, :n2])
                 if self.vnorm:
@@ -249,7 +252,10 @@ class PPO(AlgoBase):  # ppo.py:49-106
                         nat.ptr(stats), self.hp, nat.ptr(train_state.grads),
                         lo, nat.ptr(self.ws), strm), "ppo_minibatch_grad")
                 if self.dp.world_size > 1:
-                    yield ("allreduce", train_state.grads)
+                    if self.dp.comm is not None:
+                        self.dp.native_all_reduce_sum_(train_state.grads)
+                    else:
+                        yield ("allreduce", train_state.grads)
                 train_state.optimizer_step(policy_state)
                 metrics = user_metrics_cb(metrics, e, {"sequence_ids": seqs}, policy_state,
                                           train_state)

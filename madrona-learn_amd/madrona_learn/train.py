@@ -247,6 +247,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     # policy placement: which train policies this rank holds, and the ranks it
     # shares gradients with (dist.policy_placement)
     policy_ids, dp = policy_placement(num_policies)
+    dp.enable_native(device)  # RCCL on the compute stream (inside the captured graph)
     rank, W = world()
 
     # Global semantics (the reference's meaning of the config, cfg.py:68-96):
