@@ -58,6 +58,12 @@ int mlearn_abi_version(void);
 /* out[i] = philox4x32(ctr[i], {k0,k1}); ctr/out are [n][4] uint32 in HBM. */
 int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,
                       int64_t n, mlearn_stream_t stream);
+/* The LSTM cell's gate activations as the fused kernels compute them
+ * (v_exp_f32 / v_rcp_f32 sigmoid and tanh, odd series below |x| < 1/8;
+ * flax OptimizedLSTMCell gates, rnn.py:30-36): sigmoid_out[i], tanh_out[i]
+ * of x[i] (accuracy pin). */
+int mlearn_lstm_activations_f32(const float* x, int64_t n, float* sigmoid_out, float* tanh_out,
+                                mlearn_stream_t stream);
 /* The same on the host (host memory, no GPU): the control-plane draws of the
  * population ops (pbt.py:473-562 explore_param, 565-722 cull / past copy). */
 int mlearn_philox4x32_host(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,

@@ -36,7 +36,7 @@ int check_launch(const char* what);
 // ---------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG.  Identical arithmetic on host and device;
 // restated independently in oracle/ (C and numpy) and pinned by the Random123
-// known-answer vectors in tests/test_oracle_rng.py.
+// known-answer vectors in tests/test_oracle.py (test_philox_random123_kat).
 // ---------------------------------------------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 

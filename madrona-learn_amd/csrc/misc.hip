@@ -11,6 +11,7 @@
 
 #include "common.h"
 #include "dists.h"
+#include "rowtile.h"
 
 namespace ml {
 
@@ -700,6 +701,15 @@ __global__ __launch_bounds__(256) void obs_norm_update_kernel(const float* __res
 
 __global__ void obs_count_kernel(int32_t* count) { *count += 1; }
 
+// The LSTM gate activations of the fused kernels (rowtile.h sigmoidf /
+// tanh_fast) over an array: the accuracy pin of tests/test_gpu_kernels.py.
+__global__ void activations_kernel(const float* x, int64_t n, float* sig, float* th) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    sig[i] = sigmoidf(x[i]);
+    th[i] = tanh_fast(x[i]);
+}
+
 }  // namespace ml
 
 using namespace ml;
@@ -720,6 +730,16 @@ int mlearn_philox4x32(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* o
     hipLaunchKernelGGL(philox_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, S(stream),
                        (const uint4*)ctr, k0, k1, (uint4*)out, n);
     return check_launch("philox");
+}
+
+int mlearn_lstm_activations_f32(const float* x, int64_t n, float* sigmoid_out, float* tanh_out,
+                                mlearn_stream_t stream) {
+    ML_REQUIRE(n >= 0, "lstm_activations: n < 0");
+    if (n == 0) return MLEARN_OK;
+    ML_REQUIRE(x && sigmoid_out && tanh_out, "lstm_activations: null pointer");
+    hipLaunchKernelGGL(ml::activations_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       S(stream), x, n, sigmoid_out, tanh_out);
+    return check_launch("lstm_activations");
 }
 
 int mlearn_philox4x32_host(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out,

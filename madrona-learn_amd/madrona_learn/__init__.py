@@ -20,6 +20,8 @@ from .ppo import PPOConfig
 from .profile import profile
 from .train import TrainHooks, TrainingManager, init_training, stop_training, train
 from .train_state import TrainStateManager
+from .tensorboard import TensorboardWriter
+from . import pbt
 from . import models
 from . import rnn
 
@@ -30,5 +32,5 @@ __all__ = [
     "DiscreteActionDistributions", "PhiloxKey", "ObservationsEMANormalizer",
     "ObservationsCaster", "ObservationsPreprocessNoop", "ActorCritic", "BackboneEncoder",
     "RecurrentBackboneEncoder", "Backbone", "BackboneShared", "BackboneSeparate", "PPOConfig",
-    "profile",
+    "profile", "TensorboardWriter", "pbt",
 ]

@@ -99,6 +99,7 @@ _SIGNATURES = {
     "mlearn_grad_sumsq_parts": (c_int64, [c_int64]),
     "mlearn_philox4x32_host": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64]),
     "mlearn_comm_unique_id": (c_int32, [_P]),
+    "mlearn_lstm_activations_f32": (c_int32, [_P, c_int64, _P, _P, _S]),
     "mlearn_comm_init": (c_int32, [_P, c_int32, c_int32, POINTER(c_void_p)]),
     "mlearn_comm_destroy": (c_int32, [c_void_p]),
     "mlearn_allreduce_f32": (c_int32, [c_void_p, _P, c_int64, _S]),

@@ -109,12 +109,35 @@ class TrainingMetrics:
         host = self.ring[idx, policy].cpu().numpy()
         return {n: Metric.from_vector(self.per_policy, host[i]) for i, n in enumerate(self.names)}
 
-    def pretty_print(self, tab=2):
-        out = []
-        for p in range(self.num_policies):
-            if self.num_policies > 1:
-                out.append(" " * tab + f"policy {p}:")
-            for n, m in self.last(p).items():
-                out.append(" " * tab + f"{n}: mean {m.mean:.4e} std {np.sqrt(max(m.var, 0)):.4e} "
-                           f"min {m.min:.4e} max {m.max:.4e} count {m.count}")
-        print("\n".join(out))
+    def pretty_print(self, tab=2):  # metrics.py:190-217 (the last completed update)
+        tab = " " * tab
+        lines = [tab + "TrainingMetrics"]
+        vals = [self.last(p) for p in range(self.num_policies)]
+
+        def fmt(xs):
+            return ", ".join(f"{float(x): .3e}" for x in xs)
+
+        for n in self.names:
+            ms = [v[n] for v in vals]
+            lines.append(tab * 2 + f"{n}:")
+            lines.append(tab * 3 + f"Avg: {fmt(m.mean for m in ms)}")
+            lines.append(tab * 3 + f"Min: {fmt(m.min for m in ms)}")
+            lines.append(tab * 3 + f"Max: {fmt(m.max for m in ms)}")
+            lines.append(tab * 3 + f"\u03c3:   {fmt(np.sqrt(max(m.var, 0.0)) for m in ms)}")
+        print("\n".join(lines))
+
+    def tensorboard_log(self, base_update_idx, writer):  # metrics.py:219-244
+        """Every buffered update (ring slot b -> step base_update_idx + b):
+        '<name> Mean/σ/Min/Max' (per policy 'p<i>/<name> ...')."""
+        host = self.ring.cpu().numpy()  # [buf, P, names, 5]
+        for b in range(self.buffer_size):
+            step = base_update_idx + b
+            for j, n in enumerate(self.names):
+                for i in range(self.num_policies):
+                    mean, m2, mn, mx, cnt = (float(x) for x in host[b, i, j])
+                    sd = float(np.sqrt(m2 / cnt)) if cnt > 0 else 0.0
+                    pre = f"p{i}/" if self.per_policy else ""
+                    writer.scalar(f"{pre}{n} Mean", mean, step)
+                    writer.scalar(f"{pre}{n} \u03c3", sd, step)
+                    writer.scalar(f"{pre}{n} Min", mn, step)
+                    writer.scalar(f"{pre}{n} Max", mx, step)

@@ -206,3 +206,29 @@ def test_errors_are_reported(gpu):
                                   nat.stream_handle())
     assert rc == -1
     assert b"null" in nat.lib().mlearn_last_error()
+
+
+def test_lstm_activation_accuracy(gpu):
+    """The gate activations on v_exp_f32 / v_rcp_f32 (rowtile.h sigmoidf,
+    tanh_fast) against libm over a dense sweep of [-20, 20], both sides of
+    the |x| = 1/8 series cutover included: absolute error <= 2e-7 (below
+    the bf16 rounding of every stored gate, 2^-9 relative) and relative
+    error <= 4e-6 where |f(x)| >= 1e-3."""
+    from madrona_learn import _native as nat
+    xs = np.concatenate([np.linspace(-20, 20, 400001), np.linspace(-0.13, 0.13, 20001),
+                         np.nextafter(np.float32([0.125, -0.125]), 0),
+                         np.float32([0.125, -0.125, 0.0, 1e-30, -1e-30, 88.0, -88.0])])
+    x = torch.tensor(xs, dtype=torch.float32, device=gpu)
+    sg, th = torch.empty_like(x), torch.empty_like(x)
+    nat.check(nat.lib().mlearn_lstm_activations_f32(nat.ptr(x), x.numel(), nat.ptr(sg), nat.ptr(th),
+                                                   nat.stream_handle()), "activations")
+    xd = x.cpu().double().numpy()
+    ref_s = 1.0 / (1.0 + np.exp(-xd))
+    ref_t = np.tanh(xd)
+    for got, ref in ((sg.cpu().double().numpy(), ref_s), (th.cpu().double().numpy(), ref_t)):
+        err = np.abs(got - ref)
+        assert err.max() <= 2e-7, err.max()
+        big = np.abs(ref) >= 1e-3
+        assert (err[big] / np.abs(ref[big])).max() <= 4e-6
+        assert np.all(np.isfinite(got))
+    assert np.all(np.abs(th.cpu().numpy()) <= 1.0) and np.all((sg.cpu().numpy() >= 0) & (sg.cpu().numpy() <= 1))
