@@ -58,6 +58,29 @@ __device__ inline void eval_group(const float* lg, int nb, int a, float* logp, f
     *ent = e;
 }
 
+// sample_group with the Gumbel-perturbed logits already computed (nz, the
+// same values sample_group forms: lg[j] + det_gumbel(sample_uniform(j))), or
+// best() when nz is null.  Bit-identical to sample_group.
+__device__ inline void pick_group(const float* lg, const float* nz, int nb, int* action,
+                                  float* logp) {
+#pragma clang fp contract(off)
+    float mx = lg[0];
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    const float lse = mx + __logf(se);
+    const float* v = nz ? nz : lg;
+    int best = 0;
+    float bv = v[0];
+    for (int j = 1; j < nb; ++j)
+        if (v[j] > bv) {
+            bv = v[j];
+            best = j;
+        }
+    *action = best;
+    if (logp) *logp = lg[best] - lse;
+}
+
 // ---------------------------------------------------------------------------
 // SymExpTwoHotDistribution (dists.py:119-208) over the nb critic logits of a
 // DreamerV3Critic (models.py:157-174), logits already cast to f32.

@@ -354,16 +354,38 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         __syncthreads();
     }
 
-    // sample + store: one (env, group) task per thread
+    // sample + store.  Gumbel noise first, one Philox block per 4 logits of a
+    // row ((env, logit quad) tasks; the head partials' LDS is free now), then
+    // one (env, group) task per thread: argmax of the perturbed logits,
+    // log-prob from the logits (bit-identical to sample_group, dists.h)
     if (actions) {
+        float* nz = lgp;  // [32][LGS] perturbed logits
+        if (sample) {
+            const int nq = (P.A + 3) >> 2;
+            for (int task = tid; task < 32 * nq; task += THREADS) {
+                const int rr = task / nq, q = task - rr * nq;
+                const int64_t n = row0 + rr;
+                if (n >= N) continue;
+                const u32x4 u = philox4x32(
+                    u32x4{eoff + (uint32_t)n, (uint32_t)q, (uint32_t)step, (uint32_t)(step >> 32)},
+                    k0, k1);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = 4 * q + e;
+                    if (j < P.A)
+                        nz[rr * LGS + j] = lg[rr * LGS + j] + det_gumbel(u32_to_unit(u32x4_get(u, e)));
+                }
+            }
+            __syncthreads();
+        }
         for (int task = tid; task < 32 * P.K; task += THREADS) {
             const int rr = task / P.K, g = task - rr * P.K;
             const int64_t n = row0 + rr;
             if (n >= N) continue;
             int a;
             float lp;
-            sample_group(lg + rr * LGS + P.off[g], P.off[g + 1] - P.off[g], P.off[g], k0, k1,
-                         eoff + (uint32_t)n, step, sample, &a, &lp);
+            pick_group(lg + rr * LGS + P.off[g], sample ? nz + rr * LGS + P.off[g] : nullptr,
+                       P.off[g + 1] - P.off[g], &a, &lp);
             actions[n * P.K + g] = a;
             if (logp) logp[n * P.K + g] = lp;
         }

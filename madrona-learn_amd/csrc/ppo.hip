@@ -362,11 +362,16 @@ template <int H> struct StepCfg {
     static constexpr int NBW = NB / W;
 };
 
-template <typename T, int H, int L, int HC> static size_t step_lds() {
+// Per row tile: B fragments [KSH][64], row statistics [W][32][2], head
+// partials and outputs, loss partials; shared by the RTW row tiles of a
+// workgroup: LayerNorm scale/bias [L][2][H], head bias [HC], critic bins [HC].
+template <typename T, int H, int HC> constexpr size_t step_tile_lds() {
     typedef StepCfg<H> C;
     return (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) +
-           (size_t)(L * 2 * H + HC + C::W * 64 + (head_parts<HC, C::W>() + 1) * 32 * (HC + 1) +
-                    C::W * kLossSlots + HC) * 4;
+           (size_t)(C::W * 64 + (head_parts<HC, C::W>() + 1) * 32 * (HC + 1) + C::W * kLossSlots) * 4;
+}
+template <typename T, int H, int L, int HC, int RTW = 1> static size_t step_lds() {
+    return RTW * step_tile_lds<T, H, HC>() + (size_t)(L * 2 * H + 2 * HC) * 4;
 }
 
 // ReLU' threshold: rnd<T>(y) > 0  <=>  y > THR (bf16 round-to-nearest-even
@@ -403,8 +408,11 @@ struct RecK {
     const void* head_t_nat;  // head image, natural k order (kHeads)
 };
 
-template <typename T, int H, int L, int MODE = kFused, int HC = MLEARN_HEAD_COLS>
-__global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
+// RTW row tiles of 32 rows per workgroup (kFused): waves w and w + W * rt own
+// the same features of different rows, released by the same barriers, so
+// their weight-fragment loads of every product meet in the CU's L1.
+template <typename T, int H, int L, int MODE = kFused, int HC = MLEARN_HEAD_COLS, int RTW = 1>
+__global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_waves_per_eu(ML_STEP_WAVES, 8))) void ppo_step_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws, RecK rec) {
     constexpr bool kFwd = MODE != kHeads;                     // runs the trunk forward
@@ -418,16 +426,20 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     constexpr int LGS = HC + 1;  // LDS row stride of the head outputs
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, K = P.K;
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the buffer descriptors
-    frag* fr = (frag*)smem;                    // [KSH][64]
-    float* gb = (float*)(fr + KSH * 64);       // [L][2][H]
-    float* hbias = gb + L * 2 * H;             // [32]
-    float* red = hbias + HC;                   // [W][32][2]
+    // wave-uniform (SGPR) indices for the buffer descriptors: row tile rt of
+    // the workgroup, wave w of that tile
+    const int wg_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int rt = wg_wave / W, w = wg_wave - rt * W;
+    const int tid = (int)threadIdx.x - rt * THREADS, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    char* tsm = smem + (size_t)rt * step_tile_lds<T, H, HC>();
+    frag* fr = (frag*)tsm;                     // [KSH][64]
+    float* red = (float*)(fr + KSH * 64);      // [W][32][2]
     float* lgp = red + W * 64;                 // [kHeadParts][32][LGS] head partials
     float* lg = lgp + head_parts<HC, W>() * 32 * LGS;  // [32][LGS]
     float* lred = lg + 32 * LGS;               // [W][kLossSlots]
-    float* bins = lred + W * kLossSlots;       // [HC] two-hot critic bins
+    float* gb = (float*)(smem + (size_t)RTW * step_tile_lds<T, H, HC>());  // [L][2][H] (shared)
+    float* hbias = gb + L * 2 * H;             // [HC]
+    float* bins = hbias + HC;                  // [HC] two-hot critic bins
     if (kLoss && P.CB > 1)
         for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
     // LayerNorm / head-bias parameters: loads issued now, written to LDS after
@@ -446,7 +458,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
         }
         parv[k] = v;
     }
-    const int tile = blockIdx.x;
+    const int tile = (int)blockIdx.x * RTW + rt;
     const int64_t row0 = (int64_t)tile * 32;
     const int64_t row = row0 + r;
     const bool live = row < M;
@@ -854,21 +866,26 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W) __attribute__((amdgpu_waves_per
     STAMP(15);
 }
 
+#ifndef ML_STEP_RTW
+#define ML_STEP_RTW 1  // row tiles per workgroup of the fused MLP step (kFused; 2 measured slower)
+#endif
 template <typename T, int H, int L, int MODE, int HC>
 static void launch_step_hc(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                            int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                            hipStream_t s, const RecK& rec) {
-    auto k = ppo_step_kernel<T, H, L, MODE, HC>;
+    // ntiles = Mp / 32 is even (Mp is a multiple of kRowAlign = 64)
+    constexpr int RTW = (MODE == kFused && StepCfg<H>::W * ML_STEP_RTW <= 16) ? ML_STEP_RTW : 1;
+    auto k = ppo_step_kernel<T, H, L, MODE, HC, RTW>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  128 * 1024);
+                                  160 * 1024);
         attr_set = true;
     }
-    const size_t lds = step_lds<T, H, L, HC>();
-    const int threads = 64 * StepCfg<H>::W;
-    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(threads), lds, s, P, R, mb_seq, mb, M, adv_st, hp,
-                       ws, rec);
+    const size_t lds = step_lds<T, H, L, HC, RTW>();
+    const int threads = 64 * StepCfg<H>::W * RTW;
+    hipLaunchKernelGGL(k, dim3(ws.ntiles / RTW), dim3(threads), lds, s, P, R, mb_seq, mb, M,
+                       adv_st, hp, ws, rec);
 }
 template <typename T, int H, int L, int MODE = kFused>
 static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
