@@ -87,8 +87,18 @@ constexpr int kAdamBlocks = 256;
 __device__ inline float global_norm(const double* gpart, int64_t npart) {
     __shared__ double gn_red[4];
     __shared__ float gn_sh;
+    // up to 8 partials per thread loaded together (fixed summation order)
     double t = 0.0;
-    for (int64_t i = threadIdx.x; i < npart; i += 256) t += gpart[i];
+    for (int64_t i0 = threadIdx.x; i0 < npart; i0 += 8 * 256) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + (int64_t)u * 256;
+            v[u] = i < npart ? gpart[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t += v[u];
+    }
     t = wave_sum64d(t);
     if ((threadIdx.x & 63) == 0) gn_red[threadIdx.x >> 6] = t;
     __syncthreads();

@@ -190,8 +190,18 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     // layer 0: observation fragments straight from the env output (cast to
     // the compute dtype = ObservationsCaster); wave 0 copies them to the store
     // the second layer's weights (this wave's blocks) are in flight from the start
-    frag w1[KSH][NBW];
-    if (L > 1) prefetch_img<T, NBW, KSH>(w1, (const T*)P.wt[1] + (int64_t)w * NBW * KSH * 64 * E, lane);
+#ifndef ML_POL_W1_RING
+#define ML_POL_W1_RING 8  // k-steps of the second layer's weights in flight from the start (0: all)
+#endif
+    constexpr int W1R = ML_POL_W1_RING > 0 && ML_POL_W1_RING < KSH ? ML_POL_W1_RING : KSH;
+    frag w1[W1R][NBW];
+    if (L > 1) {
+        if constexpr (W1R == KSH)
+            prefetch_img<T, NBW, KSH>(w1, (const T*)P.wt[1] + (int64_t)w * NBW * KSH * 64 * E, lane);
+        else
+            gemm_lds_issue<T, NBW, KSH, W1R>(w1, (const T*)P.wt[1] + (int64_t)w * NBW * KSH * 64 * E,
+                                             lane);
+    }
     f32x16 acc[NBW];
     zero_acc<NBW>(acc);
     gemm_first<T, NBW>(acc, obs + (live ? row : 0) * D, live, D / KS,
@@ -238,7 +248,14 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         __syncthreads();
         zero_acc<NBW>(acc);
         if (l == 0)
-            gemm_pre_lds<T, NBW, KSH>(acc, w1, fr, lane);
+        {
+            if constexpr (W1R == KSH)
+                gemm_pre_lds<T, NBW, KSH>(acc, w1, fr, lane);
+            else
+                gemm_lds_run<T, NBW, KSH, W1R>(acc, w1, fr,
+                                               (const T*)P.wt[1] + (int64_t)w * NBW * KSH * 64 * E,
+                                               lane);
+        }
         else
             gemm_lds<T, NBW, KSH, 8>(acc, fr,
                                      (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);

@@ -204,6 +204,46 @@ __device__ inline void gemm_lds(f32x16 (&acc)[NOUT], const typename RT<T>::frag*
     }
 }
 
+// gemm_lds in two halves: the first DEPTH-1 k-steps of A fragments issued
+// early (before a barrier or a LayerNorm phase, so the weight stream is
+// already flowing when the product starts), then the product itself.
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_lds_issue(typename RT<T>::frag (&ra)[DEPTH][NOUT],
+                                      const T* __restrict__ img, int lane, int bstride = NKS) {
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+#pragma unroll
+    for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * bstride + s) * FB);
+}
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_lds_run(f32x16 (&acc)[NOUT], typename RT<T>::frag (&ra)[DEPTH][NOUT],
+                                    const typename RT<T>::frag* fr, const T* __restrict__ img,
+                                    int lane, int bstride = NKS) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    frag b = fr[lane];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int sl = s + DEPTH - 1;
+        if (sl < NKS) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb)
+                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * bstride + sl) * FB);
+        }
+        const frag bn = s + 1 < NKS ? fr[(s + 1) * 64 + lane] : b;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) acc[nb] = MT<T>::mma(ra[s % DEPTH][nb], b, acc[nb]);
+        __builtin_amdgcn_sched_barrier(0);
+        b = bn;
+    }
+}
+
 // gemm_lds over two concatenated products acc += Img1 . B1 + Img2 . B2 (each
 // NKS k-steps, B fragments from LDS) as ONE ring of 2 NKS steps, so the
 // weight prefetch does not drain between them.

@@ -7,4 +7,4 @@ for f in csrc/*.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DML_STAMPS -w -c $f -o build_stamps/$(basename $f .hip).o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build_stamps/*.o -o madrona_learn/_lib/libmlearn_stamps.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build_stamps/*.o -o madrona_learn/_lib/libmlearn_stamps.so -L/opt/rocm/lib -lrccl
