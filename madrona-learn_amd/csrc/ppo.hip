@@ -108,11 +108,15 @@ static uint64_t* g_stamp_buf = nullptr;
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Split-K plan of one weight gradient [I][J] over Mp rows: ~128 workgroups.
+// Split-K plan of one weight gradient [I][J] over Mp rows: ~ML_WG_TARGET
+// workgroups per weight.
+#ifndef ML_WG_TARGET
+#define ML_WG_TARGET 128
+#endif
 static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
-    int64_t s = 128 / tiles;
+    int64_t s = ML_WG_TARGET / tiles;
     if (s < 1) s = 1;
     if (s > chunks) s = chunks;
     int64_t per = (chunks + s - 1) / s;
