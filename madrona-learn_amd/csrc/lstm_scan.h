@@ -323,3 +323,169 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_dfeat_kernel(LstmK R, 
         store4(drow + 8 * g + 4 * h, acc[0][4 * g], acc[0][4 * g + 1], acc[0][4 * g + 2],
                acc[0][4 * g + 3]);
 }
+
+// ---------------------------------------------------------------------------
+// Per-step scans: one launch per time step with a one-wave workgroup per (32
+// sequences, 32-unit block), (mb / 32) x (H / 32) workgroups, so the
+// recurrence runs on every CU (the persistent scans above keep H / 32 waves
+// on only mb / 32 CUs, each streaming the whole Wh image every step).  The
+// carries cross the launch boundary through memory: h and c into step t are
+// the rows hin / cin written by step t - 1 (cleared where dones[t - 1]), the
+// c cotangent into step t is dcc [Mp][H] f32 written by step t + 1.  B
+// fragments are read straight from the natural-order rows (RT<T>::row): no
+// LDS, no barrier.  The MFMA sequences and the cell arithmetic are those of
+// the persistent scans, so gates, c, h and dG are bit-identical to them.
+// ---------------------------------------------------------------------------
+template <typename T, int H>
+__global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
+    const float4* __restrict__ gin, const T* __restrict__ sh, const T* __restrict__ sc,
+    LstmWsK lw, int t) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NW = H / 32;
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    const int tile = blockIdx.x, w = blockIdx.y;
+    const int m = tile * 32 + r;
+    const int64_t f = (int64_t)t * mb + m;
+    // carry rows into step t: the sequence's rnn_start_states (rollouts.py:
+    // 533-537) at step 0 (also written out as the step's hin / cin rows for
+    // the backward and the weight gradient), else the rows step t - 1 wrote
+    const T *hrow, *crow;
+    if (t == 0) {
+        const int64_t seq = mb_seq[m];
+        const int64_t c = seq / ro.N, b = seq - c * ro.N;
+        hrow = sh + (c * ro.ld + b) * H;
+        crow = sc + (c * ro.ld + b) * H;
+    } else {
+        hrow = (const T*)lw.hin + f * H;
+        crow = (const T*)lw.cin + f * H;
+    }
+    frag hb[KSH];
+#pragma unroll
+    for (int s = 0; s < KSH; ++s) hb[s] = RT<T>::row(hrow, s, h);
+    float cc[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int u0 = w * 32 + 8 * j + 4 * h;
+        const float4 cv = load4(crow + u0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cc[4 * j + e] = f4get(cv, e);
+        if (t == 0) {
+            const float4 hv = load4(hrow + u0);
+            store4((T*)lw.hin + f * H + u0, hv.x, hv.y, hv.z, hv.w);
+            store4((T*)lw.cin + f * H + u0, cv.x, cv.y, cv.z, cv.w);
+        }
+    }
+    f32x16 acc[4];
+    {
+        const float4* gi = gin + gin_base((int64_t)t * (mb / 32) + tile, NW, w) + lane;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 x = gi[(4 * g + c) * 64];
+                acc[g][4 * c] = x.x;
+                acc[g][4 * c + 1] = x.y;
+                acc[g][4 * c + 2] = x.z;
+                acc[g][4 * c + 3] = x.w;
+            }
+    }
+    gemm_ring<T, 4, KSH, 8>(acc, hb, KSH, (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
+    const bool more = t + 1 < ro.bptt;
+    const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+    const float keep = done ? 0.f : 1.f;
+    T* gts = (T*)lw.gates + f * 4 * H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int u0 = w * 32 + 8 * j + 4 * h;
+        float gi[4], gf[4], gg[4], go[4], cn[4], hn[4], hc[4], ck[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e, u = u0 + e;
+            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + R.bias[u], acc[1][q] + R.bias[H + u],
+                                               acc[2][q] + R.bias[2 * H + u],
+                                               acc[3][q] + R.bias[3 * H + u], cc[q]);
+            gi[e] = o.i;
+            gf[e] = o.f;
+            gg[e] = o.g;
+            go[e] = o.o;
+            cn[e] = o.c;
+            hn[e] = o.h;
+            ck[e] = keep * o.c;
+            hc[e] = keep * o.h;
+        }
+        store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
+        store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
+        store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
+        store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
+        store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
+        store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
+        if (more) {
+            store4((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
+            store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
+        }
+    }
+}
+
+template <typename T, int H>
+__global__ __launch_bounds__(64) void lstm_bwd_step_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
+    float* colpart, int CP, int cp0, int t) {
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NU = H / 32;
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    const int tile = blockIdx.x, w = blockIdx.y;
+    const int m0 = tile * 32, m = m0 + r;
+    const int bptt = ro.bptt;
+    const int64_t fs = (int64_t)t * mb + m;
+    const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    if (t + 1 < bptt)  // dh_t = dG_{t+1} Wh^T (h-cotangent block w of w_bwd)
+        gemm_stream<T, 1, NKS, 8>(acc, (const T*)lw.dg + (fs + mb) * 4 * H,
+                                  (const T*)R.w_bwd + (int64_t)(NU + w) * NKS * 64 * E, lane);
+    const T* gts = (const T*)lw.gates + fs * 4 * H;
+    T* dgs = (T*)lw.dg + fs * 4 * H;
+    float dpi[16], dpf[16], dpg[16], dpo[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int u0 = w * 32 + 8 * j + 4 * h;
+        const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
+        const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
+        const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
+        const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
+        const float4 ci = load4((const T*)lw.cin + fs * H + u0);
+        const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(lw.dcc + fs * H + u0);
+        float dco[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e;
+            const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
+            const float dh = f4get(dho, e) + (cut ? 0.f : acc[0][q]);
+            const float tc = tanh_fast(f4get(c4, e));
+            const float dout = dh * tc;
+            const float dc = f4get(dcin, e) + dh * o_ * (1.f - tc * tc);
+            dpi[q] = rnd<T>((dc * g_) * i_ * (1.f - i_));
+            dpf[q] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
+            dpg[q] = rnd<T>((dc * i_) * (1.f - g_ * g_));
+            dpo[q] = rnd<T>(dout * o_ * (1.f - o_));
+            dco[e] = dc * f_;
+        }
+        if (t > 0) *(float4*)(lw.dcc + (fs - mb) * H + u0) = make_float4(dco[0], dco[1], dco[2], dco[3]);
+        store4(dgs + u0, dpi[4 * j], dpi[4 * j + 1], dpi[4 * j + 2], dpi[4 * j + 3]);
+        store4(dgs + H + u0, dpf[4 * j], dpf[4 * j + 1], dpf[4 * j + 2], dpf[4 * j + 3]);
+        store4(dgs + 2 * H + u0, dpg[4 * j], dpg[4 * j + 1], dpg[4 * j + 2], dpg[4 * j + 3]);
+        store4(dgs + 3 * H + u0, dpo[4 * j], dpo[4 * j + 1], dpo[4 * j + 2], dpo[4 * j + 3]);
+    }
+    // bias gradient: column sums of dG over this tile's 32 rows
+    const int qs = col_sum16_index(lane);
+    float* cp = colpart + (int64_t)(((int64_t)t * mb + m0) / 32) * CP + cp0;
+    const int uq = w * 32 + feat(0, qs, h);
+    const float si = col_sum16(dpi, lane), sf = col_sum16(dpf, lane);
+    const float sg = col_sum16(dpg, lane), so = col_sum16(dpo, lane);
+    if ((lane & 16) == 0) {
+        cp[uq] = si;
+        cp[H + uq] = sf;
+        cp[2 * H + uq] = sg;
+        cp[3 * H + uq] = so;
+    }
+}

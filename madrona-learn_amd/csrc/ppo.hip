@@ -71,6 +71,7 @@ struct LstmWsK {
     void* dhout;  // [Mp][H]  d loss / d h_t from the heads
     void* dfeat;  // [Mp][H]  d loss / d trunk output
     void* gin;    // [Mp/32][H/32][16][64] float4: F Wi in accumulator order (lstm_gin_kernel)
+    float* dcc;   // [Mp][H] f32  c cotangent into step t (per-step reverse scan)
 };
 
 struct WsK {
@@ -174,6 +175,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         lw.dhout = take(Mp * H * es);
         lw.dfeat = take(Mp * H * es);
         lw.gin = take(Mp * 4 * H * sizeof(float));
+        lw.dcc = (float*)take(Mp * H * sizeof(float));
         if (LW) *LW = lw;
     }
     if (W) *W = w;
@@ -1465,8 +1467,18 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, feat,
                            (float4*)lw.gin);
     }
-    // forward scan: one persistent launch (a workgroup per 32 sequences)
-    {
+#ifndef ML_LSTM_PERSISTENT
+#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
+#endif
+    // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
+    // workgroups (ML_LSTM_PERSISTENT: one persistent launch, a workgroup per
+    // 32 sequences)
+    if (!ML_LSTM_PERSISTENT) {
+        for (int t = 0; t < bptt; ++t)
+            hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s,
+                               RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
+                               (const T*)start_c, lw, t);
+    } else {
         const size_t lds = (size_t)KSH * 64 * FR;
         auto k = lstm_fwd_scan_kernel<T, H>;
         static bool attr_set = false;
@@ -1482,7 +1494,11 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     step(std::integral_constant<int, kHeads>{});
     // reverse scan
     const int cp0 = L * 2 * H + head_cols(p);
-    {
+    if (!ML_LSTM_PERSISTENT) {
+        for (int t = bptt - 1; t >= 0; --t)
+            hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s,
+                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+    } else {
         const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
         auto k = lstm_bwd_scan_kernel<T, H>;
         static bool attr_set = false;

@@ -244,6 +244,41 @@ __device__ inline void gemm_lds_run(f32x16 (&acc)[NOUT], typename RT<T>::frag (&
     }
 }
 
+// acc[nb] += sum_s Img[block nb][step s] x row-fragment(s) with BOTH operands
+// streamed: A fragments from the image and B fragments (natural k order) from
+// this lane's row in memory, DEPTH k-steps of each in flight.
+template <typename T, int NOUT, int NKS, int DEPTH>
+__device__ inline void gemm_stream(f32x16 (&acc)[NOUT], const T* __restrict__ brow,
+                                   const T* __restrict__ img, int lane) {
+    typedef typename RT<T>::frag frag;
+    constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+    const int voff = lane * RT<T>::E * (int)sizeof(T);
+    const int h = lane >> 5;
+    frag ra[DEPTH][NOUT], rb[DEPTH];
+#pragma unroll
+    for (int s = 0; s < DEPTH - 1; ++s) {
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * NKS + s) * FB);
+        rb[s] = RT<T>::row(brow, s, h);
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int sl = s + DEPTH - 1;
+        if (sl < NKS) {
+#pragma unroll
+            for (int nb = 0; nb < NOUT; ++nb)
+                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * NKS + sl) * FB);
+            rb[sl % DEPTH] = RT<T>::row(brow, sl, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < NOUT; ++nb)
+            acc[nb] = MT<T>::mma(ra[s % DEPTH][nb], rb[s % DEPTH], acc[nb]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // gemm_lds over two concatenated products acc += Img1 . B1 + Img2 . B2 (each
 // NKS k-steps, B fragments from LDS) as ONE ring of 2 NKS steps, so the
 // weight prefetch does not drain between them.
