@@ -167,7 +167,7 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     achieved = step_flop / t_step / 1e12
     traffic, pmc_name = pmc_traffic("ppo_step")
     roof = {
-        "kernel": "ppo_step_kernel<bf16,256,2,0,32> (mlearn_ppo_minibatch_fwd_bwd)",
+        "kernel": "ppo_step_kernel<bf16,256,2,0,32,1> (mlearn_ppo_minibatch_fwd_bwd)",
         "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
         "frac": achieved / BF16_PEAK_TFS, "traffic": traffic,
         "traffic_source": (f"profiles/pmc_r02.json ({pmc_name})" if traffic is not None
@@ -175,6 +175,11 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
         "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
         "units_per_launch": M, "flop_per_unit": fwd + bwd,
         "algorithmic_bytes_per_launch": 184 * M,
+        # the measured traffic is dominated by the weight-gradient operands the
+        # kernel writes for wgrad_kernel (X_0, A_l, dZ_l, d head rows in bf16,
+        # 2,240 B/row = 147 MB at 65,536 rows)
+        "traffic_note": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE); includes the "
+                        "2240 B/row weight-gradient operand spill",
     }
 
     # rollout policy step (forward + sample) over this rank's envs
