@@ -362,7 +362,10 @@ int mlearn_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn_roll
  * its own (one launch): fills the workspace with the weight-gradient
  * operands and the per-tile partials, no reduction into a gradient.  Used to
  * time the dominant kernel (bench.py roofline) and by callers that schedule
- * the reduction themselves. */
+ * the reduction themselves.  With env MLEARN_A0_RECOMPUTE=1, bf16 policies
+ * with >= 2 layers and obs_dim <= 64 keep the first layer's per-row LayerNorm
+ * statistics instead of its post-activation rows (the weight-gradient stage
+ * recomputes those). */
 int mlearn_ppo_minibatch_fwd_bwd(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
                                  const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
                                  const mlearn_ppo_hparams* hp, void* workspace,

@@ -55,8 +55,17 @@ constexpr int kLossSlots = 20;   // per tile doubles
 #endif
 constexpr int kColChunks = 32;   // first-level chunks of the per-tile column partials
 constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
-constexpr int kWgChunk = 32;     // weight-gradient K chunk (rows of the minibatch)
+#ifndef ML_WG_CHUNK
+#define ML_WG_CHUNK 32  // weight-gradient K chunk of the bf16 kernel (rows of the minibatch)
+#endif
+// weight-gradient K chunk (rows of the minibatch staged per LDS stage); f32 keeps 32
+template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_CHUNK : 32; }
+static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
 constexpr int kRowAlign = 64;    // Mp granularity
+#ifndef ML_WG_WAVES
+#define ML_WG_WAVES 2  // waves per SIMD the weight-gradient kernel is register-budgeted for
+#endif
+constexpr int kRecMaxD = 64;     // widest observation the weight-gradient A_0 recompute takes
 constexpr int kMaxJobs = MLEARN_MAX_LAYERS + 3;  // weight-gradient jobs
 
 // LSTM scan buffers of the recurrent update (rows f = t * mb + m, compute
@@ -89,6 +98,8 @@ struct WsK {
     int64_t Mp;
     int ntiles;                         // Mp / 32
     int CP;                             // L*2*H + 32
+    float* lnst;                        // [Mp][2] layer-0 LayerNorm {mean, rstd} (a0r)
+    int a0r;                            // A_0 not spilled: wgrad recomputes it (kFused)
     uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
 
@@ -114,7 +125,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 #ifndef ML_WG_TARGET
 #define ML_WG_TARGET 128
 #endif
-static void plan_splits(int I, int J, int64_t Mp, int* splits, int64_t* rps) {
+static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int64_t* rps) {
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
     int64_t s = ML_WG_TARGET / tiles;
@@ -151,6 +162,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         w.dz[l] = take(Mp * H * es);
     }
     w.dhead = take(Mp * HC * es);
+    w.lnst = (float*)take(Mp * 2 * sizeof(float));
     w.colpart = (float*)take(tiles * w.CP * sizeof(float));
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
@@ -159,7 +171,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     for (int l = 0; l < njobs; ++l) {
         const int I = l >= L ? H : (l == 0 ? D : H);
         const int J = l == L ? HC : (l > L ? 4 * H : H);
-        plan_splits(I, J, Mp, &w.splits[l], &w.rps[l]);
+        plan_splits(I, J, Mp, wg_chunk_es(es), &w.splits[l], &w.rps[l]);
         w.slab_off[l] = so;
         so += (int64_t)w.splits[l] * I * J;
     }
@@ -359,6 +371,15 @@ __device__ inline void loss_value_twohot_g(const HpK& hp, float* lg, int A, int 
 // statistics [W][32][2], head partials [head_parts][32][HC+1], logits /
 // d logits [32][HC+1], loss partials [W][kLossSlots], critic bins [HC].
 // ---------------------------------------------------------------------------
+#ifndef ML_STORE_LATE
+// 1: every spill store of the step kernel is issued AFTER the weight loads of
+// the product that follows it (vmcnt counts loads and stores in issue order,
+// so a store batch issued first delays the product's first load wait)
+#define ML_STORE_LATE 1
+#endif
+#ifndef ML_STEP_RING
+#define ML_STEP_RING 8  // k-steps of weight fragments in flight in the step kernel's trunk products
+#endif
 #ifndef ML_STEP_MAXW
 #define ML_STEP_MAXW 8  // waves per workgroup of the fused step kernel (feature split)
 #endif
@@ -504,12 +525,31 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
     word aw[NBW][8];     // post-activation of the current layer
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
+    // post-activation rows A_l (weight-gradient operands), row-major
+    auto store_act = [&](int l) {
+        const bool skip = MODE == kTrunkBwd || (MODE == kFused && l == 0 && ws.a0r);
+        if (skip) return;
+        T* arow = (T*)ws.a[l] + row * H;
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                Pk<T>::store4(arow + (w * NBW + i) * 32 + 8 * g + 4 * h, aw[i][2 * g],
+                              aw[i][2 * g + 1]);
+    };
 #pragma unroll
     for (int l = 0; l < (kFwd ? L : 0); ++l) {
         if (l > 0) {
             zero_acc<NBW>(acc);
-            gemm_lds<T, NBW, KSH, 8>(acc, fr, (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E,
-                                     lane);
+            const T* img = (const T*)P.wt[l] + (int64_t)w * NBW * KSH * 64 * E;
+#if ML_STORE_LATE
+            frag ra[ML_STEP_RING][NBW];
+            gemm_lds_issue<T, NBW, KSH, ML_STEP_RING>(ra, img, lane);
+            store_act(l - 1);  // A_{l-1}, behind this product's first weight loads
+            gemm_lds_run<T, NBW, KSH, ML_STEP_RING>(acc, ra, fr, img, lane);
+#else
+            gemm_lds<T, NBW, KSH, ML_STEP_RING>(acc, fr, img, lane);
+#endif
             STAMP(4);
         }
         f2 x2[NBW][8];
@@ -536,15 +576,10 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         rstd_r[l] = rstd;
         STAMP(2 + 3 * l);
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
-        if (MODE != kTrunkBwd) {
-            T* arow = (T*)ws.a[l] + row * H;
-#pragma unroll
-            for (int i = 0; i < NBW; ++i)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    Pk<T>::store4(arow + (w * NBW + i) * 32 + 8 * g + 4 * h, aw[i][2 * g],
-                                  aw[i][2 * g + 1]);
-        }
+        if (MODE == kFused && l == 0 && ws.a0r && w == 0 && h == 0)
+            *(float2*)(ws.lnst + 2 * row) = make_float2(mean, rstd);
+        // the last layer's rows go out behind the head's weight loads (HC = 32)
+        if (!ML_STORE_LATE || (l + 1 == L && (MODE != kFused || HC != 32))) store_act(l);
         if (l + 1 < L) {
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
@@ -582,6 +617,21 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
             const T* himg = (const T*)(MODE == kHeads ? rec.head_t_nat : P.head_t);
             f32x16 ha[1];
             zero_acc<1>(ha);
+#if ML_STORE_LATE
+            if constexpr (MODE == kFused) {
+                // every head weight fragment of this wave in flight, then the
+                // last layer's rows, then the product
+                constexpr int HS = NBW * SPB;
+                constexpr int FB = 64 * E * (int)sizeof(T);
+                const __amdgpu_buffer_rsrc_t hrs = img_rsrc(himg + (int64_t)w * HS * 64 * E);
+                frag hA[HS];
+#pragma unroll
+                for (int s2 = 0; s2 < HS; ++s2) hA[s2] = img_load<T>(hrs, lane * E * (int)sizeof(T), s2 * FB);
+                store_act(L - 1);
+#pragma unroll
+                for (int s2 = 0; s2 < HS; ++s2) ha[0] = MT<T>::mma(hA[s2], hb[s2], ha[0]);
+            } else
+#endif
             gemm_ring<T, 1, NBW * SPB, NBW * SPB < 8 ? NBW * SPB : 8>(
                 ha, hb, NBW * SPB, himg + (int64_t)w * NBW * SPB * 64 * E, lane);
 #pragma unroll
@@ -715,6 +765,24 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         ws.loss_part[(int64_t)tile * kLossSlots + tid] = v;
     }
     STAMP(8);
+#if ML_STORE_LATE
+    // the backward head product's weight fragments go out before the stores below
+    constexpr int kHeadPre = KSHD * NBW <= 16 ? KSHD : 0;
+#else
+    constexpr int kHeadPre = 0;
+#endif
+    frag hbw[kHeadPre > 0 ? kHeadPre : 1][NBW];
+#if ML_STORE_LATE
+    const T* hbimg = (const T*)P.head + (int64_t)w * NBW * KSHD * 64 * E;
+    if constexpr (kHeadPre > 0) {
+        const __amdgpu_buffer_rsrc_t hrs = img_rsrc(hbimg);
+#pragma unroll
+        for (int s2 = 0; s2 < kHeadPre; ++s2)
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb)
+                hbw[s2][nb] = img_load<T>(hrs, lane * E * (int)sizeof(T), (nb * KSHD + s2) * 64 * E * (int)sizeof(T));
+    }
+#endif
     // d head: row-major store (wgrad operand) and the head-bias column
     // partials (one 32-column block per wave)
     if (w == 0) {
@@ -739,8 +807,15 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         for (int s = 0; s < KSHD; ++s) db[s] = RT<T>::row_lds(lg + r * LGS, s, h);
         zero_acc<NBW>(acc);
         // dA_{L-1}^T = Head . dHead^T  (this wave's feature blocks)
-        gemm_ring<T, NBW, KSHD, 2>(acc, db, KSHD,
-                                   (const T*)P.head + (int64_t)w * NBW * KSHD * 64 * E, lane);
+        if constexpr (kHeadPre > 0) {
+#pragma unroll
+            for (int s2 = 0; s2 < kHeadPre; ++s2)
+#pragma unroll
+                for (int nb = 0; nb < NBW; ++nb) acc[nb] = MT<T>::mma(hbw[s2][nb], db[s2], acc[nb]);
+        } else {
+            gemm_ring<T, NBW, KSHD, 2>(acc, db, KSHD,
+                                       (const T*)P.head + (int64_t)w * NBW * KSHD * 64 * E, lane);
+        }
     }
     }  // kLoss
     if constexpr (MODE == kHeads) {
@@ -782,6 +857,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         float* cp = ws.colpart + (int64_t)tile * ws.CP + l * 2 * H;
         f2 su2 = {0.f, 0.f}, sv2 = {0.f, 0.f};
         f2 zc2[NBW][8], u2[NBW][8];
+        float cpb[NBW], cpg[NBW];  // this lane's LayerNorm bias / scale column partials
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
             const int nb = w * NBW + i;
@@ -814,14 +890,19 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                 }
             }
             // LayerNorm scale/bias partials: column sums over the tile's rows
-            const float tgs = col_sum16(pg, lane);
-            const float tbs = col_sum16(pb, lane);
-            if ((lane & 16) == 0) {
-                const int f = feat(nb, qs, h);
-                cp[f] = tbs;
-                cp[H + f] = tgs;
-            }
+            cpg[i] = col_sum16(pg, lane);
+            cpb[i] = col_sum16(pb, lane);
         }
+        auto store_cp = [&]() {
+            if ((lane & 16) == 0)
+#pragma unroll
+                for (int i = 0; i < NBW; ++i) {
+                    const int f = feat(w * NBW + i, qs, h);
+                    cp[f] = cpb[i];
+                    cp[H + f] = cpg[i];
+                }
+        };
+        if (!ML_STORE_LATE) store_cp();
         STAMP(10 + 3 * (L - 1 - l));
         float su = sum_halves(su2.x + su2.y);
         float sv = sum_halves(sv2.x + sv2.y);
@@ -843,16 +924,23 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         word dzw[NBW][8];
         T* dzrow = (T*)ws.dz[l] + row * H;
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) {
+        for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const f2 d = r2 * u2[i][k] + (ca2 * zc2[i][k] + cb2);
                 dzw[i][k] = Pk<T>::pack(d.x, d.y);
             }
+        auto store_dz = [&]() {
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                Pk<T>::store4(dzrow + (w * NBW + i) * 32 + 8 * g + 4 * h, dzw[i][2 * g],
-                              dzw[i][2 * g + 1]);
+            for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    Pk<T>::store4(dzrow + (w * NBW + i) * 32 + 8 * g + 4 * h, dzw[i][2 * g],
+                                  dzw[i][2 * g + 1]);
+        };
+        if (!ML_STORE_LATE || l == 0) {
+            if (ML_STORE_LATE) store_cp();
+            store_dz();
         }
         STAMP(11 + 3 * (L - 1 - l));
         if (l > 0) {
@@ -861,11 +949,23 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
 #pragma unroll
                 for (int t = 0; t < SPB; ++t)
                     fr[((w * NBW + i) * SPB + t) * 64 + lane] = Pk<T>::frag(dzw[i], t);
+            const T* img = (const T*)P.w[l] + (int64_t)w * NBW * KSH * 64 * E;
+#if ML_STORE_LATE
+            // dA_{l-1}^T = W_l . dZ_l^T (this wave's feature blocks): weight loads
+            // first, then this layer's column partials and dZ rows
+            frag ra[ML_STEP_RING][NBW];
+            gemm_lds_issue<T, NBW, KSH, ML_STEP_RING>(ra, img, lane);
+            store_cp();
+            store_dz();
+            __syncthreads();
+            zero_acc<NBW>(acc);
+            gemm_lds_run<T, NBW, KSH, ML_STEP_RING>(acc, ra, fr, img, lane);
+#else
             __syncthreads();
             zero_acc<NBW>(acc);
             // dA_{l-1}^T = W_l . dZ_l^T  (this wave's feature blocks)
-            gemm_lds<T, NBW, KSH, 8>(acc, fr, (const T*)P.w[l] + (int64_t)w * NBW * KSH * 64 * E,
-                                     lane);
+            gemm_lds<T, NBW, KSH, ML_STEP_RING>(acc, fr, img, lane);
+#endif
             STAMP(12 + 3 * (L - 1 - l));
         }
     }
@@ -922,17 +1022,25 @@ struct WgJob {
     float* out;
     int64_t rps;
     int I, J, ti, tj, splits, wg0;
+    int rec;  // X is A_0 recomputed from X_0 (wgrad_tile<T, true>)
 };
 struct WgJobs {
     WgJob job[kMaxJobs];
     int n;
     int64_t Mp;
     int nwg, ncol, ncolx;  // weight-gradient blocks, column-sum blocks (ncolx per chunk)
+    // A_0 recompute (jobs with rec): layer-0 weight image, LayerNorm scale /
+    // bias, per-row {mean, rstd}, observation width
+    const void* w0img;
+    const float* g0;
+    const float* b0;
+    const float* lnst;
+    int D;
 };
 
 template <typename T> struct WgCfg {
     static constexpr int LD = sizeof(T) == 2 ? 160 : 132;  // LDS row (elements)
-    static constexpr size_t buf = (size_t)kWgChunk * LD * sizeof(T);  // one operand, one stage
+    static constexpr size_t buf = (size_t)wg_chunk<T>() * LD * sizeof(T);  // one operand, one stage
     static constexpr size_t lds = 4 * buf;
 };
 
@@ -964,29 +1072,26 @@ template <> struct WgFrag<float> {
 __device__ inline void colsum_block(const WsK& ws, int bx, int c);
 __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K, float* out);
 
-// Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
-// level of the column partials; one more (if loss_out) the loss metrics.
-template <typename T>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
-                                                    float* loss_out) {
-    if ((int)blockIdx.x >= jobs.nwg) {
-        const int b = blockIdx.x - jobs.nwg;
-        if (b < jobs.ncol) colsum_block(ws, b % jobs.ncolx, b / jobs.ncolx);
-        else loss_block(ws, hp, M, K, loss_out);
-        return;
-    }
+// Weight-gradient tile (i0, j0) of job J over its split's rows.  REC: the X
+// operand is the first layer's post-activation A_0, recomputed chunk by chunk
+// from the gathered observations X_0 (ws.x0) and the per-row LayerNorm
+// statistics the step kernel saved (ws.lnst), instead of read back from a
+// spilled [Mp][H] copy: relu(LN_0(X_0 W_0)) with the step kernel's MFMA
+// sequence (gemm_first: k-steps in ascending order) and its LayerNorm
+// arithmetic (ln_pack_stats / ln_apply), so the operand is bit-identical.
+template <typename T, bool REC>
+__device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local, char* smem) {
+    constexpr int kWgChunk = wg_chunk<T>();
     constexpr int VPC = 16 / sizeof(T);                  // elements per 16-B chunk
     constexpr int CPR = kWgTile / VPC;                   // chunks per tile row
     constexpr int PER = kWgChunk * CPR / 256;            // chunks per thread per operand
     constexpr int LD = WgCfg<T>::LD, KSTEPS = kWgChunk / MT<T>::KS;
+    constexpr int RB = kWgChunk / 32;                    // 32-row blocks per chunk (REC)
+    constexpr int XKS = REC ? kRecMaxD / RT<T>::KS : 1;  // max first-layer k-steps
     typedef __attribute__((ext_vector_type(4))) uint32_t u4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename RT<T>::frag frag;
     T* lds = (T*)smem;  // [stage][operand][kWgChunk][LD]
 
-    int jb = 0;
-    while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
-    const WgJob& J = jobs.job[jb];
-    const int local = blockIdx.x - J.wg0;
     const int nt = J.ti * J.tj;
     int split, t;
     if ((J.splits & 7) == 0 && (J.wg0 & 7) == 0) {
@@ -1012,29 +1117,79 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp,
     const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
     const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
 
+    // REC: this wave recomputes A_0 features [i0 + 32 w, i0 + 32 w + 32) of
+    // the chunk's rows; its W_0 image fragments stay in registers, the
+    // LayerNorm scale / bias of layer 0 are staged in LDS after the buffers
+    const int D = jobs.D, dks = REC ? D / RT<T>::KS : 0, h = lane >> 5, r = lane & 31;
+    frag wa[XKS];
+    float* gm = (float*)(smem + WgCfg<T>::lds);  // [2][H] (REC)
+    if constexpr (REC) {
+        const int H = J.I;
+        for (int i = tid; i < 2 * H; i += 256) gm[i] = i < H ? jobs.g0[i] : jobs.b0[i - H];
+        const T* img = (const T*)jobs.w0img + (int64_t)((i0 >> 5) + w) * dks * 64 * RT<T>::E;
+        const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+        const int voff = lane * RT<T>::E * (int)sizeof(T);
+#pragma unroll
+        for (int s = 0; s < XKS; ++s)
+            if (s < dks) wa[s] = img_load<T>(rs, voff, s * 64 * RT<T>::E * (int)sizeof(T));
+    }
+
     // two register sets of staged rows: chunk c + 2 is in flight while chunk c
     // is multiplied out of LDS and chunk c + 1 is written to the other buffer
-    u4 rx[2][PER], ry[2][PER];
-    auto gload = [&](int c, u4 (&gx)[PER], u4 (&gy)[PER]) {
+    u4 rx[2][REC ? 1 : PER], ry[2][PER];
+    frag xb[2][REC ? RB : 1][XKS];  // REC: X_0 row fragments of the chunk's row blocks
+    float2 st[2][REC ? RB : 1];      // REC: {mean, rstd} of those rows
+    auto gload = [&](int c, int set) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
             const u4 zero = {0u, 0u, 0u, 0u};
-            gx[u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
-            gy[u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
+            if constexpr (!REC)
+                rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
+            ry[set][u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
+        }
+        if constexpr (REC) {
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+                const int64_t row = mb0 + 32 * b + r;
+#pragma unroll
+                for (int s = 0; s < XKS; ++s)
+                    if (s < dks) xb[set][b][s] = RT<T>::row(X + row * D, s, h);
+                st[set][b] = *(const float2*)(jobs.lnst + 2 * row);
+            }
         }
     };
-    auto sstore = [&](int stage, const u4 (&gx)[PER], const u4 (&gy)[PER]) {
+    auto sstore = [&](int stage, int set) {
         T* xs = lds + (size_t)stage * 2 * kWgChunk * LD;
         T* ys = xs + kWgChunk * LD;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
-            *(u4*)(xs + rr * LD + cc) = gx[u];
-            *(u4*)(ys + rr * LD + cc) = gy[u];
+            if constexpr (!REC) *(u4*)(xs + rr * LD + cc) = rx[set][u];
+            *(u4*)(ys + rr * LD + cc) = ry[set][u];
+        }
+        if constexpr (REC) {
+            if (i0 + 32 * w < J.I) {
+#pragma unroll
+                for (int b = 0; b < RB; ++b) {
+                    f32x16 acc[1];
+                    zero_acc<1>(acc);
+#pragma unroll
+                    for (int s = 0; s < XKS; ++s)
+                        if (s < dks) acc[0] = MT<T>::mma(wa[s], xb[set][b][s], acc[0]);
+                    typename Pk<T>::word zw[1][8], aw[1][8];
+                    f2 x2[1][8];
+                    float sum, sq;
+                    ln_pack_stats<T, 1>(acc, zw, x2, sum, sq);
+                    ln_apply<T, 1>(x2, st[set][b].x, st[set][b].y, gm, J.I, (i0 >> 5) + w, h, aw);
+                    T* xrow = xs + (32 * b + r) * LD + 32 * w;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Pk<T>::store4(xrow + 8 * g + 4 * h, aw[0][2 * g], aw[0][2 * g + 1]);
+                }
+            }
         }
     };
     f32x16 acc[2][2];
@@ -1058,25 +1213,26 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp,
                 for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a], fb[b], acc[a][b]);
         }
     };
-    gload(0, rx[0], ry[0]);
-    if (nchunks > 1) gload(1, rx[1], ry[1]);
-    sstore(0, rx[0], ry[0]);
-    if (nchunks > 2) gload(2, rx[0], ry[0]);
+    gload(0, 0);
+    if (nchunks > 1) gload(1, 1);
+    if constexpr (REC) __syncthreads();  // LayerNorm parameters staged
+    sstore(0, 0);
+    if (nchunks > 2) gload(2, 0);
     __syncthreads();
     for (int c = 0; c < nchunks; c += 2) {
         // even chunk c: buffer 0; chunk c + 1 waits in set 1
         compute(0);
         if (c + 1 < nchunks) {
-            sstore(1, rx[1], ry[1]);
-            if (c + 3 < nchunks) gload(c + 3, rx[1], ry[1]);
+            sstore(1, 1);
+            if (c + 3 < nchunks) gload(c + 3, 1);
         }
         __syncthreads();
         if (c + 1 >= nchunks) break;
         // odd chunk c + 1: buffer 1; chunk c + 2 waits in set 0
         compute(1);
         if (c + 2 < nchunks) {
-            sstore(0, rx[0], ry[0]);
-            if (c + 4 < nchunks) gload(c + 4, rx[0], ry[0]);
+            sstore(0, 0);
+            if (c + 4 < nchunks) gload(c + 4, 0);
         }
         __syncthreads();
     }
@@ -1092,6 +1248,31 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp,
                 const int j = j0 + jw + 32 * b + (lane & 31);
                 if (i < J.I && j < J.J) out[(int64_t)i * J.J + j] = acc[a][b][e];
             }
+}
+
+// Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
+// level of the column partials; one more (if loss_out) the loss metrics.
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES, 8))) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
+                                                    float* loss_out) {
+    if ((int)blockIdx.x >= jobs.nwg) {
+        const int b = blockIdx.x - jobs.nwg;
+        if (b < jobs.ncol) colsum_block(ws, b % jobs.ncolx, b / jobs.ncolx);
+        else loss_block(ws, hp, M, K, loss_out);
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int jb = 0;
+    while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
+    const WgJob& J = jobs.job[jb];
+    const int local = blockIdx.x - J.wg0;
+    if constexpr (std::is_same<T, bf16>::value) {
+        if (J.rec) {
+            wgrad_tile<T, true>(jobs, J, local, smem);
+            return;
+        }
+    }
+    wgrad_tile<T, false>(jobs, J, local, smem);
 }
 
 
@@ -1324,6 +1505,20 @@ __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K
     }
 }
 
+// MLEARN_A0_RECOMPUTE=1: A_0 is recomputed by the weight-gradient launch
+// instead of spilled by the step kernel (bf16, at least two layers,
+// D <= kRecMaxD).  Off by default: measured at the headline config the step
+// kernel gains 7 us per launch and the weight-gradient launch loses 36 us (the
+// recompute sits on its per-chunk critical path); kept for the A/B and pinned
+// bit-identical to the spill path (tests/test_gpu_fullsize.py).
+static bool a0_recompute(const mlearn_mlp_policy& p) {
+    if (p.dtype != MLEARN_DTYPE_BF16 || p.num_layers < 2 || p.obs_dim > kRecMaxD ||
+        p.obs_dim % 16 != 0)
+        return false;
+    const char* e = getenv("MLEARN_A0_RECOMPUTE");
+    return e && e[0] == '1';
+}
+
 template <typename T, int H>
 static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
                             const int32_t* mb_seq, int mb, const float* adv_st,
@@ -1335,6 +1530,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 #ifdef ML_STAMPS
     ws.stamps = g_stamp_buf;
 #endif
+    ws.a0r = a0_recompute(p);
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values, ro.dones,
                ro.T, ro.bptt_len, ro.N, ro.ld ? ro.ld : ro.N};
@@ -1365,12 +1561,18 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     WgJobs jobs{};
     jobs.n = L + 1;
     jobs.Mp = ws.Mp;
+    jobs.w0img = P.wt[0];
+    jobs.g0 = P.lns[0];
+    jobs.b0 = P.lnb[0];
+    jobs.lnst = ws.lnst;
+    jobs.D = p.obs_dim;
     int wg = 0;
     for (int l = 0; l <= L; ++l) {
         WgJob& J = jobs.job[l];
         J.I = l == L ? H : (l == 0 ? p.obs_dim : H);
         J.J = l == L ? head_cols(p) : H;
-        J.X = l == 0 ? ws.x0 : ws.a[l - 1];
+        J.rec = l == 1 && ws.a0r;
+        J.X = l == 0 || J.rec ? ws.x0 : ws.a[l - 1];
         J.Y = l == L ? ws.dhead : ws.dz[l];
         J.out = ws.slab + ws.slab_off[l];
         J.rps = ws.rps[l];
@@ -1392,7 +1594,8 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
             attr_set = true;
         }
         const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
+        const size_t lds = WgCfg<T>::lds + (ws.a0r ? 2 * H * sizeof(float) : 0);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, jobs, ws, hp, M,
                            p.actions.num_groups, loss_out);
     }
     LayoutK Lk = make_layout(p);

@@ -8,6 +8,6 @@ mkdir -p build_var_$name
 for f in csrc/*.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -w "$@" -c $f -o build_var_$name/$(basename $f .hip).o &
 done
-wait
+wait; for f in build_var_$name/*.o; do :; done; [ $(ls build_var_$name/*.o | wc -l) -eq $(ls csrc/*.hip | wc -l) ] || { echo "variant build failed"; exit 1; }
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build_var_$name/*.o -o madrona_learn/_lib/libmlearn_$name.so -L/opt/rocm/lib -lrccl
 rm -rf build_var_$name
