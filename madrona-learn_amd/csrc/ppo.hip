@@ -63,7 +63,7 @@ template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_C
 static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
 constexpr int kRowAlign = 64;    // Mp granularity
 #ifndef ML_WG_WAVES
-#define ML_WG_WAVES 2  // waves per SIMD the weight-gradient kernel is register-budgeted for
+#define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif
 constexpr int kRecMaxD = 64;     // widest observation the weight-gradient A_0 recompute takes
 constexpr int kMaxJobs = MLEARN_MAX_LAYERS + 3;  // weight-gradient jobs
@@ -125,10 +125,21 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 #ifndef ML_WG_TARGET
 #define ML_WG_TARGET 128
 #endif
+#ifndef ML_WG_CPW
+#define ML_WG_CPW 32  // > 0: split every weight into splits of this many chunks (balanced per-WG work)
+#endif
 static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int64_t* rps) {
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
     int64_t s = ML_WG_TARGET / tiles;
+    // balanced: splits of ML_WG_CPW chunks, at most 2 x the target workgroups
+    // per weight (the MLP trunk / head weights of <= 4 tiles; the LSTM's wide
+    // gate weights keep the target)
+    if (ML_WG_CPW > 0 && tiles <= 4) {
+        int64_t b = (chunks + ML_WG_CPW - 1) / ML_WG_CPW;
+        if (b > 8) b = (b + 7) / 8 * 8;  // multiples of 8 keep the XCD-aware tile mapping
+        s = b < 2 * s ? b : 2 * s;
+    }
     if (s < 1) s = 1;
     if (s > chunks) s = chunks;
     int64_t per = (chunks + s - 1) / s;
@@ -519,7 +530,9 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
 #pragma unroll
     for (int k = 0; k < NPAR; ++k)
         if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
-    __syncthreads();  // LayerNorm parameters staged
+    // LayerNorm parameters staged: the first LayerNorm's statistics barrier
+    // orders them before their first read (ln_apply)
+    if constexpr (!kFwd) __syncthreads();
     typedef typename Pk<T>::word word;
     word zr[L][NBW][8];  // this wave's Dense outputs (exact in the compute dtype)
     word aw[NBW][8];     // post-activation of the current layer
@@ -1252,8 +1265,8 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
 
 // Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
 // level of the column partials; one more (if loss_out) the loss metrics.
-template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES, 8))) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
+template <typename T, bool REC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(REC ? 2 : ML_WG_WAVES, 8))) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
                                                     float* loss_out) {
     if ((int)blockIdx.x >= jobs.nwg) {
         const int b = blockIdx.x - jobs.nwg;
@@ -1266,7 +1279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES
     while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
     const WgJob& J = jobs.job[jb];
     const int local = blockIdx.x - J.wg0;
-    if constexpr (std::is_same<T, bf16>::value) {
+    if constexpr (REC && std::is_same<T, bf16>::value) {
         if (J.rec) {
             wgrad_tile<T, true>(jobs, J, local, smem);
             return;
@@ -1586,17 +1599,28 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     jobs.ncolx = (ws.CP + 255) / 256;
     jobs.ncol = jobs.ncolx * kColChunks;
     {
-        auto k = wgrad_kernel<T>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)WgCfg<T>::lds);
-            attr_set = true;
-        }
         const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
-        const size_t lds = WgCfg<T>::lds + (ws.a0r ? 2 * H * sizeof(float) : 0);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, jobs, ws, hp, M,
-                           p.actions.num_groups, loss_out);
+        if (ws.a0r) {
+            const size_t lds = WgCfg<T>::lds + 2 * H * sizeof(float);
+            static bool attr_set = false;
+            if (!attr_set) {
+                (void)hipFuncSetAttribute((const void*)wgrad_kernel<T, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((wgrad_kernel<T, true>), dim3(blocks), dim3(256), lds, s, jobs, ws,
+                               hp, M, p.actions.num_groups, loss_out);
+        } else {
+            static bool attr_set = false;
+            if (!attr_set) {
+                (void)hipFuncSetAttribute((const void*)wgrad_kernel<T, false>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)WgCfg<T>::lds);
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((wgrad_kernel<T, false>), dim3(blocks), dim3(256), WgCfg<T>::lds,
+                               s, jobs, ws, hp, M, p.actions.num_groups, loss_out);
+        }
     }
     LayoutK Lk = make_layout(p);
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
@@ -1750,7 +1774,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     jobs.ncolx = (ws.CP + 255) / 256;
     jobs.ncol = jobs.ncolx * kColChunks;
     {
-        auto k = wgrad_kernel<T>;
+        auto k = wgrad_kernel<T, false>;
         static bool attr_set = false;
         if (!attr_set) {
             (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
