@@ -211,7 +211,8 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
 #pragma unroll
     for (int k = 0; k < NPAR; ++k)
         if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
-    __syncthreads();  // LayerNorm parameters staged
+    // LayerNorm parameters staged: the first LayerNorm's statistics barrier
+    // orders them (and the LSTM bias / critic bins) before their first read
     typedef typename Pk<T>::word word;
     word aw[NBW][8];
     for (int l = 0;; ++l) {
