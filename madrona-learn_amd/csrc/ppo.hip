@@ -132,13 +132,14 @@ static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
     int64_t s = ML_WG_TARGET / tiles;
-    // balanced: splits of ML_WG_CPW chunks, at most 2 x the target workgroups
-    // per weight (the MLP trunk / head weights of <= 4 tiles; the LSTM's wide
-    // gate weights keep the target)
+    // balanced: splits of at most ML_WG_CPW chunks (never fewer workgroups than
+    // the target: small per-rank minibatches under data parallelism keep their
+    // parallelism), at most 2 x the target per weight (the MLP trunk / head
+    // weights of <= 4 tiles; the LSTM's wide gate weights keep the target)
     if (ML_WG_CPW > 0 && tiles <= 4) {
         int64_t b = (chunks + ML_WG_CPW - 1) / ML_WG_CPW;
         if (b > 8) b = (b + 7) / 8 * 8;  // multiples of 8 keep the XCD-aware tile mapping
-        s = b < 2 * s ? b : 2 * s;
+        if (b > s) s = b < 2 * s ? b : 2 * s;
     }
     if (s < 1) s = 1;
     if (s > chunks) s = chunks;
