@@ -100,6 +100,7 @@ struct WsK {
     int CP;                             // L*2*H + 32
     float* lnst;                        // [Mp][2] layer-0 LayerNorm {mean, rstd} (a0r)
     int a0r;                            // A_0 not spilled: wgrad recomputes it (kFused)
+    int zs;                             // a[0] holds Z_0 (ppo_rows_kernel): wgrad applies LN_0 + ReLU
     uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
 
@@ -249,12 +250,14 @@ __device__ inline float ppo_obj(const HpK& hp, float lpa, float old_lp, float ad
 
 // Group of at most MAXB logits held in registers (fixed width, masked): no
 // dynamically indexed register arrays.
-template <int MAXB>
-__device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a, float old_lp,
+// S: storage of the logits row (f32, or the compute dtype bf16 when every
+// consumer of the d logits rounds them to it anyway).
+template <int MAXB, typename S>
+__device__ inline void loss_group_fixed(const HpK& hp, S* lg, int nb, int a, float old_lp,
                                         float adv, float ecoef, float objw, LossAcc& m) {
     float v[MAXB];
 #pragma unroll
-    for (int j = 0; j < MAXB; ++j) v[j] = j < nb ? lg[j] : -3.4e38f;
+    for (int j = 0; j < MAXB; ++j) v[j] = j < nb ? to_f32(lg[j]) : -3.4e38f;
     float mx = v[0];
 #pragma unroll
     for (int j = 1; j < MAXB; ++j) mx = fmaxf(mx, v[j]);
@@ -278,32 +281,33 @@ __device__ inline void loss_group_fixed(const HpK& hp, float* lg, int nb, int a,
     for (int j = 0; j < MAXB; ++j) {
         const float p = ex[j] * inv;
         const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((v[j] - lse) + ent);
-        if (j < nb) lg[j] = d * hp.loss_scale;
+        if (j < nb) lg[j] = cvt<S>(d * hp.loss_scale);
     }
 }
 
 // Any group size (<= 31): three passes over the logits in LDS.
-__device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float old_lp, float adv,
+template <typename S>
+__device__ inline void loss_group(const HpK& hp, S* lg, int nb, int a, float old_lp, float adv,
                                   float ecoef, float objw, LossAcc& m) {
     if (nb <= 8) {
         loss_group_fixed<8>(hp, lg, nb, a, old_lp, adv, ecoef, objw, m);
         return;
     }
-    float mx = lg[0];
-    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, lg[j]);
+    float mx = to_f32(lg[0]);
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, to_f32(lg[j]));
     float se = 0.f;
-    for (int j = 0; j < nb; ++j) se += __expf(lg[j] - mx);
+    for (int j = 0; j < nb; ++j) se += __expf(to_f32(lg[j]) - mx);
     const float inv = 1.0f / se;
     const float lse = mx + __logf(se);
     float ent = 0.f;
-    for (int j = 0; j < nb; ++j) ent -= (__expf(lg[j] - mx) * inv) * (lg[j] - lse);
-    const float g_lp = ppo_obj(hp, lg[a] - lse, old_lp, adv, ent, ecoef, objw, m);
+    for (int j = 0; j < nb; ++j) ent -= (__expf(to_f32(lg[j]) - mx) * inv) * (to_f32(lg[j]) - lse);
+    const float g_lp = ppo_obj(hp, to_f32(lg[a]) - lse, old_lp, adv, ent, ecoef, objw, m);
     const float ce = ecoef * hp.inv_sk;
     for (int j = 0; j < nb; ++j) {
-        const float lj = lg[j];
+        const float lj = to_f32(lg[j]);
         const float p = __expf(lj - mx) * inv;
         const float d = g_lp * ((j == a ? 1.f : 0.f) - p) + ce * p * ((lj - lse) + ent);
-        lg[j] = d * hp.loss_scale;
+        lg[j] = cvt<S>(d * hp.loss_scale);
     }
 }
 
@@ -311,9 +315,10 @@ __device__ inline void loss_group(const HpK& hp, float* lg, int nb, int a, float
 // zeroes columns A+1..HC-1.
 // vn (normalize_values, may be null) = {mu', inv_sigma'} after this
 // minibatch's update and {mu, sigma} before it (mlearn_value_norm_chain).
-__device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float R, float ov,
+template <typename S>
+__device__ inline void loss_value(const HpK& hp, S* lg, int A, int HC, float R, float ov,
                                   LossAcc& m, const float* vn) {
-    const float V = lg[A];
+    const float V = to_f32(lg[A]);
     // target: the return normalised with the updated estimates (ppo.py:209-211)
     const float tgt = vn ? (R - vn[0]) * vn[1] : R;
     float vpred = V, dvp = 1.f;
@@ -334,8 +339,8 @@ __device__ inline void loss_value(const HpK& hp, float* lg, int A, int HC, float
         vl = 0.5f * e * e;
         dvl = e;
     }
-    lg[A] = hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale;
-    for (int j = A + 1; j < HC; ++j) lg[j] = 0.f;
+    lg[A] = cvt<S>(hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale);
+    for (int j = A + 1; j < HC; ++j) lg[j] = cvt<S>(0.f);
     // value error: the critic inverted with the previous estimates (ppo.py:193-195)
     const float verr = fabsf((vn ? V * vn[3] + vn[2] : V) - R);
     m.svl += vl;
@@ -887,7 +892,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                     const f2 bb = p ? f2{B.z, B.w} : f2{B.x, B.y};
                     const f2 zc = Pk<T>::unpack(zr[l][i][k]) - m2;
                     const f2 xh = zc * r2;
-                    const f2 y = zc * (r2 * gg) + bb;
+                    const f2 y = __builtin_elementwise_fma(zc, r2 * gg, bb);
                     // ReLU' (rnd<T>(y) > 0 <=> y > thr); padding rows carry no gradient
                     const f2 dy = {((y.x > thr) & live) ? acc[i][2 * k] : 0.f,
                                    ((y.y > thr) & live) ? acc[i][2 * k + 1] : 0.f};
@@ -1018,6 +1023,8 @@ static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_s
                                                             rec);
 }
 
+#include "ppo_rows.h"
+
 // ---------------------------------------------------------------------------
 // Weight gradients dW[i][j] = sum_m X[m][i] * Y[m][j] for every weight of the
 // policy in one launch (X, Y row-major [Mp][I] / [Mp][J], written by the step
@@ -1036,7 +1043,8 @@ struct WgJob {
     float* out;
     int64_t rps;
     int I, J, ti, tj, splits, wg0;
-    int rec;  // X is A_0 recomputed from X_0 (wgrad_tile<T, true>)
+    int rec;   // X is A_0 recomputed from X_0 (wgrad_tile<T, true>)
+    int zrec;  // X holds Z_0: staged as A_0 = relu(LN_0(Z_0)) (ppo_rows_kernel spill)
 };
 struct WgJobs {
     WgJob job[kMaxJobs];
@@ -1153,6 +1161,23 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
     u4 rx[2][REC ? 1 : PER], ry[2][PER];
     frag xb[2][REC ? RB : 1][XKS];  // REC: X_0 row fragments of the chunk's row blocks
     float2 st[2][REC ? RB : 1];      // REC: {mean, rstd} of those rows
+    // Z_0 staging (J.zrec, bf16): this thread's 8 columns are fixed (cc below)
+    // -> their LayerNorm scale / bias in registers, per-row {mean, rstd} per chunk
+    constexpr bool ZR = !REC && std::is_same<T, bf16>::value;
+    const bool zrec = ZR && J.zrec;
+    float zg[ZR ? VPC : 1], zb[ZR ? VPC : 1];
+    float2 zst[2][ZR ? PER : 1];
+    if constexpr (ZR) {
+        if (zrec) {
+            const int cc0 = (tid % CPR) * VPC;
+#pragma unroll
+            for (int e = 0; e < VPC; ++e) {
+                const int col = i0 + cc0 + e < J.I ? i0 + cc0 + e : 0;
+                zg[e] = jobs.g0[col];
+                zb[e] = jobs.b0[col];
+            }
+        }
+    }
     auto gload = [&](int c, int set) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
@@ -1163,6 +1188,8 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
             if constexpr (!REC)
                 rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
             ry[set][u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
+            if constexpr (ZR)
+                if (zrec) zst[set][u] = *(const float2*)(jobs.lnst + 2 * (mb0 + rr));
         }
         if constexpr (REC) {
 #pragma unroll
@@ -1182,6 +1209,18 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
+            if constexpr (ZR) {
+                if (zrec) {
+                    // A_0 = relu(LN_0(Z_0)) with ln_apply's operations (ln_act)
+                    typedef __bf16 bf16x8l __attribute__((ext_vector_type(8)));
+                    const bf16x8l z = __builtin_bit_cast(bf16x8l, rx[set][u]);
+                    bf16x8l a;
+#pragma unroll
+                    for (int e = 0; e < VPC; ++e)
+                        a[e] = (bf16)ln_act((float)z[e], zst[set][u].x, zst[set][u].y, zg[e], zb[e]);
+                    rx[set][u] = __builtin_bit_cast(u4, a);
+                }
+            }
             if constexpr (!REC) *(u4*)(xs + rr * LD + cc) = rx[set][u];
             *(u4*)(ys + rr * LD + cc) = ry[set][u];
         }
@@ -1564,11 +1603,17 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
 
-    switch (p.num_layers) {
-        case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+    const bool rows = !ws.a0r && rows_ok(p);
+    ws.zs = rows && !kRowsKeepZ0;
+    if (rows) {
+        launch_rows(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
+    } else {
+        switch (p.num_layers) {
+            case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+            case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+            case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+            default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        }
     }
     if (step_only) return check_launch("ppo_minibatch_fwd_bwd");
     const int L = p.num_layers;
@@ -1586,6 +1631,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
         J.I = l == L ? H : (l == 0 ? p.obs_dim : H);
         J.J = l == L ? head_cols(p) : H;
         J.rec = l == 1 && ws.a0r;
+        J.zrec = l == 1 && ws.zs;
         J.X = l == 0 || J.rec ? ws.x0 : ws.a[l - 1];
         J.Y = l == L ? ws.dhead : ws.dz[l];
         J.out = ws.slab + ws.slab_off[l];

@@ -649,11 +649,18 @@ __device__ inline void ln_apply(const f2 (&x2)[NBW][8], float mean, float rstd, 
         for (int g = 0; g < 4; ++g) {
             const int f0 = (nb0 + i) * 32 + 8 * g + 4 * h;
             const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + H + f0);
-            const f2 y0 = (x2[i][2 * g] - m2) * (r2 * f2{G.x, G.y}) + f2{B.x, B.y};
-            const f2 y1 = (x2[i][2 * g + 1] - m2) * (r2 * f2{G.z, G.w}) + f2{B.z, B.w};
+            // explicit fma: the weight-gradient launch recomputes A_0 from Z_0
+            // with the same operations (ln_act), bit for bit
+            const f2 y0 = __builtin_elementwise_fma(x2[i][2 * g] - m2, r2 * f2{G.x, G.y}, f2{B.x, B.y});
+            const f2 y1 = __builtin_elementwise_fma(x2[i][2 * g + 1] - m2, r2 * f2{G.z, G.w}, f2{B.z, B.w});
             aw[i][2 * g] = Pk<T>::pack(fmaxf(y0.x, 0.f), fmaxf(y0.y, 0.f));
             aw[i][2 * g + 1] = Pk<T>::pack(fmaxf(y1.x, 0.f), fmaxf(y1.y, 0.f));
         }
+}
+
+// Scalar form of ln_apply for one element (same operations, same bits).
+__device__ inline float ln_act(float x, float mean, float rstd, float g, float b) {
+    return fmaxf(__builtin_fmaf(x - mean, rstd * g, b), 0.f);
 }
 
 // Lane-private LDS spill of one accumulator block (16 values) in the compute

@@ -224,6 +224,9 @@ def test_a0_recompute_bit_identical(gpu, monkeypatch, T, N, D, H, L, mb, bptt):
     s = _device_store(gpu, st, torch.bfloat16)
     adv = ref.gather_minibatch(st, rows)["advantages"].astype(np.float64)
     stats = (adv.mean(), adv.var())
+    # the A_0 recompute is a mode of ppo_step_kernel: keep the headline shape
+    # off the row-split kernel (tests/test_gpu_rows.py pins that one)
+    monkeypatch.setenv("MLEARN_ROWS", "0")
     monkeypatch.setenv("MLEARN_A0_RECOMPUTE", "0")
     g0, o0 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
     monkeypatch.setenv("MLEARN_A0_RECOMPUTE", "1")
