@@ -162,16 +162,25 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
 
     t_step = time_call(step, iters, stream)
     M = algo.mb * algo.bptt
-    fwd, bwd, _ = flop_per_sample(A1=ps.arch.num_logits + ps.arch.critic_bins)
+    A1 = ps.arch.num_logits + ps.arch.critic_bins
+    fwd, bwd, _ = flop_per_sample(A1=A1)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
+    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip)
+    HC = 32 if A1 <= 32 else 96
+    rows = (os.environ.get("MLEARN_ROWS") == "1" and HC == 32 and ps.arch.critic_bins == 1)
+    kname = ("ppo_rows_kernel" if rows else
+             f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>")
     traffic, pmc_name = pmc_traffic("ppo_step")
+    if pmc_name is None or (("ppo_rows_kernel" in pmc_name) != rows) or \
+            (not rows and f"Li{HC}ELi1E" not in pmc_name):
+        traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {
-        "kernel": "ppo_step_kernel<bf16,256,2,0,32,1> (mlearn_ppo_minibatch_fwd_bwd)",
+        "kernel": f"{kname} (mlearn_ppo_minibatch_fwd_bwd)",
         "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
         "frac": achieved / BF16_PEAK_TFS, "traffic": traffic,
-        "traffic_source": (f"profiles/pmc_r02.json ({pmc_name})" if traffic is not None
-                           else None),
+        "traffic_source": (f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc_name})"
+                           if traffic is not None else None),
         "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
         "units_per_launch": M, "flop_per_unit": fwd + bwd,
         "algorithmic_bytes_per_launch": 184 * M,
@@ -196,36 +205,46 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     extra = {"policy_step": {"bound": "mfma", "envs": n_local, "avg_launch_us": t_pol * 1e6,
                              "achieved": pol_flop / t_pol / 1e12, "unit": "TFLOP/s",
                              "frac": pol_flop / t_pol / 1e12 / BF16_PEAK_TFS}}
+    # the product path writes only the advantages (returns = advantages +
+    # values are formed by their consumers); "materialised" = the 8 B/elem
+    # form (value normaliser / compute_advantages=False paths).  frac_read
+    # is capped by read / (read + write) x the achievable copy bandwidth:
+    # 9/13 x 6.29/8 = 0.54 derived, 9/17 x 6.29/8 = 0.42 materialised
     gae = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-           "bytes_per_env": {"read": T * 9 + 4, "write": T * 8}}
+           "bytes_per_env": {"read": T * 9 + 4, "write": T * 4},
+           "frac_read_ceiling": (T * 9 + 4) / (T * 13 + 4) * 6290.0 / HBM_PEAK_GBS}
     for name, n in (("operating_point", n_local), ("sweep_point", 1 << 22)):
-        sec, rd, wr = gae_roofline(dev, n, iters=50 if n < (1 << 20) else 20)
-        gae[name] = {"N": n, "avg_launch_us": sec * 1e6,
-                     "achieved_read": rd / sec / 1e9, "achieved_read_write": (rd + wr) / sec / 1e9,
-                     "frac_read": rd / sec / 1e9 / HBM_PEAK_GBS,
-                     "frac_read_write": (rd + wr) / sec / 1e9 / HBM_PEAK_GBS}
+        for mat in (False, True):
+            sec, rd, wr = gae_roofline(dev, n, iters=50 if n < (1 << 20) else 20, returns=mat)
+            key = name + ("_materialised_returns" if mat else "")
+            gae[key] = {"N": n, "avg_launch_us": sec * 1e6,
+                        "achieved_read": rd / sec / 1e9,
+                        "achieved_read_write": (rd + wr) / sec / 1e9,
+                        "frac_read": rd / sec / 1e9 / HBM_PEAK_GBS,
+                        "frac_read_write": (rd + wr) / sec / 1e9 / HBM_PEAK_GBS}
     extra["gae"] = gae
     return roof, extra
 
 
-def gae_roofline(dev, N, iters=50):
+def gae_roofline(dev, N, iters=50, returns=False):
     from madrona_learn import _native as nat
     r = torch.randn((T, N), device=dev)
     v = torch.randn((T, N), device=dev)
     d = (torch.rand((T, N), device=dev) < 0.05).to(torch.uint8)
     b = torch.randn(N, device=dev)
     adv = torch.empty_like(r)
-    ret = torch.empty_like(r)
+    ret = torch.empty_like(r) if returns else None
     s = torch.cuda.Stream(device=dev)
     L = nat.lib()
 
     def call():
         nat.check(L.mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b), nat.ptr(adv),
-                                   nat.ptr(ret), T, N, 0.99, 0.95, nat.stream_handle(s)))
+                                   nat.ptr(ret) if returns else None, T, N, 0.99, 0.95,
+                                   nat.stream_handle(s)))
 
     sec = time_call(call, iters, s)
     read = T * N * (4 + 4 + 1) + 4 * N
-    write = 8 * T * N
+    write = (8 if returns else 4) * T * N
     return sec, read, write
 
 
@@ -291,7 +310,14 @@ def main():
     ap.add_argument("--bptt-chunks", type=int, default=1)
     ap.add_argument("--critic", choices=["scalar", "twohot"], default="scalar",
                     help="DenseLayerCritic (SURVEY B1) or DreamerV3Critic (63-bin two-hot)")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="one process, one GPU: time rank 0's share of a W-rank headline job "
+                         "(65536/W envs, minibatch slices of 2048/W seqs, every minibatch's "
+                         "gradient all-reduce a real RCCL call on a one-rank communicator) and "
+                         "the N=1 headline, and print the implied 1->W strong scaling")
     args = ap.parse_args()
+    if args.emulate_world > 1:
+        return emulate_world(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -365,6 +391,11 @@ def main():
                        "steps_per_update": T, "parallelism": f"dp{world}",
                        "critic": args.critic,
                        "hip_graph": not args.no_graph},
+            # how the data-parallel collectives ran (a SCALE record can be checked
+            # against this): "rccl_in_graph" = C ABI RCCL communicator on the
+            # compute stream inside the HIP graph; "torch_distributed" = host
+            # round trips between graph segments (reason on stderr); "none" = 1 GPU
+            "collectives": mgr.dp.collectives, "rccl_ranks": mgr.dp.comm_ranks,
         }
     if rank == 0 and not args.no_roofline and args.config != "lstm":
         result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev, n_rank)
@@ -375,6 +406,53 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _time_updates(mgr, steps, warmup):
+    for _ in range(warmup):
+        mgr.update_iter()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mgr.update_iter()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def emulate_world(args):
+    """Strong-scaling projection on one GPU: rank 0's share of a W-rank
+    headline job (MLEARN_EMULATE_WORLD, madrona_learn.dist), then the N=1
+    headline in the same process.  The share's per-update time bounds the
+    W-GPU time from below by everything but the xGMI transfer of the
+    collectives (each is issued as a one-rank RCCL all-reduce at its place
+    in the graph)."""
+    W = int(args.emulate_world)
+    total = TOTAL_ENVS["headline"]
+    if total % W or MB % W:
+        raise SystemExit(f"--emulate-world {W} must divide {total} envs and {MB} seqs")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    os.environ["MLEARN_EMULATE_WORLD"] = str(W)
+    mgr = make(dev, total, 0, total // W, use_graph=not args.no_graph)
+    coll = mgr.dp.collectives
+    t_w = _time_updates(mgr, args.steps, args.warmup)
+    del mgr
+    torch.cuda.empty_cache()
+    os.environ.pop("MLEARN_EMULATE_WORLD")
+    mgr = make(dev, total, 0, total, use_graph=not args.no_graph)
+    t_1 = _time_updates(mgr, args.steps, args.warmup)
+    print(json.dumps({
+        "metric": "env-steps/sec whole-node, 65536-env PPO, at 1/2/4/8 MI355X (projection)",
+        "emulated_world": W, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_update_rank_share": t_w * 1e3,
+        "implied_whole_node_env_steps_per_s": total * T / t_w,
+        "n1_ms_per_update": t_1 * 1e3, "n1_env_steps_per_s": total * T / t_1,
+        "implied_scaling_1_to_W": t_1 / t_w,
+        "collectives": coll,
+        "config": {"envs_per_rank": total // W, "minibatch_slice_seqs": MB // W,
+                   "optimizer_steps_per_update": EPOCHS * (total // W) // (MB // W)},
+        "note": "one process: the W-rank all-reduces run as one-rank RCCL calls, so the "
+                "projection leaves out their xGMI transfer (0.36 MB per minibatch)"}))
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 8
+#define MLEARN_ABI_VERSION 9
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -81,7 +81,10 @@ int mlearn_counters_add(uint64_t* ctr, int32_t n, const uint64_t* deltas /* host
 /* ---------------------------------------------------------------------- */
 /* Reverse-time GAE scan over [T][N] (algo_common.py:84-130) fused with
  * returns = advantages + values (rollouts.py:761-769).  dones are bytes
- * (bool, rollouts.py:454-455,933).  bootstrap is [N]. */
+ * (bool, rollouts.py:454-455,933).  bootstrap is [N].  returns may be NULL:
+ * only the advantages are written (4 B per element instead of 8) and the
+ * consumers form returns = advantages + values themselves, the same f32
+ * addition (mlearn_rollout_view.returns = NULL, mlearn_metric_job.x2). */
 int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
                    const float* bootstrap, float* advantages, float* returns, int32_t T,
                    int64_t N, float gamma, float gae_lambda, mlearn_stream_t stream);
@@ -193,6 +196,18 @@ int mlearn_obs_norm_update(const float* obs_stats, int32_t steps, int64_t tiles,
                            int32_t obs_dim, float decay, float eps, float* est, int32_t* count,
                            mlearn_stream_t stream);
 
+/* EMANormalizer.update_input_stats (moving_avg.py:107-130) of one [rows][dim]
+ * f32 batch: batch mean and population variance per column, merged into the
+ * running cur_stats = [2][dim] {mean | var} with n_a = num_prev_updates;
+ * out_stats [2][dim] (may alias cur_stats).  rows < 2^24. */
+int mlearn_ema_input_stats(const float* x, int64_t rows, int32_t dim, const float* cur_stats,
+                           int32_t num_prev_updates, float* out_stats, mlearn_stream_t stream);
+/* EMANormalizer.update_estimates (moving_avg.py:132-180): est [5][dim] =
+ * mu, inv_sigma, sigma, mu_biased, sigma_sq_biased (in/out) from input_stats
+ * [2][dim]; count = the int32 update counter N (in/out, device). */
+int mlearn_ema_update_estimates(const float* input_stats, int32_t dim, float decay, float eps,
+                                float* est, int32_t* count, mlearn_stream_t stream);
+
 /* Post-step bookkeeping of the PREVIOUS env step (rollouts.py:933-973), fused
  * into the next policy launch; same arithmetic as mlearn_rollout_post_step. */
 typedef struct mlearn_post_step {
@@ -240,6 +255,9 @@ typedef struct mlearn_metric_job {
                         /*    env columns of the [T][N] store) */
     int32_t abs_value;  /* 1: metric of |x| (ppo.py:358 'Value Errors') */
     int32_t pad;
+    const float* x2;    /* NULL, or a second array of the same shape: the metric is of x + x2
+                           (the 'Est Returns' = advantages + values of a GAE that did not
+                           materialise returns) */
 } mlearn_metric_job;
 
 int64_t mlearn_metrics_workspace_bytes(int32_t num_jobs);
@@ -262,7 +280,8 @@ typedef struct mlearn_rollout_view {
     const int32_t* actions;   /* [T][N][K] */
     const float* log_probs;   /* [T][N][K] */
     const float* advantages;  /* [T][N] */
-    const float* returns;     /* [T][N] */
+    const float* returns;     /* [T][N]; NULL: returns = advantages + values (GAE without
+                                 materialised returns, mlearn_gae_f32) */
     const float* values;      /* [T][N] */
     const uint8_t* dones;     /* [T][N] sequence breaks (recurrent policies; may be NULL) */
     int32_t T;                /* steps per update */

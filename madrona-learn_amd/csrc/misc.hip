@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rewa
             }
             int64_t o = (int64_t)t * N + n0;
             gae_store<VEC>(adv + o, a);
-            gae_store<VEC>(ret + o, rt);
+            if (ret) gae_store<VEC>(ret + o, rt);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = nxt[u];
@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256) void metrics_partial_kernel(MetricJobs jobs, d
     double s = 0, q = 0;
     float mn = 3.402823466e+38f, mx = -3.402823466e+38f;
     for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * 256) {
-        float x = J.cols ? J.x[(i / J.cols) * J.ld + i % J.cols] : J.x[i];
+        const int64_t e = J.cols ? (i / J.cols) * J.ld + i % J.cols : i;
+        float x = J.x[e];
+        if (J.x2) x = x + J.x2[e];  // (commutative: = advantages + values of the GAE)
         if (J.abs_value) x = fabsf(x);
         s += x;
         q += (double)x * x;
@@ -623,6 +625,84 @@ __device__ inline void chan_merge(float& n, float& m, float& M2, float nb, float
     n = nn;
 }
 
+// EMANormalizer.update_estimates (moving_avg.py:132-180) of column f:
+// est = [5][D] mu, inv_sigma, sigma, mu_biased, sigma_sq_biased; Nold = the
+// update count before this update.
+__device__ inline void ema_update_col(int f, int D, float a_mean, float a_var, float decay,
+                                      float eps, float* est, int32_t Nold) {
+#pragma clang fp contract(off)
+    float* mu = est;
+    float* inv_sigma = est + D;
+    float* sigma = est + 2 * D;
+    float* mu_b = est + 3 * D;
+    float* s2_b = est + 4 * D;
+    const float oma = decay;
+    const float alpha = 1.0f - oma;
+    const int32_t Nnew = Nold + 1;
+    const float mean_delta = a_mean - mu[f];
+    const float nmb = oma * mu_b[f] + alpha * a_mean;
+    const float ns2b = oma * s2_b[f] + alpha * a_var +
+                       ((float)Nold / (float)Nnew) * (oma * alpha) * (mean_delta * mean_delta);
+    const float bc = -1.0f / expm1f((float)Nnew * logf(oma));
+    const float nmu = nmb * bc;
+    const float ns2 = ns2b * bc;
+    const float ninv = rsqrtf(fmaxf(ns2, eps));
+    mu[f] = nmu;
+    inv_sigma[f] = ninv;
+    sigma[f] = 1.0f / ninv;
+    mu_b[f] = nmb;
+    s2_b[f] = ns2b;
+}
+
+// EMANormalizer.update_input_stats (moving_avg.py:107-130) of a [rows][D]
+// f32 batch: per column (one block each) the batch mean and population
+// variance by Chan merges of the threads' Welford partials in a fixed tree
+// order, then the weighted merge with the running (mean, var) at
+// num_prev_updates = n_a.  cur and out are [2][D] (mean | var; may alias).
+__global__ __launch_bounds__(256) void ema_input_stats_kernel(const float* __restrict__ x,
+                                                              int64_t rows, int D,
+                                                              const float* cur, int n_prev,
+                                                              float* out) {
+#pragma clang fp contract(off)
+    __shared__ float sn[4], sm[4], sM[4];
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float n = 0.f, m = 0.f, M2 = 0.f;
+    for (int64_t r = tid; r < rows; r += 256) chan_merge(n, m, M2, 1.f, x[r * D + f], 0.f);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float n2 = __shfl_xor(n, o), m2 = __shfl_xor(m, o), M22 = __shfl_xor(M2, o);
+        if ((lane & o) == 0) {
+            chan_merge(n, m, M2, n2, m2, M22);
+        } else {  // the lower lane is the left operand on both sides
+            float nl = n2, ml = m2, Ml = M22;
+            chan_merge(nl, ml, Ml, n, m, M2);
+            n = nl, m = ml, M2 = Ml;
+        }
+    }
+    if (lane == 0) {
+        sn[w] = n;
+        sm[w] = m;
+        sM[w] = M2;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    n = sn[0], m = sm[0], M2 = sM[0];
+    for (int u = 1; u < 4; ++u) chan_merge(n, m, M2, sn[u], sm[u], sM[u]);
+    const float b_mean = m, b_var = rows > 0 ? M2 / (float)rows : 0.f;
+    const float a_mean = cur[f], a_var = cur[D + f];
+    const float delta = b_mean - a_mean;
+    const float b_w = 1.0f / (float)(n_prev + 1);
+    const float a_w = 1.0f - b_w;
+    out[f] = a_mean + delta * b_w;
+    out[D + f] = a_w * a_var + b_w * b_var + (delta * delta) * a_w * b_w;
+}
+
+__global__ void ema_update_kernel(const float* __restrict__ stats, int D, float decay, float eps,
+                                  float* est, const int32_t* count) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < D) ema_update_col(f, D, stats[f], stats[D + f], decay, eps, est, *count);
+}
+
 __global__ __launch_bounds__(256) void obs_norm_update_kernel(const float* __restrict__ st,
                                                               int steps, int64_t tiles, int64_t N,
                                                               int D, float decay, float eps,
@@ -675,28 +755,7 @@ __global__ __launch_bounds__(256) void obs_norm_update_kernel(const float* __res
     }
     if (tid != 0) return;
     // update_estimates (moving_avg.py:132-180)
-    const int32_t Nold = *count;  // bumped by obs_count_kernel after every block has run
-    float* mu = est;
-    float* inv_sigma = est + D;
-    float* sigma = est + 2 * D;
-    float* mu_b = est + 3 * D;
-    float* s2_b = est + 4 * D;
-    const float oma = decay;
-    const float alpha = 1.0f - oma;
-    const int32_t Nnew = Nold + 1;
-    const float mean_delta = a_mean - mu[f];
-    const float nmb = oma * mu_b[f] + alpha * a_mean;
-    const float ns2b = oma * s2_b[f] + alpha * a_var +
-                       ((float)Nold / (float)Nnew) * (oma * alpha) * (mean_delta * mean_delta);
-    const float bc = -1.0f / expm1f((float)Nnew * logf(oma));
-    const float nmu = nmb * bc;
-    const float ns2 = ns2b * bc;
-    const float ninv = rsqrtf(fmaxf(ns2, eps));
-    mu[f] = nmu;
-    inv_sigma[f] = ninv;
-    sigma[f] = 1.0f / ninv;
-    mu_b[f] = nmb;
-    s2_b[f] = ns2b;
+    ema_update_col(f, D, a_mean, a_var, decay, eps, est, *count);  // count bumped after every block
 }
 
 __global__ void obs_count_kernel(int32_t* count) { *count += 1; }
@@ -762,8 +821,8 @@ int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* don
                    float gamma, float gae_lambda, mlearn_stream_t stream) {
     ML_REQUIRE(T >= 0 && N >= 0, "gae: negative size");
     if (T == 0 || N == 0) return MLEARN_OK;
-    ML_REQUIRE(rewards && values && dones && bootstrap && advantages && returns,
-               "gae: null pointer");
+    ML_REQUIRE(rewards && values && dones && bootstrap && advantages,
+               "gae: null pointer");  // (returns may be NULL: not materialised)
     ML_REQUIRE(N <= ((int64_t)1 << 28), "gae: N > 2^28 columns");
     float gl = gamma * gae_lambda;  // cfg.gamma * cfg.gae_lambda (algo_common.py:120)
     // Blocks of 64 below 2^20 columns so more CUs share the serial T loop (the
@@ -917,7 +976,8 @@ int mlearn_adv_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t
 
 int mlearn_return_stats(const mlearn_rollout_view* ro, const int32_t* perm, int32_t num_mb,
                         int32_t mb_size, double* partials, mlearn_stream_t stream) {
-    ML_REQUIRE(ro && perm && partials, "return_stats: null pointer");
+    ML_REQUIRE(ro && perm && partials && ro->returns,
+               "return_stats: null pointer (the value normaliser needs materialised returns)");
     return minibatch_sums(ro, ro->returns, perm, num_mb, mb_size, partials, S(stream));
 }
 
@@ -1007,6 +1067,26 @@ int mlearn_obs_norm_update(const float* obs_stats, int32_t steps, int64_t tiles,
                        obs_stats, steps, tiles, N, obs_dim, decay, eps, est, count);
     hipLaunchKernelGGL(obs_count_kernel, dim3(1), dim3(1), 0, S(stream), count);
     return check_launch("obs_norm_update");
+}
+
+int mlearn_ema_input_stats(const float* x, int64_t rows, int32_t dim, const float* cur_stats,
+                           int32_t num_prev_updates, float* out_stats, mlearn_stream_t stream) {
+    ML_REQUIRE(rows >= 0 && dim >= 1 && num_prev_updates >= 0, "ema_input_stats: bad sizes");
+    ML_REQUIRE((x || rows == 0) && cur_stats && out_stats, "ema_input_stats: null pointer");
+    ML_REQUIRE(rows < ((int64_t)1 << 24), "ema_input_stats: rows >= 2^24 (f32 counts)");
+    hipLaunchKernelGGL(ema_input_stats_kernel, dim3((unsigned)dim), dim3(256), 0, S(stream), x,
+                       rows, dim, cur_stats, num_prev_updates, out_stats);
+    return check_launch("ema_input_stats");
+}
+
+int mlearn_ema_update_estimates(const float* input_stats, int32_t dim, float decay, float eps,
+                                float* est, int32_t* count, mlearn_stream_t stream) {
+    ML_REQUIRE(dim >= 1 && input_stats && est && count, "ema_update_estimates: bad arguments");
+    ML_REQUIRE(decay > 0.f && decay < 1.f, "ema_update_estimates: decay must be in (0, 1)");
+    hipLaunchKernelGGL(ema_update_kernel, dim3((unsigned)((dim + 255) / 256)), dim3(256), 0,
+                       S(stream), input_stats, dim, decay, eps, est, count);
+    hipLaunchKernelGGL(obs_count_kernel, dim3(1), dim3(1), 0, S(stream), count);
+    return check_launch("ema_update_estimates");
 }
 
 }  // extern "C"

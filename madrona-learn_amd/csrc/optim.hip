@@ -126,23 +126,34 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x < 4 * kMaxSlots) sh[threadIdx.x / kMaxSlots][threadIdx.x % kMaxSlots] = 0.f;
+    // this thread's first parameter is in flight while the global norm is
+    // reduced (the common case at <= kAdamBlocks x 256 parameters: one each)
+    const int64_t p0 = blockIdx.x * (int64_t)256 + threadIdx.x;
+    const bool have0 = p0 < Lk.total;
+    float g0 = 0.f, m0 = 0.f, v0 = 0.f, q0 = 0.f;
+    if (have0) {
+        g0 = grads[p0];
+        m0 = m[p0];
+        v0 = v[p0];
+        q0 = params[p0];
+    }
+    const int count = step[0] + 1;
     const float gn = global_norm(gpart, npart);  // (its barriers also order the sh zeroing)
-    for (int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x; p - threadIdx.x < Lk.total;
-         p += (int64_t)gridDim.x * 256) {
+    for (int64_t p = p0; p - threadIdx.x < Lk.total; p += (int64_t)gridDim.x * 256) {
         float contrib = 0.f;
         int slot = -2;
         // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
         const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
         if (p < Lk.total && !pad) {
-            float g = grads[p];
+            const bool first = p == p0;
+            float g = first ? g0 : grads[p];
             if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
-            const int count = step[0] + 1;
-            const float mm = (1.f - b1) * g + b1 * m[p];
-            const float vv = (1.f - b2) * (g * g) + b2 * v[p];
+            const float mm = (1.f - b1) * g + b1 * (first ? m0 : m[p]);
+            const float vv = (1.f - b2) * (g * g) + b2 * (first ? v0 : v[p]);
             const float mhat = mm / (1.f - powf(b1, (float)count));
             const float vhat = vv / (1.f - powf(b2, (float)count));
             const float u = mhat / (sqrtf(vhat) + eps);
-            const float np = params[p] + (-lr) * u;
+            const float np = (first ? q0 : params[p]) + (-lr) * u;
             m[p] = mm;
             v[p] = vv;
             params[p] = np;
@@ -220,6 +231,8 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
     __shared__ double red[4][kMaxSlots];
     __shared__ float sq[kMaxSlots];
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
+    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
+    const float val0 = p < Lk.total ? params[p] : 0.f;  // in flight under the slot reduction
     for (int sl = 0; sl < nslot; ++sl) {
         double t = 0;
         for (int b = threadIdx.x; b < nblk; b += 256) t += ppart[(int64_t)b * nslot + sl];
@@ -232,10 +245,9 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
         sq[sl] = (float)(((red[0][sl] + red[1][sl]) + red[2][sl]) + red[3][sl]);
     }
     __syncthreads();
-    const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     if (p == 0 && step) step[0] += 1;
     if (p >= Lk.total) return;
-    float val = params[p];
+    float val = val0;
     const int slot = proj_slot(Lk, p);
     if (slot >= 2 * Lk.L) {  // LSTM gate kernel (ppo.py:303-310 on each ii..ho kernel)
         if (norm_params) val = (init_norms[Lk.L + slot - 2 * Lk.L] * val) / sqrtf(sq[slot]);

@@ -425,6 +425,13 @@ template <> __device__ inline float relu_thr<float>() { return 0.f; }
 template <> __device__ inline float relu_thr<bf16>() { return __builtin_bit_cast(float, 0x00008000u); }
 
 
+// Return of store row q: the stored column, or advantages + values when the
+// GAE did not materialise it (mlearn_rollout_view.returns = NULL): the same
+// f32 addition as gae_kernel's, so the same bits.
+__device__ inline float ret_at(const RolloutK& ro, int64_t q) {
+    return ro.ret ? ro.ret[q] : ro.adv[q] + ro.values[q];
+}
+
 // Store row of minibatch row f (32-bit index math: rows, sequences and N are
 // < 2^31, checked on the host).
 __device__ inline int64_t store_row(const RolloutK& ro, const int32_t* mb_seq, int mb, int64_t f) {
@@ -519,7 +526,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
             t_act = ro.actions[tsr * K + tg];
             t_lp = ro.logp[tsr * K + tg];
         } else {
-            t_ret = ro.ret[tsr];
+            t_ret = ret_at(ro, tsr);
             if (ro.values) t_val = ro.values[tsr];
         }
     }
@@ -725,7 +732,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                 adv = ro.adv[q];
                 act = g < K ? ro.actions[q * K + g] : 0;
                 olp = g < K ? ro.logp[q * K + g] : 0.f;
-                ret = g < K ? 0.f : ro.ret[q];
+                ret = g < K ? 0.f : ret_at(ro, q);
                 oval = (g < K || !ro.values) ? 0.f : ro.values[q];
             }
             if (g < K) {
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                     for (int j = P.A + sub; j < HC; j += G) lr[j] = 0.f;
                     continue;
                 }
-                const float R = ro.ret[store_row(ro, mb_seq, mb, f)];
+                const float R = ret_at(ro, store_row(ro, mb_seq, mb, f));
                 loss_value_twohot_g<G>(hp, lr, P.A, P.CB, HC, bins, R, sub, m);
             }
         }
@@ -1466,7 +1473,21 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
             const int I = l == 0 ? Lk.D : H;
             const float* sp = ws.slab + ws.slab_off[l] + (p0 - Lk.w_off[l]) + 4 * c;
             const int64_t stride = (int64_t)I * H;
-            for (int k = g; k < ws.splits[l]; k += kRgGroups) {
+            // four splits' loads in flight at a time, summed in split order
+            int k = g;
+            for (; k + 3 * kRgGroups < ws.splits[l]; k += 4 * kRgGroups) {
+                float4 x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = *(const float4*)(sp + (k + u * kRgGroups) * stride);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v[0] += x[u].x;
+                    v[1] += x[u].y;
+                    v[2] += x[u].z;
+                    v[3] += x[u].w;
+                }
+            }
+            for (; k < ws.splits[l]; k += kRgGroups) {
                 const float4 x = *(const float4*)(sp + k * stride);
                 v[0] += x.x;
                 v[1] += x.y;
@@ -1877,7 +1898,8 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");
     ML_REQUIRE(ro->ld == 0 || ro->ld >= ro->N, "ppo: ld %lld < N %lld", (long long)ro->ld,
                (long long)ro->N);
-    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
+    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages &&
+                   (ro->returns || ro->values),
                "ppo: null rollout array");
     ML_REQUIRE(!hp->clip_value_loss || ro->values, "ppo: clip_value_loss needs values");
     ML_REQUIRE(!hp->normalize_values || policy->critic_bins == 1,
@@ -1932,7 +1954,8 @@ int mlearn_lstm_ppo_minibatch_grad(const mlearn_mlp_policy* policy, const mlearn
                "lstm ppo: N and rows per minibatch must be < 2^31");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "lstm ppo: bad bptt_len");
     ML_REQUIRE(ro->ld == 0 || ro->ld >= ro->N, "lstm ppo: ld < N");
-    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages && ro->returns,
+    ML_REQUIRE(ro->obs && ro->actions && ro->log_probs && ro->advantages &&
+                   (ro->returns || ro->values),
                "lstm ppo: null rollout array");
     ML_REQUIRE(!hp->clip_value_loss || ro->values, "lstm ppo: clip_value_loss needs values");
     ML_REQUIRE(!hp->normalize_values || policy->critic_bins == 1,

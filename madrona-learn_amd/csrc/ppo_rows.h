@@ -436,7 +436,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(ML_ROW
                     t_act[k] = ro.actions[q * K + g];
                     t_lp[k] = ro.logp[q * K + g];
                 } else {
-                    t_ret[k] = ro.ret[q];
+                    t_ret[k] = ret_at(ro, q);
                     if (ro.values) t_val[k] = ro.values[q];
                 }
             }
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(ML_ROW
                     adv = ro.adv[q];
                     act = g < K ? ro.actions[q * K + g] : 0;
                     olp = g < K ? ro.logp[q * K + g] : 0.f;
-                    ret = g < K ? 0.f : ro.ret[q];
+                    ret = g < K ? 0.f : ret_at(ro, q);
                     oval = (g < K || !ro.values) ? 0.f : ro.values[q];
                 }
                 if (g < K) {

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -45,7 +45,7 @@ class MlpPolicy(Structure):
 
 class MetricJob(Structure):
     _fields_ = [("x", c_void_p), ("n", c_int64), ("cols", c_int64), ("ld", c_int64),
-                ("abs_value", c_int32), ("pad", c_int32)]
+                ("abs_value", c_int32), ("pad", c_int32), ("x2", c_void_p)]
 
 
 class PostStep(Structure):
@@ -106,6 +106,8 @@ _SIGNATURES = {
     "mlearn_allreduce_f64": (c_int32, [c_void_p, _P, c_int64, _S]),
     "mlearn_philox4x32": (c_int32, [_P, c_uint32, c_uint32, _P, c_int64, _S]),
     "mlearn_counters_add": (c_int32, [_P, c_int32, POINTER(c_uint64), _S]),
+    "mlearn_ema_input_stats": (c_int32, [_P, c_int64, c_int32, _P, c_int32, _P, _S]),
+    "mlearn_ema_update_estimates": (c_int32, [_P, c_int32, c_float, c_float, _P, _P, _S]),
     "mlearn_gae_f32": (c_int32, [_P, _P, _P, _P, _P, _P, c_int32, c_int64, c_float, c_float, _S]),
     "mlearn_gae_vnorm_f32": (c_int32, [_P, _P, _P, _P, _P, c_int64, _P, _P, c_int32, c_int64,
                                        c_float, c_float, _S]),

@@ -50,7 +50,9 @@ def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=No
     bootstrap are normalised critic outputs, inverted first (rollouts.py:726-738);
     column n uses estimate n // norm_cols.
 
-    Returns (advantages, returns), both [T, N] f32."""
+    Returns (advantages, returns), both [T, N] f32; ``out_ret=False``: the
+    returns are not materialised (the GAE writes 4 B per element instead of
+    8; consumers form advantages + values) and None is returned for them."""
     T = cfg.steps_per_update
     N = rewards.numel() // T
     r = _tn(rewards, T, N, torch.float32)
@@ -60,6 +62,13 @@ def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=No
     b = bootstrap_values.reshape(N).to(torch.float32).contiguous()
     adv = out_adv if out_adv is not None else torch.empty((T, N), dtype=torch.float32,
                                                           device=r.device)
+    if out_ret is False:
+        if value_norm is not None:
+            raise ValueError("the value normaliser's statistics need materialised returns")
+        nat.check(nat.lib().mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b),
+                                           nat.ptr(adv), None, T, N, float(cfg.gamma),
+                                           float(cfg.gae_lambda), nat.stream_handle()), "gae")
+        return adv, None
     ret = out_ret if out_ret is not None else torch.empty_like(adv)
     if value_norm is not None:
         nat.check(nat.lib().mlearn_gae_vnorm_f32(

@@ -17,6 +17,7 @@ torch.distributed between captured graph segments.
 
 import ctypes
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -24,6 +25,14 @@ import torch.distributed as dist
 
 def _initialized():
     return dist.is_available() and dist.is_initialized()
+
+
+def emulated_world():
+    """MLEARN_EMULATE_WORLD=W (single process, no process group): run rank 0's
+    share of a W-rank job on this GPU (bench.py --emulate-world), with a
+    one-rank RCCL communicator standing in for the group's collectives."""
+    w = int(os.environ.get("MLEARN_EMULATE_WORLD", "1") or 1)
+    return w if w > 1 and not _initialized() else 1
 
 
 class DataParallel:
@@ -41,29 +50,48 @@ class DataParallel:
             self.world_size = dist.get_world_size(group)
 
         self.comm = None  # RCCL communicator owned by libmlearn (enable_native)
+        self.comm_ranks = 0  # ranks of that communicator
+        # how the group's collectives run: "none" (one rank), "rccl_in_graph"
+        # (C ABI communicator on the compute stream), "torch_distributed"
+        self.collectives = "none" if self.world_size <= 1 else "torch_distributed"
+        self.native_reason = None  # why the native path is off (None: on or not needed)
+
+    def _fallback(self, why):
+        self.native_reason = why
+        if self.world_size > 1:
+            print(f"[madrona_learn] rank {self.rank}: RCCL-in-graph collectives off ({why}); "
+                  "using torch.distributed between graph segments", file=sys.stderr, flush=True)
+        return False
 
     def enable_native(self, device):
         """Bootstrap this group's RCCL communicator in the C ABI: the group's
-        first rank makes the unique id, torch.distributed broadcasts it, every
-        member calls mlearn_comm_init.  A sum of rank ids through the new
-        communicator must come out right on every rank, else the group keeps
-        the torch.distributed path."""
-        if self.world_size <= 1 or os.environ.get("MLEARN_NATIVE_COLLECTIVES", "1") == "0":
+        first rank makes the unique id, torch.distributed broadcasts it
+        (with that rank's success flag, so no rank calls ncclCommInitRank on
+        an id that was never made), every member calls mlearn_comm_init.  A
+        sum of rank ids through the new communicator must come out right on
+        every rank, else the group keeps the torch.distributed path and says
+        why on stderr."""
+        if self.world_size <= 1:
             return False
+        if os.environ.get("MLEARN_NATIVE_COLLECTIVES", "1") == "0":
+            return self._fallback("MLEARN_NATIVE_COLLECTIVES=0")
         if dist.get_backend(self.group) != "nccl":
-            return False
+            return self._fallback(f"backend {dist.get_backend(self.group)}")
         from . import _native as nat
         L = nat.lib()
-        idt = torch.zeros(128, dtype=torch.uint8, device=device)
-        ok = True
+        idt = torch.zeros(129, dtype=torch.uint8, device=device)  # 128-byte id + ok flag
         if self.rank == 0:
             buf = (ctypes.c_uint8 * 128)()
-            ok = L.mlearn_comm_unique_id(buf) == 0
-            idt.copy_(torch.tensor(list(buf), dtype=torch.uint8))
+            made = L.mlearn_comm_unique_id(buf) == 0
+            idt[:128].copy_(torch.tensor(list(buf), dtype=torch.uint8))
+            idt[128] = 1 if made else 0
         dist.broadcast(idt, src=self.root, group=self.group)
-        ids = (ctypes.c_uint8 * 128)(*idt.cpu().tolist())
+        host = idt.cpu().tolist()
+        if host[128] != 1:
+            return self._fallback("mlearn_comm_unique_id failed on the group's first rank")
+        ids = (ctypes.c_uint8 * 128)(*host[:128])
         comm = ctypes.c_void_p()
-        ok = ok and L.mlearn_comm_init(ids, self.world_size, self.rank, ctypes.byref(comm)) == 0
+        ok = L.mlearn_comm_init(ids, self.world_size, self.rank, ctypes.byref(comm)) == 0
         if ok:
             t = torch.full((4,), float(self.rank + 1), dtype=torch.float32, device=device)
             ok = L.mlearn_allreduce_f32(comm, nat.ptr(t), 4, nat.stream_handle()) == 0
@@ -75,8 +103,11 @@ class DataParallel:
         if int(flag.item()) != 1:
             if comm.value:
                 L.mlearn_comm_destroy(comm)
-            return False
+            return self._fallback("communicator init or self-check failed on "
+                                  + ("this rank" if not ok else "another rank"))
         self.comm = comm
+        self.comm_ranks = self.world_size
+        self.collectives = "rccl_in_graph"
         return True
 
     def all_reduce_sum_(self, t: torch.Tensor):
@@ -103,11 +134,46 @@ class DataParallel:
             dist.barrier(group=self.group)
 
 
+class EmulatedDataParallel(DataParallel):
+    """Rank 0 of a W-rank data-parallel group, alone on one GPU (bench.py
+    --emulate-world W): the shard, minibatch slices and per-minibatch
+    collectives of that rank, each collective a real RCCL all-reduce on a
+    one-rank communicator (same launch, in the same graph position; the
+    xGMI transfer of the W-rank ring is what it leaves out)."""
+
+    def __init__(self, world_size):
+        super().__init__(solo=True)
+        self.world_size = int(world_size)
+        self.collectives = "rccl_in_graph (1-rank emulation)"
+
+    def enable_native(self, device):
+        from . import _native as nat
+        L = nat.lib()
+        buf = (ctypes.c_uint8 * 128)()
+        comm = ctypes.c_void_p()
+        if L.mlearn_comm_unique_id(buf) != 0 or L.mlearn_comm_init(buf, 1, 0,
+                                                                   ctypes.byref(comm)) != 0:
+            raise RuntimeError("emulated world: one-rank RCCL communicator failed: "
+                               + L.mlearn_last_error().decode(errors="replace"))
+        self.comm = comm
+        self.comm_ranks = 1
+        return True
+
+    def all_reduce_sum_(self, t):
+        return t
+
+    def broadcast_(self, t):
+        return t
+
+    def barrier(self):
+        pass
+
+
 def world():
     """(global rank, world size) of this process."""
     if _initialized():
         return dist.get_rank(), dist.get_world_size()
-    return 0, 1
+    return 0, emulated_world()
 
 
 def policy_placement(num_policies):
@@ -124,7 +190,8 @@ def policy_placement(num_policies):
     rank, W = world()
     P = int(num_policies)
     if P == 1:
-        return [0], DataParallel()
+        ew = emulated_world()
+        return [0], (EmulatedDataParallel(ew) if ew > 1 else DataParallel())
     if W % P == 0:
         G = W // P
         groups = [dist.new_group(list(range(p * G, (p + 1) * G))) for p in range(P)] \

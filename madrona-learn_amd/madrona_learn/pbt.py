@@ -164,17 +164,28 @@ class MovingEpisodeScore:  # train_state.py:24-27
         return [self.mean, self.var, self.N]
 
 
-def pbt_update_fitness(policy_columns, episode_scores, dones):
+def pbt_update_fitness(policy_columns, episode_scores, dones, team_size=1):
     """pbt.py:382-470 for the self-play split: ``policy_columns`` = [(score,
-    col0, ncols)] per local policy (its MovingEpisodeScore and env columns),
-    ``episode_scores`` [N] f32 (get_episode_scores_fn of the episode
-    results), ``dones`` [N].  Device tensor ops only (graph-capturable)."""
-    d = dones.reshape(-1).bool()
+    col0, ncols)] per local policy (its MovingEpisodeScore and agent
+    columns), ``episode_scores`` f32 per match ([N / team_size]:
+    get_episode_scores_fn of each match's episode result) or per agent ([N],
+    agent 0 of each match counts), ``dones`` [N] per agent.  As the reference
+    (pbt.py:390-396), only agent 0 of every match counts: dones reshaped to
+    [matches, team_size], column 0.  Device tensor ops only (graph-capturable)."""
+    ts = int(team_size)
+    dn = dones.reshape(-1)
+    d = dn.reshape(-1, ts)[:, 0].bool()
     x = episode_scores.reshape(-1).float()
+    if ts > 1 and x.numel() == dn.numel():
+        x = x.reshape(-1, ts)[:, 0]
+    if x.numel() != d.numel():
+        raise ValueError(f"episode scores: {x.numel()} values for {d.numel()} matches")
     nmax = torch.iinfo(torch.int32).max
     for sc, c0, n in policy_columns:
-        v = d[c0:c0 + n]
-        xs = x[c0:c0 + n]
+        if c0 % ts or n % ts:
+            raise ValueError("a policy's agent columns must hold whole matches")
+        v = d[c0 // ts:(c0 + n) // ts]
+        xs = x[c0 // ts:(c0 + n) // ts]
         xn = v.sum().to(torch.int32)
         xnf = xn.float()
         cnt = torch.clamp(xnf, min=1.0)
@@ -201,8 +212,10 @@ def check_overwrite(cfg, mean, var, N, src, dst):
     with np.errstate(divide="ignore", invalid="ignore"):
         s2 = f(var[src]) / f(N[src]) + f(var[dst]) / f(N[dst])
         t = (f(mean[src]) - f(mean[dst])) / np.sqrt(f(s2))
-        p = f(1.0) - f(0.5 * (1.0 + math.erf(float(t) / math.sqrt(2.0)))) \
-            if np.isfinite(t) else f(np.nan)
+    # t = +/-inf (both variances 0, N > 0, different means) gives p = 0 / 1 as
+    # in the reference's 1 - cdf(t); only t = NaN (N = 0) never overwrites
+    # (math.erf maps +/-inf to +/-1 and propagates NaN)
+    p = f(1.0) - f(0.5 * (1.0 + math.erf(float(t) / math.sqrt(2.0))))
     return bool(p < f(0.20))
 
 

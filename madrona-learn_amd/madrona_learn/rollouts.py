@@ -140,7 +140,13 @@ class RolloutStore:
         self.rewards = torch.zeros((T, N), dtype=f32, device=device)
         self.dones = torch.zeros((T, N), dtype=torch.uint8, device=device)
         self.advantages = torch.zeros((T, N), dtype=f32, device=device)
-        self.returns = torch.zeros((T, N), dtype=f32, device=device)
+        # returns = advantages + values (rollouts.py:761-769).  With
+        # derive_returns (GAE path without a value normaliser) the GAE writes
+        # only the advantages and every consumer forms the sum (the same f32
+        # addition): the [T][N] column below is then not written and
+        # `returns` reads as advantages + values
+        self._returns = torch.zeros((T, N), dtype=f32, device=device)
+        self.derive_returns = False
         self.env_returns_trace = torch.zeros((T, N), dtype=f32, device=device)
         self.bootstrap = torch.zeros((N,), dtype=f32, device=device)
         # rnn_start_states (rollouts.py:528-537): the carry entering every BPTT
@@ -150,6 +156,10 @@ class RolloutStore:
             self.start_h = torch.zeros((num_chunks, N, rnn_hidden), dtype=compute_dtype,
                                        device=device)
             self.start_c = torch.zeros_like(self.start_h)
+
+    @property
+    def returns(self):
+        return self.advantages + self.values if self.derive_returns else self._returns
 
     def as_dict(self):
         return {"obs": self.obs, "actions": self.actions, "log_probs": self.log_probs,
@@ -168,7 +178,7 @@ class RolloutStore:
         v.actions = self.actions.data_ptr() + col0 * K * 4
         v.log_probs = self.log_probs.data_ptr() + col0 * K * 4
         v.advantages = self.advantages.data_ptr() + col0 * 4
-        v.returns = self.returns.data_ptr() + col0 * 4
+        v.returns = None if self.derive_returns else self._returns.data_ptr() + col0 * 4
         v.values = self.values.data_ptr() + col0 * 4
         v.dones = self.dones.data_ptr() + col0
         v.T = self.T
@@ -228,6 +238,9 @@ class RolloutManager:  # rollouts.py:373-826
             assert ps.arch == arch, "population policies must share one architecture"
         self.store = RolloutStore(self.T, self.N, arch.obs_dim, arch.num_groups, arch.dtype,
                                   self.policy_state.device, self.C, arch.lstm_hidden)
+        # GAE without a value normaliser: returns not materialised (RolloutStore)
+        self.store.derive_returns = bool(train_cfg.compute_advantages and
+                                         not train_cfg.normalize_values)
         self.R = arch.lstm_hidden
         if self.R:
             # the live recurrent carry (c_states, h_states) of rollouts.py:898-901,
@@ -255,11 +268,14 @@ class RolloutManager:  # rollouts.py:373-826
         for p in range(self.P):
             c0 = p * self.B
             jobs = (nat.MetricJob * 6)()
-            srcs = [(s.rewards, TN, self.B), (s.values, TN, self.B), (s.returns, TN, self.B),
+            srcs = [(s.rewards, TN, self.B), (s.values, TN, self.B), (s._returns, TN, self.B),
                     (s.env_returns_trace, TN, self.B), (s.bootstrap, self.B, 0),
                     (s.advantages, TN, self.B)]
             for i, (x, n, cols) in enumerate(srcs[:self._nmet]):
                 jobs[i].x = x.data_ptr() + c0 * 4
+                if i == 2 and s.derive_returns:  # 'Est Returns' = values + advantages
+                    jobs[i].x = s.values.data_ptr() + c0 * 4
+                    jobs[i].x2 = s.advantages.data_ptr() + c0 * 4
                 jobs[i].n = n
                 jobs[i].cols = cols if self.P > 1 else 0
                 jobs[i].ld = self.N
@@ -393,7 +409,8 @@ class RolloutManager:  # rollouts.py:373-826
                 from .pbt import pbt_update_fitness
                 pbt_update_fitness([(ps.episode_score, p * B, B)
                                     for p, ps in enumerate(self.policies)],
-                                   self.get_episode_scores(res), dn)
+                                   self.get_episode_scores(res), dn,
+                                   team_size=self.train_cfg.num_agents_per_world)
         # bootstrap values (rollouts.py:607-635), with the last post-step
         obs = self.prep_obs(rollout_state.cur_obs)
         for p, ps in enumerate(self.policies):
@@ -409,10 +426,11 @@ class RolloutManager:  # rollouts.py:373-826
             s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
         if self.use_advantages:
             compute_advantages(self.train_cfg, s.rewards, s.values, s.dones, s.bootstrap,
-                               out_adv=s.advantages, out_ret=s.returns,
+                               out_adv=s.advantages,
+                               out_ret=False if s.derive_returns else s._returns,
                                value_norm=train_state_mgr.value_norm, norm_cols=self.B)
         else:
-            compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s.returns)
+            compute_returns(self.train_cfg, s.rewards, s.dones, s.bootstrap, out=s._returns)
         for p in range(self.P):
             nat.check(L.mlearn_metrics_f32(self._jobs[p], self._nmet,
                                            nat.ptr(metrics.slots("Rewards", self._nmet, policy=p)),

@@ -10,6 +10,7 @@ data-parallel collectives (if any) issued between graph segments.
 """
 
 import os
+import re
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, Optional
 
@@ -156,13 +157,14 @@ class TrainingManager:  # train.py:35-64
         (rollouts.py:206-215, 300-309)."""
         torch.cuda.synchronize()
         os.makedirs(path, exist_ok=True)
-        self.state.save(self.update_idx, os.path.join(path, f"{self.update_idx}.pt"),
+        rank, W = world()
+        self.state.save(self.update_idx, os.path.join(path, _ckpt_name(self.update_idx, rank, W)),
                         extra={"rollout": self._rollout_state_dict()})
 
     def load_ckpt(self, path):  # train.py:48-49
         """A file written by save_ckpt, or its directory (latest update)."""
         torch.cuda.synchronize()
-        path = _ckpt_file(path)
+        path = _ckpt_file(path, *world())
         self.state, self.update_idx = self.state.load(path)
         sd = torch.load(path, map_location="cpu", weights_only=True)
         if "rollout" in sd:
@@ -190,12 +192,21 @@ class TrainingManager:  # train.py:35-64
             load(sd["sim"])
 
 
-def _ckpt_file(path):
+def _ckpt_name(update_idx, rank=0, world_size=1):
+    """<update_idx>.pt on one rank; <update_idx>.r<rank>.pt per rank of a
+    multi-rank job (each rank's file carries its own env shard, rollout
+    state and the policies placed on it)."""
+    return f"{update_idx}.pt" if world_size == 1 else f"{update_idx}.r{rank}.pt"
+
+
+def _ckpt_file(path, rank=0, world_size=1):
+    """A checkpoint file, or in a directory this rank's latest one."""
     if os.path.isdir(path):
-        ids = [int(f[:-3]) for f in os.listdir(path) if f.endswith(".pt") and f[:-3].isdigit()]
+        pat = re.compile(r"^(\d+)\.pt$" if world_size == 1 else rf"^(\d+)\.r{rank}\.pt$")
+        ids = [int(m.group(1)) for m in map(pat.match, os.listdir(path)) if m]
         if not ids:
-            raise FileNotFoundError(f"no checkpoint in {path}")
-        path = os.path.join(path, f"{max(ids)}.pt")
+            raise FileNotFoundError(f"no checkpoint of rank {rank}/{world_size} in {path}")
+        path = os.path.join(path, _ckpt_name(max(ids), rank, world_size))
     return path
 
 
@@ -336,7 +347,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         # train.py:353-354: the train state; the minibatch RNG position (the
         # epoch counter) is restored with it, like the reference's advanced
         # update_prng_key
-        path = _ckpt_file(restore_ckpt)
+        path = _ckpt_file(restore_ckpt, rank, W)
         tsm, start = tsm.load(path)
         ckpt_rollout = torch.load(path, map_location="cpu", weights_only=True).get("rollout")
         if ckpt_rollout is not None:

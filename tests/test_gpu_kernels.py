@@ -62,6 +62,14 @@ def test_gae_bitexact(gpu, T, N):
     # and within 1e-5 rel of the fp64 restatement
     fa, _ = ref.gae(r, v, d, b, 0.99, 0.95)
     np.testing.assert_allclose(adv.cpu().numpy(), fa, rtol=1e-5, atol=1e-5)
+    # returns not materialised (the product path): identical advantages, and
+    # the consumers' advantages + values equal the materialised returns bit for bit
+    adv2, none = compute_advantages(C, torch.from_numpy(r).to(gpu), torch.from_numpy(v).to(gpu),
+                                    torch.from_numpy(d).to(gpu), torch.from_numpy(b).to(gpu),
+                                    out_ret=False)
+    assert none is None
+    assert np.array_equal(adv2.cpu().numpy(), ea)
+    assert np.array_equal((adv2 + torch.from_numpy(v).to(gpu)).cpu().numpy(), er)
 
 
 def test_returns_bitexact(gpu):

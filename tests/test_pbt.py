@@ -91,6 +91,70 @@ def test_fitness_ema_matches_oracle():
         assert scores[p].N.item() == state[p][2]
 
 
+@pytest.mark.parametrize("team", [2, 4])
+@pytest.mark.parametrize("per_agent", [False, True])
+def test_fitness_counts_agent_zero_of_each_match(team, per_agent):
+    """pbt.py:390-396: dones reshaped to [matches, team_size] and only agent 0
+    of a match counts; episode scores are per match (or per agent, agent 0
+    taken).  A match ending counts once, not team_size times."""
+    from madrona_learn import pbt
+    rng = np.random.default_rng(7)
+    M, P = 48, 2                      # matches, policies (contiguous self-play split)
+    N, Bm = M * team, M // P          # agents, matches per policy
+    scores = [pbt.MovingEpisodeScore("cpu") for _ in range(P)]
+    state = [(np.float32(0), np.float32(0), 0) for _ in range(P)]
+    for step in range(12):
+        match_done = rng.random(M) < 0.3
+        dn = np.repeat(match_done, team)           # every agent of a match ends together
+        dn[1::team] = rng.random(M) < 0.5          # other agents' flags must not matter
+        dn[::team] = match_done
+        res = rng.standard_normal(M).astype(np.float32)
+        x = np.repeat(res, team) if per_agent else res
+        pbt.pbt_update_fitness([(scores[p], p * Bm * team, Bm * team) for p in range(P)],
+                               torch.from_numpy(x), torch.from_numpy(dn), team_size=team)
+        for p in range(P):
+            sl = slice(p * Bm, (p + 1) * Bm)
+            state[p] = oref.update_fitness(*state[p], res[sl], match_done[sl])
+    for p in range(P):
+        np.testing.assert_allclose(scores[p].mean.item(), state[p][0], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(scores[p].var.item(), state[p][1], rtol=1e-4, atol=1e-7)
+        assert scores[p].N.item() == state[p][2]
+
+
+def test_check_overwrite_zero_variance():
+    """Both variances 0 with N > 0 and different means: t = +/-inf, the
+    reference's p = 1 - cdf(t) is 0 (overwrite) or 1 (keep); N = 0 gives
+    NaN (never overwrite)."""
+    from madrona_learn import pbt
+    cases = [([1.0, 2.0], [0.0, 0.0], [5, 7]), ([2.0, 1.0], [0.0, 0.0], [5, 7]),
+             ([1.0, 1.0], [0.0, 0.0], [5, 7]), ([1.0, 2.0], [0.0, 0.0], [0, 7]),
+             ([1.0, 2.0], [0.5, 0.0], [3, 0]), ([-1.0, 3.0], [0.0, 1e-3], [4, 9])]
+    for mean, var, N in cases:
+        m, v, n = (np.asarray(a, np.float32) for a in (mean, var, N))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            want = oref.check_overwrite(m, v, n, 1, 0)
+        assert pbt.check_overwrite(None, m, v, n, 1, 0) == want, (mean, var, N)
+    # the zero-variance case the fix is about: source better -> overwrite
+    assert pbt.check_overwrite(None, np.float32([1, 2]), np.float32([0, 0]), np.float32([5, 7]),
+                               1, 0)
+
+
+def test_checkpoint_file_per_rank(tmp_path):
+    """Multi-rank jobs write <update>.r<rank>.pt and each rank restores its own
+    latest file; a one-rank job keeps <update>.pt."""
+    from madrona_learn.train import _ckpt_file, _ckpt_name
+    assert _ckpt_name(7) == "7.pt" and _ckpt_name(7, 1, 2) == "7.r1.pt"
+    for name in ("3.pt", "9.pt", "3.r0.pt", "3.r1.pt", "12.r0.pt", "5.r1.pt"):
+        (tmp_path / name).write_bytes(b"")
+    assert _ckpt_file(str(tmp_path)).endswith("9.pt")
+    assert _ckpt_file(str(tmp_path), 0, 2).endswith("12.r0.pt")
+    assert _ckpt_file(str(tmp_path), 1, 2).endswith("5.r1.pt")
+    with pytest.raises(FileNotFoundError):
+        _ckpt_file(str(tmp_path), 2, 4)
+    f = str(tmp_path / "5.r1.pt")
+    assert _ckpt_file(f, 0, 2) == f
+
+
 def test_cull_plan_matches_oracle():
     from madrona_learn import pbt
     rng = np.random.default_rng(1)

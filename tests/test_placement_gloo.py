@@ -37,6 +37,10 @@ def worker(rank, port, outdir):
             res[P] = (ids, dp.rank, dp.world_size, dp.root, float(t), float(b))
         with pytest.raises(ValueError):
             policy_placement(3)
+        # the native (RCCL-in-graph) path is off on gloo, and says why
+        _, dp = policy_placement(1)
+        res["native"] = (dp.enable_native(torch.device("cpu")), dp.collectives, dp.native_reason,
+                         dp.comm_ranks)
         torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -57,3 +61,4 @@ def test_policy_placement_world4(tmp_path):
         assert res[r][4] == ([r], 0, 1, r, float(r + 1), float(r + 100))
         # P = 8: two whole policies per rank
         assert res[r][8] == ([2 * r, 2 * r + 1], 0, 1, r, float(r + 1), float(r + 100))
+        assert res[r]["native"] == (False, "torch_distributed", "backend gloo", 0)
