@@ -544,43 +544,80 @@ __device__ inline u32x4 env_obs_words(uint32_t k0, uint32_t k1, uint32_t g, int 
                       k1 ^ 0x5eedu);
 }
 
-// state[n] = {episode step, env step lo, env step hi, 0}; one lane per
-// (env, 4 features); the first quad's lane also advances the env and emits
-// reward/done.
+// One env's reward / done / state advance (its counter {env, 2^31, step}).
+__device__ inline void env_advance(int4* state, const int32_t* actions, int K, int64_t n,
+                                   uint32_t g, uint32_t k0, uint32_t k1, float* rew,
+                                   uint8_t* done, int4 st) {
+#pragma clang fp contract(off)
+    const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
+    int s = st.x + 1;
+    int L = env_episode_len(g);
+    bool d = s >= L;
+    u32x4 r = philox4x32(u32x4{g, 0x80000000u, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
+                         k1 ^ 0x5eedu);
+    float u = u32_to_unit(r.x);
+    float a0 = actions ? (float)actions[n * K] : 0.f;
+    rew[n] = (u * 2.0f - 1.0f) + 0.01f * a0;
+    done[n] = d ? 1 : 0;
+    const uint64_t ns = step + 1;
+    state[n] = make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
+}
+
+// state[n] = {episode step, env step lo, env step hi, 0}.  A workgroup owns
+// EB = 256 / Q envs (Q = ceil(D / 4) <= 64): one lane per (env, 4 features)
+// for the observations, then the first EB lanes advance the EB envs (reward,
+// done, state) after a barrier that orders every lane's state read before the
+// writes.  The reward draws run once per workgroup, in wave 0, instead of one
+// extra divergent Philox pass in every wave; 32-bit index math.
 __global__ __launch_bounds__(256) void env_step_kernel(int4* state, const int32_t* actions,
                                                        int K, int64_t N, int D, uint32_t k0,
                                                        uint32_t k1, uint32_t eoff, float* obs,
                                                        float* rew, uint8_t* done) {
 #pragma clang fp contract(off)
     const int Q = (D + 3) >> 2;
-    int64_t task = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (task >= N * Q) return;
-    int64_t n = task / Q;
-    int q = (int)(task - n * Q);
-    uint32_t g = eoff + (uint32_t)n;
-    int4 st = state[n];
+    const int EB = 256 / Q;
+    const int tid = (int)threadIdx.x;
+    const int ln = (int)((uint32_t)tid / (uint32_t)Q), q = tid - ln * Q;
+    const int64_t n0 = (int64_t)blockIdx.x * EB;
+    const int64_t n = n0 + ln;
+    if (ln < EB && n < N) {
+        const uint32_t g = eoff + (uint32_t)n;
+        const int4 st = state[n];
+        const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
+        const u32x4 w = env_obs_words(k0, k1, g, q, step);
+        float* o = obs + n * D + 4 * q;
+        if ((D & 3) == 0 && ((uintptr_t)obs & 15) == 0) {
+            *(float4*)o = make_float4(env_obs_word(w.x), env_obs_word(w.y), env_obs_word(w.z),
+                                      env_obs_word(w.w));
+        } else {
+            for (int j = 0; j < 4 && 4 * q + j < D; ++j) o[j] = env_obs_word(u32x4_get(w, j));
+        }
+    }
+    __syncthreads();
+    const int64_t m = n0 + tid;
+    if (tid < EB && m < N)
+        env_advance(state, actions, K, m, eoff + (uint32_t)m, k0, k1, rew, done, state[m]);
+}
+
+// Observation dimensions above 256 (Q > 64): one lane per (env, 4 features),
+// the first quad's lane also advances the env (all quads of an env read the
+// state in the same pass before that lane's write: Q lanes per env, wave-ordered).
+__global__ __launch_bounds__(256) void env_step_wide_kernel(int4* state, const int32_t* actions,
+                                                            int K, int64_t N, int D, uint32_t k0,
+                                                            uint32_t k1, uint32_t eoff, float* obs,
+                                                            float* rew, uint8_t* done) {
+#pragma clang fp contract(off)
+    const int Q = (D + 3) >> 2;
+    const int64_t n = (int64_t)blockIdx.x;
+    const uint32_t g = eoff + (uint32_t)n;
+    const int4 st = state[n];
     const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
-    const u32x4 w = env_obs_words(k0, k1, g, q, step);
-    float* o = obs + n * D + 4 * q;
-    if ((D & 3) == 0 && ((uintptr_t)obs & 15) == 0) {
-        *(float4*)o = make_float4(env_obs_word(w.x), env_obs_word(w.y), env_obs_word(w.z),
-                                  env_obs_word(w.w));
-    } else {
-        for (int j = 0; j < 4 && 4 * q + j < D; ++j) o[j] = env_obs_word(u32x4_get(w, j));
+    for (int q = (int)threadIdx.x; q < Q; q += 256) {
+        const u32x4 w = env_obs_words(k0, k1, g, q, step);
+        for (int j = 0; j < 4 && 4 * q + j < D; ++j) obs[n * D + 4 * q + j] = env_obs_word(u32x4_get(w, j));
     }
-    if (q == 0) {
-        int s = st.x + 1;
-        int L = env_episode_len(g);
-        bool d = s >= L;
-        u32x4 r = philox4x32(u32x4{g, 0x80000000u, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
-                             k1 ^ 0x5eedu);
-        float u = u32_to_unit(r.x);
-        float a0 = actions ? (float)actions[n * K] : 0.f;
-        rew[n] = (u * 2.0f - 1.0f) + 0.01f * a0;
-        done[n] = d ? 1 : 0;
-        const uint64_t ns = step + 1;
-        state[n] = make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
-    }
+    __syncthreads();
+    if (threadIdx.x == 0) env_advance(state, actions, K, n, g, k0, k1, rew, done, st);
 }
 
 __global__ __launch_bounds__(256) void env_reset_kernel(int4* state, int64_t N, int D,
@@ -1038,10 +1075,17 @@ int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int
     if (N == 0) return MLEARN_OK;
     ML_REQUIRE(state && obs && rewards && dones, "env_step: null pointer");
     ML_REQUIRE((uintptr_t)state % 16 == 0, "env_step: state must be 16-byte aligned");
-    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(N * ((obs_dim + 3) / 4), 256)), dim3(256), 0,
-                       S(stream),
-                       (int4*)state, actions, K, N, obs_dim, k0, k1, env_offset, obs, rewards,
-                       dones);
+    const int Q = (obs_dim + 3) / 4;
+    if (Q <= 64) {
+        const int EB = 256 / Q;
+        hipLaunchKernelGGL(env_step_kernel, dim3((unsigned)((N + EB - 1) / EB)), dim3(256), 0,
+                           S(stream), (int4*)state, actions, K, N, obs_dim, k0, k1, env_offset,
+                           obs, rewards, dones);
+    } else {
+        hipLaunchKernelGGL(env_step_wide_kernel, dim3((unsigned)N), dim3(256), 0, S(stream),
+                           (int4*)state, actions, K, N, obs_dim, k0, k1, env_offset, obs, rewards,
+                           dones);
+    }
     return check_launch("env_step");
 }
 

@@ -127,7 +127,23 @@ struct CarryK {
 struct EvalK {
     const int32_t* actions;
     float* entropies;
+    uint64_t* stamps;  // diagnostic builds only (ML_STAMPS): [blocks][W][16]
 };
+
+#ifdef ML_STAMPS
+static uint64_t* g_pol_stamp_buf = nullptr;
+#define PSTAMP(i)                                                                      \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        if (ev.stamps && actions && lane == 0)                                         \
+            ev.stamps[((int64_t)blockIdx.x * W + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
+#else
+#define PSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
 
 // RNN: the LSTM cell (RecurrentBackboneEncoder, actor_critic.py:173-177)
 // sits between the trunk and the heads.  The trunk output fragments (from
@@ -137,7 +153,10 @@ struct EvalK {
 // order), so the cell update is register-local and h' lands in exactly the
 // layout the heads consume.
 template <typename T, int H, bool RNN, int HC>
-__global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
+#ifndef ML_POL_WAVES
+#define ML_POL_WAVES 1  // waves per SIMD the rollout policy kernel is register-budgeted for (1: compiler choice)
+#endif
+__global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_POL_WAVES, 8))) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
     uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev) {
@@ -186,6 +205,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
     if (post.rew && tid < 32 && row0 + tid < N) post_step_row(post, row0 + tid);
     const uint64_t step = (step_ctr ? *step_ctr : 0ull) + step_add;
     const float invH = 1.0f / (float)H;
+    PSTAMP(0);
 
     // layer 0: observation fragments straight from the env output (cast to
     // the compute dtype = ObservationsCaster); wave 0 copies them to the store
@@ -208,6 +228,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
                        (const T*)P.wt[0] + (int64_t)w * NBW * (D / KS) * 64 * E,
                        (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane,
                        P.obs_mu, P.obs_inv);
+    PSTAMP(1);
 #pragma unroll
     for (int k = 0; k < NPAR; ++k)
         if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
@@ -238,6 +259,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         const float mean = sum * invH;
         const float var = fmaxf(sq * invH - mean * mean, 0.f);
         const float rstd = rsqrtf(var + 1e-6f);
+        PSTAMP(2 + 2 * (l < 1 ? l : 1));
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
         if (l + 1 == L && !RNN) break;
 #pragma unroll
@@ -260,7 +282,9 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         else
             gemm_lds<T, NBW, KSH, 8>(acc, fr,
                                      (const T*)P.wt[l + 1] + (int64_t)w * NBW * KSH * 64 * E, lane);
+        PSTAMP(3);
     }
+    PSTAMP(5);
 
     if constexpr (RNN) {
         // carry rows, cleared where the previous env step was done (rollouts.py:942)
@@ -371,6 +395,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
         }
         __syncthreads();
     }
+    PSTAMP(6);
 
     // sample + store.  Gumbel noise first, one Philox block per 4 logits of a
     // row ((env, logit quad) tasks; the head partials' LDS is free now), then
@@ -396,6 +421,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             }
             __syncthreads();
         }
+        PSTAMP(7);
         for (int task = tid; task < 32 * P.K; task += THREADS) {
             const int rr = task / P.K, g = task - rr * P.K;
             const int64_t n = row0 + rr;
@@ -407,6 +433,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             actions[n * P.K + g] = a;
             if (logp) logp[n * P.K + g] = lp;
         }
+        PSTAMP(8);
     } else if (ev.actions) {
         for (int task = tid; task < 32 * P.K; task += THREADS) {
             const int rr = task / P.K, g = task - rr * P.K;
@@ -457,6 +484,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) void policy_step_kernel(
             }
         }
     }
+    PSTAMP(9);
 }
 
 template <typename T, int H, bool RNN, int HC> static size_t policy_step_lds(int L) {
@@ -482,9 +510,15 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
         attr_set = true;
     }
     const int grid = (int)((N + 31) / 32);
+#ifdef ML_STAMPS
+    EvalK evs = ev;
+    evs.stamps = g_pol_stamp_buf;
+#else
+    const EvalK& evs = ev;
+#endif
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
                        (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
-                       post, R, cy, ev);
+                       post, R, cy, evs);
     return check_launch("policy_rollout_step");
 }
 
@@ -602,3 +636,8 @@ extern "C" int32_t mlearn_head_cols(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;
     return head_cols(*policy);
 }
+
+#ifdef ML_STAMPS
+// diagnostic builds only: phase timestamps of the rollout policy kernel
+extern "C" void mlearn_debug_set_policy_stamp_buffer(uint64_t* buf) { ml::g_pol_stamp_buf = buf; }
+#endif

@@ -6,7 +6,10 @@ the whole job; each rank simulates its N-env shard and contributes 16
 sequences to every global minibatch.  After one update (eager) and two more
 (HIP-graph replay) both ranks must hold identical parameters, and the first
 update must equal the oracle's single-process update over the union of both
-ranks' minibatches (f32 mode, tolerances of test_gpu_train)."""
+ranks' minibatches: f32 at H=64 (tolerances of test_gpu_train), and bf16 at
+H=256 (the production width; 256 envs and 32 sequences per rank per
+minibatch) held to the per-tensor bound of tests/bf16_bound.py against the
+oracle's bf16 and f32 modes (ref.ppo_update(stores=[rank0, rank1]))."""
 
 import os
 import socket
@@ -19,7 +22,8 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 BUCKETS = [4, 8, 5, 5, 2, 2]
-N, D, H, T = 64, 64, 64, 32
+D, T = 64, 32
+CASES = {"f32": (torch.float32, 64, 64, 16), "bf16": (torch.bfloat16, 256, 256, 32)}
 
 
 def _free_port():
@@ -28,7 +32,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def worker(rank, world, port, outdir):
+def worker(rank, world, port, outdir, mode):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -39,12 +43,12 @@ def worker(rank, world, port, outdir):
         from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        dtype = torch.float32
+        dtype, N, H, mbl = CASES[mode]
         env = DummyVecEnv(N, D, 6, seed=2, env_offset=rank * N, device=dev)
         cfg = ml.TrainConfig(
             num_worlds=world * N, num_agents_per_world=1, num_updates=3,
             actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
-            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=16 * world, clip_coef=0.2,
+            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=mbl * world, clip_coef=0.2,
                                        value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                        max_grad_norm=0.5),
             num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=5, metrics_buffer_size=4,
@@ -55,7 +59,7 @@ def worker(rank, world, port, outdir):
             critic=DenseLayerCritic(dtype)))
         mgr = ml.init_training(dev, cfg, env.sim_fns(), policy, use_graph=True)
         ps, ts = mgr.state.policy_states, mgr.state.train_states
-        assert mgr.rollout_mgr.N == N and mgr.algo.mb == 16, "global config must split per rank"
+        assert mgr.rollout_mgr.N == N and mgr.algo.mb == mbl, "global config must split per rank"
         p0 = ps.params.cpu().numpy()
         mgr.update_iter()
         torch.cuda.synchronize()
@@ -74,9 +78,11 @@ def worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_dp_two_ranks_one_gpu(tmp_path, mode):
     from oracle import ppo_ref as ref
-    mp.spawn(worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    _, N, H, mbl = CASES[mode]
+    mp.spawn(worker, args=(2, _free_port(), str(tmp_path), mode), nprocs=2, join=True)
     r = [np.load(os.path.join(tmp_path, f"rank{i}.npz")) for i in range(2)]
     p3 = [np.load(os.path.join(tmp_path, f"rank{i}_p3.npy")) for i in range(2)]
     assert np.array_equal(r[0]["p0"], r[1]["p0"]), "initial params differ across ranks"
@@ -89,8 +95,17 @@ def test_dp_two_ranks_one_gpu(tmp_path):
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
           "normalize_advantages": True}
     z = np.zeros_like(p0)
-    p_ref, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay,
-                                 r[0]["init_norms"].astype(np.float64), num_epochs=2,
-                                 minibatch_size=16, bptt=T, key=tuple(int(x) for x in r[0]["key"]),
-                                 epoch_base=0, mode="f32", lr=3e-4, max_grad_norm=0.5)
-    np.testing.assert_allclose(r[0]["p1"], p_ref, rtol=1e-4, atol=2e-5)
+    upd = dict(num_epochs=2, minibatch_size=mbl, bptt=T,
+               key=tuple(int(x) for x in r[0]["key"]), epoch_base=0, lr=3e-4, max_grad_norm=0.5)
+    norms = r[0]["init_norms"].astype(np.float64)
+    p_ref, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay, norms,
+                                 mode=mode, **upd)
+    if mode == "f32":
+        np.testing.assert_allclose(r[0]["p1"], p_ref, rtol=1e-4, atol=2e-5)
+        return
+    from tests.bf16_bound import check_bf16_update
+    p_f32, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay, norms,
+                                 mode="f32", **upd)
+    check_bf16_update("dp_world2_H256_bf16", r[0]["p1"], p0, p_ref, p_f32, lay)
+    dg, dr = r[0]["p1"] - p0, p_ref - p0
+    assert dg @ dr / (np.linalg.norm(dg) * np.linalg.norm(dr)) > 0.99

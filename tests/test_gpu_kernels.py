@@ -157,9 +157,13 @@ def test_minibatch_perm_bitexact(gpu, n):
     assert np.array_equal(got, ref.epoch_permutation(11, 22, 7, 3, n))
 
 
-def test_env_bitexact(gpu):
+@pytest.mark.parametrize("D", [64, 48, 18, 1100])
+def test_env_bitexact(gpu, D):
+    """Q = ceil(D / 4) quads per env: 16 (16 envs per workgroup), 12 (21, not
+    dividing 256), 5 (a ragged last quad) and 275 (the one-env-per-workgroup
+    kernel for D > 256)."""
     from madrona_learn.envs import DummyVecEnv
-    N, D = 300, 64
+    N = 300
     env = DummyVecEnv(N, D, 6, seed=3, env_offset=1000, device=gpu)
     oenv = onat.Env(N, D, env.k0, env.k1, 1000)
     o = env.init()["obs"].cpu().numpy()

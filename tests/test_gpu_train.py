@@ -126,7 +126,15 @@ def test_full_update_matches_oracle(gpu, mode, dtype, chunks, CB, N, H, mb):
         assert close.mean() >= 0.999, close.mean()
         assert cos > 0.999
     else:
-        assert cos > 0.97, cos
+        # per-tensor bound from the oracle's own bf16-vs-f32 effect (tests/bf16_bound.py)
+        from tests.bf16_bound import check_bf16_update
+        pf, _, _ = ref.ppo_update(
+            p0, (zeros, zeros.copy(), 0), [store], hp, BUCKETS, lay,
+            ps.init_norms.cpu().numpy().astype(np.float64), num_epochs=2, minibatch_size=mb,
+            bptt=cfg.steps_per_update // chunks, key=ts.update_prng_key, epoch_base=0,
+            mode="f32", lr=3e-4, max_grad_norm=0.5)
+        check_bf16_update(f"train_N{N}_H{H}_C{chunks}_CB{CB}", got, p0, p1, pf, lay)
+        assert cos > 0.99, cos
     assert int(ts.step.item()) == 2 * (cfg.num_worlds * chunks // mb)
     last = mgr.metrics.last()
     np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
