@@ -59,7 +59,7 @@ def envs_per_rank(config, world):
 
 
 def make(dev, total_envs, env_offset, n_local, dtype=torch.bfloat16, use_graph=True,
-         config="headline", chunks=1, critic="scalar"):
+         config="headline", chunks=1, critic="scalar", fused_sim=True):
     """init_training on this rank: the config is GLOBAL (num_worlds =
     total_envs, minibatch_size = MB sequences); the sim plugin serves this
     rank's shard of n_local envs starting at env_offset."""
@@ -96,7 +96,8 @@ def make(dev, total_envs, env_offset, n_local, dtype=torch.bfloat16, use_graph=T
     import contextlib
     import io
     with contextlib.redirect_stdout(io.StringIO()):
-        mgr = ml.init_training(dev, cfg, env.sim_fns(), policy, use_graph=use_graph)
+        mgr = ml.init_training(dev, cfg, env.sim_fns(fused=fused_sim), policy,
+                               use_graph=use_graph)
     return mgr
 
 
@@ -308,6 +309,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--config", choices=["headline", "b1", "lstm", "pbt"], default="headline")
     ap.add_argument("--bptt-chunks", type=int, default=1)
+    ap.add_argument("--separate-sim", action="store_true",
+                    help="run the synthetic sim's step as its own launch between the policy "
+                         "launches (as a user sim plugin runs) instead of fused into them")
     ap.add_argument("--critic", choices=["scalar", "twohot"], default="scalar",
                     help="DenseLayerCritic (SURVEY B1) or DreamerV3Critic (63-bin two-hot)")
     ap.add_argument("--emulate-world", type=int, default=1,
@@ -340,7 +344,8 @@ def main():
     total = TOTAL_ENVS[args.config]
     n_rank = envs_per_rank(args.config, world)
     mgr = make(dev, total, rank * n_rank, n_rank, use_graph=not args.no_graph,
-               config=args.config, chunks=args.bptt_chunks, critic=args.critic)
+               config=args.config, chunks=args.bptt_chunks, critic=args.critic,
+               fused_sim=not args.separate_sim)
     for _ in range(args.warmup):
         mgr.update_iter()
     torch.cuda.synchronize()
@@ -390,7 +395,11 @@ def main():
                        "global_minibatch_seqs": MB, "minibatches_per_epoch": nmb,
                        "steps_per_update": T, "parallelism": f"dp{world}",
                        "critic": args.critic,
-                       "hip_graph": not args.no_graph},
+                       "hip_graph": not args.no_graph,
+                       # the built-in synthetic sim's step: inside the rollout policy
+                       # launch (mlearn_policy_rollout_step_env) or its own launch
+                       "sim_step": "separate_launch" if args.separate_sim
+                       else "fused_into_policy_launch"},
             # how the data-parallel collectives ran (a SCALE record can be checked
             # against this): "rccl_in_graph" = C ABI RCCL communicator on the
             # compute stream inside the HIP graph; "torch_distributed" = host
@@ -433,13 +442,15 @@ def emulate_world(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     os.environ["MLEARN_EMULATE_WORLD"] = str(W)
-    mgr = make(dev, total, 0, total // W, use_graph=not args.no_graph)
+    mgr = make(dev, total, 0, total // W, use_graph=not args.no_graph,
+               fused_sim=not args.separate_sim)
     coll = mgr.dp.collectives
     t_w = _time_updates(mgr, args.steps, args.warmup)
     del mgr
     torch.cuda.empty_cache()
     os.environ.pop("MLEARN_EMULATE_WORLD")
-    mgr = make(dev, total, 0, total, use_graph=not args.no_graph)
+    mgr = make(dev, total, 0, total, use_graph=not args.no_graph,
+               fused_sim=not args.separate_sim)
     t_1 = _time_updates(mgr, args.steps, args.warmup)
     print(json.dumps({
         "metric": "env-steps/sec whole-node, 65536-env PPO, at 1/2/4/8 MI355X (projection)",

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 9
+#define MLEARN_ABI_VERSION 10
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -547,6 +547,38 @@ int mlearn_dummy_env_step(int32_t* state, const int32_t* actions, int32_t K, int
 int mlearn_dummy_env_reset(int32_t* state, int64_t N, int32_t obs_dim, uint32_t k0,
                            uint32_t k1, uint32_t env_offset, float* obs,
                            mlearn_stream_t stream);
+
+/* The same env step fused into the rollout policy launch that produced the
+ * actions (no separate sim launch, no host round trip): after the sample,
+ * each workgroup advances its own envs from their first action, writing the
+ * next observations over the launch's obs input (env->obs must equal obs),
+ * rewards and dones (which the NEXT launch's post-step reads: post->rewards /
+ * post->dones must be env->rewards / env->dones), bit-identical to
+ * mlearn_dummy_env_step on the same actions.  Only for this built-in sim:
+ * a user sim plugin keeps its own step between the policy launches. */
+typedef struct mlearn_dummy_env {
+    int32_t* state;     /* [N][4], 16-byte aligned */
+    float* obs;         /* [N][obs_dim] */
+    float* rewards;     /* [N] */
+    uint8_t* dones;     /* [N] */
+    uint32_t k0, k1;    /* env keys (not the policy's sampling keys) */
+    uint32_t env_offset;
+    uint32_t pad;
+} mlearn_dummy_env;
+int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float* obs, int64_t N,
+                                   void* obs_store, int32_t* actions, float* log_probs,
+                                   float* values, uint32_t k0, uint32_t k1,
+                                   const uint64_t* step_ctr, uint64_t step, uint32_t env_offset,
+                                   int32_t sample, const mlearn_post_step* post,
+                                   const mlearn_dummy_env* env, mlearn_stream_t stream);
+int mlearn_lstm_policy_rollout_step_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                        const mlearn_lstm_carry* carry, const float* obs,
+                                        int64_t N, void* obs_store, int32_t* actions,
+                                        float* log_probs, float* values, uint32_t k0, uint32_t k1,
+                                        const uint64_t* step_ctr, uint64_t step,
+                                        uint32_t env_offset, int32_t sample,
+                                        const mlearn_post_step* post, const mlearn_dummy_env* env,
+                                        mlearn_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
 /* Data-parallel collectives on the compute stream  */

@@ -489,3 +489,178 @@ __global__ __launch_bounds__(64) void lstm_bwd_step_kernel(
         cp[3 * H + uq] = so;
     }
 }
+
+// ---------------------------------------------------------------------------
+// Per-step scans with four waves per (32 sequences, 32-unit block) workgroup
+// (ML_LSTM_STEP4, the default): the step's product is split over the waves
+// so each wave's serial MFMA chain and weight stream are a quarter of the
+// one-wave kernels' above, and 4x as many waves cover the chip.
+//   forward:  wave g computes gate block g (Gin_t + h Wh, its 16 KB slice of
+//             Wh); the pre-activations meet in LDS; wave j then runs the cell
+//             for register quad j (units 8j + 4h .. +3 of the block).  Same
+//             MFMA sequence per gate block and same cell arithmetic as
+//             lstm_fwd_step_kernel: gates, c, h bit-identical to it.
+//   backward: wave g computes dG_{t+1}[:, gate g] Wh_g^T (a quarter of the
+//             K = 4H reduction), the four partials are summed in fixed order
+//             ((p0 + p1) + p2) + p3 (deterministic; the f32 rounding differs
+//             from the single 4H-long chain), then wave j runs the cell
+//             backward for register quad j; the bias column partials are
+//             32-lane butterfly sums.
+// ---------------------------------------------------------------------------
+template <typename T, int H>
+__global__ __launch_bounds__(256) void lstm_fwd_step4_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
+    const float4* __restrict__ gin, const T* __restrict__ sh, const T* __restrict__ sc,
+    LstmWsK lw, int t) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NW = H / 32;
+    __shared__ float pre[4][16][64];  // gate block g, accumulator register q, lane
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // gate (product) / register quad (cell)
+    const int tile = blockIdx.x, w = blockIdx.y;
+    const int m = tile * 32 + r;
+    const int64_t f = (int64_t)t * mb + m;
+    const T *hrow, *crow;
+    if (t == 0) {
+        const int64_t seq = mb_seq[m];
+        const int64_t c = seq / ro.N, b = seq - c * ro.N;
+        hrow = sh + (c * ro.ld + b) * H;
+        crow = sc + (c * ro.ld + b) * H;
+    } else {
+        hrow = (const T*)lw.hin + f * H;
+        crow = (const T*)lw.cin + f * H;
+    }
+    frag hb[KSH];
+#pragma unroll
+    for (int s = 0; s < KSH; ++s) hb[s] = RT<T>::row(hrow, s, h);
+    f32x16 acc[1];
+    {
+        const float4* gi = gin + gin_base((int64_t)t * (mb / 32) + tile, NW, w) + lane;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float4 x = gi[(4 * g + c) * 64];
+            acc[0][4 * c] = x.x;
+            acc[0][4 * c + 1] = x.y;
+            acc[0][4 * c + 2] = x.z;
+            acc[0][4 * c + 3] = x.w;
+        }
+    }
+    gemm_ring<T, 1, KSH, 8>(acc, hb, KSH, (const T*)R.wh_nat + ((int64_t)w * 4 + g) * KSH * 64 * E,
+                            lane);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pre[g][q][lane] = acc[0][q];
+    // cell of register quad j = g: the c carry and the done flag load under the barrier
+    const int j = g, u0 = w * 32 + 8 * j + 4 * h;
+    const float4 cv = load4(crow + u0);
+    if (t == 0) {
+        const float4 hv = load4(hrow + u0);
+        store4((T*)lw.hin + f * H + u0, hv.x, hv.y, hv.z, hv.w);
+        store4((T*)lw.cin + f * H + u0, cv.x, cv.y, cv.z, cv.w);
+    }
+    const bool more = t + 1 < ro.bptt;
+    const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+    const float keep = done ? 0.f : 1.f;
+    __syncthreads();
+    T* gts = (T*)lw.gates + f * 4 * H;
+    float gi[4], gf[4], gg[4], go[4], cn[4], hn[4], hc[4], ck[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int q = 4 * j + e, u = u0 + e;
+        const CellOut o = lstm_cell_fwd<T>(pre[0][q][lane] + R.bias[u], pre[1][q][lane] + R.bias[H + u],
+                                           pre[2][q][lane] + R.bias[2 * H + u],
+                                           pre[3][q][lane] + R.bias[3 * H + u], f4get(cv, e));
+        gi[e] = o.i;
+        gf[e] = o.f;
+        gg[e] = o.g;
+        go[e] = o.o;
+        cn[e] = o.c;
+        hn[e] = o.h;
+        ck[e] = keep * o.c;
+        hc[e] = keep * o.h;
+    }
+    store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
+    store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
+    store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
+    store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
+    store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
+    store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
+    if (more) {
+        store4((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
+        store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
+    }
+}
+
+// Sum over the 32 lanes of this lane's half wave (fixed butterfly).
+__device__ inline float half_sum32(float x) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+template <typename T, int H>
+__global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
+    float* colpart, int CP, int cp0, int t) {
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NQ = NKS / 4, NU = H / 32;
+    __shared__ float part[4][16][64];  // K quarter g, accumulator register q, lane
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // K quarter (product) / register quad (cell)
+    const int tile = blockIdx.x, w = blockIdx.y;
+    const int m0 = tile * 32, m = m0 + r;
+    const int bptt = ro.bptt;
+    const int64_t fs = (int64_t)t * mb + m;
+    const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    if (t + 1 < bptt)  // quarter g of dh_t = dG_{t+1} Wh^T: gate g's H columns of dG
+        gemm_stream<T, 1, NQ, 8>(acc, (const T*)lw.dg + (fs + mb) * 4 * H + g * H,
+                                 (const T*)R.w_bwd + ((int64_t)(NU + w) * NKS + g * NQ) * 64 * E,
+                                 lane);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
+    // cell backward of register quad j = g: its operands load under the barrier
+    const int j = g, u0 = w * 32 + 8 * j + 4 * h;
+    const T* gts = (const T*)lw.gates + fs * 4 * H;
+    const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
+    const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
+    const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
+    const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
+    const float4 ci = load4((const T*)lw.cin + fs * H + u0);
+    const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(lw.dcc + fs * H + u0);
+    __syncthreads();
+    float dpi[4], dpf[4], dpg[4], dpo[4], dco[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int q = 4 * j + e;
+        const float dhh = ((part[0][q][lane] + part[1][q][lane]) + part[2][q][lane]) + part[3][q][lane];
+        const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
+        const float dh = f4get(dho, e) + (cut ? 0.f : dhh);
+        const float tc = tanh_fast(f4get(c4, e));
+        const float dout = dh * tc;
+        const float dc = f4get(dcin, e) + dh * o_ * (1.f - tc * tc);
+        dpi[e] = rnd<T>((dc * g_) * i_ * (1.f - i_));
+        dpf[e] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
+        dpg[e] = rnd<T>((dc * i_) * (1.f - g_ * g_));
+        dpo[e] = rnd<T>(dout * o_ * (1.f - o_));
+        dco[e] = dc * f_;
+    }
+    if (t > 0) *(float4*)(lw.dcc + (fs - mb) * H + u0) = make_float4(dco[0], dco[1], dco[2], dco[3]);
+    T* dgs = (T*)lw.dg + fs * 4 * H;
+    store4(dgs + u0, dpi[0], dpi[1], dpi[2], dpi[3]);
+    store4(dgs + H + u0, dpf[0], dpf[1], dpf[2], dpf[3]);
+    store4(dgs + 2 * H + u0, dpg[0], dpg[1], dpg[2], dpg[3]);
+    store4(dgs + 3 * H + u0, dpo[0], dpo[1], dpo[2], dpo[3]);
+    // bias gradient: column sums of dG over this tile's 32 rows (units u0 .. u0 + 3)
+    float* cp = colpart + (int64_t)(((int64_t)t * mb + m0) / 32) * CP + cp0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float si = half_sum32(dpi[e]), sf = half_sum32(dpf[e]);
+        const float sg = half_sum32(dpg[e]), so = half_sum32(dpo[e]);
+        if (r == 0) {
+            cp[u0 + e] = si;
+            cp[H + u0 + e] = sf;
+            cp[2 * H + u0 + e] = sg;
+            cp[3 * H + u0 + e] = so;
+        }
+    }
+}

@@ -11,6 +11,7 @@
 
 #include "common.h"
 #include "dists.h"
+#include "env.h"
 #include "rowtile.h"
 
 namespace ml {
@@ -528,41 +529,6 @@ __global__ __launch_bounds__(256) void post_step_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 // Synthetic dummy vec-env (bench/test sim plugin).
 // ---------------------------------------------------------------------------
-__host__ __device__ inline int env_episode_len(uint32_t g) { return 16 + (int)((g * 7u) % 33u); }
-
-// One Philox4x32-10 call per 4 features (counter {env, f / 4, step}):
-// feature f reads word f % 4 as four bytes b_i, s = sum (b_i + 0.5) / 256
-// (Irwin-Hall n = 4 of 8-bit uniforms, exact in f32), obs = (s - 2) sqrt(3):
-// mean 0, variance 1.  CPU twin: oracle/ref_rng.c obs_feature.
-__device__ inline float env_obs_word(uint32_t w) {
-#pragma clang fp contract(off)
-    const uint32_t b = (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24) + 2u;
-    return ((float)b * 0.00390625f - 2.0f) * 1.73205077648162841796875f;
-}
-__device__ inline u32x4 env_obs_words(uint32_t k0, uint32_t k1, uint32_t g, int q, uint64_t step) {
-    return philox4x32(u32x4{g, (uint32_t)q, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
-                      k1 ^ 0x5eedu);
-}
-
-// One env's reward / done / state advance (its counter {env, 2^31, step}).
-__device__ inline void env_advance(int4* state, const int32_t* actions, int K, int64_t n,
-                                   uint32_t g, uint32_t k0, uint32_t k1, float* rew,
-                                   uint8_t* done, int4 st) {
-#pragma clang fp contract(off)
-    const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
-    int s = st.x + 1;
-    int L = env_episode_len(g);
-    bool d = s >= L;
-    u32x4 r = philox4x32(u32x4{g, 0x80000000u, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
-                         k1 ^ 0x5eedu);
-    float u = u32_to_unit(r.x);
-    float a0 = actions ? (float)actions[n * K] : 0.f;
-    rew[n] = (u * 2.0f - 1.0f) + 0.01f * a0;
-    done[n] = d ? 1 : 0;
-    const uint64_t ns = step + 1;
-    state[n] = make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
-}
-
 // state[n] = {episode step, env step lo, env step hi, 0}.  A workgroup owns
 // EB = 256 / Q envs (Q = ceil(D / 4) <= 64): one lane per (env, 4 features)
 // for the observations, then the first EB lanes advance the EB envs (reward,
@@ -583,15 +549,8 @@ __global__ __launch_bounds__(256) void env_step_kernel(int4* state, const int32_
     if (ln < EB && n < N) {
         const uint32_t g = eoff + (uint32_t)n;
         const int4 st = state[n];
-        const uint64_t step = ((uint64_t)(uint32_t)st.z << 32) | (uint32_t)st.y;
-        const u32x4 w = env_obs_words(k0, k1, g, q, step);
-        float* o = obs + n * D + 4 * q;
-        if ((D & 3) == 0 && ((uintptr_t)obs & 15) == 0) {
-            *(float4*)o = make_float4(env_obs_word(w.x), env_obs_word(w.y), env_obs_word(w.z),
-                                      env_obs_word(w.w));
-        } else {
-            for (int j = 0; j < 4 && 4 * q + j < D; ++j) o[j] = env_obs_word(u32x4_get(w, j));
-        }
+        env_obs_quad(obs + n * D + 4 * q, D, k0, k1, g, q, env_step_of(st),
+                     (D & 3) == 0 && ((uintptr_t)obs & 15) == 0);
     }
     __syncthreads();
     const int64_t m = n0 + tid;

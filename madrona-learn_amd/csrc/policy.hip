@@ -11,6 +11,7 @@
 
 #include "common.h"
 #include "dists.h"
+#include "env.h"
 #include "rowtile.h"
 
 namespace ml {
@@ -154,12 +155,16 @@ static uint64_t* g_pol_stamp_buf = nullptr;
 // layout the heads consume.
 template <typename T, int H, bool RNN, int HC>
 #ifndef ML_POL_WAVES
-#define ML_POL_WAVES 1  // waves per SIMD the rollout policy kernel is register-budgeted for (1: compiler choice)
+#define ML_POL_WAVES 1  // waves per SIMD the recurrent rollout policy kernel is register-budgeted for (1: compiler choice)
 #endif
-__global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_eu(ML_POL_WAVES, 8))) void policy_step_kernel(
+#ifndef ML_POL_MLP_WAVES
+#define ML_POL_MLP_WAVES 3  // the feed-forward kernel: 3 waves per SIMD (<= 168 VGPRs, 3 workgroups per CU)
+#endif
+__global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_eu(RNN ? ML_POL_WAVES : ML_POL_MLP_WAVES, 8))) void policy_step_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev) {
+    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev,
+    EnvK env) {
     typedef typename RT<T>::frag frag;
     typedef PolCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
@@ -345,6 +350,38 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
         }
     }
 
+    // fused env step (mlearn_policy_rollout_step_env): the next observations
+    // depend only on the env state, not on the actions, so they are drawn
+    // here, behind the trunk, and stored once every wave is past its reads of
+    // this launch's observation rows (after the heads' barrier; with the
+    // observation statistics, which read the rows last, at the end)
+    const bool fenv = env.state && actions;
+    const int EQ = D >> 2;  // quads per env (D is a multiple of 16)
+    constexpr int kEnvQ = 2;  // quads per thread drawn early (32 * EQ <= kEnvQ * THREADS)
+    const bool env_early = fenv && 32 * EQ <= kEnvQ * THREADS;
+    float4 enq[kEnvQ];
+    if (env_early) {
+#pragma unroll
+        for (int u = 0; u < kEnvQ; ++u) {
+            const int task = tid + u * THREADS, rr = task / EQ, q = task - rr * EQ;
+            const int64_t n = row0 + rr;
+            if (task < 32 * EQ && n < N) {
+                const u32x4 wv = env_obs_words(env.k0, env.k1, env.eoff + (uint32_t)n, q,
+                                               env_step_of(env.state[n]));
+                enq[u] = make_float4(env_obs_word(wv.x), env_obs_word(wv.y), env_obs_word(wv.z),
+                                     env_obs_word(wv.w));
+            }
+        }
+    }
+    auto env_store_obs = [&]() {
+#pragma unroll
+        for (int u = 0; u < kEnvQ; ++u) {
+            const int task = tid + u * THREADS, rr = task / EQ, q = task - rr * EQ;
+            const int64_t n = row0 + rr;
+            if (task < 32 * EQ && n < N) *(float4*)(env.obs + n * D + 4 * q) = enq[u];
+        }
+    };
+
     // actor + critic heads (dists.py:22, models.py:154): lg[row][j] =
     // rnd(rnd(a . W) + rnd(b)).  Head width 32: each wave multiplies its own
     // features (B fragments from registers), partials summed in wave order.
@@ -395,6 +432,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
         }
         __syncthreads();
     }
+    if (env_early && !P.obs_stats) env_store_obs();
     PSTAMP(6);
 
     // sample + store.  Gumbel noise first, one Philox block per 4 logits of a
@@ -432,6 +470,17 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
                        P.off[g + 1] - P.off[g], &a, &lp);
             actions[n * P.K + g] = a;
             if (logp) logp[n * P.K + g] = lp;
+            // fused env: reward, done and state advance of env n from its first
+            // action (every lane's state read above is behind the heads' barrier)
+            if (fenv && g == 0) {
+                const int4 st = env.state[n];
+                if (!env_early) {  // the late observation draws read the pre-step counter here
+                    ((uint32_t*)red)[2 * rr] = (uint32_t)st.y;
+                    ((uint32_t*)red)[2 * rr + 1] = (uint32_t)st.z;
+                }
+                env_advance_a0(env.state, n, env.eoff + (uint32_t)n, env.k0, env.k1, (float)a,
+                               env.rew, env.done, st);
+            }
         }
         PSTAMP(8);
     } else if (ev.actions) {
@@ -484,6 +533,25 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
             }
         }
     }
+    // fused env, late path: observation statistics read this launch's rows
+    // last, or the observation is too wide for the early draws
+    if (fenv && (P.obs_stats || !env_early)) {
+        __syncthreads();
+        if (env_early) {
+            env_store_obs();
+        } else {
+            // pre-step counters from the pick loop (LDS)
+            const uint32_t* sc = (const uint32_t*)red;
+            for (int task = tid; task < 32 * EQ; task += THREADS) {
+                const int rr = task / EQ, q = task - rr * EQ;
+                const int64_t n = row0 + rr;
+                if (n >= N) continue;
+                const uint64_t step = ((uint64_t)sc[2 * rr + 1] << 32) | sc[2 * rr];
+                env_obs_quad(env.obs + n * D + 4 * q, D, env.k0, env.k1, env.eoff + (uint32_t)n, q,
+                             step, true);
+            }
+        }
+    }
     PSTAMP(9);
 }
 
@@ -500,7 +568,7 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
                               int32_t* actions, float* logp, float* values, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
                               const PostK& post, const LstmK& R, const CarryK& cy, const EvalK& ev,
-                              hipStream_t s) {
+                              const EnvK& env, hipStream_t s) {
     const size_t lds = policy_step_lds<T, H, RNN, HC>(P.L);
     auto kern = policy_step_kernel<T, H, RNN, HC>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
@@ -518,7 +586,7 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
 #endif
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
                        (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
-                       post, R, cy, evs);
+                       post, R, cy, evs, env);
     return check_launch("policy_rollout_step");
 }
 
@@ -527,7 +595,8 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
                               void* obs_store, int32_t* actions, float* log_probs, float* values,
                               uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint64_t step,
                               uint32_t env_offset, int32_t sample, const mlearn_post_step* post,
-                              mlearn_stream_t stream, EvalK ev = EvalK{}) {
+                              mlearn_stream_t stream, EvalK ev = EvalK{},
+                              const mlearn_dummy_env* denv = nullptr) {
     int rc = lstm ? validate_lstm(policy, lstm) : validate_policy(policy);
     if (rc) return rc;
     ML_REQUIRE(N >= 0, "policy_rollout_step: N < 0");
@@ -551,6 +620,20 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
         pk = PostK{post->rewards, post->dones, post->store_rewards, post->store_dones,
                    post->env_returns, post->env_returns_trace, post->gamma};
     }
+    EnvK ek{};
+    if (denv) {
+        ML_REQUIRE(actions, "policy_rollout_step_env: the fused env step needs actions");
+        ML_REQUIRE(denv->state && denv->obs && denv->rewards && denv->dones,
+                   "policy_rollout_step_env: null env pointer");
+        ML_REQUIRE(denv->obs == obs,
+                   "policy_rollout_step_env: env->obs must be the launch's obs input (the next "
+                   "observations overwrite it in place)");
+        ML_REQUIRE((uintptr_t)denv->state % 16 == 0, "policy_rollout_step_env: state alignment");
+        ML_REQUIRE(!post || (post->rewards == denv->rewards && post->dones == denv->dones),
+                   "policy_rollout_step_env: post-step must read the env's rewards / dones");
+        ek = EnvK{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
+                  denv->env_offset};
+    }
     LstmK R{};
     CarryK cy{};
     if (lstm) {
@@ -566,10 +649,10 @@ static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \
     (lstm ? launch_policy_step<T, HH, true, HC>(P, obs, N, obs_store, actions, log_probs, values, \
                                                 k0, k1, step_ctr, step, env_offset, sample, pk, R, \
-                                                cy, ev, s)                                        \
+                                                cy, ev, ek, s)                                    \
           : launch_policy_step<T, HH, false, HC>(P, obs, N, obs_store, actions, log_probs, values, \
                                                  k0, k1, step_ctr, step, env_offset, sample, pk, R, \
-                                                 cy, ev, s))
+                                                 cy, ev, ek, s))
 #define ML_LAUNCH(T, HH) \
     (P.HC == MLEARN_HEAD_COLS ? ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS) : ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS_MAX))
 #define ML_DISPATCH(T)                      \
@@ -600,6 +683,32 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
                                           const mlearn_post_step* post, mlearn_stream_t stream) {
     return rollout_step_entry(policy, nullptr, nullptr, obs, N, obs_store, actions, log_probs,
                               values, k0, k1, step_ctr, step, env_offset, sample, post, stream);
+}
+
+extern "C" int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float* obs,
+                                              int64_t N, void* obs_store, int32_t* actions,
+                                              float* log_probs, float* values, uint32_t k0,
+                                              uint32_t k1, const uint64_t* step_ctr, uint64_t step,
+                                              uint32_t env_offset, int32_t sample,
+                                              const mlearn_post_step* post,
+                                              const mlearn_dummy_env* env, mlearn_stream_t stream) {
+    ML_REQUIRE(env, "policy_rollout_step_env: null env descriptor");
+    return rollout_step_entry(policy, nullptr, nullptr, obs, N, obs_store, actions, log_probs,
+                              values, k0, k1, step_ctr, step, env_offset, sample, post, stream,
+                              EvalK{}, env);
+}
+
+extern "C" int mlearn_lstm_policy_rollout_step_env(
+    const mlearn_mlp_policy* policy, const mlearn_lstm* lstm, const mlearn_lstm_carry* carry,
+    const float* obs, int64_t N, void* obs_store, int32_t* actions, float* log_probs,
+    float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint64_t step,
+    uint32_t env_offset, int32_t sample, const mlearn_post_step* post, const mlearn_dummy_env* env,
+    mlearn_stream_t stream) {
+    ML_REQUIRE(lstm, "lstm rollout step: null lstm descriptor");
+    ML_REQUIRE(env, "policy_rollout_step_env: null env descriptor");
+    return rollout_step_entry(policy, lstm, carry, obs, N, obs_store, actions, log_probs, values,
+                              k0, k1, step_ctr, step, env_offset, sample, post, stream, EvalK{},
+                              env);
 }
 
 extern "C" int mlearn_lstm_policy_rollout_step(

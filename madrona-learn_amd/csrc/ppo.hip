@@ -1765,14 +1765,23 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
 #ifndef ML_LSTM_PERSISTENT
 #define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
 #endif
+#ifndef ML_LSTM_STEP4
+#define ML_LSTM_STEP4 1  // per-step scans with 4 waves per (32 sequences, 32 units) (0: one wave)
+#endif
     // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
     // workgroups (ML_LSTM_PERSISTENT: one persistent launch, a workgroup per
     // 32 sequences)
     if (!ML_LSTM_PERSISTENT) {
-        for (int t = 0; t < bptt; ++t)
-            hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s,
-                               RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
-                               (const T*)start_c, lw, t);
+        for (int t = 0; t < bptt; ++t) {
+            if (ML_LSTM_STEP4)
+                hipLaunchKernelGGL((lstm_fwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0,
+                                   s, RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
+                                   (const T*)start_c, lw, t);
+            else
+                hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
+                                   s, RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
+                                   (const T*)start_c, lw, t);
+        }
     } else {
         const size_t lds = (size_t)KSH * 64 * FR;
         auto k = lstm_fwd_scan_kernel<T, H>;
@@ -1790,9 +1799,14 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // reverse scan
     const int cp0 = L * 2 * H + head_cols(p);
     if (!ML_LSTM_PERSISTENT) {
-        for (int t = bptt - 1; t >= 0; --t)
-            hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s,
-                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+        for (int t = bptt - 1; t >= 0; --t) {
+            if (ML_LSTM_STEP4)
+                hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0,
+                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+            else
+                hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
+                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+        }
     } else {
         const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
         auto k = lstm_bwd_scan_kernel<T, H>;

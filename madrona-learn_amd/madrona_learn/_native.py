@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -89,6 +89,12 @@ class LstmCarry(Structure):  # mlearn_lstm_carry
                 ("commit", c_int32), ("pad", c_int32), ("clear", c_void_p)]
 
 
+class DummyEnv(Structure):  # mlearn_dummy_env
+    _fields_ = [("state", c_void_p), ("obs", c_void_p), ("rewards", c_void_p),
+                ("dones", c_void_p), ("k0", c_uint32), ("k1", c_uint32),
+                ("env_offset", c_uint32), ("pad", c_uint32)]
+
+
 _S = c_void_p  # hipStream_t
 _P = c_void_p
 
@@ -121,6 +127,15 @@ _SIGNATURES = {
     "mlearn_policy_rollout_step": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P,
                                              c_uint32, c_uint32, _P, c_uint64, c_uint32, c_int32,
                                              POINTER(PostStep), _S]),
+    "mlearn_policy_rollout_step_env": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P,
+                                                 _P, c_uint32, c_uint32, _P, c_uint64, c_uint32,
+                                                 c_int32, POINTER(PostStep), POINTER(DummyEnv),
+                                                 _S]),
+    "mlearn_lstm_policy_rollout_step_env": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm),
+                                                      POINTER(LstmCarry), _P, c_int64, _P, _P, _P,
+                                                      _P, c_uint32, c_uint32, _P, c_uint64,
+                                                      c_uint32, c_int32, POINTER(PostStep),
+                                                      POINTER(DummyEnv), _S]),
     "mlearn_policy_evaluate": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P, _S]),
     "mlearn_lstm_policy_evaluate": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                               _P, c_int64, _P, _P, _P, _P, _S]),

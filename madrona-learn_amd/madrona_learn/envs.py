@@ -5,7 +5,9 @@ protocol (rollouts.py:206-215, 905-936): ``init() -> {'state', 'obs'}`` and
 ``step({'state', 'actions', 'resets', 'sim_ctrl', 'pbt'}) -> {'state', 'obs',
 'rewards', 'dones'}``.  One HIP launch per step (misc.hip env_step_kernel).
 Deterministic: staggered fixed episode lengths, Philox observations and
-rewards, reward depends on action[0].
+rewards, reward depends on action[0].  With ``sim_fns()['native_step']`` the
+rollout fuses the step into the policy launch (policy.hip), which removes the
+sim launch and its round trip from every env step.
 """
 
 import torch
@@ -60,6 +62,34 @@ class DummyVecEnv:
             self.state[m] = ckpts.to(self.state.device)[m]
         return self.obs
 
-    def sim_fns(self):
-        return {"init": self.init, "step": self.step, "get_ckpts": self.get_ckpts,
-                "load_ckpts": self.load_ckpts}
+    def native_step(self, col0=0, ncols=None):
+        """Descriptor of this sim's step for the env columns [col0, col0 +
+        ncols), run inside the rollout policy launch that samples their
+        actions (mlearn_policy_rollout_step_env; bit-identical to step()).
+        Outputs land in the same state / obs / rewards / dones tensors."""
+        ncols = self.N - col0 if ncols is None else ncols
+        assert 0 <= col0 and col0 + ncols <= self.N
+        d = nat.DummyEnv()
+        d.state = self.state.data_ptr() + col0 * 16
+        d.obs = self.obs.data_ptr() + col0 * self.D * 4
+        d.rewards = self.rewards.data_ptr() + col0 * 4
+        d.dones = self.dones.data_ptr() + col0
+        d.k0, d.k1 = self.k0, self.k1
+        d.env_offset = (self.env_offset + col0) & 0xFFFFFFFF
+        return d
+
+    def native_outputs(self):
+        """The step() output dict the fused step fills."""
+        return {"state": self.state, "obs": self.obs, "rewards": self.rewards,
+                "dones": self.dones}
+
+    def sim_fns(self, fused=True):
+        """The reference's sim_fns dict (rollouts.py:206-215, 905-936); with
+        fused=True also 'native_step' (this build's extension): the rollout
+        then runs the env step inside the policy launch instead of calling
+        'step' between launches."""
+        fns = {"init": self.init, "step": self.step, "get_ckpts": self.get_ckpts,
+               "load_ckpts": self.load_ckpts}
+        if fused:
+            fns["native_step"] = self
+        return fns

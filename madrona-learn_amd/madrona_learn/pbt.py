@@ -19,17 +19,22 @@ and the initial hyperparameter draw of train.py:320-351).
   one per GPU in config P): a copy between ranks is a point-to-point
   transfer of the policy's tensors (RCCL send/recv over xGMI, gloo on CPU);
   the compute weight images are rebuilt on the receiving GPU.
-* ``pbt_past_update`` (pbt.py:685-722): past-policy snapshots.  The fused
-  path trains self-play populations (num_past_policies == 0, where the
-  reference returns the state unchanged).
+* ``pbt_past_update`` (pbt.py:684-722): past-policy snapshots.  The
+  num_past_policies past slots (``TrainStateManager.past_list``, replicated on
+  every rank, initialised from train policy j mod P as train_state.py:489-498
+  tiles them) hold a policy state without optimizer state; each call picks a
+  uniform train policy and overwrites the least fit past slot with it when
+  _check_overwrite passes.  Past policies are snapshots only: past-play
+  matchmaking (pbt.py:135-247) is outside the fused path, so no env plays
+  them and their fitness stays what was copied.
 
 RNG: jax.random's threefry splits are replaced by Philox4x32-10 counters
 (the C ABI's ``mlearn_philox4x32_host``): the population key is
 ``TrainStateManager.pbt_rng`` = int64 [k0, k1, op counter]; op c draws for
 population slot s and stream q (0 lr, 1 entropy, 2 + i reward
 hyperparameter i) the words of counter {c, s, q, 0}: word 0 decides
-resample vs perturb, word 1 is the value's uniform; the cull's source pick
-of pbt_past_update would use stream 0x7fffffff.  Uniforms are
+resample vs perturb, word 1 is the value's uniform; pbt_past_update's
+source pick uses slot 0, stream 0x7fffffff.  Uniforms are
 ``u32_to_unit`` (csrc/common.h).  oracle/pbt_ref.py restates all of it.
 """
 
@@ -333,9 +338,96 @@ def pbt_cull_update(cfg, tsm, num_cull_policies: int):
     return tsm, plan
 
 
+# ---------------------------------------------------------------------------
+# past-policy snapshots
+# ---------------------------------------------------------------------------
+class PastPolicy:
+    """Past slot ``policy_id`` (the reference's policy_states[P + j]): the
+    policy state of a train policy at the time it was saved — parameters,
+    observation-normaliser estimates, fitness — without optimizer state."""
+
+    def __init__(self, policy_id, like):
+        self.policy_id = int(policy_id)
+        self.params = torch.zeros_like(like.params)
+        self.obs_est = None if like.obs_est is None else torch.zeros_like(like.obs_est)
+        self.obs_count = None if like.obs_est is None else torch.zeros_like(like.obs_count)
+        self.episode_score = MovingEpisodeScore(like.params.device)
+
+    def tensors(self):
+        t = [self.params]
+        if self.obs_est is not None:
+            t += [self.obs_est, self.obs_count]
+        return t + self.episode_score.tensors()
+
+    def state_dict(self):
+        return {"policy_id": self.policy_id, "tensors": [x.detach().cpu() for x in self.tensors()]}
+
+    def load_state_dict(self, sd):
+        for a, b in zip(self.tensors(), sd["tensors"]):
+            a.copy_(b)
+
+
+def _policy_tensors(ps):
+    t = [ps.params]
+    if ps.obs_est is not None:
+        t += [ps.obs_est, ps.obs_count]
+    return t + ps.episode_score.tensors()
+
+
+def snapshot_policy(tsm, src_pid, past, P):
+    """past := train policy src_pid's policy state on every rank (a broadcast
+    from src's first holder)."""
+    rank, W = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+    root = _holders(src_pid, P, W)[0]
+    if rank == root:
+        local = {ts.policy_id: ps for ps, ts in zip(tsm.policy_list, tsm.train_list)}
+        for a, b in zip(past.tensors(), _policy_tensors(local[src_pid])):
+            a.copy_(b)
+    if W > 1:
+        for t in past.tensors():
+            dist.broadcast(t, root)
+
+
+def init_past_policies(cfg, tsm):
+    """TrainStateManager.past_list: num_past_policies snapshots, slot j a copy
+    of train policy j mod P's initial state (train_state.py:489-498)."""
+    P, Q = int(cfg.pbt.num_train_policies), int(cfg.pbt.num_past_policies)
+    like = tsm.policy_list[0]
+    tsm.past_list = []
+    for j in range(Q):
+        pp = PastPolicy(P + j, like)
+        snapshot_policy(tsm, j % P, pp, P)
+        tsm.past_list.append(pp)
+    return tsm
+
+
+def past_update_plan(key, op, mean, var, N, P, Q):
+    """(src, dst, overwrite) of pbt_past_update; mean / var / N cover the P
+    train then the Q past policies."""
+    u, _ = _draws(key, op, 0, 0x7FFFFFFF)
+    src = min(int(np.float32(u) * np.float32(P)), P - 1)  # random.randint(0, P)
+    dst = P + int(np.argmin(np.asarray(mean, np.float32)[P:P + Q]))  # jnp.argmin: first minimum
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return src, dst, check_overwrite(cfg=None, mean=mean, var=var, N=N, src=src, dst=dst)
+
+
 def pbt_past_update(cfg, tsm):
-    """pbt.py:685-722: no past policies on the fused path (the reference
-    returns the state unchanged when num_past_policies == 0)."""
+    """pbt.py:684-722: a uniform train policy overwrites the least fit past
+    slot when the one-sided test passes.  The plan is kept in
+    ``tsm.last_past_update`` (the reference prints it)."""
     if cfg.pbt.num_past_policies == 0:
         return tsm
-    raise NotImplementedError("past-policy snapshots need past-play matchmaking (pbt.py:135-247)")
+    P, Q = int(cfg.pbt.num_train_policies), int(cfg.pbt.num_past_policies)
+    if len(getattr(tsm, "past_list", None) or []) != Q:
+        raise ValueError(f"TrainStateManager holds no {Q} past policies (init_past_policies)")
+    k0, k1, op = _split(tsm.pbt_rng)
+    mean, var, N = gather_fitness(tsm, P)
+    e = [p.episode_score for p in tsm.past_list]
+    mean = np.concatenate([mean, [float(x.mean[0]) for x in e]])
+    var = np.concatenate([var, [float(x.var[0]) for x in e]])
+    N = np.concatenate([N, [float(x.N[0]) for x in e]])
+    src, dst, ok = past_update_plan((k0, k1), op, mean, var, N, P, Q)
+    if ok:
+        snapshot_policy(tsm, src, tsm.past_list[dst - P], P)
+    tsm.last_past_update = (src, dst, ok)
+    return tsm

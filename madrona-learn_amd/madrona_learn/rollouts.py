@@ -2,8 +2,9 @@
 
 ``RolloutManager.collect`` runs the reference's rollout_loop (rollouts.py:
 829-978) as, per step: one fused HIP launch for preprocess + policy +
-sample + store (policy.hip), the user's sim step, and one post-step launch
-(rewards/dones store, env returns).  Then the bootstrap critic, GAE/returns
+sample + store (policy.hip) with the previous step's post-step (rewards /
+dones store, env returns), then the user's sim step (the built-in synthetic
+sim's step runs inside the same launch instead, envs.DummyVecEnv.native_step).  Then the bootstrap critic, GAE/returns
 and the rollout metrics.  No finalize transpose (rollouts.py:786-804): the
 store stays [T][N] = [C][T/C][P][B] and the PPO kernels index sequences
 directly.
@@ -69,9 +70,12 @@ class RolloutConfig:  # rollouts.py:28-134 (self-play / single-policy path)
 
 class RolloutState:  # rollouts.py:171-309
     def __init__(self, cfg, step_fn, sim_state, cur_obs, prng_key, rnn_states, sim_ctrl,
-                 env_returns, counters, policy_assignments):
+                 env_returns, counters, policy_assignments, native_step=None):
         self.cfg = cfg
         self.step_fn = step_fn
+        # the built-in synthetic sim's fused step (envs.DummyVecEnv.native_step),
+        # or None: the sim's 'step' runs between the policy launches
+        self.native_step = native_step
         self.sim_state = sim_state
         self.cur_obs = cur_obs
         self.prng_key = prng_key
@@ -99,6 +103,7 @@ class RolloutState:  # rollouts.py:171-309
             # self-play: every agent runs policy 0 (pbt.py:130-133)
             policy_assignments=torch.zeros((rollout_cfg.sim_batch_size, 1), dtype=torch.int32,
                                            device=dev),
+            native_step=sim_fns.get("native_step"),
         )
 
 
@@ -335,6 +340,17 @@ class RolloutManager:  # rollouts.py:373-826
             off += len(b)
         return out
 
+    def _env_desc(self, sim, p):
+        """nat.DummyEnv of policy p's env columns (cached per sim)."""
+        key = (id(sim), p)
+        if not hasattr(self, "_env_descs"):
+            self._env_descs = {}
+        d = self._env_descs.get(key)
+        if d is None:
+            d = sim.native_step(p * self.B, self.B)
+            self._env_descs[key] = d
+        return d
+
     def add_metrics(self, train_cfg, names):  # rollouts.py:482-499
         return list(names) + ROLLOUT_METRICS[:self._nmet]
 
@@ -376,22 +392,30 @@ class RolloutManager:  # rollouts.py:373-826
         step_ctr = rollout_state.counters[0:1]
         B = self.B
         posts = [None] * self.P  # post-step of env step t-1, fused into the policy launches of t
+        sim = rollout_state.native_step
         for t in range(self.T):
             obs = self.prep_obs(rollout_state.cur_obs)
+            # the built-in sim steps inside the policy launches when they read
+            # its observation buffer directly (no preprocessing copy)
+            fused = sim is not None and obs.data_ptr() == sim.obs.data_ptr()
             for p, ps in enumerate(self.policies):
                 c = slice(p * B, (p + 1) * B)
                 ps.rollout_step(obs[c], s.obs[t, c], s.actions[t, c], s.log_probs[t, c],
                                 s.values[t, c], key, step_ctr, t, self.env_offset + p * B,
                                 sample=True, post=posts[p],
-                                carry=self._carry(rollout_state, p, t) if self.R else None)
-            step_input = {
-                "state": rollout_state.sim_state,
-                "actions": self._sim_actions(t),
-                "resets": self._resets,
-                "sim_ctrl": rollout_state.sim_ctrl,
-                "pbt": {"policy_assignments": rollout_state.policy_assignments},
-            }
-            out = rollout_state.step_fn(step_input)
+                                carry=self._carry(rollout_state, p, t) if self.R else None,
+                                env=self._env_desc(sim, p) if fused else None)
+            if fused:
+                out = sim.native_outputs()
+            else:
+                step_input = {
+                    "state": rollout_state.sim_state,
+                    "actions": self._sim_actions(t),
+                    "resets": self._resets,
+                    "sim_ctrl": rollout_state.sim_ctrl,
+                    "pbt": {"policy_assignments": rollout_state.policy_assignments},
+                }
+                out = rollout_state.step_fn(step_input)
             rew = out["rewards"].reshape(-1)
             if rew.dtype != torch.float32:
                 rew = rew.float()

@@ -250,10 +250,12 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     num_policies = 1
     if cfg.pbt is not None:
         pbt = cfg.pbt
-        if pbt.num_past_policies != 0 or pbt.self_play_portion != 1.0:
+        if pbt.self_play_portion != 1.0 or pbt.past_play_portion != 0.0 or \
+                pbt.cross_play_portion != 0.0:
             raise NotImplementedError(
                 "populations run the self-play split (pbt.py:130-133); past/cross-play "
-                "matchmaking (pbt.py:135-247) is outside the fused path")
+                "matchmaking (pbt.py:135-247) is outside the fused path (past policies are "
+                "kept as snapshots, pbt_past_update)")
         num_policies = int(pbt.num_train_policies)
     # policy placement: which train policies this rank holds, and the ranks it
     # shares gradients with (dist.policy_placement)
@@ -341,6 +343,9 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         from .pbt import new_pbt_rng, sample_initial_hyperparams
         tsm.pbt_rng = new_pbt_rng(cfg.seed)
         sample_initial_hyperparams(cfg, tsm)
+        if cfg.pbt.num_past_policies > 0:
+            from .pbt import init_past_policies
+            init_past_policies(cfg, tsm)
     start = 0
     ckpt_rollout = None
     if restore_ckpt is not None:

@@ -285,24 +285,35 @@ class PolicyState:
 
     # -- kernels ------------------------------------------------------------
     def rollout_step(self, obs, obs_store, actions, log_probs, values, key, step_ctr, step,
-                     env_offset=0, sample=True, post=None, carry=None):
+                     env_offset=0, sample=True, post=None, carry=None, env=None):
         """ActorCritic.rollout + store (actor_critic.py:74-96, rollouts.py:637-668);
         post: optional nat.PostStep of the previous env step; carry: the
-        nat.LstmCarry of a recurrent policy."""
+        nat.LstmCarry of a recurrent policy; env: optional nat.DummyEnv of the
+        built-in synthetic sim, whose step on the sampled actions then runs
+        in the same launch (mlearn_policy_rollout_step_env)."""
         N = obs.shape[0]
+        L = nat.lib()
         if self.lstm_desc is not None:
             self._check_carry(carry)
-            nat.check(nat.lib().mlearn_lstm_policy_rollout_step(
-                self.desc, self.lstm_desc, carry, nat.ptr(obs, torch.float32, name="obs"), N,
-                nat.ptr(obs_store), nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values),
-                key[0], key[1], nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post,
-                nat.stream_handle()), "lstm_policy_rollout_step")
+            args = (self.desc, self.lstm_desc, carry, nat.ptr(obs, torch.float32, name="obs"), N,
+                    nat.ptr(obs_store), nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values),
+                    key[0], key[1], nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post)
+            if env is None:
+                nat.check(L.mlearn_lstm_policy_rollout_step(*args, nat.stream_handle()),
+                          "lstm_policy_rollout_step")
+            else:
+                nat.check(L.mlearn_lstm_policy_rollout_step_env(*args, env, nat.stream_handle()),
+                          "lstm_policy_rollout_step_env")
             return
-        nat.check(nat.lib().mlearn_policy_rollout_step(
-            self.desc, nat.ptr(obs, torch.float32, name="obs"), N, nat.ptr(obs_store),
-            nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values), key[0], key[1],
-            nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post,
-            nat.stream_handle()), "policy_rollout_step")
+        args = (self.desc, nat.ptr(obs, torch.float32, name="obs"), N, nat.ptr(obs_store),
+                nat.ptr(actions), nat.ptr(log_probs), nat.ptr(values), key[0], key[1],
+                nat.ptr(step_ctr), step, env_offset, 1 if sample else 0, post)
+        if env is None:
+            nat.check(L.mlearn_policy_rollout_step(*args, nat.stream_handle()),
+                      "policy_rollout_step")
+        else:
+            nat.check(L.mlearn_policy_rollout_step_env(*args, env, nat.stream_handle()),
+                      "policy_rollout_step_env")
 
     def _check_carry(self, carry):
         if not isinstance(carry, nat.LstmCarry) or not carry.h or not carry.c:
@@ -451,6 +462,7 @@ class TrainStateManager:  # train_state.py:139-304
     pbt_rng: Any = None
     user_state: Any = None
     value_norm: Any = None  # [P][8] f32 value-normaliser estimates (normalize_values)
+    past_list: Any = None   # past-policy snapshots (pbt.PastPolicy), every rank
 
     @property
     def policy_list(self):
@@ -471,7 +483,8 @@ class TrainStateManager:  # train_state.py:139-304
                 "train": [t.state_dict() for t in self.train_list],
                 "pbt_rng": self.pbt_rng if isinstance(self.pbt_rng, (torch.Tensor, type(None)))
                 else None,
-                "user_state": _ckpt_safe(self.user_state)}
+                "user_state": _ckpt_safe(self.user_state),
+                "past": [p.state_dict() for p in (self.past_list or [])]}
 
     def load_state_dict(self, sd):
         pol, tr = sd["policies"], sd["train"]
@@ -486,6 +499,12 @@ class TrainStateManager:  # train_state.py:139-304
             self.user_state = sd["user_state"]
         if sd.get("pbt_rng") is not None:
             self.pbt_rng = sd["pbt_rng"]
+        past = sd.get("past") or []
+        if len(past) != len(self.past_list or []):
+            raise ValueError(f"checkpoint holds {len(past)} past policies, expected "
+                             f"{len(self.past_list or [])}")
+        for p, d in zip(self.past_list or [], past):
+            p.load_state_dict(d)
         return self
 
     def save(self, update_idx, path, extra=None):  # train_state.py:145-163

@@ -7,6 +7,8 @@ Follows src/madrona_learn/pbt.py of the reference:
   pbt_update_fitness          pbt.py:382-470 (EMA decay 0.9999)
   _check_overwrite            pbt.py:565-600 (one-sided test, p < 0.20)
   pbt_cull_update             pbt.py:609-682 (argsort, bottom <- top)
+  pbt_past_update             pbt.py:684-722 (random train source -> least fit past slot)
+  past snapshots' initial     train_state.py:489-498 (past j = train j mod P, tiled)
 with the RNG contract of madrona_learn/pbt.py (Philox4x32-10 counters
 {op, slot, stream, 0} on the population key replacing jax.random.split /
 uniform; the reference's threefry streams cannot be reproduced without JAX:
@@ -112,3 +114,24 @@ def cull_plan(mean, var, N, num_train, num_cull):
     with np.errstate(divide="ignore", invalid="ignore"):
         return [(int(d), int(s), check_overwrite(mean, var, N, s, d))
                 for d, s in zip(bottom, top)]
+
+
+def past_update_plan(k0, k1, op, mean, var, N, num_train, num_past):
+    """(src, dst, overwrite) of pbt_past_update (pbt.py:684-722): the source
+    is a uniform train policy (random.randint(0, num_train), here counter
+    {op, 0, 0x7fffffff, 0} word 0 -> floor(u * num_train)), the destination
+    the least fit past policy (jnp.argmin: the first minimum), overwritten
+    when _check_overwrite passes.  mean / var / N cover train then past
+    policies."""
+    u, _ = draws(k0, k1, op, 0, 0x7FFFFFFF)
+    src = min(int(f32(u) * f32(num_train)), num_train - 1)
+    past = np.asarray(mean, np.float32)[num_train:num_train + num_past]
+    dst = num_train + int(np.argmin(past))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return src, dst, check_overwrite(mean, var, N, src, dst)
+
+
+def initial_past_sources(num_train, num_past):
+    """Train policy whose initial state past slot j copies (the tile of
+    train_state.py:489-498)."""
+    return [j % num_train for j in range(num_past)]

@@ -1,0 +1,89 @@
+"""The built-in synthetic sim's step fused into the rollout policy launch
+(mlearn_policy_rollout_step_env, envs.DummyVecEnv.native_step) is
+bit-identical to calling the sim's own step between the launches
+(mlearn_dummy_env_step): same store, env state, observations, rewards,
+dones and parameters after whole update iterations, eager and graph-captured,
+for MLP / population / LSTM policies, including a partial last workgroup of
+envs.  The oracle parity of the fused path itself is tests/test_gpu_train.py
+(the store against the oracle env, bit for bit), which runs fused by default."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BUCKETS = [4, 8, 5, 5, 2, 2]
+
+
+def _manager(gpu, fused, dtype, N, H, mb, P=1, lstm=False, use_graph=False):
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from tests.test_gpu_train import make_policy
+    env = DummyVecEnv(N, 64, 6, seed=4, device=gpu)
+    pbt = None
+    if P > 1:
+        pbt = ml.PBTConfig(num_teams=1, team_size=1, num_train_policies=P, num_past_policies=0,
+                           self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0)
+    cfg = ml.TrainConfig(
+        num_worlds=N, num_agents_per_world=1, num_updates=2,
+        actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=32,
+        lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=mb, clip_coef=0.2,
+                                   value_loss_coef=0.5, entropy_coef={"actions": 0.01},
+                                   max_grad_norm=0.5),
+        num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=11, metrics_buffer_size=4,
+        dreamer_v3_critic=False, compute_dtype=dtype, pbt=pbt)
+    if lstm:
+        from tests.test_gpu_lstm import make_actor_critic
+        pol = ml.Policy(actor_critic=make_actor_critic(H, 2, dtype, 1),
+                        obs_preprocess=ml.ObservationsCaster.create(dtype))
+    else:
+        pol = make_policy(dtype, H)
+    fns = env.sim_fns(fused=fused)
+    assert ("native_step" in fns) == fused
+    return env, ml.init_training(gpu, cfg, fns, pol, use_graph=use_graph)
+
+
+@pytest.mark.parametrize("dtype,N,H,mb,P,lstm,graph", [
+    (torch.float32, 80, 64, 16, 1, False, False),    # partial last workgroup (80 = 2.5 x 32)
+    (torch.bfloat16, 1024, 256, 256, 1, False, True),
+    (torch.float32, 128, 64, 16, 2, False, True),     # population: one launch per policy
+    (torch.float32, 64, 64, 32, 1, True, False)])     # LSTM carry + done clears
+def test_fused_env_step_is_bit_identical(gpu, dtype, N, H, mb, P, lstm, graph):
+    env_a, a = _manager(gpu, True, dtype, N, H, mb, P, lstm, graph)
+    env_b, b = _manager(gpu, False, dtype, N, H, mb, P, lstm, graph)
+    for _ in range(2):
+        a.update_iter()
+        b.update_iter()
+    torch.cuda.synchronize()
+    sa, sb = a.rollout_mgr.store, b.rollout_mgr.store
+    for k, v in sa.as_dict().items():
+        assert torch.equal(v, sb.as_dict()[k]), k
+    assert torch.equal(sa.env_returns_trace, sb.env_returns_trace)
+    assert torch.equal(sa.bootstrap, sb.bootstrap)
+    for x, y in ((env_a.state, env_b.state), (env_a.obs, env_b.obs),
+                 (env_a.rewards, env_b.rewards), (env_a.dones, env_b.dones)):
+        assert torch.equal(x, y)
+    pa = a.state.policy_list if P > 1 else [a.state.policy_states]
+    pb = b.state.policy_list if P > 1 else [b.state.policy_states]
+    for x, y in zip(pa, pb):
+        assert torch.equal(x.params, y.params)
+    # the fused run issued no sim launch: its env buffers moved anyway
+    assert int(env_a.state[:, 1].min().item()) == 64
+
+
+def test_fused_env_rejects_foreign_obs(gpu):
+    """env->obs must be the launch's own obs input (the next observations
+    overwrite it in place)."""
+    import madrona_learn as ml  # noqa: F401
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    _, mgr = _manager(gpu, True, torch.float32, 64, 64, 16)
+    ps = mgr.state.policy_states
+    env = DummyVecEnv(64, 64, 6, seed=1, device=gpu)
+    env.init()
+    other = torch.zeros_like(env.obs)
+    s = mgr.rollout_mgr.store
+    with pytest.raises(RuntimeError, match="env->obs"):
+        ps.rollout_step(other, s.obs[0], s.actions[0], s.log_probs[0], s.values[0],
+                        (1, 2), mgr.rollout.counters[0:1], 0, env=env.native_step())
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION

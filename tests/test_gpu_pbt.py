@@ -175,3 +175,51 @@ def test_cull_update_gpu(gpu):
     mgr.update_iter()
     torch.cuda.synchronize()
     assert all(torch.isfinite(ps.params).all() for ps in pss)
+
+
+def test_past_update_gpu(gpu, tmp_path):
+    """TrainConfig.pbt with past policies (snapshots, no past play): the
+    past slots start as copies of train policy j mod P, pbt_past_update
+    follows the oracle's plan and copies the source's policy state into the
+    least fit slot, and the past slots survive a checkpoint round trip."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn import pbt
+    from madrona_learn.envs import DummyVecEnv
+    from oracle import pbt_ref as oref
+    from tests.test_gpu_train import make_policy
+    env = DummyVecEnv(128, D, 6, seed=3, device=gpu)
+    cfg, _, _ = _setup(gpu, torch.float32, N=128, H=64, P=2, mb=16)
+    cfg = dataclasses.replace(cfg, pbt=dataclasses.replace(cfg.pbt, num_past_policies=3))
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.float32, 64),
+                           use_graph=False)
+    pss, past = mgr.state.policy_list, mgr.state.past_list
+    assert [p.policy_id for p in past] == [2, 3, 4]
+    for j, p in enumerate(past):
+        assert torch.equal(p.params, pss[oref.initial_past_sources(2, 3)[j]].params)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    fit = [(1.0, 1.0, 40), (4.0, 1.0, 40), (0.0, 1.0, 30), (-6.0, 1.0, 30), (0.0, 1.0, 30)]
+    for e, (m, v, n) in zip([p.episode_score for p in pss + past], fit):
+        e.mean.fill_(m)
+        e.var.fill_(v)
+        e.N.fill_(n)
+    op = int(mgr.state.pbt_rng[2])
+    k0, k1 = (int(x) for x in mgr.state.pbt_rng[:2])
+    before = [p.params.clone() for p in pss]
+    pbt.pbt_past_update(cfg, mgr.state)
+    want = oref.past_update_plan(k0, k1, op, np.array([f[0] for f in fit], np.float32),
+                                 np.array([f[1] for f in fit], np.float32),
+                                 np.array([f[2] for f in fit], np.float64), 2, 3)
+    assert mgr.state.last_past_update == want
+    src, dst, ok = want
+    assert dst == 3 and ok
+    assert torch.equal(past[1].params, before[src])
+    assert float(past[1].episode_score.mean) == fit[src][0]
+    # checkpoint round trip of the past slots
+    mgr.save_ckpt(str(tmp_path))
+    saved = [p.params.clone() for p in past]
+    for p in past:
+        p.params.zero_()
+    mgr.load_ckpt(str(tmp_path))
+    assert all(torch.equal(a.params, b) for a, b in zip(mgr.state.past_list, saved))

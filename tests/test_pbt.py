@@ -239,3 +239,87 @@ def test_cull_copies_across_ranks_gloo():
     ur, up = oref.draws(1, 2, 0, 0, 0)
     want = oref.explore_param(ur, up, src_ts.hyper_params.lr, EXPLORES[0], 0.2)
     assert np.float32(lr0) == np.float32(want) and lr1 == src_ts.hyper_params.lr
+
+
+# ---------------------------------------------------------------------------
+# past-policy snapshots (pbt_past_update, pbt.py:684-722)
+# ---------------------------------------------------------------------------
+def test_past_update_plan_matches_oracle():
+    from madrona_learn import pbt
+    rng = np.random.default_rng(7)
+    for trial in range(60):
+        P, Q = int(rng.integers(1, 6)), int(rng.integers(1, 5))
+        mean = rng.standard_normal(P + Q).astype(np.float32)
+        if trial % 3 == 0:
+            mean[P:] = mean[P]  # ties: jnp.argmin takes the first minimum
+        var = (rng.random(P + Q).astype(np.float32) + 0.1) * (0 if trial % 7 == 0 else 1)
+        N = rng.integers(0 if trial % 5 == 0 else 1, 40, P + Q).astype(np.float64)
+        got = pbt.past_update_plan((0x1234 + trial, 0x5678), trial, mean, var, N, P, Q)
+        want = oref.past_update_plan(0x1234 + trial, 0x5678, trial, mean, var, N, P, Q)
+        assert got == want
+        assert 0 <= got[0] < P and P <= got[1] < P + Q
+    assert oref.initial_past_sources(3, 5) == [0, 1, 2, 0, 1]
+
+
+def _past_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from madrona_learn import pbt
+        ps, ts = _fake_member(rank, 10 + rank)
+        ps.episode_score.mean.fill_(5.0 if rank == 1 else -5.0)
+        ps.episode_score.var.fill_(1.0)
+        ps.episode_score.N.fill_(50)
+        tsm = types.SimpleNamespace(policy_list=[ps], train_list=[ts],
+                                    pbt_rng=torch.tensor([3, 4, 0], dtype=torch.int64))
+        cfg = types.SimpleNamespace(pbt=types.SimpleNamespace(num_train_policies=2,
+                                                              num_past_policies=3))
+        pbt.init_past_policies(cfg, tsm)
+        init = [p.params.clone() for p in tsm.past_list]
+        # past slot fitness: slot 1 is the least fit and has data, so a train
+        # policy with many good episodes overwrites it
+        for j, p in enumerate(tsm.past_list):
+            p.episode_score.mean.fill_([0.0, -9.0, 0.0][j])
+            p.episode_score.var.fill_(1.0)
+            p.episode_score.N.fill_(20)
+        pbt.pbt_past_update(cfg, tsm)
+        q.put((rank, init, tsm.last_past_update, [p.params.clone() for p in tsm.past_list],
+               [float(p.episode_score.mean) for p in tsm.past_list], int(tsm.pbt_rng[2])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_past_snapshots_across_ranks_gloo():
+    """World 2, one train policy per rank: the past slots start as copies of
+    train policy j mod P on every rank, and pbt_past_update broadcasts the
+    chosen source's state into the least fit slot on both ranks."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_past_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    members = [_fake_member(r, 10 + r)[0] for r in range(2)]
+    for r in range(2):
+        init, plan, past, means, ctr = res[r]
+        for j in range(3):
+            assert torch.equal(init[j], members[j % 2].params)
+        src, dst, ok = plan
+        mean = np.array([-5.0, 5.0, 0.0, -9.0, 0.0], np.float32)
+        want = oref.past_update_plan(3, 4, 0, mean, np.ones(5, np.float32),
+                                     np.array([50, 50, 20, 20, 20.0]), 2, 3)
+        assert (src, dst, ok) == want and dst == 3
+        if ok:
+            assert torch.equal(past[1], members[src].params)
+            assert means[1] == [-5.0, 5.0][src]
+        assert torch.equal(past[0], members[0].params) and torch.equal(past[2], members[0].params)
+        assert ctr == 1
+    assert res[0][1] == res[1][1]
