@@ -126,12 +126,12 @@ def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
     return fwd, bwd_dx, wgrad
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r03.json")
 
 
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
-    of this round (profiles/pmc_r02.json, tools/pmc_traffic.py): FETCH_SIZE
+    of this round (profiles/pmc_r03.json, tools/pmc_traffic.py): FETCH_SIZE
     doubled (gfx950 reports half the bytes of 16-B streaming reads,
     MI355X_MICROARCH.md HBM) + WRITE_SIZE, with the profiled kernel's name.
     (None, None) when no summary is committed."""

@@ -294,20 +294,33 @@ def copy_policy(tsm, src_pid, dst_pid, P):
 
 def gather_fitness(tsm, P):
     """(mean, var, N) float64 numpy arrays over all P train policies, the same
-    on every rank (one all-reduce; a DP group's root contributes)."""
+    on every rank (one all-reduce).  A policy held by one rank reports its
+    MovingEpisodeScore as is.  Under data parallelism (G = W / P holders,
+    each scoring the episodes of its own env shard) the holders' estimates
+    are pooled — N = sum N_g, mean = sum N_g m_g / N, var = sum N_g (v_g +
+    (m_g - mean)^2) / N — so the fitness covers all of the policy's envs
+    as the reference's does (pbt.py:382-470 over every env of the policy)."""
     rank, W = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
     dev = tsm.policy_list[0].params.device
-    buf = torch.zeros((P, 3), dtype=torch.float64, device=dev)
+    buf = torch.zeros((P, 6), dtype=torch.float64, device=dev)
     for ps, ts in zip(tsm.policy_list, tsm.train_list):
+        e = ps.episode_score
+        m, v, n = e.mean[0].double(), e.var[0].double(), e.N[0].double()
         if _holders(ts.policy_id, P, W)[0] == rank:
-            e = ps.episode_score
-            buf[ts.policy_id, 0] = e.mean[0].double()
-            buf[ts.policy_id, 1] = e.var[0].double()
-            buf[ts.policy_id, 2] = e.N[0].double()
+            buf[ts.policy_id, 0], buf[ts.policy_id, 1], buf[ts.policy_id, 2] = m, v, n
+        buf[ts.policy_id, 3] += n  # pooled sums over every holder
+        buf[ts.policy_id, 4] += n * m
+        buf[ts.policy_id, 5] += n * (v + m * m)
     if W > 1:
         dist.all_reduce(buf)
     h = buf.cpu().numpy()
-    return h[:, 0], h[:, 1], h[:, 2]
+    mean, var, N = h[:, 0].copy(), h[:, 1].copy(), h[:, 2].copy()
+    for pid in range(P):
+        if len(_holders(pid, P, W)) > 1 and h[pid, 3] > 0:
+            N[pid] = h[pid, 3]
+            mean[pid] = h[pid, 4] / N[pid]
+            var[pid] = max(h[pid, 5] / N[pid] - mean[pid] * mean[pid], 0.0)
+    return mean, var, N
 
 
 def cull_plan(cfg, mean, var, N, P, num_cull):

@@ -323,3 +323,43 @@ def test_past_snapshots_across_ranks_gloo():
         assert torch.equal(past[0], members[0].params) and torch.equal(past[2], members[0].params)
         assert ctr == 1
     assert res[0][1] == res[1][1]
+
+
+def _pool_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from madrona_learn import pbt
+        ps, ts = _fake_member(0, 10)  # one policy, held by both ranks (G = 2)
+        ps.episode_score.mean.fill_([1.0, 4.0][rank])
+        ps.episode_score.var.fill_([0.5, 2.0][rank])
+        ps.episode_score.N.fill_([10, 30][rank])
+        tsm = types.SimpleNamespace(policy_list=[ps], train_list=[ts])
+        q.put((rank, pbt.gather_fitness(tsm, 1)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fitness_pooled_over_dp_holders_gloo():
+    """A policy trained by 2 data-parallel ranks: its fitness pools both
+    holders' episode statistics (each scores its own env shard)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pool_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        mean, var, N = res[r]
+        assert N[0] == 40
+        assert abs(mean[0] - (10 * 1.0 + 30 * 4.0) / 40) < 1e-12
+        want_var = (10 * (0.5 + 1.0) + 30 * (2.0 + 16.0)) / 40 - mean[0] ** 2
+        assert abs(var[0] - want_var) < 1e-12

@@ -17,7 +17,8 @@ out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/pmc_summary.json"
 KEYS = {"ppo_step": r"ppo_step_kernel", "wgrad": r"wgrad_kernel", "policy_step": r"policy_step_kernel",
         "gae": r"gae_kernel", "reduce_grads": r"reduce_grads_kernel", "env_step": r"env_step_kernel",
         "adam": r"adam_kernel", "project": r"project_kernel", "sumsq": r"sumsq_partial_kernel",
-        "optim": r"optim_fused_kernel"}
+        "optim": r"optim_fused_kernel", "lstm_fwd_step": r"lstm_fwd_step", "lstm_bwd_step": r"lstm_bwd_step",
+        "lstm_gin": r"lstm_gin_kernel", "lstm_dfeat": r"lstm_dfeat_kernel"}
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 names = {}
 for f in sorted(glob.glob(f"{root}/p*/*counter_collection.csv")):
