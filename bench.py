@@ -399,7 +399,9 @@ def main():
                        # the built-in synthetic sim's step: inside the rollout policy
                        # launch (mlearn_policy_rollout_step_env) or its own launch
                        "sim_step": "separate_launch" if args.separate_sim
-                       else "fused_into_policy_launch"},
+                       else ("fused_into_policy_launch"
+                             if os.environ.get("MLEARN_WHOLE_ROLLOUT", "1") == "0"
+                             else "whole_rollout_one_launch")},
             # how the data-parallel collectives ran (a SCALE record can be checked
             # against this): "rccl_in_graph" = C ABI RCCL communicator on the
             # compute stream inside the HIP graph; "torch_distributed" = host

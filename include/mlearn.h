@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 10
+#define MLEARN_ABI_VERSION 11
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -571,6 +571,35 @@ int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float*
                                    const uint64_t* step_ctr, uint64_t step, uint32_t env_offset,
                                    int32_t sample, const mlearn_post_step* post,
                                    const mlearn_dummy_env* env, mlearn_stream_t stream);
+/* The whole rollout of the synthetic sim in ONE launch: for t = 0 .. T-1 the
+ * rollout step of mlearn_policy_rollout_step_env (post-step of t-1, policy,
+ * sample, store row t, env step), then the bootstrap critic at t = T with the
+ * post-step of T-1 (and, for a recurrent policy, the carry cleared where
+ * that step ended an episode), each workgroup running every step of its own
+ * 32 envs back to back.  Store pointers are [T][ld][...] views of this
+ * policy's env columns; bit-identical to T + 1 per-step launches. */
+typedef struct mlearn_rollout_out {
+    void* obs;                  /* [T][ld][obs_dim] compute dtype, or NULL */
+    int32_t* actions;           /* [T][ld][K] */
+    float* log_probs;           /* [T][ld][K] */
+    float* values;              /* [T][ld] */
+    float* rewards;             /* [T][ld] store rewards */
+    uint8_t* dones;             /* [T][ld] store dones */
+    float* env_returns_trace;   /* [T][ld] or NULL */
+    float* bootstrap;           /* [N] critic at t = T */
+    float* env_returns;         /* [N] running discounted return (in/out) */
+    void* start_h;              /* [C][ld][H] rnn_start_states (recurrent policies) */
+    void* start_c;
+    int32_t T, bptt_len;
+    int64_t ld;
+    float gamma;
+    int32_t pad;
+} mlearn_rollout_out;
+int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                              const mlearn_lstm_carry* carry, const float* obs, int64_t N,
+                              const mlearn_rollout_out* out, uint32_t k0, uint32_t k1,
+                              const uint64_t* step_ctr, uint32_t env_offset,
+                              const mlearn_dummy_env* env, mlearn_stream_t stream);
 int mlearn_lstm_policy_rollout_step_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                                         const mlearn_lstm_carry* carry, const float* obs,
                                         int64_t N, void* obs_store, int32_t* actions,

@@ -105,13 +105,26 @@ __device__ inline void post_step_row(const PostK& p, int64_t n) {
 // heads split the reduction instead: each wave multiplies its own features,
 // partials are summed in wave order.
 #ifndef ML_POL_MAXW
-#define ML_POL_MAXW 4  // waves per workgroup of the rollout policy kernel (feature split)
+#define ML_POL_MAXW 4  // waves per workgroup, feed-forward policy (feature split; 8 measured 54.3 vs 42.4 us)
 #endif
-template <int H> struct PolCfg {
+#ifndef ML_POL_RNN_MAXW
+#define ML_POL_RNN_MAXW 8  // waves per workgroup, recurrent policy (4: 284 VGPRs, one wave per SIMD)
+#endif
+#ifndef ML_ROLL_MLP_WAVES
+#define ML_ROLL_MLP_WAVES 3  // whole-rollout kernel, feed-forward: 3 waves per SIMD (3 workgroups per CU)
+#endif
+#ifndef ML_ROLL_RNN_WAVES
+#define ML_ROLL_RNN_WAVES 3  // whole-rollout kernel, recurrent: 3 waves per SIMD (no spill; 4: 11.71 vs 11.65 ms)
+#endif
+template <int H, int MAXW = ML_POL_MAXW> struct PolCfg {
     static constexpr int NB = H / 32;
-    static constexpr int W = NB < ML_POL_MAXW ? NB : ML_POL_MAXW;
+    static constexpr int W = NB < MAXW ? NB : MAXW;
     static constexpr int NBW = NB / W;
 };
+// The feature split of a policy kernel (the per-step and the whole-rollout
+// kernels use the same one, so they compute the same bits).
+template <bool RNN> constexpr int pol_maxw() { return RNN ? ML_POL_RNN_MAXW : ML_POL_MAXW; }
+template <int H, bool RNN> constexpr int pol_threads() { return 64 * PolCfg<H, pol_maxw<RNN>()>::W; }
 
 // Carry of a recurrent policy (mlearn_lstm_carry).
 struct CarryK {
@@ -137,7 +150,7 @@ static uint64_t* g_pol_stamp_buf = nullptr;
     do {                                                                               \
         __builtin_amdgcn_sched_barrier(0);                                             \
         if (ev.stamps && actions && lane == 0)                                         \
-            ev.stamps[((int64_t)blockIdx.x * W + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+            ev.stamps[((int64_t)tile * W + w) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
         __builtin_amdgcn_sched_barrier(0);                                             \
     } while (0)
 #else
@@ -153,26 +166,31 @@ static uint64_t* g_pol_stamp_buf = nullptr;
 // hidden units (8 accumulator blocks, weight images in unit-block gate
 // order), so the cell update is register-local and h' lands in exactly the
 // layout the heads consume.
-template <typename T, int H, bool RNN, int HC>
+template <typename T, int H, bool RNN, int HC, int MAXW>
 #ifndef ML_POL_WAVES
 #define ML_POL_WAVES 1  // waves per SIMD the recurrent rollout policy kernel is register-budgeted for (1: compiler choice)
 #endif
 #ifndef ML_POL_MLP_WAVES
 #define ML_POL_MLP_WAVES 3  // the feed-forward kernel: 3 waves per SIMD (<= 168 VGPRs, 3 workgroups per CU)
 #endif
-__global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_eu(RNN ? ML_POL_WAVES : ML_POL_MLP_WAVES, 8))) void policy_step_kernel(
-    PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
+__device__ __forceinline__ void policy_step_body(
+    const PolicyK& P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
     float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev,
-    EnvK env) {
+    uint64_t step_add, uint32_t eoff, int sample, const PostK& post, const LstmK& R,
+    const CarryK& cy, const EvalK& ev, const EnvK& env, int tile) {
     typedef typename RT<T>::frag frag;
-    typedef PolCfg<H> C;
+    typedef PolCfg<H, MAXW> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
     constexpr int E = RT<T>::E, KS = RT<T>::KS, SPB = RT<T>::SPB, KSH = H / KS;
     constexpr int KSD = 256 / KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int D = P.D, L = P.L;
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    // (opaque copy of the lane index: in the rollout kernel's step loop the
+    // body's lane-derived addresses are then recomputed per step instead of
+    // hoisted out of the loop and held live across it)
+    int tid_o = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid_o));
+    const int tid = tid_o, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the buffer descriptors
     frag* fr = (frag*)smem;                               // [KSH][64] B fragments
     float* gb = (float*)(fr + KSH * 64);                  // [L][2][H]
@@ -204,7 +222,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
         for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
     if (P.CB > 1)
         for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
-    const int64_t row0 = (int64_t)blockIdx.x * 32;
+    const int64_t row0 = (int64_t)tile * 32;
     const int64_t row = row0 + r;
     const bool live = row < N;
     if (post.rew && tid < 32 && row0 + tid < N) post_step_row(post, row0 + tid);
@@ -500,7 +518,7 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
     // feature (rows q, q + 4, ...), two passes
     if (P.obs_stats && actions && step_add < (uint64_t)P.obs_steps) {
         const int nrow = (int)(N - row0 < 32 ? N - row0 : 32);
-        float* out = P.obs_stats + ((int64_t)step_add * P.obs_tiles + blockIdx.x) * D * 2;
+        float* out = P.obs_stats + ((int64_t)step_add * P.obs_tiles + tile) * D * 2;
         for (int f0 = 0; f0 < D; f0 += THREADS / 4) {
             const int f = f0 + tid / 4, q = tid % 4;
             const float* col = obs + row0 * D + (f < D ? f : 0);
@@ -555,8 +573,77 @@ __global__ __launch_bounds__(64 * PolCfg<H>::W) __attribute__((amdgpu_waves_per_
     PSTAMP(9);
 }
 
-template <typename T, int H, bool RNN, int HC> static size_t policy_step_lds(int L) {
-    typedef PolCfg<H> C;
+template <typename T, int H, bool RNN, int HC>
+__global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_waves_per_eu(RNN ? ML_POL_WAVES : ML_POL_MLP_WAVES, 8))) void policy_step_kernel(
+    PolicyK P, const float* __restrict__ obs, int64_t N, T* obs_store, int32_t* actions,
+    float* logp, float* values, uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
+    uint64_t step_add, uint32_t eoff, int sample, PostK post, LstmK R, CarryK cy, EvalK ev,
+    EnvK env) {
+    policy_step_body<T, H, RNN, HC, pol_maxw<RNN>()>(P, obs, N, obs_store, actions, logp, values, k0, k1,
+                                                 step_ctr, step_add, eoff, sample, post, R, cy, ev,
+                                                 env, blockIdx.x);
+}
+
+// Whole rollout of the built-in synthetic sim in one launch
+// (mlearn_policy_rollout_env): the sim step depends only on its own env, so a
+// workgroup runs all T steps of its 32 envs back to back — policy step t
+// (with the post-step of t - 1 and the fused env step), then the bootstrap
+// critic at t = T — and takes its next env tile after that.  Identical
+// per-step arithmetic and counters to T + 1 launches of policy_step_kernel.
+struct RollK {
+    void* obs;           // [T][ld][D] store rows (compute dtype) or null
+    int32_t* actions;    // [T][ld][K]
+    float* logp;         // [T][ld][K]
+    float* values;       // [T][ld]
+    float* rewards;      // [T][ld] store rewards
+    uint8_t* dones;      // [T][ld] store dones
+    float* trace;        // [T][ld] env-return trace or null
+    float* bootstrap;    // [N]
+    float* env_returns;  // [N]
+    void* start_h;       // [C][ld][H] rnn start states (recurrent)
+    void* start_c;
+    int T, bptt;
+    int64_t ld;
+    float gamma;
+};
+
+template <typename T, int H, bool RNN, int HC>
+__global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_waves_per_eu(RNN ? ML_ROLL_RNN_WAVES : ML_ROLL_MLP_WAVES, 8))) void policy_rollout_kernel(
+    PolicyK P, const float* __restrict__ obs, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
+    const uint64_t* step_ctr, uint32_t eoff, LstmK R, CarryK cy0, EnvK env) {
+    const int ntiles = (int)((N + 31) / 32);
+    for (int tile = blockIdx.x; tile < ntiles; tile += (int)gridDim.x) {
+#pragma clang loop unroll(disable)
+        for (int t = 0; t <= rk.T; ++t) {
+            // the previous step's LDS reads (and its env outputs, read by this
+            // step's post-step and first product) are ordered by the barrier
+            if (t > 0 || tile != (int)blockIdx.x) __syncthreads();
+            const bool act = t < rk.T;
+            const int64_t so = (int64_t)t * rk.ld;
+            PostK post{};
+            if (t > 0)
+                post = PostK{env.rew, env.done, rk.rewards + so - rk.ld, rk.dones + so - rk.ld,
+                             rk.env_returns, rk.trace ? rk.trace + so - rk.ld : nullptr, rk.gamma};
+            CarryK cy = cy0;
+            if constexpr (RNN) {
+                const bool cs = act && t % rk.bptt == 0;
+                const int64_t co = (int64_t)(t / rk.bptt) * rk.ld * H;
+                cy.sh = cs ? (void*)((T*)rk.start_h + co) : nullptr;
+                cy.sc = cs ? (void*)((T*)rk.start_c + co) : nullptr;
+                cy.commit = act ? 1 : 0;
+            }
+            policy_step_body<T, H, RNN, HC, pol_maxw<RNN>()>(
+                P, obs, N, (act && rk.obs) ? (T*)rk.obs + so * P.D : nullptr,
+                act ? rk.actions + so * P.K : nullptr, act ? rk.logp + so * P.K : nullptr,
+                act ? rk.values + so : rk.bootstrap, k0, k1, step_ctr, (uint64_t)t, eoff, 1, post,
+                R, cy, EvalK{}, act ? env : EnvK{}, tile);
+        }
+    }
+}
+
+template <typename T, int H, bool RNN, int HC, int MAXW = ML_POL_MAXW>
+static size_t policy_step_lds(int L) {
+    typedef PolCfg<H, MAXW> C;
     const size_t frags = (size_t)(H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
     return frags * (RNN ? 2 : 1) +
            (size_t)(L * 2 * H + HC + C::W * 64 + (head_parts<HC, C::W>() + 1) * 32 * (HC + 1) +
@@ -569,7 +656,7 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
                               const uint64_t* step_ctr, uint64_t step, uint32_t eoff, int sample,
                               const PostK& post, const LstmK& R, const CarryK& cy, const EvalK& ev,
                               const EnvK& env, hipStream_t s) {
-    const size_t lds = policy_step_lds<T, H, RNN, HC>(P.L);
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(P.L);
     auto kern = policy_step_kernel<T, H, RNN, HC>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
     if (!attr_set) {
@@ -584,10 +671,76 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
 #else
     const EvalK& evs = ev;
 #endif
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PolCfg<H>::W), lds, s, P, obs, N,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(pol_threads<H, RNN>()), lds, s, P, obs, N,
                        (T*)obs_store, actions, logp, values, k0, k1, step_ctr, step, eoff, sample,
                        post, R, cy, evs, env);
     return check_launch("policy_rollout_step");
+}
+
+static bool getenv_is(const char* name, char c) {
+    const char* e = getenv(name);
+    return e && e[0] == c;
+}
+
+// The whole rollout as one launch when every env tile gets a resident
+// workgroup (MLEARN_ROLLOUT_PER_STEP=1 forces the per-step launches).
+template <typename T, int H, bool RNN, int HC>
+static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
+                                 uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
+                                 const LstmK& R, const CarryK& cy, const EnvK& env, hipStream_t s) {
+    constexpr int NT = pol_threads<H, RNN>();
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(P.L);
+    auto kern = policy_rollout_kernel<T, H, RNN, HC>;
+    static bool attr_set = false;
+    static int per_cu = 0, cus = 0;
+    if (!attr_set) {  // once per instantiation (kept out of graph capture)
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NT, lds) !=
+                hipSuccess)
+            per_cu = cus = 0;
+        attr_set = true;
+    }
+    const int64_t tiles = (N + 31) / 32;
+    const int64_t slots = (int64_t)per_cu * cus;
+    if (slots > 0 && tiles <= slots && !getenv_is("MLEARN_ROLLOUT_PER_STEP", '1')) {
+        // every env tile has a resident workgroup: the T + 1 steps run back to
+        // back inside each workgroup, no launch boundary between them
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(NT), lds, s, P, obs, N, rk, k0, k1,
+                           step_ctr, eoff, R, cy, env);
+        return check_launch("policy_rollout_env");
+    }
+    // more env tiles than resident workgroups: a workgroup would run several
+    // tiles' whole rollouts in series, and the last round's quantisation costs
+    // what the launch boundaries save (measured: 1.93 vs 1.65 ms at 2 048
+    // tiles on 768 slots), so the steps go out as T + 1 launches of the
+    // per-step kernel (same body, same bits)
+    for (int t = 0; t <= rk.T; ++t) {
+        const bool act = t < rk.T;
+        const int64_t so = (int64_t)t * rk.ld;
+        PostK post{};
+        if (t > 0)
+            post = PostK{env.rew, env.done, rk.rewards + so - rk.ld, rk.dones + so - rk.ld,
+                         rk.env_returns, rk.trace ? rk.trace + so - rk.ld : nullptr, rk.gamma};
+        CarryK c = cy;
+        if (RNN) {
+            const bool cs = act && t % rk.bptt == 0;
+            const int64_t co = (int64_t)(t / rk.bptt) * rk.ld * H;
+            c.sh = cs ? (void*)((T*)rk.start_h + co) : nullptr;
+            c.sc = cs ? (void*)((T*)rk.start_c + co) : nullptr;
+            c.commit = act ? 1 : 0;
+        }
+        const int rc = launch_policy_step<T, H, RNN, HC>(
+            P, obs, N, (act && rk.obs) ? (T*)rk.obs + so * P.D : nullptr,
+            act ? rk.actions + so * P.K : nullptr, act ? rk.logp + so * P.K : nullptr,
+            act ? rk.values + so : rk.bootstrap, k0, k1, step_ctr, (uint64_t)t, eoff, 1, post, R, c,
+            EvalK{}, act ? env : EnvK{}, s);
+        if (rc) return rc;
+    }
+    return MLEARN_OK;
 }
 
 static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
@@ -683,6 +836,68 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
                                           const mlearn_post_step* post, mlearn_stream_t stream) {
     return rollout_step_entry(policy, nullptr, nullptr, obs, N, obs_store, actions, log_probs,
                               values, k0, k1, step_ctr, step, env_offset, sample, post, stream);
+}
+
+extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                         const mlearn_lstm_carry* carry, const float* obs,
+                                         int64_t N, const mlearn_rollout_out* out, uint32_t k0,
+                                         uint32_t k1, const uint64_t* step_ctr,
+                                         uint32_t env_offset, const mlearn_dummy_env* denv,
+                                         mlearn_stream_t stream) {
+    int rc = lstm ? validate_lstm(policy, lstm) : validate_policy(policy);
+    if (rc) return rc;
+    ML_REQUIRE(N >= 0, "policy_rollout_env: N < 0");
+    if (N == 0) return MLEARN_OK;
+    ML_REQUIRE(obs && out && denv, "policy_rollout_env: null obs / out / env");
+    ML_REQUIRE(out->T >= 1 && out->bptt_len >= 1 && out->T % out->bptt_len == 0 && out->ld >= N,
+               "policy_rollout_env: bad T / bptt / ld");
+    ML_REQUIRE(out->actions && out->log_probs && out->values && out->rewards && out->dones &&
+                   out->bootstrap && out->env_returns,
+               "policy_rollout_env: null store pointer");
+    ML_REQUIRE(denv->state && denv->obs == obs && denv->rewards && denv->dones,
+               "policy_rollout_env: env->obs must be the obs input; null env pointer");
+    ML_REQUIRE((uintptr_t)obs % 16 == 0 && (uintptr_t)denv->state % 16 == 0 &&
+                   (!out->obs || (uintptr_t)out->obs % 16 == 0),
+               "policy_rollout_env: obs / state / store alignment");
+    ML_REQUIRE(!policy->obs_stats || policy->obs_stats_tiles >= (N + 31) / 32,
+               "policy_rollout_env: obs_stats_tiles %lld < ceil(N / 32)",
+               (long long)policy->obs_stats_tiles);
+    LstmK R{};
+    CarryK cy{};
+    if (lstm) {
+        ML_REQUIRE(carry && carry->h && carry->c && out->start_h && out->start_c,
+                   "lstm rollout: null carry / start states");
+        R = make_lstm_k(*lstm);
+        cy = CarryK{carry->h, carry->c, nullptr, nullptr, 1, nullptr};
+    }
+    RollK rk{out->obs, out->actions, out->log_probs, out->values, out->rewards, out->dones,
+             out->env_returns_trace, out->bootstrap, out->env_returns, out->start_h, out->start_c,
+             out->T, out->bptt_len, out->ld, out->gamma};
+    EnvK ek{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
+            denv->env_offset};
+    PolicyK P = make_policy_k(*policy);
+    hipStream_t s = S(stream);
+#define ML_LAUNCH_HC(T, HH, HC)                                                                 \
+    (lstm ? launch_policy_rollout<T, HH, true, HC>(P, obs, N, rk, k0, k1, step_ctr, env_offset, R, \
+                                                   cy, ek, s)                                     \
+          : launch_policy_rollout<T, HH, false, HC>(P, obs, N, rk, k0, k1, step_ctr, env_offset, R, \
+                                                    cy, ek, s))
+#define ML_LAUNCH(T, HH) \
+    (P.HC == MLEARN_HEAD_COLS ? ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS) : ML_LAUNCH_HC(T, HH, MLEARN_HEAD_COLS_MAX))
+#define ML_DISPATCH(T)                      \
+    switch (policy->hidden) {               \
+        case 64: return ML_LAUNCH(T, 64);   \
+        case 128: return ML_LAUNCH(T, 128); \
+        default: return ML_LAUNCH(T, 256);  \
+    }
+    if (policy->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
+#undef ML_LAUNCH
+#undef ML_LAUNCH_HC
 }
 
 extern "C" int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float* obs,

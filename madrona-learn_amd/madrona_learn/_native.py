@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -95,6 +95,15 @@ class DummyEnv(Structure):  # mlearn_dummy_env
                 ("env_offset", c_uint32), ("pad", c_uint32)]
 
 
+class RolloutOut(Structure):  # mlearn_rollout_out
+    _fields_ = [("obs", c_void_p), ("actions", c_void_p), ("log_probs", c_void_p),
+                ("values", c_void_p), ("rewards", c_void_p), ("dones", c_void_p),
+                ("env_returns_trace", c_void_p), ("bootstrap", c_void_p),
+                ("env_returns", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
+                ("T", c_int32), ("bptt_len", c_int32), ("ld", c_int64), ("gamma", c_float),
+                ("pad", c_int32)]
+
+
 _S = c_void_p  # hipStream_t
 _P = c_void_p
 
@@ -136,6 +145,10 @@ _SIGNATURES = {
                                                       _P, c_uint32, c_uint32, _P, c_uint64,
                                                       c_uint32, c_int32, POINTER(PostStep),
                                                       POINTER(DummyEnv), _S]),
+    "mlearn_policy_rollout_env": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
+                                            _P, c_int64,
+                                            POINTER(RolloutOut), c_uint32, c_uint32, _P,
+                                            c_uint32, POINTER(DummyEnv), _S]),
     "mlearn_policy_evaluate": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P, _S]),
     "mlearn_lstm_policy_evaluate": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                               _P, c_int64, _P, _P, _P, _P, _S]),

@@ -68,6 +68,14 @@ class RolloutConfig:  # rollouts.py:28-134 (self-play / single-policy path)
         )
 
 
+def _whole_rollout():
+    """The built-in sim's rollout as one launch per policy
+    (mlearn_policy_rollout_env); MLEARN_WHOLE_ROLLOUT=0 keeps one launch per
+    step with the sim step fused into it (mlearn_policy_rollout_step_env)."""
+    import os
+    return os.environ.get("MLEARN_WHOLE_ROLLOUT", "1") != "0"
+
+
 class RolloutState:  # rollouts.py:171-309
     def __init__(self, cfg, step_fn, sim_state, cur_obs, prng_key, rnn_states, sim_ctrl,
                  env_returns, counters, policy_assignments, native_step=None):
@@ -393,6 +401,18 @@ class RolloutManager:  # rollouts.py:373-826
         B = self.B
         posts = [None] * self.P  # post-step of env step t-1, fused into the policy launches of t
         sim = rollout_state.native_step
+        obs0 = self.prep_obs(rollout_state.cur_obs)
+        if sim is not None and obs0.data_ptr() == sim.obs.data_ptr() and _whole_rollout():
+            # the built-in sim: every step + the bootstrap in one launch per policy
+            for p, ps in enumerate(self.policies):
+                c = slice(p * B, (p + 1) * B)
+                ps.rollout_all(obs0[c], self._rollout_out(rollout_state, p, gamma), key, step_ctr,
+                               self.env_offset + p * B, self._env_desc(sim, p),
+                               carry=self._carry(rollout_state, p, 0) if self.R else None)
+            out = sim.native_outputs()
+            rollout_state.sim_state = out["state"]
+            rollout_state.cur_obs = out["obs"]
+            return self._finish(train_state_mgr, rollout_state, metrics, user_hooks)
         for t in range(self.T):
             obs = self.prep_obs(rollout_state.cur_obs)
             # the built-in sim steps inside the policy launches when they read
@@ -441,6 +461,39 @@ class RolloutManager:  # rollouts.py:373-826
             c = slice(p * B, (p + 1) * B)
             ps.critic_only(obs[c], s.bootstrap[c], post=posts[p],
                            carry=self._carry(rollout_state, p, self.T) if self.R else None)
+        return self._finish(train_state_mgr, rollout_state, metrics, user_hooks)
+
+    def _rollout_out(self, rollout_state, p, gamma):
+        """nat.RolloutOut of policy p's store columns (cached)."""
+        if not hasattr(self, "_routs"):
+            self._routs = {}
+        s = self.store
+        key = (p, rollout_state.env_returns.data_ptr())
+        o = self._routs.get(key)
+        if o is None:
+            c0 = p * self.B
+            o = nat.RolloutOut()
+            o.obs = s.obs.data_ptr() + c0 * s.obs.shape[2] * s.obs.element_size()
+            o.actions = s.actions.data_ptr() + c0 * s.actions.shape[2] * 4
+            o.log_probs = s.log_probs.data_ptr() + c0 * s.log_probs.shape[2] * 4
+            o.values = s.values.data_ptr() + c0 * 4
+            o.rewards = s.rewards.data_ptr() + c0 * 4
+            o.dones = s.dones.data_ptr() + c0
+            o.env_returns_trace = s.env_returns_trace.data_ptr() + c0 * 4
+            o.bootstrap = s.bootstrap.data_ptr() + c0 * 4
+            o.env_returns = rollout_state.env_returns.data_ptr() + c0 * 4
+            if self.R:
+                es = s.start_h.element_size()
+                o.start_h = s.start_h.data_ptr() + c0 * self.R * es
+                o.start_c = s.start_c.data_ptr() + c0 * self.R * es
+            o.T, o.bptt_len, o.ld, o.gamma = self.T, self.bptt, self.N, gamma
+            self._routs[key] = o
+        return o
+
+    def _finish(self, train_state_mgr, rollout_state, metrics, user_hooks):
+        s = self.store
+        L = nat.lib()
+        strm = nat.stream_handle()
         # obs statistics -> normaliser estimates for the next rollout
         # (update_state, train.py:193-204; the update trains on the stored,
         # already normalised observations)

@@ -13,6 +13,7 @@ from dataclasses import dataclass, field
 from typing import Any, Optional
 
 import numpy as np
+
 import torch
 
 from . import _native as nat
@@ -314,6 +315,20 @@ class PolicyState:
         else:
             nat.check(L.mlearn_policy_rollout_step_env(*args, env, nat.stream_handle()),
                       "policy_rollout_step_env")
+
+    def rollout_all(self, obs, out, key, step_ctr, env_offset, env, carry=None):
+        """The whole rollout of the built-in synthetic sim in one launch
+        (mlearn_policy_rollout_env): T rollout steps with the fused env step
+        and post-steps, then the bootstrap critic; `out` is the
+        nat.RolloutOut of this policy's store columns, `carry` the
+        nat.LstmCarry (h, c) of a recurrent policy."""
+        if self.lstm_desc is not None:
+            self._check_carry(carry)
+        N = obs.shape[0]
+        nat.check(nat.lib().mlearn_policy_rollout_env(
+            self.desc, self.lstm_desc, carry if self.lstm_desc is not None else None,
+            nat.ptr(obs, torch.float32, name="obs"), N, out, key[0], key[1], nat.ptr(step_ctr),
+            env_offset, env, nat.stream_handle()), "policy_rollout_env")
 
     def _check_carry(self, carry):
         if not isinstance(carry, nat.LstmCarry) or not carry.h or not carry.c:

@@ -1,7 +1,8 @@
 """The built-in synthetic sim's step fused into the rollout policy launch
 (mlearn_policy_rollout_step_env, envs.DummyVecEnv.native_step) is
 bit-identical to calling the sim's own step between the launches
-(mlearn_dummy_env_step): same store, env state, observations, rewards,
+(mlearn_dummy_env_step), and so is the whole rollout as one launch
+(mlearn_policy_rollout_env): same store, env state, observations, rewards,
 dones and parameters after whole update iterations, eager and graph-captured,
 for MLP / population / LSTM policies, including a partial last workgroup of
 envs.  The oracle parity of the fused path itself is tests/test_gpu_train.py
@@ -43,12 +44,20 @@ def _manager(gpu, fused, dtype, N, H, mb, P=1, lstm=False, use_graph=False):
     return env, ml.init_training(gpu, cfg, fns, pol, use_graph=use_graph)
 
 
+@pytest.mark.parametrize("mode", ["one_launch", "c_per_step", "py_per_step"])
 @pytest.mark.parametrize("dtype,N,H,mb,P,lstm,graph", [
     (torch.float32, 80, 64, 16, 1, False, False),    # partial last workgroup (80 = 2.5 x 32)
     (torch.bfloat16, 1024, 256, 256, 1, False, True),
     (torch.float32, 128, 64, 16, 2, False, True),     # population: one launch per policy
+    (torch.bfloat16, 128, 256, 32, 1, True, False),   # LSTM H = 256: carry, start states, clears
     (torch.float32, 64, 64, 32, 1, True, False)])     # LSTM carry + done clears
-def test_fused_env_step_is_bit_identical(gpu, dtype, N, H, mb, P, lstm, graph):
+def test_fused_env_step_is_bit_identical(gpu, monkeypatch, mode, dtype, N, H, mb, P, lstm, graph):
+    """one_launch: the whole rollout + bootstrap in one launch per policy
+    (mlearn_policy_rollout_env); c_per_step: the same entry's per-step
+    launches (taken when the env tiles outnumber the resident workgroups);
+    py_per_step: one rollout_step_env call per step from the host."""
+    monkeypatch.setenv("MLEARN_WHOLE_ROLLOUT", "0" if mode == "py_per_step" else "1")
+    monkeypatch.setenv("MLEARN_ROLLOUT_PER_STEP", "1" if mode == "c_per_step" else "0")
     env_a, a = _manager(gpu, True, dtype, N, H, mb, P, lstm, graph)
     env_b, b = _manager(gpu, False, dtype, N, H, mb, P, lstm, graph)
     for _ in range(2):
