@@ -166,7 +166,7 @@ static uint64_t* g_pol_stamp_buf = nullptr;
 // hidden units (8 accumulator blocks, weight images in unit-block gate
 // order), so the cell update is register-local and h' lands in exactly the
 // layout the heads consume.
-template <typename T, int H, bool RNN, int HC, int MAXW>
+template <typename T, int H, bool RNN, int HC, int MAXW, bool STAGED = false>
 #ifndef ML_POL_WAVES
 #define ML_POL_WAVES 1  // waves per SIMD the recurrent rollout policy kernel is register-budgeted for (1: compiler choice)
 #endif
@@ -204,24 +204,27 @@ __device__ __forceinline__ void policy_step_body(
     frag* frh = (frag*)(bins + HC);                       // [KSH][64] carry fragments (RNN)
     // LayerNorm / head-bias parameters: loads issued now, written to LDS after
     // the first product (their latency hides under the observation loads)
-    constexpr int NPAR = (MLEARN_MAX_LAYERS * 2 * H + HC + THREADS - 1) / THREADS;
+    // (STAGED: the whole-rollout kernel staged them once, before its step loop)
+    constexpr int NPAR = STAGED ? 1 : (MLEARN_MAX_LAYERS * 2 * H + HC + THREADS - 1) / THREADS;
     float parv[NPAR];
+    if constexpr (!STAGED) {
 #pragma unroll
-    for (int k = 0; k < NPAR; ++k) {
-        const int i = tid + k * THREADS;
-        float v = 0.f;
-        if (i < L * 2 * H) {
-            const int l = i / (2 * H), c = i - l * 2 * H;
-            v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
-        } else if (i < L * 2 * H + HC) {
-            v = P.head_b[i - L * 2 * H];
+        for (int k = 0; k < NPAR; ++k) {
+            const int i = tid + k * THREADS;
+            float v = 0.f;
+            if (i < L * 2 * H) {
+                const int l = i / (2 * H), c = i - l * 2 * H;
+                v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
+            } else if (i < L * 2 * H + HC) {
+                v = P.head_b[i - L * 2 * H];
+            }
+            parv[k] = v;
         }
-        parv[k] = v;
+        if constexpr (RNN)
+            for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
+        if (P.CB > 1)
+            for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
     }
-    if constexpr (RNN)
-        for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
-    if (P.CB > 1)
-        for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
     const int64_t row0 = (int64_t)tile * 32;
     const int64_t row = row0 + r;
     const bool live = row < N;
@@ -252,9 +255,11 @@ __device__ __forceinline__ void policy_step_body(
                        (w == 0 && obs_store && live) ? obs_store + row * D : nullptr, lane,
                        P.obs_mu, P.obs_inv);
     PSTAMP(1);
+    if constexpr (!STAGED) {
 #pragma unroll
-    for (int k = 0; k < NPAR; ++k)
-        if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
+        for (int k = 0; k < NPAR; ++k)
+            if (tid + k * THREADS < L * 2 * H + HC) gb[tid + k * THREADS] = parv[k];
+    }
     // LayerNorm parameters staged: the first LayerNorm's statistics barrier
     // orders them (and the LSTM bias / critic bins) before their first read
     typedef typename Pk<T>::word word;
@@ -612,6 +617,34 @@ __global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_wave
     PolicyK P, const float* __restrict__ obs, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
     const uint64_t* step_ctr, uint32_t eoff, LstmK R, CarryK cy0, EnvK env) {
     const int ntiles = (int)((N + 31) / 32);
+    {
+        // LayerNorm / head-bias parameters, LSTM bias, critic bins: staged
+        // once for every step (the body's first statistics barrier orders them)
+        constexpr int THREADS = pol_threads<H, RNN>();
+        constexpr int KSH = H / RT<T>::KS;
+        constexpr int LGS = HC + 1;
+        constexpr int W = THREADS / 64;
+        extern __shared__ __attribute__((aligned(16))) char smem[];
+        float* gb = (float*)((typename RT<T>::frag*)smem + KSH * 64);
+        float* hbias = gb + P.L * 2 * H;
+        float* rbias = hbias + HC + W * 64 + head_parts<HC, W>() * 32 * LGS + 32 * LGS;
+        float* bins = rbias + (RNN ? 4 * H : 0);
+        const int tid = threadIdx.x;
+        for (int i = tid; i < P.L * 2 * H + HC; i += THREADS) {
+            float v;
+            if (i < P.L * 2 * H) {
+                const int l = i / (2 * H), c = i - l * 2 * H;
+                v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
+            } else {
+                v = P.head_b[i - P.L * 2 * H];
+            }
+            gb[i] = v;
+        }
+        if constexpr (RNN)
+            for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
+        if (P.CB > 1)
+            for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
+    }
     for (int tile = blockIdx.x; tile < ntiles; tile += (int)gridDim.x) {
 #pragma clang loop unroll(disable)
         for (int t = 0; t <= rk.T; ++t) {
@@ -632,7 +665,7 @@ __global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_wave
                 cy.sc = cs ? (void*)((T*)rk.start_c + co) : nullptr;
                 cy.commit = act ? 1 : 0;
             }
-            policy_step_body<T, H, RNN, HC, pol_maxw<RNN>()>(
+            policy_step_body<T, H, RNN, HC, pol_maxw<RNN>(), true>(
                 P, obs, N, (act && rk.obs) ? (T*)rk.obs + so * P.D : nullptr,
                 act ? rk.actions + so * P.K : nullptr, act ? rk.logp + so * P.K : nullptr,
                 act ? rk.values + so : rk.bootstrap, k0, k1, step_ctr, (uint64_t)t, eoff, 1, post,
@@ -706,18 +739,21 @@ static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, 
     }
     const int64_t tiles = (N + 31) / 32;
     const int64_t slots = (int64_t)per_cu * cus;
-    if (slots > 0 && tiles <= slots && !getenv_is("MLEARN_ROLLOUT_PER_STEP", '1')) {
-        // every env tile has a resident workgroup: the T + 1 steps run back to
-        // back inside each workgroup, no launch boundary between them
-        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(NT), lds, s, P, obs, N, rk, k0, k1,
+    if (slots > 0 && !getenv_is("MLEARN_ROLLOUT_PER_STEP", '1')) {
+        // the T + 1 steps back to back inside each workgroup, no launch
+        // boundary between them; with more env tiles than resident
+        // workgroups, ceil(tiles / slots) tiles per workgroup in series
+        // (headline: 2 048 tiles, 768 slots, 3 per workgroup; 1.648 ms vs
+        // 33 per-step launches ~1.65-1.70 ms, +1 % on the update; the W = 8
+        // share: one tile per workgroup, 3.91 vs 3.99 ms)
+        const int64_t per = (tiles + slots - 1) / slots;
+        const int64_t grid = (tiles + per - 1) / per;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, s, P, obs, N, rk, k0, k1,
                            step_ctr, eoff, R, cy, env);
         return check_launch("policy_rollout_env");
     }
-    // more env tiles than resident workgroups: a workgroup would run several
-    // tiles' whole rollouts in series, and the last round's quantisation costs
-    // what the launch boundaries save (measured: 1.93 vs 1.65 ms at 2 048
-    // tiles on 768 slots), so the steps go out as T + 1 launches of the
-    // per-step kernel (same body, same bits)
+    // MLEARN_ROLLOUT_PER_STEP=1 (or no occupancy answer): the same body as
+    // T + 1 launches of the per-step kernel (same bits)
     for (int t = 0; t <= rk.T; ++t) {
         const bool act = t < rk.T;
         const int64_t so = (int64_t)t * rk.ld;

@@ -54,7 +54,7 @@ def _manager(gpu, fused, dtype, N, H, mb, P=1, lstm=False, use_graph=False):
 def test_fused_env_step_is_bit_identical(gpu, monkeypatch, mode, dtype, N, H, mb, P, lstm, graph):
     """one_launch: the whole rollout + bootstrap in one launch per policy
     (mlearn_policy_rollout_env); c_per_step: the same entry's per-step
-    launches (taken when the env tiles outnumber the resident workgroups);
+    launches (MLEARN_ROLLOUT_PER_STEP=1);
     py_per_step: one rollout_step_env call per step from the host."""
     monkeypatch.setenv("MLEARN_WHOLE_ROLLOUT", "0" if mode == "py_per_step" else "1")
     monkeypatch.setenv("MLEARN_ROLLOUT_PER_STEP", "1" if mode == "c_per_step" else "0")
