@@ -324,6 +324,18 @@ __global__ __launch_bounds__(scan_threads<H>()) void lstm_dfeat_kernel(LstmK R, 
                acc[0][4 * g + 3]);
 }
 
+// k-steps of Wh (and, backward, dG) fragments in flight per wave in the
+// per-step scans (DEPTH > k-steps: the whole product's loads issued up front)
+#ifndef ML_LSTM_FWD_DEPTH
+#define ML_LSTM_FWD_DEPTH 8
+#endif
+#ifndef ML_LSTM_FWD4_DEPTH
+#define ML_LSTM_FWD4_DEPTH 8
+#endif
+#ifndef ML_LSTM_BWD4_DEPTH
+#define ML_LSTM_BWD4_DEPTH 8
+#endif
+
 // ---------------------------------------------------------------------------
 // Per-step scans: one launch per time step with a one-wave workgroup per (32
 // sequences, 32-unit block), (mb / 32) x (H / 32) workgroups, so the
@@ -340,7 +352,7 @@ template <typename T, int H>
 __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
     LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
     const float4* __restrict__ gin, const T* __restrict__ sh, const T* __restrict__ sc,
-    LstmWsK lw, int t) {
+    LstmWsK lw, int t, const T* __restrict__ feat) {
     typedef typename RT<T>::frag frag;
     constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NW = H / 32;
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
@@ -377,7 +389,17 @@ __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
         }
     }
     f32x16 acc[4];
-    {
+    if (feat) {
+        // the input product F Wi in this launch (F = the step's trunk output
+        // rows): the same k-step sequence into the same zeroed accumulators
+        // as lstm_gin_kernel, so the gates are bit-identical to reading Gin
+        frag fb[KSH];
+#pragma unroll
+        for (int s = 0; s < KSH; ++s) fb[s] = RT<T>::row(feat + f * H, s, h);
+        zero_acc<4>(acc);
+        gemm_ring<T, 4, KSH, ML_LSTM_FWD_DEPTH>(acc, fb, KSH,
+                                                (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
+    } else {
         const float4* gi = gin + gin_base((int64_t)t * (mb / 32) + tile, NW, w) + lane;
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -390,9 +412,19 @@ __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
                 acc[g][4 * c + 3] = x.w;
             }
     }
-    gemm_ring<T, 4, KSH, 8>(acc, hb, KSH, (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
+    // the cell's other operands (done flag: two dependent loads; the biases)
+    // in flight under the product: gemm_ring's scheduling fences would
+    // otherwise leave their round trips after the last MFMA
     const bool more = t + 1 < ro.bptt;
     const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+    float bz[4][16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bz[g][4 * j + e] = R.bias[g * H + w * 32 + 8 * j + 4 * h + e];
+    gemm_ring<T, 4, KSH, ML_LSTM_FWD_DEPTH>(acc, hb, KSH, (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
     const float keep = done ? 0.f : 1.f;
     T* gts = (T*)lw.gates + f * 4 * H;
 #pragma unroll
@@ -402,9 +434,8 @@ __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int q = 4 * j + e, u = u0 + e;
-            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + R.bias[u], acc[1][q] + R.bias[H + u],
-                                               acc[2][q] + R.bias[2 * H + u],
-                                               acc[3][q] + R.bias[3 * H + u], cc[q]);
+            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + bz[0][q], acc[1][q] + bz[1][q],
+                                               acc[2][q] + bz[2][q], acc[3][q] + bz[3][q], cc[q]);
             gi[e] = o.i;
             gf[e] = o.f;
             gg[e] = o.g;
@@ -545,11 +576,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_step4_kernel(
             acc[0][4 * c + 3] = x.w;
         }
     }
-    gemm_ring<T, 1, KSH, 8>(acc, hb, KSH, (const T*)R.wh_nat + ((int64_t)w * 4 + g) * KSH * 64 * E,
-                            lane);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) pre[g][q][lane] = acc[0][q];
-    // cell of register quad j = g: the c carry and the done flag load under the barrier
+    // cell of register quad j = g: the c carry, the done flag and the biases
+    // load under the product
     const int j = g, u0 = w * 32 + 8 * j + 4 * h;
     const float4 cv = load4(crow + u0);
     if (t == 0) {
@@ -559,6 +587,15 @@ __global__ __launch_bounds__(256) void lstm_fwd_step4_kernel(
     }
     const bool more = t + 1 < ro.bptt;
     const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
+    float bz[4][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) bz[gg][e] = R.bias[gg * H + u0 + e];
+    gemm_ring<T, 1, KSH, ML_LSTM_FWD4_DEPTH>(acc, hb, KSH, (const T*)R.wh_nat + ((int64_t)w * 4 + g) * KSH * 64 * E,
+                            lane);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pre[g][q][lane] = acc[0][q];
     const float keep = done ? 0.f : 1.f;
     __syncthreads();
     T* gts = (T*)lw.gates + f * 4 * H;
@@ -566,9 +603,9 @@ __global__ __launch_bounds__(256) void lstm_fwd_step4_kernel(
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int q = 4 * j + e, u = u0 + e;
-        const CellOut o = lstm_cell_fwd<T>(pre[0][q][lane] + R.bias[u], pre[1][q][lane] + R.bias[H + u],
-                                           pre[2][q][lane] + R.bias[2 * H + u],
-                                           pre[3][q][lane] + R.bias[3 * H + u], f4get(cv, e));
+        const CellOut o = lstm_cell_fwd<T>(pre[0][q][lane] + bz[0][e], pre[1][q][lane] + bz[1][e],
+                                           pre[2][q][lane] + bz[2][e], pre[3][q][lane] + bz[3][e],
+                                           f4get(cv, e));
         gi[e] = o.i;
         gf[e] = o.f;
         gg[e] = o.g;
@@ -610,15 +647,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
     const int bptt = ro.bptt;
     const int64_t fs = (int64_t)t * mb + m;
     const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
-    f32x16 acc[1];
-    zero_acc<1>(acc);
-    if (t + 1 < bptt)  // quarter g of dh_t = dG_{t+1} Wh^T: gate g's H columns of dG
-        gemm_stream<T, 1, NQ, 8>(acc, (const T*)lw.dg + (fs + mb) * 4 * H + g * H,
-                                 (const T*)R.w_bwd + ((int64_t)(NU + w) * NKS + g * NQ) * 64 * E,
-                                 lane);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
-    // cell backward of register quad j = g: its operands load under the barrier
+    // cell backward of register quad j = g: its operands load under the
+    // product (gemm_stream's scheduling fences would otherwise leave their
+    // round trip after the last MFMA)
     const int j = g, u0 = w * 32 + 8 * j + 4 * h;
     const T* gts = (const T*)lw.gates + fs * 4 * H;
     const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
@@ -627,6 +658,14 @@ __global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
     const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
     const float4 ci = load4((const T*)lw.cin + fs * H + u0);
     const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(lw.dcc + fs * H + u0);
+    f32x16 acc[1];
+    zero_acc<1>(acc);
+    if (t + 1 < bptt)  // quarter g of dh_t = dG_{t+1} Wh^T: gate g's H columns of dG
+        gemm_stream<T, 1, NQ, ML_LSTM_BWD4_DEPTH>(acc, (const T*)lw.dg + (fs + mb) * 4 * H + g * H,
+                                 (const T*)R.w_bwd + ((int64_t)(NU + w) * NKS + g * NQ) * 64 * E,
+                                 lane);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
     __syncthreads();
     float dpi[4], dpf[4], dpg[4], dpo[4], dco[4];
 #pragma unroll

@@ -1749,8 +1749,19 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     const T* feat = (const T*)ws.a[L - 1];
     constexpr int KSH = H / RT<T>::KS, NKS = 4 * H / RT<T>::KS;
     constexpr size_t FR = sizeof(typename RT<T>::frag);
-    // hoisted input product Gin = F Wi over every row (full grid)
-    {
+#ifndef ML_LSTM_FUSED_GIN
+#define ML_LSTM_FUSED_GIN 1  // 1-wave forward steps compute F Wi themselves (no Gin round trip)
+#endif
+#ifndef ML_LSTM_PERSISTENT
+#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
+#endif
+#ifndef ML_LSTM_FWD4
+#define ML_LSTM_FWD4 0  // forward scan steps with 4 waves per (32 sequences, 32 units): 11.37 vs 10.99 us, off
+#endif
+    const bool fused_gin = ML_LSTM_FUSED_GIN && !ML_LSTM_PERSISTENT && !ML_LSTM_FWD4;
+    // hoisted input product Gin = F Wi over every row (full grid), unless the
+    // forward steps compute it
+    if (!fused_gin) {
         const size_t lds = (size_t)KSH * 64 * FR;
         auto k = lstm_gin_kernel<T, H>;
         static bool attr_set = false;
@@ -1762,12 +1773,6 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, feat,
                            (float4*)lw.gin);
     }
-#ifndef ML_LSTM_PERSISTENT
-#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
-#endif
-#ifndef ML_LSTM_FWD4
-#define ML_LSTM_FWD4 0  // forward scan steps with 4 waves per (32 sequences, 32 units): 11.37 vs 10.99 us, off
-#endif
 #ifndef ML_LSTM_BWD4
 #define ML_LSTM_BWD4 1  // reverse scan steps with 4 waves per (32 sequences, 32 units): 13.06 vs 13.45 us
 #endif
@@ -1783,7 +1788,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
             else
                 hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
                                    s, RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
-                                   (const T*)start_c, lw, t);
+                                   (const T*)start_c, lw, t, fused_gin ? feat : nullptr);
         }
     } else {
         const size_t lds = (size_t)KSH * 64 * FR;
