@@ -637,36 +637,71 @@ __device__ inline float half_sum32(float x) {
 template <typename T, int H>
 __global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
     LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
-    float* colpart, int CP, int cp0, int t) {
+    float* colpart, int CP, int cp0, int t, int dfeat) {
     constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NQ = NKS / 4, NU = H / 32;
-    __shared__ float part[4][16][64];  // K quarter g, accumulator register q, lane
+    __shared__ float part[4][16][64];   // K quarter g, accumulator register q, lane
+    __shared__ float partf[4][16][64];  // the same for dF_{t+1} (dfeat)
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // K quarter (product) / register quad (cell)
     const int tile = blockIdx.x, w = blockIdx.y;
     const int m0 = tile * 32, m = m0 + r;
     const int bptt = ro.bptt;
-    const int64_t fs = (int64_t)t * mb + m;
-    const bool cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+    // t = -1 (dfeat only): the trailing launch that forms dF_0 from dG_0
+    const bool cell = t >= 0, prod = t + 1 < bptt;
+    const int64_t fs = (int64_t)t * mb + m;  // (not dereferenced at t = -1)
     // cell backward of register quad j = g: its operands load under the
     // product (gemm_stream's scheduling fences would otherwise leave their
     // round trip after the last MFMA)
     const int j = g, u0 = w * 32 + 8 * j + 4 * h;
-    const T* gts = (const T*)lw.gates + fs * 4 * H;
-    const float4 dho = load4((const T*)lw.dhout + fs * H + u0);
-    const float4 gi = load4(gts + u0), gf = load4(gts + H + u0);
-    const float4 gg = load4(gts + 2 * H + u0), go = load4(gts + 3 * H + u0);
-    const float4 c4 = load4((const T*)lw.cout + fs * H + u0);
-    const float4 ci = load4((const T*)lw.cin + fs * H + u0);
-    const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(lw.dcc + fs * H + u0);
-    f32x16 acc[1];
-    zero_acc<1>(acc);
-    if (t + 1 < bptt)  // quarter g of dh_t = dG_{t+1} Wh^T: gate g's H columns of dG
-        gemm_stream<T, 1, NQ, ML_LSTM_BWD4_DEPTH>(acc, (const T*)lw.dg + (fs + mb) * 4 * H + g * H,
-                                 (const T*)R.w_bwd + ((int64_t)(NU + w) * NKS + g * NQ) * 64 * E,
-                                 lane);
+    bool cut = true;
+    float4 dho, gi, gf, gg, go, c4, ci, dcin;
+    if (cell) {
+        cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+        const T* gts = (const T*)lw.gates + fs * 4 * H;
+        dho = load4((const T*)lw.dhout + fs * H + u0);
+        gi = load4(gts + u0);
+        gf = load4(gts + H + u0);
+        gg = load4(gts + 2 * H + u0);
+        go = load4(gts + 3 * H + u0);
+        c4 = load4((const T*)lw.cout + fs * H + u0);
+        ci = load4((const T*)lw.cin + fs * H + u0);
+        dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(lw.dcc + fs * H + u0);
+    }
+    // quarter g (gate g's H columns of dG_{t+1}) of dh_t = dG_{t+1} Wh^T
+    // (acc[1]) and, with dfeat, of dF_{t+1} = dG_{t+1} Wi^T for feature block w
+    // (acc[0]): one stream of the dG rows feeds both (w_bwd blocks w and NU + w)
+    f32x16 acc[2];
+    zero_acc<2>(acc);
+    if (prod) {
+        const T* brow = (const T*)lw.dg + (fs + mb) * 4 * H + g * H;
+        if (dfeat)
+            gemm_stream<T, 2, NQ, ML_LSTM_BWD4_DEPTH>(
+                acc, brow, (const T*)R.w_bwd + ((int64_t)w * NKS + g * NQ) * 64 * E, lane, NU * NKS);
+        else {
+            f32x16 a1[1] = {acc[1]};
+            gemm_stream<T, 1, NQ, ML_LSTM_BWD4_DEPTH>(
+                a1, brow, (const T*)R.w_bwd + ((int64_t)(NU + w) * NKS + g * NQ) * 64 * E, lane);
+            acc[1] = a1[0];
+        }
+    }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
+    for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[1][q];
+    if (dfeat) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) partf[g][q][lane] = acc[0][q];
+    }
     __syncthreads();
+    if (dfeat && prod) {
+        // dF_{t+1} row m, features u0 .. u0 + 3: quarters summed in fixed order
+        float d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e;
+            d[e] = ((partf[0][q][lane] + partf[1][q][lane]) + partf[2][q][lane]) + partf[3][q][lane];
+        }
+        store4((T*)lw.dfeat + (fs + mb) * H + u0, d[0], d[1], d[2], d[3]);
+    }
+    if (!cell) return;
     float dpi[4], dpf[4], dpg[4], dpo[4], dco[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {

@@ -149,6 +149,25 @@ static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int
     *splits = (int)((Mp + *rps - 1) / *rps);
 }
 
+#ifndef ML_LSTM_FUSED_GIN
+#define ML_LSTM_FUSED_GIN 1  // 1-wave forward steps compute F Wi themselves (no Gin round trip)
+#endif
+#ifndef ML_LSTM_PERSISTENT
+#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
+#endif
+#ifndef ML_LSTM_FWD4
+#define ML_LSTM_FWD4 0  // forward scan steps with 4 waves per (32 sequences, 32 units): 11.37 vs 10.99 us, off
+#endif
+// the forward steps compute the LSTM input product (no Gin buffer)
+constexpr bool kLstmFusedGin = ML_LSTM_FUSED_GIN && !ML_LSTM_PERSISTENT && !ML_LSTM_FWD4;
+#ifndef ML_LSTM_BWD4
+#define ML_LSTM_BWD4 1  // reverse scan steps with 4 waves per (32 sequences, 32 units): 13.06 vs 13.45 us
+#endif
+#ifndef ML_LSTM_FUSED_DFEAT
+#define ML_LSTM_FUSED_DFEAT 1  // 4-wave reverse steps also form dF_{t+1} = dG_{t+1} Wi^T (no dfeat launch)
+#endif
+constexpr bool kLstmFusedDfeat = ML_LSTM_FUSED_DFEAT && ML_LSTM_BWD4 && !ML_LSTM_PERSISTENT;
+
 // Carve the workspace; returns total bytes (base may be null to size only).
 // lstm (may be null): recurrent policy; mb = sequences per minibatch.
 static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
@@ -199,7 +218,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         lw.dg = take(Mp * 4 * H * es);
         lw.dhout = take(Mp * H * es);
         lw.dfeat = take(Mp * H * es);
-        lw.gin = take(Mp * 4 * H * sizeof(float));
+        lw.gin = kLstmFusedGin ? nullptr : take(Mp * 4 * H * sizeof(float));
         lw.dcc = (float*)take(Mp * H * sizeof(float));
         if (LW) *LW = lw;
     }
@@ -1749,16 +1768,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     const T* feat = (const T*)ws.a[L - 1];
     constexpr int KSH = H / RT<T>::KS, NKS = 4 * H / RT<T>::KS;
     constexpr size_t FR = sizeof(typename RT<T>::frag);
-#ifndef ML_LSTM_FUSED_GIN
-#define ML_LSTM_FUSED_GIN 1  // 1-wave forward steps compute F Wi themselves (no Gin round trip)
-#endif
-#ifndef ML_LSTM_PERSISTENT
-#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
-#endif
-#ifndef ML_LSTM_FWD4
-#define ML_LSTM_FWD4 0  // forward scan steps with 4 waves per (32 sequences, 32 units): 11.37 vs 10.99 us, off
-#endif
-    const bool fused_gin = ML_LSTM_FUSED_GIN && !ML_LSTM_PERSISTENT && !ML_LSTM_FWD4;
+    const bool fused_gin = kLstmFusedGin;
     // hoisted input product Gin = F Wi over every row (full grid), unless the
     // forward steps compute it
     if (!fused_gin) {
@@ -1773,9 +1783,6 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, feat,
                            (float4*)lw.gin);
     }
-#ifndef ML_LSTM_BWD4
-#define ML_LSTM_BWD4 1  // reverse scan steps with 4 waves per (32 sequences, 32 units): 13.06 vs 13.45 us
-#endif
     // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
     // workgroups (ML_LSTM_PERSISTENT: one persistent launch, a workgroup per
     // 32 sequences)
@@ -1810,11 +1817,15 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         for (int t = bptt - 1; t >= 0; --t) {
             if (ML_LSTM_BWD4)
                 hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0,
-                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t,
+                                   (int)kLstmFusedDfeat);
             else
                 hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
                                    s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
         }
+        if (kLstmFusedDfeat)  // dF_0 from dG_0 (every other dF_{t+1} came with step t)
+            hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
+                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, -1, 1);
     } else {
         const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
         auto k = lstm_bwd_scan_kernel<T, H>;
@@ -1827,8 +1838,9 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
         hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb, lw,
                            ws.colpart, ws.CP, cp0);
     }
-    // hoisted d-feature product dF = dG Wi^T over every row (full grid)
-    {
+    // hoisted d-feature product dF = dG Wi^T over every row (full grid),
+    // unless the reverse steps formed it
+    if (!kLstmFusedDfeat) {
         const size_t lds = (size_t)NKS * 64 * FR;
         auto k = lstm_dfeat_kernel<T, H>;
         static bool attr_set = false;

@@ -246,10 +246,11 @@ __device__ inline void gemm_lds_run(f32x16 (&acc)[NOUT], typename RT<T>::frag (&
 
 // acc[nb] += sum_s Img[block nb][step s] x row-fragment(s) with BOTH operands
 // streamed: A fragments from the image and B fragments (natural k order) from
-// this lane's row in memory, DEPTH k-steps of each in flight.
+// this lane's row in memory, DEPTH k-steps of each in flight.  bstride:
+// k-steps between consecutive output blocks of the image (default NKS).
 template <typename T, int NOUT, int NKS, int DEPTH>
 __device__ inline void gemm_stream(f32x16 (&acc)[NOUT], const T* __restrict__ brow,
-                                   const T* __restrict__ img, int lane) {
+                                   const T* __restrict__ img, int lane, int bstride = NKS) {
     typedef typename RT<T>::frag frag;
     constexpr int FB = 64 * RT<T>::E * (int)sizeof(T);
     const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
@@ -259,7 +260,7 @@ __device__ inline void gemm_stream(f32x16 (&acc)[NOUT], const T* __restrict__ br
 #pragma unroll
     for (int s = 0; s < DEPTH - 1; ++s) {
 #pragma unroll
-        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * NKS + s) * FB);
+        for (int nb = 0; nb < NOUT; ++nb) ra[s][nb] = img_load<T>(rs, voff, (nb * bstride + s) * FB);
         rb[s] = RT<T>::row(brow, s, h);
     }
 #pragma unroll
@@ -268,7 +269,7 @@ __device__ inline void gemm_stream(f32x16 (&acc)[NOUT], const T* __restrict__ br
         if (sl < NKS) {
 #pragma unroll
             for (int nb = 0; nb < NOUT; ++nb)
-                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * NKS + sl) * FB);
+                ra[sl % DEPTH][nb] = img_load<T>(rs, voff, (nb * bstride + sl) * FB);
             rb[sl % DEPTH] = RT<T>::row(brow, sl, h);
         }
         __builtin_amdgcn_sched_barrier(0);
