@@ -29,6 +29,15 @@ run bench_pbt 300 python bench.py --config pbt --steps 5 --warmup 2 --no-cpu-bas
 run prof_headline 420 rocprofv3 --kernel-trace --stats -d "$out/prof_headline" -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 run prof_lstm 420 rocprofv3 --kernel-trace --stats -d "$out/prof_lstm" -o run --output-format csv -- python bench.py --config lstm --steps 5 --warmup 2 --no-cpu-baseline --no-roofline
 for f in bench_headline bench_separate emulate8 bench_b1 bench_twohot bench_lstm bench_lstm_c2 bench_pbt; do
-  python -c "import json; d=json.load(open('$out/$f.out')); print('$f', round(d.get('ms_per_step', d.get('ms_per_update_rank_share', 0)),3), d.get('value', d.get('implied_scaling_1_to_W')))"
+  tail -1 "$out/$f.out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$f', round(d.get('ms_per_step', d.get('ms_per_update_rank_share', 0)),3), d.get('value', d.get('implied_scaling_1_to_W')))"
 done
+if [ "${PMC:-0}" = 1 ]; then
+  rm -rf gpurun_out/pmc
+  KRE='ppo_step|wgrad|policy_rollout|gae|reduce_grads|adam|project' bash tools/gpu_pmc.sh > "$out/pmc.log" 2>&1 || { echo pmc failed; tail "$out/pmc.log"; exit 1; }
+  cat "$out/pmc.log"
+  python tools/pmc_traffic.py gpurun_out/pmc "$out/pmc_headline.json" && mv gpurun_out/pmc "$out/pmc_headline"
+  KRE='lstm|wgrad|project|policy_rollout|ppo_step' BENCH_ARGS='--config lstm' bash tools/gpu_pmc.sh > "$out/pmc_lstm.log" 2>&1 || { echo pmc lstm failed; tail "$out/pmc_lstm.log"; exit 1; }
+  cat "$out/pmc_lstm.log"
+  python tools/pmc_traffic.py gpurun_out/pmc "$out/pmc_lstm.json" && mv gpurun_out/pmc "$out/pmc_lstm"
+fi
 exit 0
