@@ -53,9 +53,18 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
                                                             double* part) {
     __shared__ double sh[4];
     double s = 0;
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        double v = g[i];
-        s += v * v;
+    // eight of this thread's strided elements in flight at a time, summed in index order
+    const int64_t st = (int64_t)gridDim.x * 256;
+    for (int64_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += 8 * st) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = i0 + u * st < n ? g[i0 + u * st] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * st < n) {
+                const double v = x[u];
+                s += v * v;
+            }
     }
     s = wave_sum64d(s);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
@@ -114,6 +123,7 @@ __device__ inline float global_norm(const double* gpart, int64_t npart) {
     return gn_sh;
 }
 
+template <int PRE>
 __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict__ params,
                                                    const float* __restrict__ grads,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -126,34 +136,41 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x < 4 * kMaxSlots) sh[threadIdx.x / kMaxSlots][threadIdx.x % kMaxSlots] = 0.f;
-    // this thread's first parameter is in flight while the global norm is
-    // reduced (the common case at <= kAdamBlocks x 256 parameters: one each)
+    // this thread's first PRE parameters (grid-stride) are in flight while
+    // the global norm is reduced: the headline MLP has one per thread, the
+    // recurrent layouts up to five (one loop that loads as it goes waits a
+    // memory latency per parameter); PRE = the launch's count rounded up to
+    // a power of two
+    constexpr int kAdamPre = PRE;
     const int64_t p0 = blockIdx.x * (int64_t)256 + threadIdx.x;
-    const bool have0 = p0 < Lk.total;
-    float g0 = 0.f, m0 = 0.f, v0 = 0.f, q0 = 0.f;
-    if (have0) {
-        g0 = grads[p0];
-        m0 = m[p0];
-        v0 = v[p0];
-        q0 = params[p0];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    float gq[kAdamPre], mq[kAdamPre], vq[kAdamPre], qq[kAdamPre];
+#pragma unroll
+    for (int u = 0; u < kAdamPre; ++u) {
+        const int64_t p = p0 + u * stride;
+        gq[u] = mq[u] = vq[u] = qq[u] = 0.f;
+        if (p < Lk.total) {
+            gq[u] = grads[p];
+            mq[u] = m[p];
+            vq[u] = v[p];
+            qq[u] = params[p];
+        }
     }
     const int count = step[0] + 1;
     const float gn = global_norm(gpart, npart);  // (its barriers also order the sh zeroing)
-    for (int64_t p = p0; p - threadIdx.x < Lk.total; p += (int64_t)gridDim.x * 256) {
+    auto update = [&](int64_t p, float g, float m_old, float v_old, float q_old) {
         float contrib = 0.f;
         int slot = -2;
         // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
         const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
         if (p < Lk.total && !pad) {
-            const bool first = p == p0;
-            float g = first ? g0 : grads[p];
             if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
-            const float mm = (1.f - b1) * g + b1 * (first ? m0 : m[p]);
-            const float vv = (1.f - b2) * (g * g) + b2 * (first ? v0 : v[p]);
+            const float mm = (1.f - b1) * g + b1 * m_old;
+            const float vv = (1.f - b2) * (g * g) + b2 * v_old;
             const float mhat = mm / (1.f - powf(b1, (float)count));
             const float vhat = vv / (1.f - powf(b2, (float)count));
             const float u = mhat / (sqrtf(vhat) + eps);
-            const float np = (first ? q0 : params[p]) + (-lr) * u;
+            const float np = q_old + (-lr) * u;
             m[p] = mm;
             v[p] = vv;
             params[p] = np;
@@ -168,6 +185,16 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
             x = wave_sum64(x);
             if (lane == 0) sh[w][s] += x;
         }
+    };
+#pragma unroll
+    for (int u = 0; u < kAdamPre; ++u) {
+        const int64_t p = p0 + u * stride;
+        if (p - threadIdx.x >= Lk.total) break;  // (block-uniform)
+        update(p, gq[u], mq[u], vq[u], qq[u]);
+    }
+    for (int64_t p = p0 + kAdamPre * stride; p - threadIdx.x < Lk.total; p += stride) {
+        const bool in = p < Lk.total;
+        update(p, in ? grads[p] : 0.f, in ? m[p] : 0.f, in ? v[p] : 0.f, in ? params[p] : 0.f);
     }
     __syncthreads();
     if (threadIdx.x < nslot) {
@@ -221,7 +248,7 @@ __device__ inline void write_copies(const LayoutK& Lk, const CopiesK& C, int64_t
     }
 }
 
-template <typename T>
+template <typename T, int NS>
 __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, float* params,
                                                       const float* init_norms, const double* ppart,
                                                       int nblk, int norm_params, int norm_ln,
@@ -230,14 +257,35 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
     // same fixed-order tree in every block
     __shared__ double red[4][kMaxSlots];
     __shared__ float sq[kMaxSlots];
-    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
+    constexpr int nslot = NS;  // = 2 L (+ 8 recurrent): the launch picks the instantiation
     const int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x;
     const float val0 = p < Lk.total ? params[p] : 0.f;  // in flight under the slot reduction
-    for (int sl = 0; sl < nslot; ++sl) {
-        double t = 0;
-        for (int b = threadIdx.x; b < nblk; b += 256) t += ppart[(int64_t)b * nslot + sl];
-        t = wave_sum64d(t);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][sl] = t;
+    // every slot's partials of this thread (blocks tid, tid + 256, ...) loaded
+    // together, then summed per slot in block order (one loop per slot would
+    // wait for each load before issuing the next)
+    double t[NS];
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) t[sl] = 0;
+    for (int b0 = threadIdx.x; b0 < nblk; b0 += 512) {
+        double x[2][NS];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl) {
+                const int b = b0 + 256 * u;
+                x[u][sl] = (b < nblk && sl < nslot) ? ppart[(int64_t)b * nslot + sl] : 0.0;
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl)
+                if (b0 + 256 * u < nblk && sl < nslot) t[sl] += x[u][sl];
+    }
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+        if (sl >= nslot) break;
+        const double tt = wave_sum64d(t[sl]);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][sl] = tt;
     }
     __syncthreads();
     if (threadIdx.x < nslot) {
@@ -287,6 +335,28 @@ static int64_t optim_ws_doubles(const LayoutK& k) {
     return kNormBlocks + nblk * kMaxSlots + 8 + kMaxSlots + 8;
 }
 
+template <typename T>
+static void launch_project(int nslot, dim3 grid, hipStream_t s, const LayoutK& Lk, const CopiesK& C,
+                           const mlearn_optim_state* st, const double* ppart, int ablk) {
+#define ML_PROJ(NS)                                                                            \
+    case NS:                                                                                   \
+        hipLaunchKernelGGL((project_kernel<T, NS>), grid, dim3(256), 0, s, Lk, C, st->params, \
+                           st->init_norms, ppart, ablk, st->normalize_params,                  \
+                           st->normalize_layernorms, st->step);                                \
+        break;
+    switch (nslot) {
+        ML_PROJ(2)
+        ML_PROJ(4)
+        ML_PROJ(6)
+        ML_PROJ(8)
+        ML_PROJ(10)
+        ML_PROJ(12)
+        ML_PROJ(14)
+        ML_PROJ(16)
+    }
+#undef ML_PROJ
+}
+
 }  // namespace ml
 
 using namespace ml;
@@ -320,17 +390,16 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
         hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
                            Lk.total, gpart);
     }
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
+    const int64_t nit = (Lk.total + (int64_t)ablk * 256 - 1) / ((int64_t)ablk * 256);
+    auto adam = nit <= 1 ? adam_kernel<1> : nit <= 2 ? adam_kernel<2> : nit <= 4 ? adam_kernel<4> : adam_kernel<8>;
+    hipLaunchKernelGGL(adam, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step, norm_part,
                        nparts, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm, ppart);
+    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     if (dtype == MLEARN_DTYPE_BF16)
-        hipLaunchKernelGGL(project_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const double*)ppart, ablk,
-                           st->normalize_params, st->normalize_layernorms, st->step);
+        launch_project<bf16>(nslot, dim3((unsigned)nblk), s, Lk, C, st, (const double*)ppart, ablk);
     else
-        hipLaunchKernelGGL(project_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, Lk, C,
-                           st->params, st->init_norms, (const double*)ppart, ablk,
-                           st->normalize_params, st->normalize_layernorms, st->step);
+        launch_project<float>(nslot, dim3((unsigned)nblk), s, Lk, C, st, (const double*)ppart, ablk);
     return check_launch("optim_step");
 }
 

@@ -129,10 +129,14 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 #ifndef ML_WG_CPW
 #define ML_WG_CPW 32  // > 0: split every weight into splits of this many chunks (balanced per-WG work)
 #endif
-static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int64_t* rps) {
+#ifndef ML_WG_TARGET_LSTM
+#define ML_WG_TARGET_LSTM 512  // the LSTM gate weights' (Wi, Wh) workgroup target (config L: 10.94 / 10.60 / 10.47 ms at 128 / 256 / 512)
+#endif
+static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int64_t* rps,
+                        int target = ML_WG_TARGET) {
     int tiles = ((I + kWgTile - 1) / kWgTile) * ((J + kWgTile - 1) / kWgTile);
     int64_t chunks = Mp / kWgChunk;
-    int64_t s = ML_WG_TARGET / tiles;
+    int64_t s = target / tiles;
     // balanced: splits of at most ML_WG_CPW chunks (never fewer workgroups than
     // the target: small per-rank minibatches under data parallelism keep their
     // parallelism), at most 2 x the target per weight (the MLP trunk / head
@@ -203,7 +207,8 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     for (int l = 0; l < njobs; ++l) {
         const int I = l >= L ? H : (l == 0 ? D : H);
         const int J = l == L ? HC : (l > L ? 4 * H : H);
-        plan_splits(I, J, Mp, wg_chunk_es(es), &w.splits[l], &w.rps[l]);
+        plan_splits(I, J, Mp, wg_chunk_es(es), &w.splits[l], &w.rps[l],
+                    l > L ? ML_WG_TARGET_LSTM : ML_WG_TARGET);
         w.slab_off[l] = so;
         so += (int64_t)w.splits[l] * I * J;
     }
@@ -1429,6 +1434,25 @@ int validate_lstm(const mlearn_mlp_policy* p, const mlearn_lstm* r) {
 // threads x 16 split groups; group g sums splits g, g + 16, ... and the
 // groups are combined in order through LDS.
 constexpr int kRgGroups = 16;
+// v += ld(k) for k = g, g + 16, ... < n, in that order, with four loads in
+// flight (a plain loop waits for each load before issuing the next)
+template <typename F>
+__device__ inline void rg_sum4(float (&v)[4], int g, int n, F ld) {
+    for (int k0 = g; k0 < n; k0 += 4 * kRgGroups) {
+        float4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u * kRgGroups < n) x[u] = ld(k0 + u * kRgGroups);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u * kRgGroups < n) {
+                v[0] += x[u].x;
+                v[1] += x[u].y;
+                v[2] += x[u].z;
+                v[3] += x[u].w;
+            }
+    }
+}
 __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, float* grad,
                                                            double* sumsq) {
     __shared__ float red[kRgGroups][65];
@@ -1440,40 +1464,55 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
         const int64_t q0 = p0 - Lk.lstm_off, HH = Lk.lstm_H, G = 4 * HH * HH;
         if (q0 >= 2 * G) {  // bias: column partials of d gate pre-activations
             const int col = L * 2 * H + Lk.HC + (int)(q0 - 2 * G) + 4 * c;
-            for (int k = g; k < kColChunks; k += kRgGroups) {
-                const float4 x = *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col);
-                v[0] += x.x;
-                v[1] += x.y;
-                v[2] += x.z;
-                v[3] += x.w;
-            }
+            rg_sum4(v, g, kColChunks,
+                    [&](int k) { return *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col); });
         } else {  // Wi / Wh: split-K slabs [split][H][4H]
             const int which = (int)(q0 / G);
             const float* sp = ws.slab + ws.slab_off[L + 1 + which] + (q0 - which * G) + 4 * c;
-            for (int k = g; k < ws.splits[L + 1 + which]; k += kRgGroups) {
-                const float4 x = *(const float4*)(sp + k * G);
-                v[0] += x.x;
-                v[1] += x.y;
-                v[2] += x.z;
-                v[3] += x.w;
-            }
+            rg_sum4(v, g, ws.splits[L + 1 + which],
+                    [&](int k) { return *(const float4*)(sp + (int64_t)k * G); });
         }
     } else if (p0 >= Lk.hw_off) {  // head weight (slab [split][H][32]) and head bias
+        // per parameter e: a strided sequence (base, stride, n) summed in
+        // order; the four parameters' loads are issued together
+        const float* base[4];
+        int64_t stride[4];
+        int n[4];
+        int nmax = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t p = p0 + 4 * c + e;
-            if (p >= Lk.mlp_total) break;  // (recurrent policies: alignment padding)
+            base[e] = ws.colpart2;
+            stride[e] = 0;
+            n[e] = 0;
+            if (p >= Lk.mlp_total) continue;  // (recurrent policies: alignment padding)
             if (p >= Lk.hb_off) {
-                const int col = L * 2 * H + (int)(p - Lk.hb_off);
-                for (int k = g; k < kColChunks; k += kRgGroups)
-                    v[e] += ws.colpart2[(int64_t)k * ws.CP + col];
+                base[e] = ws.colpart2 + L * 2 * H + (int)(p - Lk.hb_off);
+                stride[e] = ws.CP;
+                n[e] = kColChunks;
             } else {
                 const int64_t q = p - Lk.hw_off;
                 const int i = (int)(q / Lk.A1), j = (int)(q % Lk.A1);
-                const float* sp = ws.slab + ws.slab_off[L] + (int64_t)i * Lk.HC + j;
-                const int64_t stride = (int64_t)H * Lk.HC;
-                for (int k = g; k < ws.splits[L]; k += kRgGroups) v[e] += sp[k * stride];
+                base[e] = ws.slab + ws.slab_off[L] + (int64_t)i * Lk.HC + j;
+                stride[e] = (int64_t)H * Lk.HC;
+                n[e] = ws.splits[L];
             }
+            nmax = n[e] > nmax ? n[e] : nmax;
+        }
+        for (int k0 = g; k0 < nmax; k0 += 4 * kRgGroups) {
+            float x[4][4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u * kRgGroups;
+                    x[e][u] = k < n[e] ? base[e][k * stride[e]] : 0.f;
+                }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k0 + u * kRgGroups < n[e]) v[e] += x[e][u];
         }
     } else {
         int l = L - 1;
@@ -1481,38 +1520,13 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(LayoutK Lk, WsK ws, f
         if (p0 >= Lk.s_off[l]) {  // LayerNorm scale / bias: column partials
             const int which = p0 >= Lk.b_off[l] ? 0 : 1;  // 0: bias (beta), 1: scale (gamma)
             const int col = (l * 2 + which) * H + (int)(p0 - (which ? Lk.s_off[l] : Lk.b_off[l])) + 4 * c;
-            for (int k = g; k < kColChunks; k += kRgGroups) {
-                const float4 x = *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col);
-                v[0] += x.x;
-                v[1] += x.y;
-                v[2] += x.z;
-                v[3] += x.w;
-            }
+            rg_sum4(v, g, kColChunks,
+                    [&](int k) { return *(const float4*)(ws.colpart2 + (int64_t)k * ws.CP + col); });
         } else {  // Dense kernel: split-K slabs
             const int I = l == 0 ? Lk.D : H;
             const float* sp = ws.slab + ws.slab_off[l] + (p0 - Lk.w_off[l]) + 4 * c;
             const int64_t stride = (int64_t)I * H;
-            // four splits' loads in flight at a time, summed in split order
-            int k = g;
-            for (; k + 3 * kRgGroups < ws.splits[l]; k += 4 * kRgGroups) {
-                float4 x[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) x[u] = *(const float4*)(sp + (k + u * kRgGroups) * stride);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    v[0] += x[u].x;
-                    v[1] += x[u].y;
-                    v[2] += x[u].z;
-                    v[3] += x[u].w;
-                }
-            }
-            for (; k < ws.splits[l]; k += kRgGroups) {
-                const float4 x = *(const float4*)(sp + k * stride);
-                v[0] += x.x;
-                v[1] += x.y;
-                v[2] += x.z;
-                v[3] += x.w;
-            }
+            rg_sum4(v, g, ws.splits[l], [&](int k) { return *(const float4*)(sp + k * stride); });
         }
     }
 #pragma unroll
