@@ -169,12 +169,9 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     achieved = step_flop / t_step / 1e12
     # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip)
     HC = 32 if A1 <= 32 else 96
-    rows = (os.environ.get("MLEARN_ROWS") == "1" and HC == 32 and ps.arch.critic_bins == 1)
-    kname = ("ppo_rows_kernel" if rows else
-             f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>")
+    kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
     traffic, pmc_name = pmc_traffic("ppo_step")
-    if pmc_name is None or (("ppo_rows_kernel" in pmc_name) != rows) or \
-            (not rows and f"Li{HC}ELi1E" not in pmc_name):
+    if pmc_name is None or f"Li{HC}ELi1E" not in pmc_name:
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {
         "kernel": f"{kname} (mlearn_ppo_minibatch_fwd_bwd)",
@@ -240,7 +237,7 @@ def gae_roofline(dev, N, iters=50, returns=False):
 
     def call():
         nat.check(L.mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b), nat.ptr(adv),
-                                   nat.ptr(ret) if returns else None, T, N, 0.99, 0.95,
+                                   nat.ptr(ret) if returns else None, T, N, 0.99, 0.99 * 0.95,
                                    nat.stream_handle(s)))
 
     sec = time_call(call, iters, s)
@@ -396,12 +393,10 @@ def main():
                        "steps_per_update": T, "parallelism": f"dp{world}",
                        "critic": args.critic,
                        "hip_graph": not args.no_graph,
-                       # the built-in synthetic sim's step: inside the rollout policy
-                       # launch (mlearn_policy_rollout_step_env) or its own launch
+                       # the built-in synthetic sim's step: inside the whole-rollout
+                       # launch (mlearn_policy_rollout_env) or its own launch
                        "sim_step": "separate_launch" if args.separate_sim
-                       else ("fused_into_policy_launch"
-                             if os.environ.get("MLEARN_WHOLE_ROLLOUT", "1") == "0"
-                             else "whole_rollout_one_launch")},
+                       else "whole_rollout_one_launch"},
             # how the data-parallel collectives ran (a SCALE record can be checked
             # against this): "rccl_in_graph" = C ABI RCCL communicator on the
             # compute stream inside the HIP graph; "torch_distributed" = host

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 11
+#define MLEARN_ABI_VERSION 12
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -84,10 +84,16 @@ int mlearn_counters_add(uint64_t* ctr, int32_t n, const uint64_t* deltas /* host
  * (bool, rollouts.py:454-455,933).  bootstrap is [N].  returns may be NULL:
  * only the advantages are written (4 B per element instead of 8) and the
  * consumers form returns = advantages + values themselves, the same f32
- * addition (mlearn_rollout_view.returns = NULL, mlearn_metric_job.x2). */
+ * addition (mlearn_rollout_view.returns = NULL, mlearn_metric_job.x2).
+ * gamma_lambda is the product cfg.gamma * cfg.gae_lambda formed by the caller
+ * in double precision and rounded to f32 once: algo_common.py:120 evaluates
+ * `cfg.gamma * cfg.gae_lambda * next_advantage` left to right with Python
+ * floats (rollouts.py:406), so the constant is one f64 product that JAX's
+ * weak typing rounds to f32 (f32(gamma) * f32(lambda) differs by an ulp for
+ * e.g. 0.998 / 0.95). */
 int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
                    const float* bootstrap, float* advantages, float* returns, int32_t T,
-                   int64_t N, float gamma, float gae_lambda, mlearn_stream_t stream);
+                   int64_t N, float gamma, float gamma_lambda, mlearn_stream_t stream);
 
 /* mlearn_gae_f32 with a value normaliser (TrainConfig.normalize_values): the
  * stored values and the bootstrap are critic outputs in the normalised space
@@ -100,7 +106,7 @@ int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* don
 int mlearn_gae_vnorm_f32(const float* rewards, const float* values, const uint8_t* dones,
                          const float* bootstrap, const float* value_norm, int64_t cols_per_norm,
                          float* advantages, float* returns, int32_t T, int64_t N, float gamma,
-                         float gae_lambda, mlearn_stream_t stream);
+                         float gamma_lambda, mlearn_stream_t stream);
 
 /* Discounted returns without advantages (algo_common.py:45-81), used when
  * TrainConfig.compute_advantages is False. */
@@ -593,13 +599,23 @@ typedef struct mlearn_rollout_out {
     int32_t T, bptt_len;
     int64_t ld;
     float gamma;
-    int32_t pad;
+    int32_t max_workgroups;     /* 0: one workgroup per resident slot (every CU busy; with
+                                   more 32-env tiles than slots each workgroup runs
+                                   ceil(tiles / slots) tiles in series); > 0: at most this
+                                   many workgroups (tiles in series); < 0: T + 1 per-step
+                                   launches of the same body (same bits either way) */
 } mlearn_rollout_out;
 int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                               const mlearn_lstm_carry* carry, const float* obs, int64_t N,
                               const mlearn_rollout_out* out, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint32_t env_offset,
                               const mlearn_dummy_env* env, mlearn_stream_t stream);
+/* Workgroups mlearn_policy_rollout_env launches for N envs under
+ * max_workgroups (0 = the launch it would issue per-step: -1 means per-step
+ * launches are used, i.e. the occupancy query failed or max_workgroups < 0);
+ * tiles = ceil(N / 32) > the result means tiles run in series. */
+int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                         int64_t N, int32_t max_workgroups);
 int mlearn_lstm_policy_rollout_step_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                                         const mlearn_lstm_carry* carry, const float* obs,
                                         int64_t N, void* obs_store, int32_t* actions,

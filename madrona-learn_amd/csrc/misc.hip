@@ -856,13 +856,15 @@ int mlearn_philox4x32_host(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32
 
 int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* dones,
                    const float* bootstrap, float* advantages, float* returns, int32_t T, int64_t N,
-                   float gamma, float gae_lambda, mlearn_stream_t stream) {
+                   float gamma, float gamma_lambda, mlearn_stream_t stream) {
     ML_REQUIRE(T >= 0 && N >= 0, "gae: negative size");
     if (T == 0 || N == 0) return MLEARN_OK;
     ML_REQUIRE(rewards && values && dones && bootstrap && advantages,
                "gae: null pointer");  // (returns may be NULL: not materialised)
     ML_REQUIRE(N <= ((int64_t)1 << 28), "gae: N > 2^28 columns");
-    float gl = gamma * gae_lambda;  // cfg.gamma * cfg.gae_lambda (algo_common.py:120)
+    // cfg.gamma * cfg.gae_lambda (algo_common.py:120): one f64 product of the
+    // Python floats rounded to f32 once, formed by the caller
+    const float gl = gamma_lambda;
     // Blocks of 64 below 2^20 columns so more CUs share the serial T loop (the
     // operating point N = 8192 is latency-bound), 256 above (HBM-bound).
     if (N >= (int64_t)1 << 20) {
@@ -880,7 +882,7 @@ int mlearn_gae_f32(const float* rewards, const float* values, const uint8_t* don
 int mlearn_gae_vnorm_f32(const float* rewards, const float* values, const uint8_t* dones,
                          const float* bootstrap, const float* value_norm, int64_t cols_per_norm,
                          float* advantages, float* returns, int32_t T, int64_t N, float gamma,
-                         float gae_lambda, mlearn_stream_t stream) {
+                         float gamma_lambda, mlearn_stream_t stream) {
     ML_REQUIRE(T >= 0 && N >= 0, "gae_vnorm: negative size");
     if (T == 0 || N == 0) return MLEARN_OK;
     ML_REQUIRE(rewards && values && dones && bootstrap && advantages && returns && value_norm,
@@ -888,7 +890,7 @@ int mlearn_gae_vnorm_f32(const float* rewards, const float* values, const uint8_
     ML_REQUIRE(cols_per_norm >= 1 && N % cols_per_norm == 0,
                "gae_vnorm: N must be a multiple of cols_per_norm");
     ML_REQUIRE(N <= ((int64_t)1 << 28), "gae_vnorm: N > 2^28 columns");
-    const float gl = gamma * gae_lambda;
+    const float gl = gamma_lambda;  // formed by the caller, as in mlearn_gae_f32
     hipLaunchKernelGGL((gae_kernel<1, 16>), dim3(grid_for(N, 64)), dim3(64), 0, S(stream), rewards,
                        values, dones, bootstrap, advantages, returns, T, N, gamma, gl, value_norm,
                        cols_per_norm);

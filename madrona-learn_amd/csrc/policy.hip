@@ -610,6 +610,7 @@ struct RollK {
     int T, bptt;
     int64_t ld;
     float gamma;
+    int max_wg;          // mlearn_rollout_out.max_workgroups
 };
 
 template <typename T, int H, bool RNN, int HC>
@@ -710,19 +711,13 @@ static int launch_policy_step(const PolicyK& P, const float* obs, int64_t N, voi
     return check_launch("policy_rollout_step");
 }
 
-static bool getenv_is(const char* name, char c) {
-    const char* e = getenv(name);
-    return e && e[0] == c;
-}
-
-// The whole rollout as one launch when every env tile gets a resident
-// workgroup (MLEARN_ROLLOUT_PER_STEP=1 forces the per-step launches).
+// Workgroups of the whole-rollout launch (-1: per-step launches): one per
+// resident slot, or at most max_wg (> 0); max_wg < 0 asks for the per-step
+// launches.
 template <typename T, int H, bool RNN, int HC>
-static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
-                                 uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
-                                 const LstmK& R, const CarryK& cy, const EnvK& env, hipStream_t s) {
+static int64_t rollout_grid(int L, int64_t N, int max_wg) {
     constexpr int NT = pol_threads<H, RNN>();
-    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(P.L);
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(L);
     auto kern = policy_rollout_kernel<T, H, RNN, HC>;
     static bool attr_set = false;
     static int per_cu = 0, cus = 0;
@@ -738,21 +733,33 @@ static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, 
         attr_set = true;
     }
     const int64_t tiles = (N + 31) / 32;
-    const int64_t slots = (int64_t)per_cu * cus;
-    if (slots > 0 && !getenv_is("MLEARN_ROLLOUT_PER_STEP", '1')) {
-        // the T + 1 steps back to back inside each workgroup, no launch
-        // boundary between them; with more env tiles than resident
-        // workgroups, ceil(tiles / slots) tiles per workgroup in series
-        // (headline: 2 048 tiles, 768 slots, 3 per workgroup; 1.648 ms vs
-        // 33 per-step launches ~1.65-1.70 ms, +1 % on the update; the W = 8
-        // share: one tile per workgroup, 3.91 vs 3.99 ms)
-        const int64_t per = (tiles + slots - 1) / slots;
-        const int64_t grid = (tiles + per - 1) / per;
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, s, P, obs, N, rk, k0, k1,
-                           step_ctr, eoff, R, cy, env);
+    int64_t slots = (int64_t)per_cu * cus;
+    if (max_wg < 0 || slots <= 0) return -1;
+    if (max_wg > 0 && max_wg < slots) slots = max_wg;
+    // ceil(tiles / slots) tiles per workgroup in series (headline: 2 048
+    // tiles, 768 slots, 3 per workgroup; 1.648 ms vs 33 per-step launches
+    // ~1.65-1.70 ms, +1 % on the update; the W = 8 share: one tile per
+    // workgroup, 3.91 vs 3.99 ms)
+    const int64_t per = (tiles + slots - 1) / slots;
+    return (tiles + per - 1) / per;
+}
+
+// The whole rollout as one launch (every env tile gets a resident workgroup,
+// or tiles run in series inside the workgroups), or T + 1 per-step launches
+// of the same body when max_wg < 0.
+template <typename T, int H, bool RNN, int HC>
+static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
+                                 uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
+                                 const LstmK& R, const CarryK& cy, const EnvK& env, hipStream_t s) {
+    constexpr int NT = pol_threads<H, RNN>();
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(P.L);
+    const int64_t grid = rollout_grid<T, H, RNN, HC>(P.L, N, rk.max_wg);
+    if (grid > 0) {
+        hipLaunchKernelGGL((policy_rollout_kernel<T, H, RNN, HC>), dim3((unsigned)grid), dim3(NT),
+                           lds, s, P, obs, N, rk, k0, k1, step_ctr, eoff, R, cy, env);
         return check_launch("policy_rollout_env");
     }
-    // MLEARN_ROLLOUT_PER_STEP=1 (or no occupancy answer): the same body as
+    // max_workgroups < 0 (or no occupancy answer): the same body as
     // T + 1 launches of the per-step kernel (same bits)
     for (int t = 0; t <= rk.T; ++t) {
         const bool act = t < rk.T;
@@ -908,7 +915,7 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
     }
     RollK rk{out->obs, out->actions, out->log_probs, out->values, out->rewards, out->dones,
              out->env_returns_trace, out->bootstrap, out->env_returns, out->start_h, out->start_c,
-             out->T, out->bptt_len, out->ld, out->gamma};
+             out->T, out->bptt_len, out->ld, out->gamma, out->max_workgroups};
     EnvK ek{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
             denv->env_offset};
     PolicyK P = make_policy_k(*policy);
@@ -934,6 +941,32 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
 #undef ML_DISPATCH
 #undef ML_LAUNCH
 #undef ML_LAUNCH_HC
+}
+
+extern "C" int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* policy,
+                                                    const mlearn_lstm* lstm, int64_t N,
+                                                    int32_t max_workgroups) {
+    if ((lstm ? validate_lstm(policy, lstm) : validate_policy(policy)) || N < 1) return -1;
+    const int HC = head_cols(*policy), L = policy->num_layers;
+#define ML_GRID_HC(T, HH, HCC) \
+    (lstm ? rollout_grid<T, HH, true, HCC>(L, N, max_workgroups) \
+          : rollout_grid<T, HH, false, HCC>(L, N, max_workgroups))
+#define ML_GRID(T, HH) \
+    (HC == MLEARN_HEAD_COLS ? ML_GRID_HC(T, HH, MLEARN_HEAD_COLS) : ML_GRID_HC(T, HH, MLEARN_HEAD_COLS_MAX))
+#define ML_DISPATCH(T)                    \
+    switch (policy->hidden) {             \
+        case 64: return ML_GRID(T, 64);   \
+        case 128: return ML_GRID(T, 128); \
+        default: return ML_GRID(T, 256);  \
+    }
+    if (policy->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
+#undef ML_GRID
+#undef ML_GRID_HC
 }
 
 extern "C" int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float* obs,

@@ -65,7 +65,6 @@ constexpr int kRowAlign = 64;    // Mp granularity
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif
-constexpr int kRecMaxD = 64;     // widest observation the weight-gradient A_0 recompute takes
 constexpr int kMaxJobs = MLEARN_MAX_LAYERS + 3;  // weight-gradient jobs
 
 // LSTM scan buffers of the recurrent update (rows f = t * mb + m, compute
@@ -79,7 +78,6 @@ struct LstmWsK {
     void* dg;     // [Mp][4H] d loss / d gate pre-activations
     void* dhout;  // [Mp][H]  d loss / d h_t from the heads
     void* dfeat;  // [Mp][H]  d loss / d trunk output
-    void* gin;    // [Mp/32][H/32][16][64] float4: F Wi in accumulator order (lstm_gin_kernel)
     float* dcc;   // [Mp][H] f32  c cotangent into step t (per-step reverse scan)
 };
 
@@ -98,9 +96,6 @@ struct WsK {
     int64_t Mp;
     int ntiles;                         // Mp / 32
     int CP;                             // L*2*H + 32
-    float* lnst;                        // [Mp][2] layer-0 LayerNorm {mean, rstd} (a0r)
-    int a0r;                            // A_0 not spilled: wgrad recomputes it (kFused)
-    int zs;                             // a[0] holds Z_0 (ppo_rows_kernel): wgrad applies LN_0 + ReLU
     uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
 
@@ -153,25 +148,6 @@ static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int
     *splits = (int)((Mp + *rps - 1) / *rps);
 }
 
-#ifndef ML_LSTM_FUSED_GIN
-#define ML_LSTM_FUSED_GIN 1  // 1-wave forward steps compute F Wi themselves (no Gin round trip)
-#endif
-#ifndef ML_LSTM_PERSISTENT
-#define ML_LSTM_PERSISTENT 0  // 1: one persistent scan launch per direction (64 CUs at mb 2048)
-#endif
-#ifndef ML_LSTM_FWD4
-#define ML_LSTM_FWD4 0  // forward scan steps with 4 waves per (32 sequences, 32 units): 11.37 vs 10.99 us, off
-#endif
-// the forward steps compute the LSTM input product (no Gin buffer)
-constexpr bool kLstmFusedGin = ML_LSTM_FUSED_GIN && !ML_LSTM_PERSISTENT && !ML_LSTM_FWD4;
-#ifndef ML_LSTM_BWD4
-#define ML_LSTM_BWD4 1  // reverse scan steps with 4 waves per (32 sequences, 32 units): 13.06 vs 13.45 us
-#endif
-#ifndef ML_LSTM_FUSED_DFEAT
-#define ML_LSTM_FUSED_DFEAT 1  // 4-wave reverse steps also form dF_{t+1} = dG_{t+1} Wi^T (no dfeat launch)
-#endif
-constexpr bool kLstmFusedDfeat = ML_LSTM_FUSED_DFEAT && ML_LSTM_BWD4 && !ML_LSTM_PERSISTENT;
-
 // Carve the workspace; returns total bytes (base may be null to size only).
 // lstm (may be null): recurrent policy; mb = sequences per minibatch.
 static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
@@ -198,7 +174,6 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         w.dz[l] = take(Mp * H * es);
     }
     w.dhead = take(Mp * HC * es);
-    w.lnst = (float*)take(Mp * 2 * sizeof(float));
     w.colpart = (float*)take(tiles * w.CP * sizeof(float));
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
@@ -223,7 +198,6 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         lw.dg = take(Mp * 4 * H * es);
         lw.dhout = take(Mp * H * es);
         lw.dfeat = take(Mp * H * es);
-        lw.gin = kLstmFusedGin ? nullptr : take(Mp * 4 * H * sizeof(float));
         lw.dcc = (float*)take(Mp * H * sizeof(float));
         if (LW) *LW = lw;
     }
@@ -577,8 +551,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
     const float invH = 1.0f / (float)H;
     // post-activation rows A_l (weight-gradient operands), row-major
     auto store_act = [&](int l) {
-        const bool skip = MODE == kTrunkBwd || (MODE == kFused && l == 0 && ws.a0r);
-        if (skip) return;
+        if (MODE == kTrunkBwd) return;
         T* arow = (T*)ws.a[l] + row * H;
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
@@ -626,8 +599,6 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         rstd_r[l] = rstd;
         STAMP(2 + 3 * l);
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
-        if (MODE == kFused && l == 0 && ws.a0r && w == 0 && h == 0)
-            *(float2*)(ws.lnst + 2 * row) = make_float2(mean, rstd);
         // the last layer's rows go out behind the head's weight loads (HC = 32)
         if (!ML_STORE_LATE || (l + 1 == L && (MODE != kFused || HC != 32))) store_act(l);
         if (l + 1 < L) {
@@ -1054,8 +1025,6 @@ static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_s
                                                             rec);
 }
 
-#include "ppo_rows.h"
-
 // ---------------------------------------------------------------------------
 // Weight gradients dW[i][j] = sum_m X[m][i] * Y[m][j] for every weight of the
 // policy in one launch (X, Y row-major [Mp][I] / [Mp][J], written by the step
@@ -1074,21 +1043,12 @@ struct WgJob {
     float* out;
     int64_t rps;
     int I, J, ti, tj, splits, wg0;
-    int rec;   // X is A_0 recomputed from X_0 (wgrad_tile<T, true>)
-    int zrec;  // X holds Z_0: staged as A_0 = relu(LN_0(Z_0)) (ppo_rows_kernel spill)
 };
 struct WgJobs {
     WgJob job[kMaxJobs];
     int n;
     int64_t Mp;
     int nwg, ncol, ncolx;  // weight-gradient blocks, column-sum blocks (ncolx per chunk)
-    // A_0 recompute (jobs with rec): layer-0 weight image, LayerNorm scale /
-    // bias, per-row {mean, rstd}, observation width
-    const void* w0img;
-    const float* g0;
-    const float* b0;
-    const float* lnst;
-    int D;
 };
 
 template <typename T> struct WgCfg {
@@ -1125,24 +1085,15 @@ template <> struct WgFrag<float> {
 __device__ inline void colsum_block(const WsK& ws, int bx, int c);
 __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K, float* out);
 
-// Weight-gradient tile (i0, j0) of job J over its split's rows.  REC: the X
-// operand is the first layer's post-activation A_0, recomputed chunk by chunk
-// from the gathered observations X_0 (ws.x0) and the per-row LayerNorm
-// statistics the step kernel saved (ws.lnst), instead of read back from a
-// spilled [Mp][H] copy: relu(LN_0(X_0 W_0)) with the step kernel's MFMA
-// sequence (gemm_first: k-steps in ascending order) and its LayerNorm
-// arithmetic (ln_pack_stats / ln_apply), so the operand is bit-identical.
-template <typename T, bool REC>
+// Weight-gradient tile (i0, j0) of job J over its split's rows.
+template <typename T>
 __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local, char* smem) {
     constexpr int kWgChunk = wg_chunk<T>();
     constexpr int VPC = 16 / sizeof(T);                  // elements per 16-B chunk
     constexpr int CPR = kWgTile / VPC;                   // chunks per tile row
     constexpr int PER = kWgChunk * CPR / 256;            // chunks per thread per operand
     constexpr int LD = WgCfg<T>::LD, KSTEPS = kWgChunk / MT<T>::KS;
-    constexpr int RB = kWgChunk / 32;                    // 32-row blocks per chunk (REC)
-    constexpr int XKS = REC ? kRecMaxD / RT<T>::KS : 1;  // max first-layer k-steps
     typedef __attribute__((ext_vector_type(4))) uint32_t u4;
-    typedef typename RT<T>::frag frag;
     T* lds = (T*)smem;  // [stage][operand][kWgChunk][LD]
 
     const int nt = J.ti * J.tj;
@@ -1170,45 +1121,9 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
     const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
     const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
 
-    // REC: this wave recomputes A_0 features [i0 + 32 w, i0 + 32 w + 32) of
-    // the chunk's rows; its W_0 image fragments stay in registers, the
-    // LayerNorm scale / bias of layer 0 are staged in LDS after the buffers
-    const int D = jobs.D, dks = REC ? D / RT<T>::KS : 0, h = lane >> 5, r = lane & 31;
-    frag wa[XKS];
-    float* gm = (float*)(smem + WgCfg<T>::lds);  // [2][H] (REC)
-    if constexpr (REC) {
-        const int H = J.I;
-        for (int i = tid; i < 2 * H; i += 256) gm[i] = i < H ? jobs.g0[i] : jobs.b0[i - H];
-        const T* img = (const T*)jobs.w0img + (int64_t)((i0 >> 5) + w) * dks * 64 * RT<T>::E;
-        const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
-        const int voff = lane * RT<T>::E * (int)sizeof(T);
-#pragma unroll
-        for (int s = 0; s < XKS; ++s)
-            if (s < dks) wa[s] = img_load<T>(rs, voff, s * 64 * RT<T>::E * (int)sizeof(T));
-    }
-
     // two register sets of staged rows: chunk c + 2 is in flight while chunk c
     // is multiplied out of LDS and chunk c + 1 is written to the other buffer
-    u4 rx[2][REC ? 1 : PER], ry[2][PER];
-    frag xb[2][REC ? RB : 1][XKS];  // REC: X_0 row fragments of the chunk's row blocks
-    float2 st[2][REC ? RB : 1];      // REC: {mean, rstd} of those rows
-    // Z_0 staging (J.zrec, bf16): this thread's 8 columns are fixed (cc below)
-    // -> their LayerNorm scale / bias in registers, per-row {mean, rstd} per chunk
-    constexpr bool ZR = !REC && std::is_same<T, bf16>::value;
-    const bool zrec = ZR && J.zrec;
-    float zg[ZR ? VPC : 1], zb[ZR ? VPC : 1];
-    float2 zst[2][ZR ? PER : 1];
-    if constexpr (ZR) {
-        if (zrec) {
-            const int cc0 = (tid % CPR) * VPC;
-#pragma unroll
-            for (int e = 0; e < VPC; ++e) {
-                const int col = i0 + cc0 + e < J.I ? i0 + cc0 + e : 0;
-                zg[e] = jobs.g0[col];
-                zb[e] = jobs.b0[col];
-            }
-        }
-    }
+    u4 rx[2][PER], ry[2][PER];
     auto gload = [&](int c, int set) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
@@ -1216,21 +1131,8 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
             const u4 zero = {0u, 0u, 0u, 0u};
-            if constexpr (!REC)
-                rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
+            rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
             ry[set][u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
-            if constexpr (ZR)
-                if (zrec) zst[set][u] = *(const float2*)(jobs.lnst + 2 * (mb0 + rr));
-        }
-        if constexpr (REC) {
-#pragma unroll
-            for (int b = 0; b < RB; ++b) {
-                const int64_t row = mb0 + 32 * b + r;
-#pragma unroll
-                for (int s = 0; s < XKS; ++s)
-                    if (s < dks) xb[set][b][s] = RT<T>::row(X + row * D, s, h);
-                st[set][b] = *(const float2*)(jobs.lnst + 2 * row);
-            }
         }
     };
     auto sstore = [&](int stage, int set) {
@@ -1240,40 +1142,8 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
-            if constexpr (ZR) {
-                if (zrec) {
-                    // A_0 = relu(LN_0(Z_0)) with ln_apply's operations (ln_act)
-                    typedef __bf16 bf16x8l __attribute__((ext_vector_type(8)));
-                    const bf16x8l z = __builtin_bit_cast(bf16x8l, rx[set][u]);
-                    bf16x8l a;
-#pragma unroll
-                    for (int e = 0; e < VPC; ++e)
-                        a[e] = (bf16)ln_act((float)z[e], zst[set][u].x, zst[set][u].y, zg[e], zb[e]);
-                    rx[set][u] = __builtin_bit_cast(u4, a);
-                }
-            }
-            if constexpr (!REC) *(u4*)(xs + rr * LD + cc) = rx[set][u];
+            *(u4*)(xs + rr * LD + cc) = rx[set][u];
             *(u4*)(ys + rr * LD + cc) = ry[set][u];
-        }
-        if constexpr (REC) {
-            if (i0 + 32 * w < J.I) {
-#pragma unroll
-                for (int b = 0; b < RB; ++b) {
-                    f32x16 acc[1];
-                    zero_acc<1>(acc);
-#pragma unroll
-                    for (int s = 0; s < XKS; ++s)
-                        if (s < dks) acc[0] = MT<T>::mma(wa[s], xb[set][b][s], acc[0]);
-                    typename Pk<T>::word zw[1][8], aw[1][8];
-                    f2 x2[1][8];
-                    float sum, sq;
-                    ln_pack_stats<T, 1>(acc, zw, x2, sum, sq);
-                    ln_apply<T, 1>(x2, st[set][b].x, st[set][b].y, gm, J.I, (i0 >> 5) + w, h, aw);
-                    T* xrow = xs + (32 * b + r) * LD + 32 * w;
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) Pk<T>::store4(xrow + 8 * g + 4 * h, aw[0][2 * g], aw[0][2 * g + 1]);
-                }
-            }
         }
     };
     f32x16 acc[2][2];
@@ -1299,7 +1169,6 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
     };
     gload(0, 0);
     if (nchunks > 1) gload(1, 1);
-    if constexpr (REC) __syncthreads();  // LayerNorm parameters staged
     sstore(0, 0);
     if (nchunks > 2) gload(2, 0);
     __syncthreads();
@@ -1336,9 +1205,9 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
 
 // Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
 // level of the column partials; one more (if loss_out) the loss metrics.
-template <typename T, bool REC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(REC ? 2 : ML_WG_WAVES, 8))) void wgrad_kernel(WgJobs jobs, WsK ws, HpK hp, int64_t M, int K,
-                                                    float* loss_out) {
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES, 8))) void wgrad_kernel(
+    WgJobs jobs, WsK ws, HpK hp, int64_t M, int K, float* loss_out) {
     if ((int)blockIdx.x >= jobs.nwg) {
         const int b = blockIdx.x - jobs.nwg;
         if (b < jobs.ncol) colsum_block(ws, b % jobs.ncolx, b / jobs.ncolx);
@@ -1349,14 +1218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(REC ? 2 : M
     int jb = 0;
     while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
     const WgJob& J = jobs.job[jb];
-    const int local = blockIdx.x - J.wg0;
-    if constexpr (REC && std::is_same<T, bf16>::value) {
-        if (J.rec) {
-            wgrad_tile<T, true>(jobs, J, local, smem);
-            return;
-        }
-    }
-    wgrad_tile<T, false>(jobs, J, local, smem);
+    wgrad_tile<T>(jobs, J, blockIdx.x - J.wg0, smem);
 }
 
 
@@ -1612,20 +1474,6 @@ __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K
     }
 }
 
-// MLEARN_A0_RECOMPUTE=1: A_0 is recomputed by the weight-gradient launch
-// instead of spilled by the step kernel (bf16, at least two layers,
-// D <= kRecMaxD).  Off by default: measured at the headline config the step
-// kernel gains 7 us per launch and the weight-gradient launch loses 36 us (the
-// recompute sits on its per-chunk critical path); kept for the A/B and pinned
-// bit-identical to the spill path (tests/test_gpu_fullsize.py).
-static bool a0_recompute(const mlearn_mlp_policy& p) {
-    if (p.dtype != MLEARN_DTYPE_BF16 || p.num_layers < 2 || p.obs_dim > kRecMaxD ||
-        p.obs_dim % 16 != 0)
-        return false;
-    const char* e = getenv("MLEARN_A0_RECOMPUTE");
-    return e && e[0] == '1';
-}
-
 template <typename T, int H>
 static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
                             const int32_t* mb_seq, int mb, const float* adv_st,
@@ -1637,7 +1485,6 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 #ifdef ML_STAMPS
     ws.stamps = g_stamp_buf;
 #endif
-    ws.a0r = a0_recompute(p);
     PolicyK P = make_policy_k(p);
     RolloutK R{ro.obs, ro.actions, ro.log_probs, ro.advantages, ro.returns, ro.values, ro.dones,
                ro.T, ro.bptt_len, ro.N, ro.ld ? ro.ld : ro.N};
@@ -1657,36 +1504,23 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
 
-    const bool rows = !ws.a0r && rows_ok(p);
-    ws.zs = rows && !kRowsKeepZ0;
-    if (rows) {
-        launch_rows(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
-    } else {
-        switch (p.num_layers) {
-            case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-            case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-            case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-            default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        }
+    switch (p.num_layers) {
+        case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
     if (step_only) return check_launch("ppo_minibatch_fwd_bwd");
     const int L = p.num_layers;
     WgJobs jobs{};
     jobs.n = L + 1;
     jobs.Mp = ws.Mp;
-    jobs.w0img = P.wt[0];
-    jobs.g0 = P.lns[0];
-    jobs.b0 = P.lnb[0];
-    jobs.lnst = ws.lnst;
-    jobs.D = p.obs_dim;
     int wg = 0;
     for (int l = 0; l <= L; ++l) {
         WgJob& J = jobs.job[l];
         J.I = l == L ? H : (l == 0 ? p.obs_dim : H);
         J.J = l == L ? head_cols(p) : H;
-        J.rec = l == 1 && ws.a0r;
-        J.zrec = l == 1 && ws.zs;
-        J.X = l == 0 || J.rec ? ws.x0 : ws.a[l - 1];
+        J.X = l == 0 ? ws.x0 : ws.a[l - 1];
         J.Y = l == L ? ws.dhead : ws.dz[l];
         J.out = ws.slab + ws.slab_off[l];
         J.rps = ws.rps[l];
@@ -1701,27 +1535,14 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     jobs.ncol = jobs.ncolx * kColChunks;
     {
         const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
-        if (ws.a0r) {
-            const size_t lds = WgCfg<T>::lds + 2 * H * sizeof(float);
-            static bool attr_set = false;
-            if (!attr_set) {
-                (void)hipFuncSetAttribute((const void*)wgrad_kernel<T, true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                attr_set = true;
-            }
-            hipLaunchKernelGGL((wgrad_kernel<T, true>), dim3(blocks), dim3(256), lds, s, jobs, ws,
-                               hp, M, p.actions.num_groups, loss_out);
-        } else {
-            static bool attr_set = false;
-            if (!attr_set) {
-                (void)hipFuncSetAttribute((const void*)wgrad_kernel<T, false>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)WgCfg<T>::lds);
-                attr_set = true;
-            }
-            hipLaunchKernelGGL((wgrad_kernel<T, false>), dim3(blocks), dim3(256), WgCfg<T>::lds,
-                               s, jobs, ws, hp, M, p.actions.num_groups, loss_out);
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)wgrad_kernel<T>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)WgCfg<T>::lds);
+            attr_set = true;
         }
+        hipLaunchKernelGGL((wgrad_kernel<T>), dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws,
+                           hp, M, p.actions.num_groups, loss_out);
     }
     LayoutK Lk = make_layout(p);
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
@@ -1731,8 +1552,8 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 
 // ---------------------------------------------------------------------------
 // Recurrent update: the LSTM scan over the minibatch's sequences
-// (LSTM.sequence, rnn.py:81-111) and its reverse (BPTT), one persistent
-// launch per direction (lstm_scan.h).  Rows f = t * mb + m.
+// (LSTM.sequence, rnn.py:81-111) and its reverse (BPTT), one launch per
+// time step and direction (lstm_scan.h).  Rows f = t * mb + m.
 // ---------------------------------------------------------------------------
 #include "lstm_scan.h"
 
@@ -1780,91 +1601,18 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // trunk forward over every row (the LSTM input F = A_{L-1})
     step(std::integral_constant<int, kTrunkFwd>{});
     const T* feat = (const T*)ws.a[L - 1];
-    constexpr int KSH = H / RT<T>::KS, NKS = 4 * H / RT<T>::KS;
-    constexpr size_t FR = sizeof(typename RT<T>::frag);
-    const bool fused_gin = kLstmFusedGin;
-    // hoisted input product Gin = F Wi over every row (full grid), unless the
-    // forward steps compute it
-    if (!fused_gin) {
-        const size_t lds = (size_t)KSH * 64 * FR;
-        auto k = lstm_gin_kernel<T, H>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, feat,
-                           (float4*)lw.gin);
-    }
     // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
-    // workgroups (ML_LSTM_PERSISTENT: one persistent launch, a workgroup per
-    // 32 sequences)
-    if (!ML_LSTM_PERSISTENT) {
-        for (int t = 0; t < bptt; ++t) {
-            if (ML_LSTM_FWD4)
-                hipLaunchKernelGGL((lstm_fwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0,
-                                   s, RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
-                                   (const T*)start_c, lw, t);
-            else
-                hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
-                                   s, RK, R, mb_seq, mb, (const float4*)lw.gin, (const T*)start_h,
-                                   (const T*)start_c, lw, t, fused_gin ? feat : nullptr);
-        }
-    } else {
-        const size_t lds = (size_t)KSH * 64 * FR;
-        auto k = lstm_fwd_scan_kernel<T, H>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb,
-                           (const float4*)lw.gin, (const T*)start_h, (const T*)start_c, lw);
-    }
+    // workgroups (the input product F_t Wi inside each step)
+    for (int t = 0; t < bptt; ++t)
+        hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s, RK,
+                           R, mb_seq, mb, (const T*)start_h, (const T*)start_c, lw, t, feat);
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});
-    // reverse scan
+    // reverse scan: dh_t and dF_{t+1} per step, then dF_0 from dG_0
     const int cp0 = L * 2 * H + head_cols(p);
-    if (!ML_LSTM_PERSISTENT) {
-        for (int t = bptt - 1; t >= 0; --t) {
-            if (ML_LSTM_BWD4)
-                hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0,
-                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t,
-                                   (int)kLstmFusedDfeat);
-            else
-                hipLaunchKernelGGL((lstm_bwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0,
-                                   s, RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
-        }
-        if (kLstmFusedDfeat)  // dF_0 from dG_0 (every other dF_{t+1} came with step t)
-            hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
-                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, -1, 1);
-    } else {
-        const size_t lds = (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
-        auto k = lstm_bwd_scan_kernel<T, H>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(k, dim3(mb / 32), dim3(scan_threads<H>()), lds, s, RK, R, mb_seq, mb, lw,
-                           ws.colpart, ws.CP, cp0);
-    }
-    // hoisted d-feature product dF = dG Wi^T over every row (full grid),
-    // unless the reverse steps formed it
-    if (!kLstmFusedDfeat) {
-        const size_t lds = (size_t)NKS * 64 * FR;
-        auto k = lstm_dfeat_kernel<T, H>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(k, dim3((unsigned)(M / 32)), dim3(scan_threads<H>()), lds, s, RK, lw);
-    }
+    for (int t = bptt - 1; t >= -1; --t)
+        hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
+                           RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});
     // weight gradients: trunk, head (from the LSTM outputs), Wi, Wh
@@ -1890,7 +1638,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     jobs.ncolx = (ws.CP + 255) / 256;
     jobs.ncol = jobs.ncolx * kColChunks;
     {
-        auto k = wgrad_kernel<T, false>;
+        auto k = wgrad_kernel<T>;
         static bool attr_set = false;
         if (!attr_set) {
             (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -101,7 +101,7 @@ class RolloutOut(Structure):  # mlearn_rollout_out
                 ("env_returns_trace", c_void_p), ("bootstrap", c_void_p),
                 ("env_returns", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
                 ("T", c_int32), ("bptt_len", c_int32), ("ld", c_int64), ("gamma", c_float),
-                ("pad", c_int32)]
+                ("max_workgroups", c_int32)]
 
 
 _S = c_void_p  # hipStream_t
@@ -149,6 +149,8 @@ _SIGNATURES = {
                                             _P, c_int64,
                                             POINTER(RolloutOut), c_uint32, c_uint32, _P,
                                             c_uint32, POINTER(DummyEnv), _S]),
+    "mlearn_policy_rollout_workgroups": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm), c_int64,
+                                                   c_int32]),
     "mlearn_policy_evaluate": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P, _S]),
     "mlearn_lstm_policy_evaluate": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                               _P, c_int64, _P, _P, _P, _P, _S]),

@@ -43,6 +43,14 @@ def _tn(x, T, N, dtype):
     return x.contiguous()
 
 
+def _gamma_lambda(cfg):
+    """``cfg.gamma * cfg.gae_lambda`` as algo_common.py:120 forms it: a product
+    of two Python floats (double precision), rounded to f32 once where it
+    meets the f32 advantages (JAX weak typing) -- here by the ctypes float
+    argument of mlearn_gae_f32."""
+    return float(cfg.gamma) * float(cfg.gae_lambda)
+
+
 def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=None,
                        out_ret=None, value_norm=None, norm_cols=0):
     """algo_common.py:84-130 (+ returns = adv + values, rollouts.py:761-769).
@@ -67,18 +75,18 @@ def compute_advantages(cfg, rewards, values, dones, bootstrap_values, out_adv=No
             raise ValueError("the value normaliser's statistics need materialised returns")
         nat.check(nat.lib().mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b),
                                            nat.ptr(adv), None, T, N, float(cfg.gamma),
-                                           float(cfg.gae_lambda), nat.stream_handle()), "gae")
+                                           _gamma_lambda(cfg), nat.stream_handle()), "gae")
         return adv, None
     ret = out_ret if out_ret is not None else torch.empty_like(adv)
     if value_norm is not None:
         nat.check(nat.lib().mlearn_gae_vnorm_f32(
             nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b), nat.ptr(value_norm),
             int(norm_cols or N), nat.ptr(adv), nat.ptr(ret), T, N, float(cfg.gamma),
-            float(cfg.gae_lambda), nat.stream_handle()), "gae_vnorm")
+            _gamma_lambda(cfg), nat.stream_handle()), "gae_vnorm")
         return adv, ret
     nat.check(nat.lib().mlearn_gae_f32(nat.ptr(r), nat.ptr(v), nat.ptr(d), nat.ptr(b),
                                        nat.ptr(adv), nat.ptr(ret), T, N, float(cfg.gamma),
-                                       float(cfg.gae_lambda), nat.stream_handle()), "gae")
+                                       _gamma_lambda(cfg), nat.stream_handle()), "gae")
     return adv, ret
 
 

@@ -68,14 +68,6 @@ class RolloutConfig:  # rollouts.py:28-134 (self-play / single-policy path)
         )
 
 
-def _whole_rollout():
-    """The built-in sim's rollout as one launch per policy
-    (mlearn_policy_rollout_env); MLEARN_WHOLE_ROLLOUT=0 keeps one launch per
-    step with the sim step fused into it (mlearn_policy_rollout_step_env)."""
-    import os
-    return os.environ.get("MLEARN_WHOLE_ROLLOUT", "1") != "0"
-
-
 class RolloutState:  # rollouts.py:171-309
     def __init__(self, cfg, step_fn, sim_state, cur_obs, prng_key, rnn_states, sim_ctrl,
                  env_returns, counters, policy_assignments, native_step=None):
@@ -226,7 +218,18 @@ class RolloutManager:  # rollouts.py:373-826
     contiguous env columns [p*B, (p+1)*B) of the rank's N envs (the self-play
     split of pbt_init_matchmaking, pbt.py:130-133) and writes those columns
     of the shared [T][N] store, so the sim steps all N envs at once and GAE
-    runs over the whole store in one launch."""
+    runs over the whole store in one launch.
+
+    Launch shape of the built-in sim's rollout (same bits in every form):
+    ``whole_rollout`` (default True) runs every step and the bootstrap in one
+    launch per policy (mlearn_policy_rollout_env); False issues one
+    rollout_step_env call per step from the host.  ``rollout_workgroups`` is
+    that launch's mlearn_rollout_out.max_workgroups: 0 one workgroup per
+    resident slot, > 0 at most that many (env tiles in series), < 0 the
+    entry's own per-step launches."""
+
+    whole_rollout = True
+    rollout_workgroups = 0
 
     def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_states, env_offset=0):
         self.train_cfg = train_cfg
@@ -402,7 +405,7 @@ class RolloutManager:  # rollouts.py:373-826
         posts = [None] * self.P  # post-step of env step t-1, fused into the policy launches of t
         sim = rollout_state.native_step
         obs0 = self.prep_obs(rollout_state.cur_obs)
-        if sim is not None and obs0.data_ptr() == sim.obs.data_ptr() and _whole_rollout():
+        if sim is not None and obs0.data_ptr() == sim.obs.data_ptr() and self.whole_rollout:
             # the built-in sim: every step + the bootstrap in one launch per policy
             for p, ps in enumerate(self.policies):
                 c = slice(p * B, (p + 1) * B)
@@ -488,6 +491,7 @@ class RolloutManager:  # rollouts.py:373-826
                 o.start_c = s.start_c.data_ptr() + c0 * self.R * es
             o.T, o.bptt_len, o.ld, o.gamma = self.T, self.bptt, self.N, gamma
             self._routs[key] = o
+        o.max_workgroups = int(self.rollout_workgroups)
         return o
 
     def _finish(self, train_state_mgr, rollout_state, metrics, user_hooks):

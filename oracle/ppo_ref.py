@@ -52,13 +52,18 @@ def rnd(x, mode, ad=np.float64):
 def gae_f32(rewards, values, dones, bootstrap, gamma, lam):
     """compute_advantages (algo_common.py:84-130) + returns = adv + values
     (rollouts.py:761-769), in float32 with the reference's operation order
-    (no fused multiply-add): bit-exact twin of the HIP kernel."""
+    (no fused multiply-add): bit-exact twin of the HIP kernel.
+
+    gamma / lam are the config's Python floats.  The constant gamma * lambda
+    is their double-precision product rounded to f32 once (algo_common.py:120
+    multiplies the Python floats first, rollouts.py:406; JAX's weak typing
+    then rounds to the f32 advantage dtype), NOT f32(gamma) * f32(lambda)."""
     r = np.asarray(rewards, np.float32)
     v = np.asarray(values, np.float32)
     d = np.asarray(dones).astype(bool)
     T = r.shape[0]
     g = np.float32(gamma)
-    gl = np.float32(np.float32(gamma) * np.float32(lam))
+    gl = np.float32(float(gamma) * float(lam))
     nv = np.asarray(bootstrap, np.float32).copy()
     na = np.zeros_like(nv)
     adv = np.empty_like(r)

@@ -144,3 +144,54 @@ def test_population_policy_block_8192(gpu):
     assert int(tss[1].step.item()) == B // mb
     last = mgr.metrics.last(policy=1)
     np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
+
+
+def test_headline_rollout_tiles_in_series(gpu):
+    """The headline (BASELINE metric) rollout: 65,536 envs = 2,048 env tiles
+    on fewer resident workgroups, so mlearn_policy_rollout_env runs several
+    tiles in series per workgroup, reusing the parameters it staged in LDS
+    once.  Env tiles of the second and third rounds (and the last tile) are
+    replayed on the oracle env + policy: obs / rewards / dones / GAE bit-exact,
+    values / log-probs within the bf16 tolerance, sampled actions equal to the
+    oracle's wherever the Gumbel margin is clear."""
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    import madrona_learn as ml
+    from tests.test_gpu_train import make_policy
+    N, mb = 65536, 2048
+    env = DummyVecEnv(N, D, 6, seed=6, device=gpu)
+    cfg = _cfg(N, mb, seed=13)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.bfloat16, H),
+                           use_graph=False)
+    ps = mgr.state.policy_states
+    rm = mgr.rollout_mgr
+    grid = nat.lib().mlearn_policy_rollout_workgroups(ps.desc, None, N, 0)
+    tiles = N // 32
+    assert 0 < grid < tiles, (grid, tiles)
+    per = -(-tiles // grid)
+    assert per >= 2
+    p0 = ps.params.cpu().numpy().astype(np.float64)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = rm.store
+    lay = ref.param_layout(D, H, 2, 26)
+    picks = [grid + 3, tiles - 1] + ([2 * grid + 5] if 2 * grid + 5 < tiles else [])
+    for tile in picks:
+        e0 = tile * 32
+        c = slice(e0, e0 + 32)
+        oenv = onat.Env(32, D, env.k0, env.k1, e0)
+        oenv.reset()
+        acts = s.actions[:, c].cpu().numpy()
+        ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="bf16",
+                            gamma=cfg.gamma, actions_override=acts)
+        _check_store(s, ro, c)
+        gum = np.stack([onat.gumbel_table(*mgr.rollout.prng_key, t, e0, 32, 26)
+                        for t in range(T)])
+        noisy = ro["logits"] + gum
+        off = 0
+        for g, nb in enumerate(BUCKETS):
+            sl = noisy[..., off:off + nb]
+            srt = np.sort(sl, -1)
+            clear = (srt[..., -1] - srt[..., -2]) > 1e-2
+            assert np.array_equal(np.argmax(sl, -1)[clear], acts[..., g][clear]), (tile, g)
+            off += nb

@@ -203,35 +203,3 @@ def test_value_loss_variants(gpu, mode, dtype, clip_vl, huber, ties):
         ob, _ = ps.layout["hb"]
         np.testing.assert_allclose(g[ob + A], gflat[ob + A], rtol=1e-5 if mode == "f32" else 2e-2,
                                    atol=1e-7)
-
-
-@pytest.mark.parametrize("T,N,D,H,L,mb,bptt", [
-    (32, 8192, 64, 256, 2, 2048, 32),   # headline minibatch (65,536 rows)
-    (32, 96, 32, 128, 3, 37, 16),       # ragged rows (592 -> 640 padded), D = 32, 3 layers
-])
-def test_a0_recompute_bit_identical(gpu, monkeypatch, T, N, D, H, L, mb, bptt):
-    """The weight-gradient launch recomputes the first layer's post-activation
-    A_0 = relu(LN_0(X_0 W_0)) from the gathered observations and the step
-    kernel's per-row LayerNorm statistics instead of reading a spilled copy
-    (bf16): the gradient and the loss metrics must equal the spill path's
-    bit for bit (MLEARN_A0_RECOMPUTE=0)."""
-    ps = make_policy_state(gpu, D, H, L, torch.bfloat16, seed=41)
-    perturb(ps, 42, scale=0.2)
-    rng = np.random.default_rng(43)
-    nseq = (T // bptt) * N
-    seqs = rng.permutation(nseq)[:mb].astype(np.int32)
-    st, rows = _minibatch_store(rng, ps, T, N, D, "bf16", seqs, bptt)
-    s = _device_store(gpu, st, torch.bfloat16)
-    adv = ref.gather_minibatch(st, rows)["advantages"].astype(np.float64)
-    stats = (adv.mean(), adv.var())
-    # the A_0 recompute is a mode of ppo_step_kernel: keep the headline shape
-    # off the row-split kernel (tests/test_gpu_rows.py pins that one)
-    monkeypatch.setenv("MLEARN_ROWS", "0")
-    monkeypatch.setenv("MLEARN_A0_RECOMPUTE", "0")
-    g0, o0 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
-    monkeypatch.setenv("MLEARN_A0_RECOMPUTE", "1")
-    g1, o1 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
-    assert np.all(np.isfinite(g1)) and np.abs(g1).max() > 0
-    assert np.array_equal(g0.view(np.uint32), g1.view(np.uint32)), \
-        f"{np.count_nonzero(g0 != g1)} gradient elements differ"
-    assert np.array_equal(o0.view(np.uint32), o1.view(np.uint32))

@@ -44,22 +44,40 @@ def _manager(gpu, fused, dtype, N, H, mb, P=1, lstm=False, use_graph=False):
     return env, ml.init_training(gpu, cfg, fns, pol, use_graph=use_graph)
 
 
-@pytest.mark.parametrize("mode", ["one_launch", "c_per_step", "py_per_step"])
+@pytest.mark.parametrize("mode", ["one_launch", "multi_tile", "c_per_step", "py_per_step"])
 @pytest.mark.parametrize("dtype,N,H,mb,P,lstm,graph", [
     (torch.float32, 80, 64, 16, 1, False, False),    # partial last workgroup (80 = 2.5 x 32)
     (torch.bfloat16, 1024, 256, 256, 1, False, True),
     (torch.float32, 128, 64, 16, 2, False, True),     # population: one launch per policy
     (torch.bfloat16, 128, 256, 32, 1, True, False),   # LSTM H = 256: carry, start states, clears
     (torch.float32, 64, 64, 32, 1, True, False)])     # LSTM carry + done clears
-def test_fused_env_step_is_bit_identical(gpu, monkeypatch, mode, dtype, N, H, mb, P, lstm, graph):
+def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, graph):
     """one_launch: the whole rollout + bootstrap in one launch per policy
-    (mlearn_policy_rollout_env); c_per_step: the same entry's per-step
-    launches (MLEARN_ROLLOUT_PER_STEP=1);
+    (mlearn_policy_rollout_env, one workgroup per env tile here);
+    multi_tile: the same launch capped at 2 workgroups
+    (mlearn_rollout_out.max_workgroups = 2), so every workgroup runs several
+    env tiles in series with the parameters it staged in LDS once (the
+    headline's 2048 tiles on 768 resident workgroups take this branch);
+    c_per_step: the same entry's per-step launches (max_workgroups = -1);
     py_per_step: one rollout_step_env call per step from the host."""
-    monkeypatch.setenv("MLEARN_WHOLE_ROLLOUT", "0" if mode == "py_per_step" else "1")
-    monkeypatch.setenv("MLEARN_ROLLOUT_PER_STEP", "1" if mode == "c_per_step" else "0")
+    from madrona_learn import _native as nat
+    from madrona_learn.rollouts import RolloutManager
     env_a, a = _manager(gpu, True, dtype, N, H, mb, P, lstm, graph)
     env_b, b = _manager(gpu, False, dtype, N, H, mb, P, lstm, graph)
+    rm = a.rollout_mgr
+    rm.whole_rollout = mode != "py_per_step"
+    rm.rollout_workgroups = {"multi_tile": 2, "c_per_step": -1}.get(mode, 0)
+    ps = rm.policies[0]
+    grid = nat.lib().mlearn_policy_rollout_workgroups(ps.desc, ps.lstm_desc, rm.B,
+                                                      rm.rollout_workgroups)
+    tiles = (rm.B + 31) // 32
+    if mode == "multi_tile":
+        assert grid == 2 and tiles > 2, (grid, tiles)
+    elif mode == "c_per_step":
+        assert grid == -1
+    elif mode == "one_launch":
+        assert grid == tiles
+    assert RolloutManager.rollout_workgroups == 0  # instance setting only
     for _ in range(2):
         a.update_iter()
         b.update_iter()

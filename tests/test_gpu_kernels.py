@@ -72,6 +72,32 @@ def test_gae_bitexact(gpu, T, N):
     assert np.array_equal((adv2 + torch.from_numpy(v).to(gpu)).cpu().numpy(), er)
 
 
+@pytest.mark.parametrize("gamma,lam", [(0.998, 0.95), (0.9, 0.8), (0.9999, 0.97), (0.95, 1.0)])
+def test_gae_gamma_lambda_constant(gpu, gamma, lam):
+    """The gamma * lambda constant is the reference's single rounding
+    (algo_common.py:120 multiplies the Python floats, rollouts.py:406): at
+    0.998 / 0.95 it differs by one ulp from f32(gamma) * f32(lambda), and the
+    advantages must follow the reference's, bit for bit."""
+    from madrona_learn.algo_common import compute_advantages
+
+    class C:
+        steps_per_update = 32
+        gae_lambda = lam
+
+    C.gamma = gamma
+    rng = np.random.default_rng(17)
+    T, N = 32, 4096
+    r = rng.standard_normal((T, N)).astype(np.float32)
+    v = rng.standard_normal((T, N)).astype(np.float32)
+    d = rng.random((T, N)) < 0.03
+    b = rng.standard_normal(N).astype(np.float32)
+    adv, ret = compute_advantages(C, torch.from_numpy(r).to(gpu), torch.from_numpy(v).to(gpu),
+                                  torch.from_numpy(d).to(gpu), torch.from_numpy(b).to(gpu))
+    ea, er = ref.gae_f32(r, v, d, b, gamma, lam)
+    assert np.array_equal(adv.cpu().numpy(), ea)
+    assert np.array_equal(ret.cpu().numpy(), er)
+
+
 def test_returns_bitexact(gpu):
     from madrona_learn.algo_common import compute_returns
 

@@ -37,7 +37,7 @@ def test_gae_inverts_normalised_values(gpu):
     ret = torch.empty_like(adv)
     nat.check(nat.lib().mlearn_gae_vnorm_f32(
         nat.ptr(tr), nat.ptr(tv), nat.ptr(td), nat.ptr(tb), nat.ptr(te), B,
-        nat.ptr(adv), nat.ptr(ret), T, N, 0.99, 0.95, nat.stream_handle()), "gae_vnorm")
+        nat.ptr(adv), nat.ptr(ret), T, N, 0.99, 0.99 * 0.95, nat.stream_handle()), "gae_vnorm")
     torch.cuda.synchronize()
     cols = np.repeat(np.arange(P), B)
     vi = np.empty_like(v)

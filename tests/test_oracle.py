@@ -122,6 +122,23 @@ def test_gae_f32_matches_f64():
     np.testing.assert_allclose(a32, a64, rtol=1e-5, atol=1e-5)
 
 
+def test_gae_gamma_lambda_single_rounding():
+    """algo_common.py:120 forms cfg.gamma * cfg.gae_lambda from Python floats
+    (one f64 product, rounded to f32 once by JAX's weak typing).  The oracle
+    must use that constant: with no dones, lambda = 1 recursion check on one
+    step isolates it (A_T-1 = r + g * boot - v; A_T-2 = td + gl * A_T-1)."""
+    g, lam = 0.998, 0.95
+    gl_ref = np.float32(g * lam)
+    assert gl_ref != np.float32(np.float32(g) * np.float32(lam))  # the two roundings differ
+    r = np.array([[0.0], [0.0]], np.float32)
+    v = np.array([[0.0], [0.0]], np.float32)
+    d = np.zeros((2, 1), bool)
+    b = np.array([1.0], np.float32)
+    adv, _ = ref.gae_f32(r, v, d, b, g, lam)
+    assert adv[1, 0] == np.float32(g)
+    assert adv[0, 0] == np.float32(gl_ref * np.float32(g))
+
+
 def test_discounted_returns():
     r, v, d, b = _rvd(pdone=0.0)
     out = ref.discounted_returns_f32(r, d, b, 1.0)
