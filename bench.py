@@ -427,7 +427,7 @@ def _time_updates(mgr, steps, warmup):
 
 def emulate_world(args):
     """Strong-scaling projection on one GPU: rank 0's share of a W-rank
-    headline job (MLEARN_EMULATE_WORLD, madrona_learn.dist), then the N=1
+    headline job (madrona_learn.dist.set_emulated_world), then the N=1
     headline in the same process.  The share's per-update time bounds the
     W-GPU time from below by everything but the xGMI transfer of the
     collectives (each is issued as a one-rank RCCL all-reduce at its place
@@ -438,14 +438,15 @@ def emulate_world(args):
         raise SystemExit(f"--emulate-world {W} must divide {total} envs and {MB} seqs")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    os.environ["MLEARN_EMULATE_WORLD"] = str(W)
+    from madrona_learn import dist as mdist
+    mdist.set_emulated_world(W)
     mgr = make(dev, total, 0, total // W, use_graph=not args.no_graph,
                fused_sim=not args.separate_sim)
     coll = mgr.dp.collectives
     t_w = _time_updates(mgr, args.steps, args.warmup)
     del mgr
     torch.cuda.empty_cache()
-    os.environ.pop("MLEARN_EMULATE_WORLD")
+    mdist.set_emulated_world(1)
     mgr = make(dev, total, 0, total, use_graph=not args.no_graph,
                fused_sim=not args.separate_sim)
     t_1 = _time_updates(mgr, args.steps, args.warmup)

@@ -335,6 +335,13 @@ static int64_t optim_ws_doubles(const LayoutK& k) {
     return kNormBlocks + nblk * kMaxSlots + 8 + kMaxSlots + 8;
 }
 
+// Projection slot counts with a project_kernel instantiation: 2 L (trunk
+// kernels + LayerNorms, L <= MLEARN_MAX_LAYERS) and 2 L + 8 (the LSTM gate
+// kernels); optim_launch checks nslot against it before anything launches.
+constexpr int kMaxProjSlots = 16;
+static_assert(kMaxSlots <= kMaxProjSlots, "a projection slot count has no project_kernel instantiation");
+static bool project_slots_ok(int nslot) { return nslot >= 2 && nslot <= kMaxProjSlots && nslot % 2 == 0; }
+
 template <typename T>
 static void launch_project(int nslot, dim3 grid, hipStream_t s, const LayoutK& Lk, const CopiesK& C,
                            const mlearn_optim_state* st, const double* ppart, int ablk) {
@@ -353,6 +360,7 @@ static void launch_project(int nslot, dim3 grid, hipStream_t s, const LayoutK& L
         ML_PROJ(12)
         ML_PROJ(14)
         ML_PROJ(16)
+        default: break;  // unreachable: project_slots_ok(nslot) was required before any launch
     }
 #undef ML_PROJ
 }
@@ -374,6 +382,9 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
                    st->step && workspace,
                "optim_step: null pointer");
     ML_REQUIRE(st->max_grad_norm > 0 && st->lr >= 0, "optim_step: bad hyperparameters");
+    ML_REQUIRE(project_slots_ok(2 * Lk.L + (Lk.lstm_H ? 8 : 0)),
+               "optim_step: %d projection slots (layers %d) have no projection kernel",
+               2 * Lk.L + (Lk.lstm_H ? 8 : 0), Lk.L);
     const int64_t nblk = (Lk.total + 255) / 256;
     const int ablk = (int)(nblk < kAdamBlocks ? nblk : kAdamBlocks);
     double* gpart = (double*)workspace;
@@ -390,12 +401,12 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
         hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
                            Lk.total, gpart);
     }
+    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     const int64_t nit = (Lk.total + (int64_t)ablk * 256 - 1) / ((int64_t)ablk * 256);
     auto adam = nit <= 1 ? adam_kernel<1> : nit <= 2 ? adam_kernel<2> : nit <= 4 ? adam_kernel<4> : adam_kernel<8>;
     hipLaunchKernelGGL(adam, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step, norm_part,
                        nparts, st->lr, st->b1, st->b2, st->eps, st->max_grad_norm, ppart);
-    const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     if (dtype == MLEARN_DTYPE_BF16)
         launch_project<bf16>(nslot, dim3((unsigned)nblk), s, Lk, C, st, (const double*)ppart, ablk);
     else

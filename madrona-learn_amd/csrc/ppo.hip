@@ -47,6 +47,7 @@ struct HpK {
     int metrics;  // reduce the loss metrics (only the minibatch whose metrics are recorded)
     float loss_scale;
     float inv_sk, inv_s;
+    int row_blocks;  // mlearn_ppo_hparams.row_blocks (host-side launch choice)
 };
 
 constexpr int kLossSlots = 20;   // per tile doubles
@@ -61,7 +62,8 @@ constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 // weight-gradient K chunk (rows of the minibatch staged per LDS stage); f32 keeps 32
 template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_CHUNK : 32; }
 static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
-constexpr int kRowAlign = 64;    // Mp granularity
+constexpr int kRowAlign = 128;   // Mp granularity of the MLP update (a multiple of every wide row tile)
+constexpr int kRowAlignLstm = 64;  // the recurrent update (its scans write exactly M = mb * bptt rows)
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif
@@ -154,7 +156,8 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
                     const mlearn_lstm* lstm = nullptr, int64_t mb = 0, LstmWsK* LW = nullptr) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
-    const int64_t Mp = (M + kRowAlign - 1) / kRowAlign * kRowAlign;
+    const int64_t al = lstm ? kRowAlignLstm : kRowAlign;
+    const int64_t Mp = (M + al - 1) / al * al;
     const int64_t tiles = Mp / 32;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -1000,7 +1003,7 @@ template <typename T, int H, int L, int MODE, int HC>
 static void launch_step_hc(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                            int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                            hipStream_t s, const RecK& rec) {
-    // ntiles = Mp / 32 is even (Mp is a multiple of kRowAlign = 64)
+    // ntiles = Mp / 32 is even (Mp is a multiple of 64)
     constexpr int RTW = (MODE == kFused && StepCfg<H>::W * ML_STEP_RTW <= 16) ? ML_STEP_RTW : 1;
     auto k = ppo_step_kernel<T, H, L, MODE, HC, RTW>;
     static bool attr_set = false;  // once per instantiation (kept out of graph capture)
@@ -1023,6 +1026,61 @@ static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_s
     else
         launch_step_hc<T, H, L, MODE, MLEARN_HEAD_COLS_MAX>(P, R, mb_seq, mb, M, adv_st, hp, ws, s,
                                                             rec);
+}
+
+#include "ppo_wide.h"
+
+static int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+// The feed-forward policy's fused minibatch step on the wide-tile kernel:
+// RB row blocks per workgroup (wide_rb); sets ws.ntiles to the workgroup
+// count (the rows of ws.colpart / ws.loss_part the kernel writes).
+template <typename T, int H, int L, int HC, int RB>
+static void launch_wide_rb(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                           int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
+    auto k = ppo_wide_kernel<T, H, L, HC, RB>;
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    ws.ntiles = (int)(ws.Mp / (32 * RB));
+    const size_t lds = wide_lds<T, H, L, HC, RB>(P.D);
+    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(64 * (H / 32)), lds, s, P, R, mb_seq, mb, M, adv_st,
+                       hp, ws);
+}
+template <typename T, int H, int L, int HC>
+static void launch_wide_hc(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                           int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
+    const int rbmax = sizeof(T) == 2 ? 4 : 2;
+    const int rb = hp.row_blocks > 0 ? (hp.row_blocks < rbmax ? hp.row_blocks : rbmax)
+                                     : wide_rb<T>(ws.Mp, device_cus());
+    if constexpr (sizeof(T) == 2) {
+        if (rb == 4) return launch_wide_rb<T, H, L, HC, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
+    }
+    if (rb >= 2) return launch_wide_rb<T, H, L, HC, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
+    // fewer than two 32-row blocks per CU (e.g. a data-parallel rank's
+    // minibatch slice): one 32-row tile per workgroup, two workgroups per CU
+    launch_step_hc<T, H, L, kFused, HC>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, RecK{});
+}
+template <typename T, int H, int L>
+static void launch_wide(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                        int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
+    if (P.HC == MLEARN_HEAD_COLS)
+        launch_wide_hc<T, H, L, MLEARN_HEAD_COLS>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
+    else
+        launch_wide_hc<T, H, L, MLEARN_HEAD_COLS_MAX>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1503,12 +1561,13 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.metrics = loss_out != nullptr;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
+    hp.row_blocks = h.row_blocks;
 
     switch (p.num_layers) {
-        case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 1: launch_wide<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 2: launch_wide<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 3: launch_wide<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        default: launch_wide<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
     if (step_only) return check_launch("ppo_minibatch_fwd_bwd");
     const int L = p.num_layers;
@@ -1689,6 +1748,8 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro && mb_seq && adv_stats && hp && workspace, "ppo: null pointer");
     ML_REQUIRE(step_only || grad, "ppo: null grad");
     ML_REQUIRE(mb_size >= 1, "ppo: mb_size must be >= 1");
+    ML_REQUIRE(hp->row_blocks >= 0 && hp->row_blocks <= 4 && hp->row_blocks != 3,
+               "ppo: row_blocks must be 0, 1, 2 or 4 (got %d)", hp->row_blocks);
     ML_REQUIRE(ro->N >= 1 && ro->N < (1ll << 31) && (int64_t)mb_size * ro->bptt_len < (1ll << 31),
                "ppo: N and rows per minibatch must be < 2^31");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");

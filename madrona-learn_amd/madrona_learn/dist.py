@@ -27,12 +27,32 @@ def _initialized():
     return dist.is_available() and dist.is_initialized()
 
 
+_EMULATED_WORLD = 1
+
+
+def set_emulated_world(w):
+    """Benchmark-only (bench.py --emulate-world W, one process, one GPU): the
+    next init_training runs rank 0's share of a W-rank job on this GPU, with
+    a one-rank RCCL communicator standing in for the group's collectives and
+    the loss scaled by 1 / W.  That trains on 1 / W of the gradient, so it is
+    an explicit call (never an environment variable that could leak into a
+    real run) and is refused when a process group exists.  w = 1 turns it
+    off."""
+    global _EMULATED_WORLD
+    w = int(w)
+    if w > 1 and _initialized():
+        raise RuntimeError("emulated world: a torch.distributed process group is initialised; "
+                           "emulation is for single-process benchmarks only")
+    if w > 1:
+        import sys
+        print(f"madrona_learn: EMULATING rank 0 of a {w}-rank job on one GPU (benchmark "
+              f"projection; the update trains on 1/{w} of the gradient)", file=sys.stderr)
+    _EMULATED_WORLD = max(w, 1)
+
+
 def emulated_world():
-    """MLEARN_EMULATE_WORLD=W (single process, no process group): run rank 0's
-    share of a W-rank job on this GPU (bench.py --emulate-world), with a
-    one-rank RCCL communicator standing in for the group's collectives."""
-    w = int(os.environ.get("MLEARN_EMULATE_WORLD", "1") or 1)
-    return w if w > 1 and not _initialized() else 1
+    """The world size set_emulated_world asked for (1: no emulation)."""
+    return _EMULATED_WORLD if _EMULATED_WORLD > 1 and not _initialized() else 1
 
 
 class DataParallel:
@@ -189,6 +209,9 @@ def policy_placement(num_policies):
     Every rank calls this in the same order (new_group is collective)."""
     rank, W = world()
     P = int(num_policies)
+    if P > 1 and emulated_world() > 1:
+        raise ValueError("emulated world (set_emulated_world): populations are not emulated; "
+                         "run a real process group")
     if P == 1:
         ew = emulated_world()
         return [0], (EmulatedDataParallel(ew) if ew > 1 else DataParallel())

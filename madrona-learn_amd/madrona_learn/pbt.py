@@ -387,9 +387,13 @@ def _policy_tensors(ps):
     return t + ps.episode_score.tensors()
 
 
-def snapshot_policy(tsm, src_pid, past, P):
+def snapshot_policy(tsm, src_pid, past, P, fitness=None):
     """past := train policy src_pid's policy state on every rank (a broadcast
-    from src's first holder)."""
+    from src's first holder).  ``fitness`` = the (mean, var, N) arrays of
+    gather_fitness: the slot's MovingEpisodeScore takes src's POOLED estimate,
+    so that under data parallelism (G > 1 holders, each scoring its own env
+    shard) the past slots compare with the pooled train fitness on the same
+    footing in pbt_past_update (not the first holder's shard alone)."""
     rank, W = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
     root = _holders(src_pid, P, W)[0]
     if rank == root:
@@ -399,6 +403,12 @@ def snapshot_policy(tsm, src_pid, past, P):
     if W > 1:
         for t in past.tensors():
             dist.broadcast(t, root)
+    if fitness is not None:
+        mean, var, N = fitness
+        e = past.episode_score
+        e.mean.fill_(float(mean[src_pid]))
+        e.var.fill_(float(var[src_pid]))
+        e.N.fill_(int(round(float(N[src_pid]))))
 
 
 def init_past_policies(cfg, tsm):
@@ -407,9 +417,10 @@ def init_past_policies(cfg, tsm):
     P, Q = int(cfg.pbt.num_train_policies), int(cfg.pbt.num_past_policies)
     like = tsm.policy_list[0]
     tsm.past_list = []
+    fit = gather_fitness(tsm, P) if Q else None
     for j in range(Q):
         pp = PastPolicy(P + j, like)
-        snapshot_policy(tsm, j % P, pp, P)
+        snapshot_policy(tsm, j % P, pp, P, fitness=fit)
         tsm.past_list.append(pp)
     return tsm
 
@@ -434,13 +445,14 @@ def pbt_past_update(cfg, tsm):
     if len(getattr(tsm, "past_list", None) or []) != Q:
         raise ValueError(f"TrainStateManager holds no {Q} past policies (init_past_policies)")
     k0, k1, op = _split(tsm.pbt_rng)
-    mean, var, N = gather_fitness(tsm, P)
-    e = [p.episode_score for p in tsm.past_list]
+    fit = gather_fitness(tsm, P)
+    mean, var, N = fit
+    e = [p.episode_score for p in tsm.past_list]  # pooled when they were taken
     mean = np.concatenate([mean, [float(x.mean[0]) for x in e]])
     var = np.concatenate([var, [float(x.var[0]) for x in e]])
     N = np.concatenate([N, [float(x.N[0]) for x in e]])
     src, dst, ok = past_update_plan((k0, k1), op, mean, var, N, P, Q)
     if ok:
-        snapshot_policy(tsm, src, tsm.past_list[dst - P], P)
+        snapshot_policy(tsm, src, tsm.past_list[dst - P], P, fitness=fit)
     tsm.last_past_update = (src, dst, ok)
     return tsm

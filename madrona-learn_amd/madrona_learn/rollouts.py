@@ -166,10 +166,16 @@ class RolloutStore:
     def returns(self):
         return self.advantages + self.values if self.derive_returns else self._returns
 
-    def as_dict(self):
-        return {"obs": self.obs, "actions": self.actions, "log_probs": self.log_probs,
-                "values": self.values, "rewards": self.rewards, "dones": self.dones,
-                "advantages": self.advantages, "returns": self.returns}
+    def as_dict(self, targets=True):
+        """The store leaves; ``targets=False`` leaves out 'advantages' and
+        'returns' (the rollout before compute_advantages, as the reference
+        hands it to TrainHooks.finish_rollouts, rollouts.py:743-745)."""
+        d = {"obs": self.obs, "actions": self.actions, "log_probs": self.log_probs,
+             "values": self.values, "rewards": self.rewards, "dones": self.dones}
+        if targets:
+            d["advantages"] = self.advantages
+            d["returns"] = self.returns
+        return d
 
     def view(self, bptt_len, col0=0, ncols=None):
         """Rollout view of env columns [col0, col0 + ncols) (one policy of a
@@ -503,8 +509,24 @@ class RolloutManager:  # rollouts.py:373-826
         # already normalised observations)
         for ps in self.policies:
             ps.update_obs_norm()
-        rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
-            s.as_dict(), s.bootstrap, s.values, s.bootstrap, train_state_mgr.user_state)
+        from .train import TrainHooks
+        if type(user_hooks).finish_rollouts is not TrainHooks.finish_rollouts:
+            # rollouts.py:726-745: the hook sees the rollout before the
+            # advantages exist, plus the critic outputs inverted by the value
+            # normaliser; leaves it returns in place of the store's are copied
+            # back (e.g. reshaped rewards), so the GAE below uses them
+            vals, boot = s.values, s.bootstrap
+            vn = train_state_mgr.value_norm
+            if vn is not None:  # EMANormalizer.invert: v * sigma + mu per policy
+                sig = vn[:, 2].repeat_interleave(self.B)
+                mu = vn[:, 0].repeat_interleave(self.B)
+                vals, boot = s.values * sig + mu, s.bootstrap * sig + mu
+            before = s.as_dict(targets=False)
+            rollouts, train_state_mgr.user_state = user_hooks.finish_rollouts(
+                dict(before), s.bootstrap, vals, boot, train_state_mgr.user_state)
+            for k, v in (rollouts or {}).items():
+                if k in before and v is not before[k]:
+                    before[k].copy_(v.reshape(before[k].shape))
         if self.use_advantages:
             compute_advantages(self.train_cfg, s.rewards, s.values, s.dones, s.bootstrap,
                                out_adv=s.advantages,

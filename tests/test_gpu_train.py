@@ -231,3 +231,35 @@ def test_action_groups_match_oracle(gpu):
         max_grad_norm=0.5)
     np.testing.assert_allclose(ps.params.cpu().numpy(), p1, rtol=1e-4, atol=2e-5)
     np.testing.assert_allclose(mgr.metrics.last()["Loss"].mean, met["Loss"], rtol=1e-4, atol=1e-6)
+
+
+def test_finish_rollouts_hook_contract(gpu):
+    """TrainHooks.finish_rollouts (train.py:90-100, called at rollouts.py:743-745)
+    sees the rollout BEFORE the advantages exist, and the leaves it returns
+    replace the store's: reshaped rewards feed the GAE."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    seen = {}
+
+    class Hooks(ml.TrainHooks):
+        def finish_rollouts(self, rollouts, bootstrap_values, unnormalized_values,
+                            unnormalized_bootstrap_values, user_state):
+            seen["keys"] = sorted(rollouts)
+            seen["raw"] = rollouts["rewards"].clone()
+            out = dict(rollouts)
+            out["rewards"] = rollouts["rewards"] * 2.0 + 0.25
+            return out, user_state
+
+    env = DummyVecEnv(64, 64, 6, seed=2, device=gpu)
+    cfg = make_cfg(torch.float32)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.float32, 64),
+                           user_hooks=Hooks(), use_graph=False)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert "advantages" not in seen["keys"] and "returns" not in seen["keys"]
+    s = mgr.rollout_mgr.store
+    r = s.rewards.cpu().numpy()
+    np.testing.assert_array_equal(r, seen["raw"].cpu().numpy() * 2.0 + 0.25)
+    adv, _ = ref.gae_f32(r, s.values.cpu().numpy(), s.dones.cpu().numpy(),
+                         s.bootstrap.cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)

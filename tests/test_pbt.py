@@ -335,7 +335,14 @@ def _pool_worker(rank, port, q):
         ps.episode_score.var.fill_([0.5, 2.0][rank])
         ps.episode_score.N.fill_([10, 30][rank])
         tsm = types.SimpleNamespace(policy_list=[ps], train_list=[ts])
-        q.put((rank, pbt.gather_fitness(tsm, 1)))
+        fit = pbt.gather_fitness(tsm, 1)
+        # a past snapshot of the policy carries the pooled fitness too (so that
+        # pbt_past_update compares pooled train and past statistics)
+        cfg = types.SimpleNamespace(pbt=types.SimpleNamespace(num_train_policies=1,
+                                                              num_past_policies=1))
+        pbt.init_past_policies(cfg, tsm)
+        e = tsm.past_list[0].episode_score
+        q.put((rank, (fit, (float(e.mean), float(e.var), int(e.N)))))
     finally:
         dist.destroy_process_group()
 
@@ -358,7 +365,9 @@ def test_fitness_pooled_over_dp_holders_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(2):
-        mean, var, N = res[r]
+        (mean, var, N), past = res[r]
+        assert past[2] == 40
+        assert abs(past[0] - np.float32(mean[0])) == 0 and abs(past[1] - np.float32(var[0])) == 0
         assert N[0] == 40
         assert abs(mean[0] - (10 * 1.0 + 30 * 4.0) / 40) < 1e-12
         want_var = (10 * (0.5 + 1.0) + 30 * (2.0 + 16.0)) / 40 - mean[0] ** 2
