@@ -145,6 +145,28 @@ def pmc_traffic(kernel_key):
     return k.get("hbm_bytes_per_launch"), k.get("kernel_name")
 
 
+def step_row_blocks(M, dev):
+    """32-row blocks per workgroup of the fused step kernel at M minibatch
+    rows (csrc/ppo_wide.h wide_rb, bf16): 4 or 2 while every CU still gets a
+    workgroup, else 1 (ppo_step_kernel)."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    for rb in (4, 2):
+        if M // (32 * rb) >= cus:
+            return rb
+    return 1
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def kernel_rooflines(mgr, dev, n_local, iters=20):
     """Dominant kernel (the fused PPO minibatch fwd/loss/bwd step) plus the
     rollout policy step and GAE, each timed live with HIP events on the
@@ -167,11 +189,18 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     fwd, bwd, _ = flop_per_sample(A1=A1)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
-    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip)
+    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip:
+    # wide_rb: the widest row tile that still gives every CU a workgroup)
     HC = 32 if A1 <= 32 else 96
-    kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
+    rb = step_row_blocks(M, dev)
+    if rb > 1:
+        kname = f"ppo_wide_kernel<bf16,{HID},{LAYERS},{HC},{rb}>"
+        mangled = ("ppo_wide_kernel", f"Li{LAYERS}ELi{HC}ELi{rb}E")
+    else:
+        kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
+        mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
     traffic, pmc_name = pmc_traffic("ppo_step")
-    if pmc_name is None or f"Li{HC}ELi1E" not in pmc_name:
+    if pmc_name is None or not all(m in pmc_name for m in mangled):
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {
         "kernel": f"{kname} (mlearn_ppo_minibatch_fwd_bwd)",
@@ -189,20 +218,46 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
                         "2240 B/row weight-gradient operand spill",
     }
 
-    # rollout policy step (forward + sample) over this rank's envs
-    s = mgr.rollout_mgr.store
-    obs = torch.randn((n_local, OBS), device=dev)
-    ctr = torch.zeros(4, dtype=torch.int64, device=dev)
+    # the whole-rollout launch the update runs (mlearn_policy_rollout_env:
+    # T policy steps with the fused sim step + the bootstrap critic)
+    rm, rs = mgr.rollout_mgr, mgr.rollout
+    extra = {}
+    if rs.native_step is not None and rm.whole_rollout and ps.lstm_desc is None:
+        obs0 = rm.prep_obs(rs.cur_obs)
+        rout = rm._rollout_out(rs, 0, float(rm._cfg.reward_gamma))
+        edesc = rm._env_desc(rs.native_step, 0)
+        rstream = torch.cuda.Stream(device=dev)
 
-    def pol():
-        ps.rollout_step(obs, s.obs[0], s.actions[0], s.log_probs[0], s.values[0], (1, 2),
-                        ctr[0:1], 0)
+        def roll():
+            ps.rollout_all(obs0[:rm.B], rout, rs.prng_key, rs.counters[0:1], rm.env_offset,
+                           edesc)
 
-    t_pol = time_call(pol, iters, torch.cuda.current_stream())
-    pol_flop = fwd * n_local
-    extra = {"policy_step": {"bound": "mfma", "envs": n_local, "avg_launch_us": t_pol * 1e6,
-                             "achieved": pol_flop / t_pol / 1e12, "unit": "TFLOP/s",
-                             "frac": pol_flop / t_pol / 1e12 / BF16_PEAK_TFS}}
+        t_roll = time_call(roll, 5, rstream)
+        roll_flop = fwd * rm.B * (T + 1)
+        grid = int(L.mlearn_policy_rollout_workgroups(ps.desc, None, rm.B, rm.rollout_workgroups))
+        extra["policy_rollout"] = {
+            "kernel": "policy_rollout_kernel (mlearn_policy_rollout_env)", "bound": "mfma",
+            "envs": rm.B, "steps": T + 1, "workgroups": grid, "env_tiles": -(-rm.B // 32),
+            "avg_launch_us": t_roll * 1e6, "us_per_step": t_roll * 1e6 / (T + 1),
+            "achieved": roll_flop / t_roll / 1e12, "unit": "TFLOP/s",
+            "frac": roll_flop / t_roll / 1e12 / BF16_PEAK_TFS}
+    # one whole minibatch gradient (step + weight gradients + reduction) and
+    # one optimizer step (clip + Adam + projections + weight images)
+    grad = torch.zeros_like(mgr.state.train_list[0].grads)
+
+    def mbgrad():
+        nat.check(L.mlearn_ppo_minibatch_grad(ps.desc, algo.view, nat.ptr(seqs), algo.mb,
+                                              nat.ptr(algo.adv_stats[0, 0]), algo.hp,
+                                              nat.ptr(grad), None, nat.ptr(algo.ws),
+                                              nat.stream_handle(stream)))
+
+    t_grad = time_call(mbgrad, iters, stream)
+    ts = mgr.state.train_list[0]
+    ostream = torch.cuda.Stream(device=dev)
+    t_opt = time_call(lambda: ts.optimizer_step(ps), iters, ostream)
+    extra["minibatch"] = {"rows": M, "step_us": t_step * 1e6,
+                          "grad_us": t_grad * 1e6, "optimizer_step_us": t_opt * 1e6,
+                          "optimizer_steps_per_update": algo.E * algo.num_mb}
     # the product path writes only the advantages (returns = advantages +
     # values are formed by their consumers); "materialised" = the 8 B/elem
     # form (value normaliser / compute_advantages=False paths).  frac_read
@@ -289,7 +344,7 @@ def cpu_baseline(iters=2):
     sec = time.perf_counter() - t0
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{iters} full PPO iterations on a {n_env}-env shard ({n_env} envs x "
                       f"T={T}, 2 epochs x {n_env // mb} minibatches of {mb} seqs; same work per "
                       f"env-step as the 65536-env workload), NumPy fp32 oracle restatement, "
@@ -304,6 +359,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-separate-sim-line", action="store_true",
+                    help="skip the headline's second measurement with the sim step as its own "
+                         "launch (separate_sim_ms_per_update)")
     ap.add_argument("--config", choices=["headline", "b1", "lstm", "pbt"], default="headline")
     ap.add_argument("--bptt-chunks", type=int, default=1)
     ap.add_argument("--separate-sim", action="store_true",
@@ -349,14 +407,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-update device intervals (events between the updates, no host sync)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         mgr.update_iter()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    per_update = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -402,9 +465,24 @@ def main():
             # compute stream inside the HIP graph; "torch_distributed" = host
             # round trips between graph segments (reason on stderr); "none" = 1 GPU
             "collectives": mgr.dp.collectives, "rccl_ranks": mgr.dp.comm_ranks,
+            # device time of each timed update (HIP events between the updates):
+            # median / min / max over the K updates (value uses the wall clock above)
+            "ms_per_update_median": per_update[len(per_update) // 2],
+            "ms_per_update_min": per_update[0], "ms_per_update_max": per_update[-1],
         }
     if rank == 0 and not args.no_roofline and args.config != "lstm":
         result["roofline"], result["kernels"] = kernel_rooflines(mgr, dev, n_rank)
+    if rank == 0 and world == 1 and not args.no_separate_sim_line and args.config == "headline" \
+            and not args.separate_sim:
+        # the same job with the synthetic sim's step as its own launch between
+        # the policy launches, the path a user sim plugin takes (sim_fns 'step')
+        del mgr
+        torch.cuda.empty_cache()
+        m2 = make(dev, total, 0, n_rank, use_graph=not args.no_graph, config=args.config,
+                  chunks=args.bptt_chunks, critic=args.critic, fused_sim=False)
+        result["separate_sim_ms_per_update"] = _time_updates(m2, max(args.steps // 2, 3),
+                                                             args.warmup) * 1e3
+        del m2
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("headline", "b1"):
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:

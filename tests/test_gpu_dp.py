@@ -23,7 +23,13 @@ pytestmark = pytest.mark.gpu
 
 BUCKETS = [4, 8, 5, 5, 2, 2]
 D, T = 64, 32
-CASES = {"f32": (torch.float32, 64, 64, 16), "bf16": (torch.bfloat16, 256, 256, 32)}
+# mode -> (dtype, envs per rank N, width H, sequences per rank per minibatch, epochs)
+CASES = {"f32": (torch.float32, 64, 64, 16, 2), "bf16": (torch.bfloat16, 256, 256, 32, 2),
+         # the per-rank grid of the 8-GPU headline job (65,536 envs / 8 ranks, global
+         # minibatch 2048 = 256 sequences per rank): 8,192-row minibatch slices, the
+         # step kernel's 256 workgroups, 32 optimizer steps per epoch (one epoch
+         # keeps the oracle's host time bounded)
+         "bf16_w8grid": (torch.bfloat16, 8192, 256, 256, 1)}
 
 
 def _free_port():
@@ -43,12 +49,12 @@ def worker(rank, world, port, outdir, mode):
         from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        dtype, N, H, mbl = CASES[mode]
+        dtype, N, H, mbl, epochs = CASES[mode]
         env = DummyVecEnv(N, D, 6, seed=2, env_offset=rank * N, device=dev)
         cfg = ml.TrainConfig(
             num_worlds=world * N, num_agents_per_world=1, num_updates=3,
             actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T,
-            lr=3e-4, algo=ml.PPOConfig(num_epochs=2, minibatch_size=mbl * world, clip_coef=0.2,
+            lr=3e-4, algo=ml.PPOConfig(num_epochs=epochs, minibatch_size=mbl * world, clip_coef=0.2,
                                        value_loss_coef=0.5, entropy_coef={"actions": 0.01},
                                        max_grad_norm=0.5),
             num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=5, metrics_buffer_size=4,
@@ -78,10 +84,10 @@ def worker(rank, world, port, outdir, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("mode", ["f32", "bf16", "bf16_w8grid"])
 def test_dp_two_ranks_one_gpu(tmp_path, mode):
     from oracle import ppo_ref as ref
-    _, N, H, mbl = CASES[mode]
+    _, N, H, mbl, epochs = CASES[mode]
     mp.spawn(worker, args=(2, _free_port(), str(tmp_path), mode), nprocs=2, join=True)
     r = [np.load(os.path.join(tmp_path, f"rank{i}.npz")) for i in range(2)]
     p3 = [np.load(os.path.join(tmp_path, f"rank{i}_p3.npy")) for i in range(2)]
@@ -95,17 +101,18 @@ def test_dp_two_ranks_one_gpu(tmp_path, mode):
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
           "normalize_advantages": True}
     z = np.zeros_like(p0)
-    upd = dict(num_epochs=2, minibatch_size=mbl, bptt=T,
+    upd = dict(num_epochs=epochs, minibatch_size=mbl, bptt=T,
                key=tuple(int(x) for x in r[0]["key"]), epoch_base=0, lr=3e-4, max_grad_norm=0.5)
     norms = r[0]["init_norms"].astype(np.float64)
+    omode = "bf16" if mode.startswith("bf16") else mode
     p_ref, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay, norms,
-                                 mode=mode, **upd)
+                                 mode=omode, **upd)
     if mode == "f32":
         np.testing.assert_allclose(r[0]["p1"], p_ref, rtol=1e-4, atol=2e-5)
         return
     from tests.bf16_bound import check_bf16_update
     p_f32, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), stores, hp, BUCKETS, lay, norms,
                                  mode="f32", **upd)
-    check_bf16_update("dp_world2_H256_bf16", r[0]["p1"], p0, p_ref, p_f32, lay)
+    check_bf16_update(f"dp_world2_H256_{mode}", r[0]["p1"], p0, p_ref, p_f32, lay)
     dg, dr = r[0]["p1"] - p0, p_ref - p0
     assert dg @ dr / (np.linalg.norm(dg) * np.linalg.norm(dr)) > 0.99
