@@ -429,6 +429,37 @@ int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy);
 int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state* st,
                       void* workspace, mlearn_stream_t stream);
 
+/* The same optimizer step over the flat f32 parameter vector of ANY policy
+ * tree (the torch path of init_training for trees the fused kernels do not
+ * implement, e.g. BackboneSeparate, actor_critic.py:247-303): clip by the
+ * global gradient norm + Adam (ppo.py:84-90, 283-286), then per projection
+ * group normalize_params (ppo.py:303-310: a Dense kernel outside the actor
+ * and critic back to its initial Frobenius norm, train_state.py:413-423) or
+ * normalize_layernorms (ppo.py:312-338: a LayerNorm's scale and bias scaled
+ * together so |scale|^2 + |bias|^2 = features).  groups: DEVICE array. */
+typedef struct mlearn_flat_group {
+    int64_t offset, count;    /* kernel / LayerNorm scale: [offset, offset + count) */
+    int64_t offset2, count2;  /* LayerNorm bias (count2 = 0 for a kernel) */
+    int32_t kind;             /* 1: kernel, 2: LayerNorm */
+    int32_t features;         /* LayerNorm: F */
+    float init_norm;          /* kernel: its Frobenius norm at initialisation */
+    int32_t pad;
+} mlearn_flat_group;
+typedef struct mlearn_flat_optim {
+    float* params;            /* [n] f32 */
+    const float* grads;       /* [n] f32 (already all-reduced) */
+    float* adam_m;
+    float* adam_v;
+    int32_t* step;            /* device Adam step counter (optax count) */
+    int64_t n;
+    const mlearn_flat_group* groups;  /* device, num_groups entries */
+    int32_t num_groups;
+    float lr, b1, b2, eps, max_grad_norm;
+    int32_t normalize_params, normalize_layernorms;
+} mlearn_flat_optim;
+int64_t mlearn_flat_optim_workspace_bytes(int64_t n, int32_t num_groups);
+int mlearn_flat_optim_step(const mlearn_flat_optim* st, void* workspace, mlearn_stream_t stream);
+
 /* Refresh the compute-dtype copies (w_t, w, head_t, head, head_bias) of
  * `policy` from flat f32 params (used at init and after checkpoint loads). */
 int mlearn_policy_sync_weights(const mlearn_mlp_policy* policy, const float* params,

@@ -365,11 +365,103 @@ static void launch_project(int nslot, dim3 grid, hipStream_t s, const LayoutK& L
 #undef ML_PROJ
 }
 
+// ---------------------------------------------------------------------------
+// Flat optimizer (mlearn_flat_optim_step): any policy tree's f32 parameter
+// vector with a table of projection groups.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void flat_adam_kernel(float* __restrict__ params,
+                                                        const float* __restrict__ grads,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        const int32_t* step, int64_t n,
+                                                        const double* gpart, int64_t npart, float lr,
+                                                        float b1, float b2, float eps, float max_norm) {
+    const float gn = global_norm(gpart, npart);
+    const int count = step[0] + 1;
+    const float c1 = 1.f - powf(b1, (float)count), c2 = 1.f - powf(b2, (float)count);
+    for (int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        float g = grads[p];
+        if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
+        const float mm = (1.f - b1) * g + b1 * m[p];
+        const float vv = (1.f - b2) * (g * g) + b2 * v[p];
+        const float u = (mm / c1) / (sqrtf(vv / c2) + eps);
+        m[p] = mm;
+        v[p] = vv;
+        params[p] = params[p] + (-lr) * u;
+    }
+}
+
+// One block per group: the group's sum of squares (kernel, or LayerNorm
+// scale then bias) in a fixed order, then every element rescaled.
+__global__ __launch_bounds__(256) void flat_project_kernel(float* __restrict__ params,
+                                                           const mlearn_flat_group* groups,
+                                                           int ngroups, int norm_params,
+                                                           int norm_ln, int32_t* step) {
+    __shared__ double red[4];
+    __shared__ float sq;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && step) step[0] += 1;
+    if ((int)blockIdx.x >= ngroups) return;
+    const mlearn_flat_group gr = groups[blockIdx.x];
+    const bool on = gr.kind == 1 ? norm_params != 0 : norm_ln != 0;
+    if (!on) return;
+    double t = 0.0;
+    for (int64_t i = threadIdx.x; i < gr.count; i += 256) {
+        const double x = params[gr.offset + i];
+        t += x * x;
+    }
+    for (int64_t i = threadIdx.x; i < gr.count2; i += 256) {
+        const double x = params[gr.offset2 + i];
+        t += x * x;
+    }
+    t = wave_sum64d(t);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) sq = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+    __syncthreads();
+    if (gr.kind == 1) {  // ppo.py:307: init_norm * W / |W|
+        for (int64_t i = threadIdx.x; i < gr.count; i += 256) {
+            float* q = params + gr.offset + i;
+            *q = (gr.init_norm * *q) / sqrtf(sq);
+        }
+    } else {  // ppo.py:324-325: sqrt(F / (b.b + s.s)) * (s, b)
+        const float f = sqrtf((float)gr.features / sq);
+        for (int64_t i = threadIdx.x; i < gr.count; i += 256) params[gr.offset + i] *= f;
+        for (int64_t i = threadIdx.x; i < gr.count2; i += 256) params[gr.offset2 + i] *= f;
+    }
+}
+
 }  // namespace ml
 
 using namespace ml;
 
 extern "C" {
+
+int64_t mlearn_flat_optim_workspace_bytes(int64_t n, int32_t num_groups) {
+    if (n < 1 || num_groups < 0) return -1;
+    return (int64_t)kNormBlocks * (int64_t)sizeof(double);
+}
+
+int mlearn_flat_optim_step(const mlearn_flat_optim* st, void* workspace, mlearn_stream_t stream) {
+    ML_REQUIRE(st && st->params && st->grads && st->adam_m && st->adam_v && st->step && workspace,
+               "flat_optim_step: null pointer");
+    ML_REQUIRE(st->n >= 1 && st->num_groups >= 0 && (st->num_groups == 0 || st->groups),
+               "flat_optim_step: bad sizes");
+    ML_REQUIRE(st->max_grad_norm > 0 && st->lr >= 0, "flat_optim_step: bad hyperparameters");
+    hipStream_t s = S(stream);
+    double* gpart = (double*)workspace;
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads, st->n,
+                       gpart);
+    const int64_t nb = (st->n + 255) / 256;
+    hipLaunchKernelGGL(flat_adam_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, s,
+                       st->params, st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
+                       st->n, (const double*)gpart, (int64_t)kNormBlocks, st->lr, st->b1, st->b2,
+                       st->eps, st->max_grad_norm);
+    // (one block per group; at least one block: it also advances the step counter)
+    hipLaunchKernelGGL(flat_project_kernel, dim3((unsigned)(st->num_groups > 0 ? st->num_groups : 1)),
+                       dim3(256), 0, s, st->params, st->groups, st->num_groups,
+                       st->normalize_params, st->normalize_layernorms, st->step);
+    return check_launch("flat_optim_step");
+}
+
 
 int64_t mlearn_optim_workspace_bytes(const mlearn_mlp_policy* policy) {
     if (validate_policy(policy)) return -1;

@@ -179,6 +179,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
     const int tid = (int)threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int tile = (int)blockIdx.x;
     const int64_t row0 = (int64_t)tile * ROWS;
+    STAMP(0);
 
     // ---- loads issued up front: LayerNorm / head-bias parameters, the first
     // layer's weight fragments, the loss tasks' rollout columns, the tile's
@@ -254,12 +255,14 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
                     // natural-order fragment (s, hh) of the row: k = 16 s + 8 hh .. + 7
                     fr[((cc >> 1) * RB + rb) * 64 + rl + 32 * (cc & 1)] = __builtin_bit_cast(bf16x8, v[u]);
                 } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int k = cc * 4 + j;
-                        fr[((k >> 1) * RB + rb) * 64 + rl + 32 * (k & 1)] =
-                            __builtin_bit_cast(float, v[u][j]);
-                    }
+                    // (elements through an f32 vector: a per-element bit_cast of the
+                    // u32 vector stored element 0 four times, ROCm 7.2 gfx950)
+                    const f32x4 fv = __builtin_bit_cast(f32x4, v[u]);
+                    const int k0 = cc * 4;
+                    fr[((k0 >> 1) * RB + rb) * 64 + rl] = fv[0];
+                    fr[((k0 >> 1) * RB + rb) * 64 + rl + 32] = fv[1];
+                    fr[(((k0 >> 1) + 1) * RB + rb) * 64 + rl] = fv[2];
+                    fr[(((k0 >> 1) + 1) * RB + rb) * 64 + rl + 32] = fv[3];
                 }
             }
         }
@@ -270,6 +273,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
     if (P.CB > 1)
         for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
     __syncthreads();
+    STAMP(1);
 
     // ---- forward ----
     typedef typename Pk<T>::word word;
@@ -292,6 +296,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
         }
         (void)ra;
     }
+    STAMP(2);
     // post-activation rows A_l (weight-gradient operands), row-major
     word aw[RB][8];
     auto store_act = [&](int l) {
@@ -312,6 +317,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
             wide_issue<T, RB, ML_WIDE_RING>(ra, img, lane, KSH);
             store_act(l - 1);  // A_{l-1}, behind this product's first weight loads
             wide_run<T, RB, KSH, ML_WIDE_RING>(acc, ra, fr, img, lane);
+            STAMP(5);
         }
         // Dense output -> compute dtype, per-row partial sums over this wave's features
 #pragma unroll
@@ -328,6 +334,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
             if (h == 0) *(float2*)(red + (w * ROWS + rb * 32 + r) * 2) = make_float2(sum, sq);
         }
         __syncthreads();
+        STAMP(3 + 3 * l);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
             float2 t = *(const float2*)(red + (rb * 32 + r) * 2);
@@ -361,6 +368,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
             for (int t = 0; t < SPB; ++t) fr[((w * SPB + t) * RB + rb) * 64 + lane] = Pk<T>::frag(aw[rb], t);
         }
         __syncthreads();
+        STAMP(4 + 3 * l);
     }
 
     // ---- heads (dists.py:22, models.py:154): lg[row][j] = rnd(rnd(a . W) + rnd(b)) ----
@@ -385,6 +393,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
         }
         if (first) store_act(L - 1);
     }
+    STAMP(8);
     __syncthreads();
     for (int i = tid; i < ROWS * HC; i += THREADS) {
         const int rr = i / HC, j = i - rr * HC;
@@ -394,6 +403,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
         lg[rr * LGS + j] = rnd<T>(rnd<T>(x) + rnd<T>(hbias[j]));
     }
     __syncthreads();
+    STAMP(9);
 
     // ---- loss: one (row, group | value) task per thread (ppo.py:129-262) ----
     {
@@ -491,6 +501,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
         }
         ws.loss_part[(int64_t)tile * kLossSlots + tid] = v;
     }
+    STAMP(10);
 
     // ---- backward ----
     // dA_{L-1}^T = Head . dHead^T (this wave's feature block, every row block):
@@ -528,6 +539,7 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
         }
     }
 
+    STAMP(11);
     const int qs = col_sum16_index(lane);
     const float thr = relu_thr<T>();
 #pragma unroll
@@ -573,7 +585,9 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
             if (h == 0) *(float2*)(red + (w * ROWS + rb * 32 + r) * 2) = make_float2(su, sv);
         }
         const float cpg = col_sum16(pg, lane), cpb = col_sum16(pb, lane);
+        if (l == L - 1) STAMP(12);
         __syncthreads();
+        if (l == L - 1) STAMP(13);
         word dzw[RB][8];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
@@ -624,10 +638,12 @@ __global__ __launch_bounds__(64 * (H / 32)) __attribute__((amdgpu_waves_per_eu(k
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) zero1(acc[rb]);
             wide_run<T, RB, KSH, ML_WIDE_RING>(acc, ra, fr, img, lane);
+            if (l == L - 1) STAMP(14);
         } else {
             store_dz();
         }
     }
+    STAMP(15);
 }
 
 // Row blocks per workgroup of the wide step kernel for M minibatch rows: the

@@ -70,6 +70,20 @@ class PPOHparams(Structure):
                 ("grad_sumsq_out", c_void_p)]
 
 
+class FlatGroup(Structure):  # mlearn_flat_group
+    _fields_ = [("offset", c_int64), ("count", c_int64), ("offset2", c_int64), ("count2", c_int64),
+                ("kind", c_int32), ("features", c_int32), ("init_norm", c_float),
+                ("pad", c_int32)]
+
+
+class FlatOptim(Structure):  # mlearn_flat_optim
+    _fields_ = [("params", c_void_p), ("grads", c_void_p), ("adam_m", c_void_p),
+                ("adam_v", c_void_p), ("step", c_void_p), ("n", c_int64), ("groups", c_void_p),
+                ("num_groups", c_int32), ("lr", c_float), ("b1", c_float), ("b2", c_float),
+                ("eps", c_float), ("max_grad_norm", c_float), ("normalize_params", c_int32),
+                ("normalize_layernorms", c_int32)]
+
+
 class OptimState(Structure):
     _fields_ = [("params", c_void_p), ("grads", c_void_p), ("adam_m", c_void_p),
                 ("adam_v", c_void_p), ("init_norms", c_void_p), ("step", c_void_p),
@@ -175,6 +189,8 @@ _SIGNATURES = {
     "mlearn_obs_norm_update": (c_int32, [_P, c_int32, c_int64, c_int64, c_int32, c_float, c_float,
                                          _P, _P, _S]),
     "mlearn_optim_workspace_bytes": (c_int64, [POINTER(MlpPolicy)]),
+    "mlearn_flat_optim_workspace_bytes": (c_int64, [c_int64, c_int32]),
+    "mlearn_flat_optim_step": (c_int32, [POINTER(FlatOptim), _P, _S]),
     "mlearn_optim_step": (c_int32, [POINTER(MlpPolicy), POINTER(OptimState), _P, _S]),
     "mlearn_policy_sync_weights": (c_int32, [POINTER(MlpPolicy), _P, _S]),
     "mlearn_lstm_param_offset": (c_int64, [POINTER(MlpPolicy)]),

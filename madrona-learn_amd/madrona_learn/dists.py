@@ -55,6 +55,11 @@ class DiscreteActionDistributions:
         return self._sample(PhiloxKey(0, 0), False)[0]
 
     def action_stats(self, all_actions: torch.Tensor):  # dists.py:54-77
+        if torch.is_grad_enabled() and self.all_logits.requires_grad:
+            # differentiable form (the torch path's update, generic.py): the
+            # same kernel forward, backward through the softmax
+            from .generic import action_stats_autograd
+            return action_stats_autograd(self, all_actions)
         lg = self._logits_f32()
         N = lg.shape[0]
         K = len(self.actions_num_buckets)

@@ -17,10 +17,82 @@ from .cfg import canonical_dtype
 from .moving_avg import EMANormalizer
 
 
+def _map_obs(cb, *args):
+    """observations.py:36-57: cb(ob_name, *per-observation args) over the
+    observation names of args[0] (a dict; a bare tensor is one observation
+    named None and maps to a bare result).  The reference's vmap over the
+    policy axis has no counterpart: one policy's state per call."""
+    a0 = args[0]
+    if not isinstance(a0, dict):
+        return cb(None, *args)
+    return {k: cb(k, *[a[k] if isinstance(a, dict) else a for a in args]) for k in a0}
+
+
 @dataclass(frozen=True)
 class ObservationsPreprocess:  # observations.py:13-68
+    """The reference's plugin interface: subclasses override ``_preprocess``
+    (and, for stateful preprocessing, ``_init_state`` / ``_update_state`` /
+    ``_init_obs_stats`` / ``_update_obs_stats``).  The built-in Noop / Caster
+    / EMANormalizer run fused into the rollout kernel on the fused path; any
+    other subclass selects the torch path of init_training (generic.py),
+    which calls these hooks as rollouts.py:838-840, 670-678 and
+    train.py:193-204 do.  ``vmap`` is accepted for signature parity (one
+    policy's state per call here)."""
+
+    def preprocess(self, states, obs, vmap=False):
+        return _map_obs(lambda k, st, ob: self._preprocess(k, st, ob), _states_like(states, obs),
+                        obs)
+
+    def init_state(self, obs, vmap=False):
+        return _map_obs(self._init_state, obs)
+
+    def update_state(self, states, o_stats, vmap=False):
+        return _map_obs(self._update_state, states, o_stats)
+
+    def init_obs_stats(self, states, vmap=False):
+        return _map_obs(self._init_obs_stats, states)
+
+    def update_obs_stats(self, states, cur_obs_stats, num_prev_updates, obs, vmap=False):
+        return _map_obs(lambda k, st, cs, ob: self._update_obs_stats(k, st, cs, num_prev_updates,
+                                                                    ob),
+                        _states_like(states, obs), _states_like(cur_obs_stats, obs), obs)
+
+    def _preprocess(self, ob_name, state, ob):
+        return ob
+
+    def _init_state(self, ob_name, ob):
+        return None
+
+    def _update_state(self, ob_name, est, ob_stats):
+        return None
+
+    def _init_obs_stats(self, ob_name, est):
+        return None
+
+    def _update_obs_stats(self, ob_name, est, ob_stats, num_prev_updates, ob):
+        return None
+
+    def has_state(self):
+        """True when a subclass keeps state (overrides a state hook)."""
+        base = ObservationsPreprocess
+        return any(getattr(type(self), f) is not getattr(base, f)
+                   for f in ("_init_state", "_update_state", "_init_obs_stats",
+                             "_update_obs_stats"))
+
     def fused_cast_dtype(self, compute_dtype):
-        raise NotImplementedError
+        """The dtype the fused rollout kernel casts the observations to when
+        it implements this preprocess; NotImplementedError selects the torch
+        path (generic.py) for a user's subclass."""
+        raise NotImplementedError(
+            f"{type(self).__name__} is not one of the fused preprocessors (Noop, Caster, "
+            "EMANormalizer)")
+
+
+def _states_like(states, obs):
+    """None states for every observation name when a preprocess keeps none."""
+    if states is None and isinstance(obs, dict):
+        return {k: None for k in obs}
+    return states
 
 
 @dataclass(frozen=True)
@@ -31,6 +103,9 @@ class ObservationsPreprocessNoop(ObservationsPreprocess):
 
     def fused_cast_dtype(self, compute_dtype):
         return compute_dtype
+
+    def _preprocess(self, ob_name, state, ob):  # observations.py:157-158
+        return ob
 
 
 @dataclass(frozen=True)
@@ -47,6 +122,9 @@ class ObservationsCaster(ObservationsPreprocess):
                 "ObservationsCaster to a dtype other than TrainConfig.compute_dtype is not "
                 "supported on the fused path")
         return compute_dtype
+
+    def _preprocess(self, ob_name, state, ob):  # observations.py:147-148
+        return ob.to(canonical_dtype(self.dtype))
 
 
 @dataclass(frozen=True)
@@ -83,3 +161,32 @@ class ObservationsEMANormalizer(ObservationsPreprocess):  # observations.py:70-1
     def prep(self, ob_name, ob):
         fn = self.prep_fns.get(ob_name)
         return ob if fn is None else fn(ob)
+
+    # observations.py:93-132 (the torch path's hooks; the fused path runs the
+    # same arithmetic in the rollout kernel + mlearn_obs_norm_update)
+    def _preprocess(self, ob_name, est, ob):
+        ob = self.prep(ob_name, ob)
+        if not self.normalizes(ob_name):
+            return ob
+        return self.normalizer.normalize(est, ob)
+
+    def _init_state(self, ob_name, ob):
+        if not self.normalizes(ob_name):
+            return None
+        return self.normalizer.init_estimates(self.prep(ob_name, ob))
+
+    def _update_state(self, ob_name, est, ob_stats):
+        if not self.normalizes(ob_name):
+            return None
+        return self.normalizer.update_estimates(est, ob_stats)
+
+    def _init_obs_stats(self, ob_name, est):
+        if not self.normalizes(ob_name):
+            return None
+        return self.normalizer.init_input_stats(est)
+
+    def _update_obs_stats(self, ob_name, est, ob_stats, num_prev_updates, ob):
+        if not self.normalizes(ob_name):
+            return None
+        return self.normalizer.update_input_stats(ob_stats, num_prev_updates,
+                                                  self.prep(ob_name, ob))

@@ -252,7 +252,7 @@ class RolloutManager:  # rollouts.py:373-826
             raise ValueError(f"{self.N} envs do not split over {self.P} policies")
         self.B = self.N // self.P
         self.policy_state = self.policies[0]
-        self.prefix = self.policy_state.actor_critic.backbone.prefix
+        self.prefix = getattr(self.policy_state.actor_critic.backbone, "prefix", None)
         for ps in self.policies:
             ps.attach_obs_stats(self.T, self.N // len(self.policies))
         arch = self.policy_state.arch
@@ -405,6 +405,11 @@ class RolloutManager:  # rollouts.py:373-826
         gamma = float(self._cfg.reward_gamma)
         rollout_state, train_state_mgr.user_state = user_hooks.start_rollouts(
             rollout_state, train_state_mgr.user_state)
+        if getattr(self.policy_state, "generic", False):
+            # a tree outside the fused kernels: torch modules per step (generic.py)
+            from .generic import TorchRollout
+            TorchRollout(self).collect(rollout_state, gamma)
+            return self._finish(train_state_mgr, rollout_state, metrics, user_hooks)
         key = rollout_state.prng_key
         step_ctr = rollout_state.counters[0:1]
         B = self.B

@@ -282,6 +282,13 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     rollout_state = RolloutState.create(rollout_cfg, sim_fns, rollout_key, rnn_states,
                                         init_sim_ctrl, device=device)
 
+    generic_why = _fused_tree_problem(policy, rollout_state, sim_batch, cfg)
+    if generic_why is not None:
+        # a tree (or preprocess) the fused kernels do not implement: torch
+        # autograd over the user's modules, HIP kernels around them (generic.py)
+        return _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
+                                    num_policies, sim_batch, sim_fns, restore_ckpt, profile_port,
+                                    generic_why)
     prefix = policy.actor_critic.backbone.prefix
     from .rollouts import obs_to_matrix
     obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
@@ -370,6 +377,72 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
     print(cfg)
     mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                           update_idx=start, use_graph=use_graph, profile_port=profile_port)
+    mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
+    mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
+    return mgr
+
+
+def _fused_tree_problem(policy, rollout_state, sim_batch, cfg):
+    """None when the fused kernels implement the policy (tree and
+    preprocess), else why not (the torch path then trains it)."""
+    from .rollouts import obs_to_matrix
+    ac = policy.actor_critic
+    try:
+        prefix = ac.backbone.prefix
+        obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
+        compile_arch(ac, obs0.shape[1], cfg.compute_dtype)
+        if policy.obs_preprocess is not None:
+            policy.obs_preprocess.fused_cast_dtype(cfg.compute_dtype)
+    except (NotImplementedError, AttributeError, ValueError) as e:
+        return f"{type(e).__name__}: {e}"
+    return None
+
+
+def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
+                         num_policies, sim_batch, sim_fns, restore_ckpt, profile_port, why):
+    """init_training for a tree outside the fused kernels (generic.py): the
+    user's torch modules train under autograd, eagerly (no HIP graph), with
+    sampling, post-step, GAE, advantage statistics, action_stats and the
+    optimizer on the HIP kernels."""
+    import sys
+    from .generic import TorchPolicyState, TorchPPO, TorchTrainState
+    from .models import action_groups
+    if num_policies != 1:
+        raise NotImplementedError(f"populations need a fused policy tree ({why})")
+    if cfg.normalize_values:
+        raise NotImplementedError(f"normalize_values needs a fused policy tree ({why})")
+    print(f"[madrona_learn] policy tree outside the fused kernels ({why}): training it with "
+          "torch autograd (HIP sampling / GAE / statistics / optimizer)", file=sys.stderr)
+    buckets = [b for _, g in action_groups(cfg.actions) for b in g]
+    ps = TorchPolicyState(policy.actor_critic, policy.obs_preprocess, device,
+                          rollout_state.cur_obs, cfg.compute_dtype, buckets, cfg.seed)
+    if bool(cfg.dreamer_v3_critic) != (ps.critic_bins > 1):
+        raise ValueError(f"TrainConfig.dreamer_v3_critic={cfg.dreamer_v3_critic} does not match "
+                         f"the policy's critic ({ps.critic_bins} output bins)")
+    dp.broadcast_(ps.params)
+    algo = TorchPPO(cfg.algo.setup())
+    ts = TorchTrainState(cfg, algo.init_hyperparams(cfg), ps, _split_seed(cfg.seed, 2))
+    ts.policy_id = 0
+    tsm = TrainStateManager(policy_states=ps, train_states=ts, pbt_rng=None,
+                            user_state=user_hooks.init_user_state(), value_norm=None)
+    start = 0
+    if restore_ckpt is not None:
+        path = _ckpt_file(restore_ckpt, rank, W)
+        tsm, start = tsm.load(path)
+        ckpt_rollout = torch.load(path, map_location="cpu", weights_only=True).get("rollout")
+        if ckpt_rollout is not None:
+            rollout_state.counters[1].copy_(ckpt_rollout["counters"][1])
+    rollout_mgr = RolloutManager(cfg, rollout_state, [ps], env_offset=rank * sim_batch)
+    rollout_mgr.get_episode_scores = policy.get_episode_scores
+    names = algo.add_metrics(cfg, [])
+    names = rollout_mgr.add_metrics(cfg, names)
+    names = user_hooks.add_metrics(names)
+    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device, num_policies=1)
+    algo.prepare(cfg, ps, ts, rollout_mgr.view(0), dp, policy_idx=0)
+    algo.store = rollout_mgr.store
+    print(cfg)
+    mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, [algo], user_hooks, dp,
+                          update_idx=start, use_graph=False, profile_port=profile_port)
     mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
     mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
     return mgr

@@ -1,0 +1,162 @@
+"""Training a policy tree the fused kernels do not implement (the torch path
+of init_training, madrona_learn/generic.py): the reference trains whatever
+module the Policy holds (ppo.py:119-127, 276-281).
+
+* BackboneSeparate (actor_critic.py:247-303: separate MLP encoders for the
+  actor and the critic), f32: the rollout store against the oracle env and
+  the oracle forward, GAE bit-exact, and one full PPO update (2 epochs x 4
+  minibatches) against oracle/separate_ref.py from the same store and
+  parameters (the tolerances of tests/test_gpu_train.py's f32 update).
+* A user ObservationsPreprocess subclass (observations.py:13-68 plugin
+  interface, _preprocess overridden) on a BackboneShared MLP: trained on
+  the torch path, the store holds the preprocessed observations.
+* action_stats' autograd form (HIP forward, softmax backward) against
+  torch's own log_softmax / entropy gradients.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import native as onat
+from oracle import ppo_ref as ref
+from oracle import separate_ref as sref
+
+pytestmark = pytest.mark.gpu
+
+BUCKETS = [4, 8, 5, 5, 2, 2]
+
+
+def _cfg(N, mb, epochs=2, dtype=torch.float32):
+    import madrona_learn as ml
+    return ml.TrainConfig(
+        num_worlds=N, num_agents_per_world=1, num_updates=1,
+        actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=32, lr=3e-4,
+        algo=ml.PPOConfig(num_epochs=epochs, minibatch_size=mb, clip_coef=0.2,
+                          value_loss_coef=0.5, entropy_coef={"actions": 0.01},
+                          max_grad_norm=0.5),
+        num_bptt_chunks=1, gamma=0.99, gae_lambda=0.95, seed=3, metrics_buffer_size=4,
+        dreamer_v3_critic=False, compute_dtype=dtype)
+
+
+def _named(ps):
+    return {n: ps.params[o:o + int(np.prod(s))].cpu().numpy().astype(np.float64).reshape(s)
+            for n, o, s in ps.layout["params"]}
+
+
+def test_backbone_separate_update_matches_oracle(gpu):
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    N, H, L, mb, T = 64, 64, 2, 16, 32
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=2, device=gpu)
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneSeparate(actor_encoder=ml.BackboneEncoder(net=MLP(H, L, dt)),
+                                     critic_encoder=ml.BackboneEncoder(net=MLP(H, L, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DenseLayerCritic(dt))
+    cfg = _cfg(N, mb)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac), use_graph=True)
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    assert getattr(ps, "generic", False) and not mgr.use_graph
+    order = [n for n, _, _ in ps.layout["params"]]
+    p0 = _named(ps)
+    init_norms = {k: float(np.sqrt((v * v).sum())) for k, v in p0.items() if k.endswith("kernel")
+                  and k.startswith("backbone.")}
+    assert len(init_norms) == 2 * L and ts.num_groups == 4 * L
+    oenv = onat.Env(N, 64, env.k0, env.k1, 0)
+    oenv.reset()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    acts = s.actions.cpu().numpy()
+    obs = s.obs.float().cpu().numpy()
+    for t in range(T):
+        assert np.array_equal(obs[t], oenv.obs), t
+        o, r, d = oenv.step(acts[t])
+        assert np.array_equal(s.rewards[t].cpu().numpy(), r)
+        assert np.array_equal(s.dones[t].cpu().numpy(), d)
+    logits, V, _ = sref.forward(p0, obs.reshape(T * N, 64), L, "f32")
+    lp, _ = ref.action_stats(logits, BUCKETS, acts.reshape(T * N, 6))
+    np.testing.assert_allclose(s.values.cpu().numpy().reshape(-1), V, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(s.log_probs.cpu().numpy().reshape(-1, 6), lp, rtol=1e-4,
+                               atol=1e-4)
+    adv, _ = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(), s.dones.cpu().numpy(),
+                         s.bootstrap.cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)
+    store = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+             for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    want, _ = sref.ppo_update(dict(p0), order, store, hp, BUCKETS, L, init_norms, num_epochs=2,
+                              minibatch_size=mb, bptt=T, key=ts.update_prng_key, epoch_base=0,
+                              mode="f32", lr=3e-4, max_grad_norm=0.5)
+    got = _named(ps)
+    g = np.concatenate([got[k].reshape(-1) for k in order])
+    w = np.concatenate([want[k].reshape(-1) for k in order])
+    z = np.concatenate([p0[k].reshape(-1) for k in order])
+    # as tests/test_gpu_train.py f32: Adam takes noise-sized steps where the
+    # gradient is at the f32 summation-noise level, in both implementations
+    np.testing.assert_allclose(g, w, rtol=0, atol=1e-4)
+    close = np.abs(g - w) <= 2e-5 + 1e-4 * np.abs(w)
+    assert close.mean() >= 0.999, close.mean()
+    dg, dw = g - z, w - z
+    assert dg @ dw / (np.linalg.norm(dg) * np.linalg.norm(dw)) > 0.999
+    assert int(ts.step.item()) == 2 * (N // mb)
+    # the projections held: every trunk kernel at its initial norm
+    for k, n0 in init_norms.items():
+        np.testing.assert_allclose(np.sqrt((got[k] ** 2).sum()), n0, rtol=1e-5)
+    last = mgr.metrics.last()
+    assert np.isfinite(last["Loss"].mean)
+
+
+def test_user_preprocess_trains_on_torch_path(gpu):
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.observations import ObservationsPreprocess
+    from tests.test_gpu_train import make_policy
+
+    class Halve(ObservationsPreprocess):
+        def _preprocess(self, ob_name, state, ob):
+            return ob * 0.5
+
+    N = 64
+    env = DummyVecEnv(N, 64, 6, seed=4, device=gpu)
+    pol = make_policy(torch.float32, 64)
+    pol = ml.Policy(actor_critic=pol.actor_critic, obs_preprocess=Halve())
+    mgr = ml.init_training(gpu, _cfg(N, 16, epochs=1), env.sim_fns(), pol)
+    ps = mgr.state.policy_states
+    assert getattr(ps, "generic", False)
+    oenv = onat.Env(N, 64, env.k0, env.k1, 0)
+    oenv.reset()
+    p0 = ps.params.clone()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    np.testing.assert_array_equal(s.obs[0].cpu().numpy(), oenv.obs * np.float32(0.5))
+    assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
+
+
+def test_action_stats_autograd_matches_torch(gpu):
+    from madrona_learn.dists import DiscreteActionDistributions
+    torch.manual_seed(0)
+    lg = torch.randn((300, sum(BUCKETS)), device=gpu, dtype=torch.float32) * 3
+    acts = torch.stack([torch.randint(0, b, (300,), device=gpu) for b in BUCKETS], -1)
+    wl = torch.randn((300, 6), device=gpu)
+    we = torch.randn((300, 6), device=gpu)
+    x = lg.clone().requires_grad_(True)
+    logp, ent = DiscreteActionDistributions(BUCKETS, x).action_stats(acts)
+    ((logp * wl).sum() + (ent * we).sum()).backward()
+    y = lg.clone().requires_grad_(True)
+    lps, ents, off = [], [], 0
+    for k, b in enumerate(BUCKETS):
+        ls = torch.log_softmax(y[:, off:off + b], -1)
+        lps.append(ls.gather(1, acts[:, k:k + 1]).squeeze(1))
+        ents.append(-(ls.exp() * ls).sum(-1))
+        off += b
+    lp2, ent2 = torch.stack(lps, -1), torch.stack(ents, -1)
+    ((lp2 * wl).sum() + (ent2 * we).sum()).backward()
+    torch.testing.assert_close(logp, lp2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ent, ent2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad, y.grad, rtol=1e-4, atol=1e-5)

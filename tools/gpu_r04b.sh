@@ -17,6 +17,7 @@ run() {
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+run debug 200 python -u tools/debug_wide.py
 run t_wide 600 $PYT tests/test_gpu_policy.py tests/test_gpu_fullsize.py tests/test_gpu_configs.py
 run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 run t_all 900 $PYT tests -m gpu --deselect tests/test_gpu_policy.py --deselect tests/test_gpu_fullsize.py --deselect tests/test_gpu_configs.py
