@@ -145,17 +145,6 @@ def pmc_traffic(kernel_key):
     return k.get("hbm_bytes_per_launch"), k.get("kernel_name")
 
 
-def step_row_blocks(M, dev):
-    """32-row blocks per workgroup of the fused step kernel at M minibatch
-    rows (csrc/ppo_wide.h wide_rb, bf16): 4 or 2 while every CU still gets a
-    workgroup, else 1 (ppo_step_kernel)."""
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    for rb in (4, 2):
-        if M // (32 * rb) >= cus:
-            return rb
-    return 1
-
-
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -189,16 +178,10 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     fwd, bwd, _ = flop_per_sample(A1=A1)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
-    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip:
-    # wide_rb: the widest row tile that still gives every CU a workgroup)
+    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip)
     HC = 32 if A1 <= 32 else 96
-    rb = step_row_blocks(M, dev)
-    if rb > 1:
-        kname = f"ppo_wide_kernel<bf16,{HID},{LAYERS},{HC},{rb}>"
-        mangled = ("ppo_wide_kernel", f"Li{LAYERS}ELi{HC}ELi{rb}E")
-    else:
-        kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
-        mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
+    kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
+    mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
     traffic, pmc_name = pmc_traffic("ppo_step")
     if pmc_name is None or not all(m in pmc_name for m in mangled):
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel

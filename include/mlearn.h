@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 12
+#define MLEARN_ABI_VERSION 13
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -348,10 +348,6 @@ typedef struct mlearn_ppo_hparams {
                                               per-action-group means (ppo.py:221-239) are
                                               obj_weight[j] = K / K_g and entropy_coef[j] =
                                               c_g K / K_g for the group g holding j. */
-    int32_t row_blocks;                    /* feed-forward policies: 32-row blocks per
-                                              workgroup of the fused step (0: the widest
-                                              tile that still gives every CU a workgroup;
-                                              1, 2 or 4 force it; f32 caps at 2) */
     double* grad_sumsq_out;                /* may be NULL: per-64-parameter partial sums of
                                               grad^2 (mlearn_grad_sumsq_parts entries),
                                               written by the gradient reduction; the next

@@ -47,7 +47,6 @@ struct HpK {
     int metrics;  // reduce the loss metrics (only the minibatch whose metrics are recorded)
     float loss_scale;
     float inv_sk, inv_s;
-    int row_blocks;  // mlearn_ppo_hparams.row_blocks (host-side launch choice)
 };
 
 constexpr int kLossSlots = 20;   // per tile doubles
@@ -62,8 +61,7 @@ constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 // weight-gradient K chunk (rows of the minibatch staged per LDS stage); f32 keeps 32
 template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_CHUNK : 32; }
 static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
-constexpr int kRowAlign = 128;   // Mp granularity of the MLP update (a multiple of every wide row tile)
-constexpr int kRowAlignLstm = 64;  // the recurrent update (its scans write exactly M = mb * bptt rows)
+constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number of 32-row tiles)
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif
@@ -156,8 +154,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
                     const mlearn_lstm* lstm = nullptr, int64_t mb = 0, LstmWsK* LW = nullptr) {
     const size_t es = p.dtype == MLEARN_DTYPE_BF16 ? 2 : 4;
     const int H = p.hidden, D = p.obs_dim, L = p.num_layers;
-    const int64_t al = lstm ? kRowAlignLstm : kRowAlign;
-    const int64_t Mp = (M + al - 1) / al * al;
+    const int64_t Mp = (M + kRowAlign - 1) / kRowAlign * kRowAlign;
     const int64_t tiles = Mp / 32;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -1028,61 +1025,6 @@ static void launch_step(const PolicyK& P, const RolloutK& R, const int32_t* mb_s
                                                             rec);
 }
 
-#include "ppo_wide.h"
-
-static int device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
-// The feed-forward policy's fused minibatch step on the wide-tile kernel:
-// RB row blocks per workgroup (wide_rb); sets ws.ntiles to the workgroup
-// count (the rows of ws.colpart / ws.loss_part the kernel writes).
-template <typename T, int H, int L, int HC, int RB>
-static void launch_wide_rb(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
-                           int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
-    auto k = ppo_wide_kernel<T, H, L, HC, RB>;
-    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr_set = true;
-    }
-    ws.ntiles = (int)(ws.Mp / (32 * RB));
-    const size_t lds = wide_lds<T, H, L, HC, RB>(P.D);
-    hipLaunchKernelGGL(k, dim3(ws.ntiles), dim3(64 * (H / 32)), lds, s, P, R, mb_seq, mb, M, adv_st,
-                       hp, ws);
-}
-template <typename T, int H, int L, int HC>
-static void launch_wide_hc(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
-                           int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
-    const int rbmax = sizeof(T) == 2 ? 4 : 2;
-    const int rb = hp.row_blocks > 0 ? (hp.row_blocks < rbmax ? hp.row_blocks : rbmax)
-                                     : wide_rb<T>(ws.Mp, device_cus());
-    if constexpr (sizeof(T) == 2) {
-        if (rb == 4) return launch_wide_rb<T, H, L, HC, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
-    }
-    if (rb >= 2) return launch_wide_rb<T, H, L, HC, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
-    // fewer than two 32-row blocks per CU (e.g. a data-parallel rank's
-    // minibatch slice): one 32-row tile per workgroup, two workgroups per CU
-    launch_step_hc<T, H, L, kFused, HC>(P, R, mb_seq, mb, M, adv_st, hp, ws, s, RecK{});
-}
-template <typename T, int H, int L>
-static void launch_wide(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
-                        int64_t M, const float* adv_st, const HpK& hp, WsK& ws, hipStream_t s) {
-    if (P.HC == MLEARN_HEAD_COLS)
-        launch_wide_hc<T, H, L, MLEARN_HEAD_COLS>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
-    else
-        launch_wide_hc<T, H, L, MLEARN_HEAD_COLS_MAX>(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
-}
-
 // ---------------------------------------------------------------------------
 // Weight gradients dW[i][j] = sum_m X[m][i] * Y[m][j] for every weight of the
 // policy in one launch (X, Y row-major [Mp][I] / [Mp][J], written by the step
@@ -1263,6 +1205,9 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
 
 // Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
 // level of the column partials; one more (if loss_out) the loss metrics.
+// (The fixed-order reduction into the flat gradient is the next launch,
+// reduce_grads_kernel: folding it in as trailing blocks that wait on a
+// device-scope counter measured 2.4x slower, profiles/r04_fused_reduce_ab.txt.)
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES, 8))) void wgrad_kernel(
     WgJobs jobs, WsK ws, HpK hp, int64_t M, int K, float* loss_out) {
@@ -1532,6 +1477,25 @@ __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K
     }
 }
 
+// The gradient launches: weight-gradient tiles, column partials and loss
+// metrics; then the reduction into grad, one 64-parameter chunk per block.
+template <typename T>
+static void launch_wgrad(const WgJobs& jobs, const WsK& ws, const HpK& hp, int64_t M, int K,
+                         float* loss_out, const LayoutK& Lk, float* grad, double* sumsq,
+                         hipStream_t s) {
+    static bool attr_set = false;  // once per instantiation (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)wgrad_kernel<T>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)WgCfg<T>::lds);
+        attr_set = true;
+    }
+    const int blocks = jobs.nwg + jobs.ncol + (loss_out ? 1 : 0);
+    hipLaunchKernelGGL((wgrad_kernel<T>), dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
+                       K, loss_out);
+    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)), dim3(256), 0, s,
+                       Lk, ws, grad, sumsq);
+}
+
 template <typename T, int H>
 static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_view& ro,
                             const int32_t* mb_seq, int mb, const float* adv_st,
@@ -1561,13 +1525,12 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.metrics = loss_out != nullptr;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
-    hp.row_blocks = h.row_blocks;
 
     switch (p.num_layers) {
-        case 1: launch_wide<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 2: launch_wide<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        case 3: launch_wide<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
-        default: launch_wide<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 1: launch_step<T, H, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 2: launch_step<T, H, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        case 3: launch_step<T, H, 3>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
+        default: launch_step<T, H, 4>(P, R, mb_seq, mb, M, adv_st, hp, ws, s); break;
     }
     if (step_only) return check_launch("ppo_minibatch_fwd_bwd");
     const int L = p.num_layers;
@@ -1592,20 +1555,8 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     jobs.nwg = wg;
     jobs.ncolx = (ws.CP + 255) / 256;
     jobs.ncol = jobs.ncolx * kColChunks;
-    {
-        const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)wgrad_kernel<T>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)WgCfg<T>::lds);
-            attr_set = true;
-        }
-        hipLaunchKernelGGL((wgrad_kernel<T>), dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws,
-                           hp, M, p.actions.num_groups, loss_out);
-    }
-    LayoutK Lk = make_layout(p);
-    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)),
-                       dim3(256), 0, s, Lk, ws, grad, h.grad_sumsq_out);
+    launch_wgrad<T>(jobs, ws, hp, M, p.actions.num_groups, loss_out, make_layout(p), grad,
+                    h.grad_sumsq_out, s);
     return check_launch("ppo_minibatch_grad");
 }
 
@@ -1696,21 +1647,8 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     jobs.nwg = wg;
     jobs.ncolx = (ws.CP + 255) / 256;
     jobs.ncol = jobs.ncolx * kColChunks;
-    {
-        auto k = wgrad_kernel<T>;
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)WgCfg<T>::lds);
-            attr_set = true;
-        }
-        const int blocks = wg + jobs.ncol + (loss_out ? 1 : 0);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
-                           p.actions.num_groups, loss_out);
-    }
-    LayoutK Lk = make_layout_lstm(p, lstm);
-    hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)), dim3(256), 0,
-                       s, Lk, ws, grad, h.grad_sumsq_out);
+    launch_wgrad<T>(jobs, ws, hp, M, p.actions.num_groups, loss_out, make_layout_lstm(p, lstm),
+                    grad, h.grad_sumsq_out, s);
     return check_launch("lstm_ppo_minibatch_grad");
 }
 
@@ -1748,8 +1686,6 @@ static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view*
     ML_REQUIRE(ro && mb_seq && adv_stats && hp && workspace, "ppo: null pointer");
     ML_REQUIRE(step_only || grad, "ppo: null grad");
     ML_REQUIRE(mb_size >= 1, "ppo: mb_size must be >= 1");
-    ML_REQUIRE(hp->row_blocks >= 0 && hp->row_blocks <= 4 && hp->row_blocks != 3,
-               "ppo: row_blocks must be 0, 1, 2 or 4 (got %d)", hp->row_blocks);
     ML_REQUIRE(ro->N >= 1 && ro->N < (1ll << 31) && (int64_t)mb_size * ro->bptt_len < (1ll << 31),
                "ppo: N and rows per minibatch must be < 2^31");
     ML_REQUIRE(ro->bptt_len >= 1 && ro->T % ro->bptt_len == 0, "ppo: bad bptt_len");

@@ -199,7 +199,10 @@ class TorchPolicyState:
                 raise NotImplementedError(
                     "recurrent trees outside the fused path (RecurrentBackboneEncoder(MLP, LSTM) "
                     "is the fused recurrent policy)")
-            out, _ = self.actor_critic.rollout(PhiloxKey(0, 0), (), one)
+            # the tree's (empty) recurrent-state structure, e.g. ((), ()) for
+            # BackboneSeparate: passed wherever the tree takes rnn states
+            self.rnn0 = rnn
+            out, _ = self.actor_critic.rollout(PhiloxKey(0, 0), rnn, one)
         crit = out["critic"]
         self.critic_bins = 1 if not isinstance(crit, SymExpTwoHotDistribution) \
             else int(crit.logits.shape[-1])
@@ -404,7 +407,7 @@ class TorchRollout:
             ps.observe(t, obs)
             with torch.no_grad():
                 out, _ = ps.actor_critic.rollout(
-                    PhiloxKey(key[0], key[1], base + t, m.env_offset), (), pre)
+                    PhiloxKey(key[0], key[1], base + t, m.env_offset), ps.rnn0, pre)
             ps.codec.encode(pre, s.obs[t])
             s.actions[t].copy_(out["actions"].reshape(N, -1))
             s.log_probs[t].copy_(out["log_probs"].reshape(N, -1))
@@ -429,7 +432,7 @@ class TorchRollout:
             rollout_state.sim_state = so["state"]
             rollout_state.cur_obs = so["obs"]
         with torch.no_grad():
-            out, _ = ps.actor_critic.critic_only((), ps.preprocess(rollout_state.cur_obs))
+            out, _ = ps.actor_critic.critic_only(ps.rnn0, ps.preprocess(rollout_state.cur_obs))
         s.bootstrap.copy_(_critic_value(out["critic"]))
 
 
@@ -524,7 +527,7 @@ class TorchPPO:
         act_f = ac.actor
         # ActorCritic.update (actor_critic.py:98-128) with the autograd-capable
         # action_stats
-        feats_a, feats_c = ac.backbone.sequence((), mbd["dones"][..., None], obs, train=True)
+        feats_a, feats_c = ac.backbone.sequence(ps.rnn0, mbd["dones"][..., None], obs, train=True)
         dists = act_f(feats_a, train=True) if _takes_train(act_f) else act_f(feats_a)
         crit = ac.critic(feats_c, train=True) if _takes_train(ac.critic) else ac.critic(feats_c)
         logp, ent = action_stats_autograd(dists, mbd["actions"].reshape(T * M, -1))
