@@ -511,6 +511,23 @@ def emulate_world(args):
     mgr = make(dev, total, 0, total, use_graph=not args.no_graph,
                fused_sim=not args.separate_sim)
     t_1 = _time_updates(mgr, args.steps, args.warmup)
+    # modeled xGMI term of the W-rank collectives the emulation runs as
+    # one-rank calls: per minibatch the flat f32 gradient, per epoch the
+    # advantage sums (2 doubles per minibatch).  Ring all-reduce over W
+    # ranks: 2 (W - 1) steps of S / W bytes each, on one xGMI link per step
+    # (beta = 153 GB/s, the per-link figure of the MI355X brief) plus a fixed
+    # per-step latency alpha.  alpha is an ASSUMPTION (no measured xGMI hop
+    # latency is available to this build); the line reports it.
+    n_mb = EPOCHS * (total // W) // (MB // W)
+    grad_bytes = 4 * int(mgr.state.policy_list[0].params.numel())
+    alpha_us, beta_gbs = 2.0, 153.0
+
+    def ring_us(nbytes):
+        return 2 * (W - 1) * (alpha_us + nbytes / W / (beta_gbs * 1e3))
+    ar_grad = ring_us(grad_bytes)
+    ar_adv = ring_us(16 * (total // MB))  # 2 doubles per global minibatch of the epoch
+    modeled_ms = n_mb * ar_grad * 1e-3 + EPOCHS * ar_adv * 1e-3
+    t_w_model = t_w + modeled_ms * 1e-3
     print(json.dumps({
         "metric": "env-steps/sec whole-node, 65536-env PPO, at 1/2/4/8 MI355X (projection)",
         "emulated_world": W, "steps": args.steps, "warmup": args.warmup,
@@ -518,11 +535,20 @@ def emulate_world(args):
         "implied_whole_node_env_steps_per_s": total * T / t_w,
         "n1_ms_per_update": t_1 * 1e3, "n1_env_steps_per_s": total * T / t_1,
         "implied_scaling_1_to_W": t_1 / t_w,
+        "modeled_allreduce": {
+            "model": "ring: 2(W-1) x (alpha + S/W/beta) per all-reduce",
+            "alpha_us_per_step_assumed": alpha_us, "beta_GBs_per_link": beta_gbs,
+            "grad_bytes": grad_bytes, "grad_allreduces_per_update": n_mb,
+            "us_per_grad_allreduce": ar_grad, "adv_allreduces_per_update": EPOCHS,
+            "ms_per_update": modeled_ms},
+        "ms_per_update_rank_share_with_modeled_allreduce": t_w_model * 1e3,
+        "implied_scaling_1_to_W_with_modeled_allreduce": t_1 / t_w_model,
         "collectives": coll,
         "config": {"envs_per_rank": total // W, "minibatch_slice_seqs": MB // W,
                    "optimizer_steps_per_update": EPOCHS * (total // W) // (MB // W)},
-        "note": "one process: the W-rank all-reduces run as one-rank RCCL calls, so the "
-                "projection leaves out their xGMI transfer (0.36 MB per minibatch)"}))
+        "note": "one process: the W-rank all-reduces run as one-rank RCCL calls; "
+                "implied_scaling_1_to_W leaves out their xGMI transfer, the "
+                "_with_modeled_allreduce fields add the ring model above"}))
 
 
 if __name__ == "__main__":

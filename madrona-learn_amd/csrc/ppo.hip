@@ -457,6 +457,40 @@ struct RecK {
     const void* head_t_nat;  // head image, natural k order (kHeads)
 };
 
+// Row-major stores of a wave's NBW 32-feature blocks of its row (bf16), 16
+// bytes per lane: lane (r, h) holds features {4h..4h+3, 8+4h..8+4h+3} of
+// each 16-feature half (Pk words 4s .. 4s+3); one v_permlane32_swap per word
+// pair trades lane half h = 0's second quad for half h = 1's first, after
+// which lane (r, h) holds features 16s + 8h .. 16s + 8h + 7 -- two 16-byte
+// stores per block instead of four 8-byte ones (the spill of A_l / dZ_l is
+// the step kernel's largest store stream).
+template <int NBW, bool RESTORE>
+__device__ inline void store_rows16(bf16* rowp, int w, uint32_t (&wd)[NBW][8], int h) {
+    typedef __attribute__((ext_vector_type(4))) uint32_t u4;
+    // in place (the swap is an involution: RESTORE swaps back for a caller
+    // that reads the words again; no temporaries at the register peak)
+    auto swap = [&](int i, int s) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const auto v = __builtin_amdgcn_permlane32_swap(wd[i][4 * s + k], wd[i][4 * s + 2 + k],
+                                                            false, false);
+            wd[i][4 * s + k] = v[0];
+            wd[i][4 * s + 2 + k] = v[1];
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            swap(i, s);
+            *(u4*)(rowp + (w * NBW + i) * 32 + 16 * s + 8 * h) =
+                u4{wd[i][4 * s], wd[i][4 * s + 1], wd[i][4 * s + 2], wd[i][4 * s + 3]};
+            if (RESTORE) swap(i, s);
+        }
+}
+template <int NBW, bool RESTORE>
+__device__ inline void store_rows16(float*, int, f2 (&)[NBW][8], int) {}
+
 // RTW row tiles of 32 rows per workgroup (kFused): waves w and w + W * rt own
 // the same features of different rows, released by the same barriers, so
 // their weight-fragment loads of every product meet in the CU's L1.
@@ -550,9 +584,14 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
     float mean_r[L], rstd_r[L];
     const float invH = 1.0f / (float)H;
     // post-activation rows A_l (weight-gradient operands), row-major
-    auto store_act = [&](int l) {
+    // (keep: the caller reads aw again -- the bf16 store permutes it in place)
+    auto store_act = [&](int l, auto keep) {
         if (MODE == kTrunkBwd) return;
         T* arow = (T*)ws.a[l] + row * H;
+        if constexpr (std::is_same<T, bf16>::value) {
+            store_rows16<NBW, decltype(keep)::value>(arow, w, aw, h);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
@@ -568,7 +607,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
 #if ML_STORE_LATE
             frag ra[ML_STEP_RING][NBW];
             gemm_lds_issue<T, NBW, KSH, ML_STEP_RING>(ra, img, lane);
-            store_act(l - 1);  // A_{l-1}, behind this product's first weight loads
+            store_act(l - 1, std::false_type{});  // A_{l-1}, behind this product's first weight loads
             gemm_lds_run<T, NBW, KSH, ML_STEP_RING>(acc, ra, fr, img, lane);
 #else
             gemm_lds<T, NBW, KSH, ML_STEP_RING>(acc, fr, img, lane);
@@ -600,7 +639,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         STAMP(2 + 3 * l);
         ln_apply<T, NBW>(x2, mean, rstd, gb + l * 2 * H, H, w * NBW, h, aw);
         // the last layer's rows go out behind the head's weight loads (HC = 32)
-        if (!ML_STORE_LATE || (l + 1 == L && (MODE != kFused || HC != 32))) store_act(l);
+        if (!ML_STORE_LATE || (l + 1 == L && (MODE != kFused || HC != 32))) store_act(l, std::true_type{});
         if (l + 1 < L) {
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
@@ -648,7 +687,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                 frag hA[HS];
 #pragma unroll
                 for (int s2 = 0; s2 < HS; ++s2) hA[s2] = img_load<T>(hrs, lane * E * (int)sizeof(T), s2 * FB);
-                store_act(L - 1);
+                store_act(L - 1, std::false_type{});
 #pragma unroll
                 for (int s2 = 0; s2 < HS; ++s2) ha[0] = MT<T>::mma(hA[s2], hb[s2], ha[0]);
             } else
@@ -952,6 +991,10 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
                 dzw[i][k] = Pk<T>::pack(d.x, d.y);
             }
         auto store_dz = [&]() {
+            if constexpr (std::is_same<T, bf16>::value) {
+                store_rows16<NBW, false>(dzrow, w, dzw, h);
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < NBW; ++i)
 #pragma unroll
