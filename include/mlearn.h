@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 13
+#define MLEARN_ABI_VERSION 14
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -452,6 +452,9 @@ typedef struct mlearn_flat_optim {
     int32_t num_groups;
     float lr, b1, b2, eps, max_grad_norm;
     int32_t normalize_params, normalize_layernorms;
+    int32_t skip_nonfinite;   /* 1: a step whose gradient holds a NaN / Inf leaves params,
+                                 moments and step unchanged (the projections still run):
+                                 DynamicScale's where_finite, ppo.py:288-291 (fp16) */
 } mlearn_flat_optim;
 int64_t mlearn_flat_optim_workspace_bytes(int64_t n, int32_t num_groups);
 int mlearn_flat_optim_step(const mlearn_flat_optim* st, void* workspace, mlearn_stream_t stream);

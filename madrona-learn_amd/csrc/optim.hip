@@ -374,8 +374,12 @@ __global__ __launch_bounds__(256) void flat_adam_kernel(float* __restrict__ para
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         const int32_t* step, int64_t n,
                                                         const double* gpart, int64_t npart, float lr,
-                                                        float b1, float b2, float eps, float max_norm) {
+                                                        float b1, float b2, float eps, float max_norm,
+                                                        int skip_nonfinite) {
     const float gn = global_norm(gpart, npart);
+    // DynamicScale (ppo.py:288-291): a non-finite gradient keeps params and
+    // moments (every block reads the same norm: a uniform exit)
+    if (skip_nonfinite && !isfinite(gn)) return;
     const int count = step[0] + 1;
     const float c1 = 1.f - powf(b1, (float)count), c2 = 1.f - powf(b2, (float)count);
     for (int64_t p = blockIdx.x * (int64_t)256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
@@ -395,10 +399,16 @@ __global__ __launch_bounds__(256) void flat_adam_kernel(float* __restrict__ para
 __global__ __launch_bounds__(256) void flat_project_kernel(float* __restrict__ params,
                                                            const mlearn_flat_group* groups,
                                                            int ngroups, int norm_params,
-                                                           int norm_ln, int32_t* step) {
+                                                           int norm_ln, int32_t* step,
+                                                           const double* gpart, int64_t npart,
+                                                           int skip_nonfinite) {
     __shared__ double red[4];
     __shared__ float sq;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && step) step[0] += 1;
+    if (blockIdx.x == 0) {
+        // the step counter advances with the Adam update it counts
+        const bool fin = !skip_nonfinite || isfinite(global_norm(gpart, npart));
+        if (threadIdx.x == 0 && step && fin) step[0] += 1;
+    }
     if ((int)blockIdx.x >= ngroups) return;
     const mlearn_flat_group gr = groups[blockIdx.x];
     const bool on = gr.kind == 1 ? norm_params != 0 : norm_ln != 0;
@@ -454,11 +464,12 @@ int mlearn_flat_optim_step(const mlearn_flat_optim* st, void* workspace, mlearn_
     hipLaunchKernelGGL(flat_adam_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, s,
                        st->params, st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step,
                        st->n, (const double*)gpart, (int64_t)kNormBlocks, st->lr, st->b1, st->b2,
-                       st->eps, st->max_grad_norm);
+                       st->eps, st->max_grad_norm, st->skip_nonfinite);
     // (one block per group; at least one block: it also advances the step counter)
     hipLaunchKernelGGL(flat_project_kernel, dim3((unsigned)(st->num_groups > 0 ? st->num_groups : 1)),
                        dim3(256), 0, s, st->params, st->groups, st->num_groups,
-                       st->normalize_params, st->normalize_layernorms, st->step);
+                       st->normalize_params, st->normalize_layernorms, st->step,
+                       (const double*)gpart, (int64_t)kNormBlocks, st->skip_nonfinite);
     return check_launch("flat_optim_step");
 }
 

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -81,7 +81,7 @@ class FlatOptim(Structure):  # mlearn_flat_optim
                 ("adam_v", c_void_p), ("step", c_void_p), ("n", c_int64), ("groups", c_void_p),
                 ("num_groups", c_int32), ("lr", c_float), ("b1", c_float), ("b2", c_float),
                 ("eps", c_float), ("max_grad_norm", c_float), ("normalize_params", c_int32),
-                ("normalize_layernorms", c_int32)]
+                ("normalize_layernorms", c_int32), ("skip_nonfinite", c_int32)]
 
 
 class OptimState(Structure):

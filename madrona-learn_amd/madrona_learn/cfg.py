@@ -1,7 +1,8 @@
 """Training configuration dataclasses (mirrors src/madrona_learn/cfg.py:1-142).
 
 Field names, order and defaults are the reference's.  The one type change:
-``compute_dtype`` is a torch dtype (``torch.float32`` / ``torch.bfloat16``)
+``compute_dtype`` is a torch dtype (``torch.float32`` / ``torch.bfloat16`` on the fused
+kernels; ``torch.float16`` trains on the torch path with DynamicScale)
 instead of a jnp dtype; strings such as ``"bf16"`` are accepted too.
 """
 
@@ -72,6 +73,8 @@ class PBTConfig:  # cfg.py:49-65
 _DTYPE_ALIASES = {
     "f32": torch.float32, "fp32": torch.float32, "float32": torch.float32,
     "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+    # (after the bf16 names: "bfloat16" must not match "float16" first)
+    "fp16": torch.float16, "float16": torch.float16, "half": torch.float16,
 }
 
 
@@ -136,7 +139,8 @@ class TrainConfig:  # cfg.py:68-127
                     for pk, pv in self.pbt.__dict__.items():
                         rep += f"\n    {pk}: {pv}"
             elif k == "compute_dtype":
-                rep += "\n  compute_dtype: " + ("bf16" if v == torch.bfloat16 else "fp32")
+                rep += "\n  compute_dtype: " + {torch.bfloat16: "bf16",
+                                                 torch.float16: "fp16"}.get(v, "fp32")
             else:
                 rep += f"\n  {k}: {v}"
         return rep

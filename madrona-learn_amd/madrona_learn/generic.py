@@ -354,6 +354,13 @@ class TorchTrainState:
         d.max_grad_norm = float(hyper_params.max_grad_norm)
         d.normalize_params = 1
         d.normalize_layernorms = 1
+        # fp16: DynamicScale (train_state.py:402-403); a non-finite step keeps
+        # params and optimizer state (ppo.py:288-291)
+        self.scaler = None
+        if ps.compute_dtype == torch.float16:
+            from .dynamic_scale import DynamicScale
+            self.scaler = DynamicScale(dev)
+            d.skip_nonfinite = 1
         self.optim_desc = d
 
     def optimizer_step(self, policy_state):
@@ -361,14 +368,19 @@ class TorchTrainState:
                                                    nat.stream_handle()), "flat_optim_step")
 
     def state_dict(self):
-        return {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu(),
-                "update_prng_key": list(self.update_prng_key)}
+        sd = {"adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(), "step": self.step.cpu(),
+              "update_prng_key": list(self.update_prng_key)}
+        if self.scaler is not None:
+            sd["scaler"] = self.scaler.state_dict()
+        return sd
 
     def load_state_dict(self, sd):
         self.adam_m.copy_(sd["adam_m"])
         self.adam_v.copy_(sd["adam_v"])
         self.step.copy_(sd["step"])
         self.update_prng_key = tuple(sd["update_prng_key"])
+        if self.scaler is not None and "scaler" in sd:
+            self.scaler.load_state_dict(sd["scaler"])
 
 
 def _critic_value(crit):
@@ -605,10 +617,17 @@ class TorchPPO:
                 mbd = self._minibatch(seqs)
                 ps.grads.zero_()
                 loss, met = self._loss(ps, mbd, b.adv_stats[e, m])
-                (loss * self.loss_scale).backward()
+                sc = ts.scaler
+                if sc is None:
+                    (loss * self.loss_scale).backward()
+                else:  # DynamicScale.value_and_grad: scaled loss, f32 gradient / scale
+                    sc.scale_loss(loss * self.loss_scale).backward()
+                    sc.unscale_(ps.grads)
                 if b.dp.world_size > 1:
                     yield ("allreduce", ps.grads)
                 ts.optimizer_step(ps)
+                if sc is not None:
+                    sc.update(ps.grads)
                 if e == b.E - 1 and m == b.num_mb - 1:
                     _record_metrics(metrics, b.policy_idx, met)
                 metrics = user_metrics_cb(metrics, e, {"sequence_ids": seqs}, ps, ts)

@@ -388,6 +388,8 @@ def _fused_tree_problem(policy, rollout_state, sim_batch, cfg):
     from .rollouts import obs_to_matrix
     ac = policy.actor_critic
     try:
+        from . import _native as nat
+        nat.dtype_code(cfg.compute_dtype)  # fp16: torch path with DynamicScale
         prefix = ac.backbone.prefix
         obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
         compile_arch(ac, obs0.shape[1], cfg.compute_dtype)

@@ -111,6 +111,15 @@ def compile_arch(actor_critic: ActorCritic, obs_dim: int, compute_dtype) -> MlpA
     net = enc.net
     if not isinstance(net, MLP):
         raise NotImplementedError(f"fused path needs an MLP trunk, got {type(net).__name__}")
+    # the shapes the kernels are instantiated for (csrc/policy.hip
+    # validate_policy); any other MLP (models.py:99-119 takes any width and
+    # depth) trains on the torch path
+    if net.num_channels not in (64, 128, 256) or not 1 <= net.num_layers <= nat.MAX_LAYERS:
+        raise NotImplementedError(f"fused path: MLP width 64 / 128 / 256 and 1..{nat.MAX_LAYERS} "
+                                  f"layers, got {net.num_channels} x {net.num_layers}")
+    if not (16 <= int(obs_dim) <= 256 and int(obs_dim) % 16 == 0):
+        raise NotImplementedError(f"fused path: observation width a multiple of 16 in "
+                                  f"[16, 256], got {obs_dim}")
     critic = actor_critic.critic
     if isinstance(critic, DenseLayerCritic):
         critic_bins = 1

@@ -160,3 +160,72 @@ def test_action_stats_autograd_matches_torch(gpu):
     torch.testing.assert_close(logp, lp2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(ent, ent2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad, y.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_fp16_trains_with_dynamic_scale(gpu):
+    """compute_dtype fp16 (train_state.py:402-403, ppo.py:276-291): the
+    fused kernels are bf16 / f32, so the tree trains on the torch path with
+    DynamicScale.  A finite update moves the parameters and counts
+    fin_steps; a forced overflow (scale 2^126: the fp16 backward overflows)
+    leaves params (up to the projections), Adam moments and step unchanged
+    and halves the scale, as flax's where_finite + backoff."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from tests.test_gpu_train import make_policy
+    N, mb = 64, 16
+    env = DummyVecEnv(N, 64, 6, seed=5, device=gpu)
+    cfg = _cfg(N, mb, epochs=1, dtype=torch.float16)
+    assert "fp16" in repr(cfg)
+    pol = make_policy(torch.float16, 64)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), pol)
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    assert getattr(ps, "generic", False) and ts.scaler is not None
+    assert mgr.rollout_mgr.store.obs.dtype == torch.float16
+    p0 = ps.params.clone()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    nmb = N // mb
+    assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
+    assert int(ts.step.item()) == nmb
+    assert float(ts.scaler.scale.item()) == 65536.0 and int(ts.scaler.fin_steps.item()) == nmb
+    # overflow every minibatch of the next update
+    ts.scaler.scale.fill_(2.0 ** 126)
+    p1, m1, v1 = ps.params.clone(), ts.adam_m.clone(), ts.adam_v.clone()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert int(ts.step.item()) == nmb
+    assert torch.equal(ts.adam_m, m1) and torch.equal(ts.adam_v, v1)
+    torch.testing.assert_close(ps.params, p1, rtol=2e-6, atol=1e-7)  # re-projection only
+    assert float(ts.scaler.scale.item()) == 2.0 ** (126 - nmb)
+    assert int(ts.scaler.fin_steps.item()) == 0
+
+
+def test_mlp_width_outside_kernels_trains(gpu):
+    """models.py:99-119's MLP takes any width and depth; the kernels are
+    instantiated for 64 / 128 / 256 x 1..4, so a 96-wide 5-layer trunk trains
+    on the torch path: rollout store against the oracle env, GAE bit-exact,
+    parameters moved and finite."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from tests.test_gpu_train import make_policy
+    N, T = 64, 32
+    env = DummyVecEnv(N, 64, 6, seed=6, device=gpu)
+    cfg = _cfg(N, 16, epochs=1)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.float32, 96, L=5))
+    ps = mgr.state.policy_states
+    assert getattr(ps, "generic", False)
+    oenv = onat.Env(N, 64, env.k0, env.k1, 0)
+    oenv.reset()
+    p0 = ps.params.clone()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    acts = s.actions.cpu().numpy()
+    for t in range(T):
+        assert np.array_equal(s.obs[t].float().cpu().numpy(), oenv.obs), t
+        o, r, d = oenv.step(acts[t])
+        assert np.array_equal(s.rewards[t].cpu().numpy(), r)
+    adv, _ = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(), s.dones.cpu().numpy(),
+                         s.bootstrap.cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)
+    assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
