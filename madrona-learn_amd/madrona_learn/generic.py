@@ -194,13 +194,13 @@ class TorchPolicyState:
         torch.manual_seed(int(seed))
         with torch.no_grad():
             one = _slice_obs(pre, 0, 1)
-            rnn = self.actor_critic.init_recurrent_state(1)
-            if rnn not in ((), None) and _nonempty(rnn):
-                raise NotImplementedError(
-                    "recurrent trees outside the fused path (RecurrentBackboneEncoder(MLP, LSTM) "
-                    "is the fused recurrent policy)")
-            # the tree's (empty) recurrent-state structure, e.g. ((), ()) for
-            # BackboneSeparate: passed wherever the tree takes rnn states
+            rnn = _to_device(self.actor_critic.init_recurrent_state(1), device)
+            # recurrent trees (e.g. a multi-layer rnn.LSTM) carry their state
+            # through the rollout (rollout_state.rnn_states) and train from the
+            # per-chunk start states (TorchRollout / TorchPPO); otherwise the
+            # tree's (empty) state structure, e.g. ((), ()) for
+            # BackboneSeparate, is passed wherever the tree takes rnn states
+            self.recurrent = rnn not in ((), None) and _nonempty(rnn)
             self.rnn0 = rnn
             out, _ = self.actor_critic.rollout(PhiloxKey(0, 0), rnn, one)
         crit = out["critic"]
@@ -281,6 +281,29 @@ def _to_device(x, dev):
     if isinstance(x, (list, tuple)):
         return type(x)(_to_device(v, dev) for v in x)
     return x
+
+
+def _map_leaves(fn, x):
+    """fn over every tensor of a recurrent-state pytree (lists / tuples / dicts)."""
+    if isinstance(x, torch.Tensor):
+        return fn(x)
+    if isinstance(x, dict):
+        return {k: _map_leaves(fn, v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_map_leaves(fn, v) for v in x)
+    return x
+
+
+def _zip_leaves(fn, a, b):
+    """fn(a_leaf, b_leaf) over two pytrees of the same structure."""
+    if isinstance(a, torch.Tensor):
+        fn(a, b)
+    elif isinstance(a, dict):
+        for k in a:
+            _zip_leaves(fn, a[k], b[k])
+    elif isinstance(a, (list, tuple)):
+        for x, y in zip(a, b):
+            _zip_leaves(fn, x, y)
 
 
 def _nonempty(x):
@@ -413,13 +436,31 @@ class TorchRollout:
         base = int(rollout_state.counters[0].item())
         ps.begin_rollout()
         N = m.N
+        rec = ps.recurrent
+        if rec:
+            # the live carry in sim order (rollouts.py:898-901, 941-942) and
+            # the carry entering every BPTT chunk (rnn_start_states,
+            # rollouts.py:528-537), one [C][N][...] tensor per state leaf
+            rollout_state.rnn_states = _to_device(rollout_state.rnn_states, ps.device)
+            bptt = m.T // m.cfg.num_bptt_chunks
+            if getattr(s, "torch_start", None) is None:
+                C = m.cfg.num_bptt_chunks
+                s.torch_start = _map_leaves(
+                    lambda x: torch.zeros((C, *x.shape), dtype=x.dtype, device=x.device),
+                    rollout_state.rnn_states)
         for t in range(m.T):
             obs = rollout_state.cur_obs
             pre = ps.preprocess(obs)
             ps.observe(t, obs)
+            rnn_in = ps.rnn0
+            if rec:
+                if t % bptt == 0:
+                    _zip_leaves(lambda dst, src: dst[t // bptt].copy_(src), s.torch_start,
+                                rollout_state.rnn_states)
+                rnn_in = rollout_state.rnn_states
             with torch.no_grad():
-                out, _ = ps.actor_critic.rollout(
-                    PhiloxKey(key[0], key[1], base + t, m.env_offset), ps.rnn0, pre)
+                out, rnn_out = ps.actor_critic.rollout(
+                    PhiloxKey(key[0], key[1], base + t, m.env_offset), rnn_in, pre)
             ps.codec.encode(pre, s.obs[t])
             s.actions[t].copy_(out["actions"].reshape(N, -1))
             s.log_probs[t].copy_(out["log_probs"].reshape(N, -1))
@@ -443,8 +484,12 @@ class TorchRollout:
                 "rollout_post_step")
             rollout_state.sim_state = so["state"]
             rollout_state.cur_obs = so["obs"]
+            if rec:  # rnn_reset_fn(rnn_states, dones) (rollouts.py:941-942)
+                rollout_state.rnn_states = ps.actor_critic.clear_recurrent_state(
+                    rnn_out, so["dones"].reshape(-1) != 0)
         with torch.no_grad():
-            out, _ = ps.actor_critic.critic_only(ps.rnn0, ps.preprocess(rollout_state.cur_obs))
+            rnn_in = rollout_state.rnn_states if rec else ps.rnn0
+            out, _ = ps.actor_critic.critic_only(rnn_in, ps.preprocess(rollout_state.cur_obs))
         s.bootstrap.copy_(_critic_value(out["critic"]))
 
 
@@ -525,10 +570,14 @@ class TorchPPO:
         rows = (c[None, :] * bp + t) * N + b[None, :]          # [bptt, mb]
         flat = lambda x: x.reshape(s.T * N, *x.shape[2:])     # noqa: E731
         adv_src = s.advantages if self.view.advantages == s.advantages.data_ptr() else s.returns
-        return {"obs": flat(s.obs)[rows], "actions": flat(s.actions)[rows],
-                "log_probs": flat(s.log_probs)[rows], "values": flat(s.values)[rows],
-                "returns": flat(s.returns)[rows], "advantages": flat(adv_src)[rows],
-                "dones": flat(s.dones)[rows]}
+        out = {"obs": flat(s.obs)[rows], "actions": flat(s.actions)[rows],
+               "log_probs": flat(s.log_probs)[rows], "values": flat(s.values)[rows],
+               "returns": flat(s.returns)[rows], "advantages": flat(adv_src)[rows],
+               "dones": flat(s.dones)[rows]}
+        if getattr(s, "torch_start", None) is not None:
+            # rnn_start_states of the minibatch's sequences (chunk c, env b)
+            out["rnn_start"] = _map_leaves(lambda x: x[c, b], s.torch_start)
+        return out
 
     def _loss(self, ps, mbd, adv_stats):
         """ppo.py:129-262 on one minibatch (torch autograd through the user's
@@ -539,7 +588,8 @@ class TorchPPO:
         act_f = ac.actor
         # ActorCritic.update (actor_critic.py:98-128) with the autograd-capable
         # action_stats
-        feats_a, feats_c = ac.backbone.sequence(ps.rnn0, mbd["dones"][..., None], obs, train=True)
+        feats_a, feats_c = ac.backbone.sequence(mbd.get("rnn_start", ps.rnn0),
+                                                mbd["dones"][..., None], obs, train=True)
         dists = act_f(feats_a, train=True) if _takes_train(act_f) else act_f(feats_a)
         crit = ac.critic(feats_c, train=True) if _takes_train(ac.critic) else ac.critic(feats_c)
         logp, ent = action_stats_autograd(dists, mbd["actions"].reshape(T * M, -1))

@@ -229,3 +229,63 @@ def test_mlp_width_outside_kernels_trains(gpu):
                          s.bootstrap.cpu().numpy(), cfg.gamma, cfg.gae_lambda)
     assert np.array_equal(s.advantages.cpu().numpy(), adv)
     assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
+
+
+def test_multilayer_lstm_trains_on_torch_path(gpu):
+    """rnn.LSTM with num_layers = 2 (MultiLayerLSTMCell, rnn.py:10-45; the
+    fused kernels take one layer) trains on the torch path: the rollout
+    carries rollout_state.rnn_states, clears it where an episode ended
+    (rollouts.py:941-942) and saves the carry entering every BPTT chunk
+    (rnn_start_states, rollouts.py:528-537); the update runs LSTM.sequence from
+    those start states.  Self-consistency (parity unpinned: the oracle's LSTM
+    is one layer): replaying LSTM.sequence over each chunk's stored
+    observations from its stored start state with the rollout-time parameters
+    reproduces the stored log-probs and values."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.rnn import LSTM
+    N, T, C = 32, 32, 2
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=8, device=gpu)
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.RecurrentBackboneEncoder(
+            net=MLP(64, 1, dt), rnn=LSTM(64, 2, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DenseLayerCritic(dt))
+    cfg = ml.TrainConfig(
+        num_worlds=N, num_agents_per_world=1, num_updates=2,
+        actions={"actions": ml.DiscreteActionsConfig(BUCKETS)}, steps_per_update=T, lr=3e-4,
+        algo=ml.PPOConfig(num_epochs=1, minibatch_size=16, clip_coef=0.2, value_loss_coef=0.5,
+                          entropy_coef={"actions": 0.01}, max_grad_norm=0.5),
+        num_bptt_chunks=C, gamma=0.99, gae_lambda=0.95, seed=9, metrics_buffer_size=4,
+        dreamer_v3_critic=False, compute_dtype=dt)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac))
+    ps = mgr.state.policy_states
+    assert getattr(ps, "generic", False) and ps.recurrent
+    for it in range(2):
+        p_roll = ps.params.clone()
+        mgr.update_iter()
+        torch.cuda.synchronize()
+        s = mgr.rollout_mgr.store
+        if it == 0:  # the first chunk starts from the zero carry
+            for x in s.torch_start[0] + s.torch_start[1]:
+                assert not torch.any(x[0])
+        assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p_roll)
+        dones = s.dones
+        assert int(dones.sum()) > 0  # episodes end inside the rollout (carry clears exercised)
+        p_now = ps.params.clone()
+        ps.params.copy_(p_roll)
+        bp = T // C
+        with torch.no_grad():
+            for c in range(C):
+                start = ([x[c] for x in s.torch_start[0]], [x[c] for x in s.torch_start[1]])
+                obs = s.obs[c * bp:(c + 1) * bp].float()
+                fa, fc = ac.backbone.sequence(start, dones[c * bp:(c + 1) * bp, :, None], obs)
+                dists = ac.actor(fa)
+                lp, _ = dists.action_stats(s.actions[c * bp:(c + 1) * bp].reshape(bp * N, -1))
+                v = ac.critic(fc).reshape(bp, N)
+                torch.testing.assert_close(lp.reshape(bp, N, -1),
+                                           s.log_probs[c * bp:(c + 1) * bp], rtol=1e-4, atol=1e-5)
+                torch.testing.assert_close(v, s.values[c * bp:(c + 1) * bp], rtol=1e-4, atol=1e-5)
+        ps.params.copy_(p_now)
