@@ -14,6 +14,7 @@
 //   lstm_fwd_scan_kernel   the same steps in ONE launch (below)
 //   lstm_bwd_step4_kernel  dh_t = dG_{t+1} Wh^T and dF_{t+1} = dG_{t+1} Wi^T
 //                          from one stream of the dG rows -> cell backward
+//   lstm_bwd_scan_kernel   the same reverse steps in ONE launch (at the end)
 #pragma once
 
 // k-steps of weight fragments in flight per wave in the per-step scans
@@ -381,5 +382,141 @@ __global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
             cp[2 * H + u0 + e] = sg;
             cp[3 * H + u0 + e] = so;
         }
+    }
+}
+
+// The reverse scan as one launch (the forward's scheme): workgroup (tile, w)
+// runs every reverse step of its (32 sequences, 32-unit block) with the
+// Wh^T rows of its units (the dh half of w_bwd, 4H deep) resident in LDS;
+// the Wi^T rows (dF, off the recurrence) stream from L2 as in the per-step
+// kernel; the c cotangent stays in registers; the dG_{t+1} rows of ALL units
+// come from the tile's 8 unit-block workgroups through write-through (sc1)
+// stores, a per-tile counter and sc1 loads.  Partials reduced in the same
+// fixed order as lstm_bwd_step4_kernel (bit-identical); one 16 KB partial
+// buffer serves dh then dF.
+template <typename T, int H> constexpr size_t lstm_bscan_lds() {
+    return (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) + 4 * 16 * 64 * sizeof(float);
+}
+
+template <typename T, int H>
+__global__ __launch_bounds__(256) void lstm_bwd_scan_kernel(
+    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
+    float* colpart, int CP, int cp0, int* __restrict__ ctr) {
+    typedef typename RT<T>::frag frag;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NQ = NKS / 4, NU = H / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    frag* whT = (frag*)smem;                                   // [k-step][lane], the dh rows
+    float (*part)[16][64] = (float (*)[16][64])(whT + NKS * 64);  // [K quarter][register][lane]
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // K quarter (product) / register quad (cell)
+    const int tile = blockIdx.x, w = blockIdx.y;
+    const int m0 = tile * 32, m = m0 + r;
+    const int bptt = ro.bptt;
+    {
+        const frag* src = (const frag*)((const T*)R.w_bwd + (int64_t)(NU + w) * NKS * 64 * E);
+        for (int i = tid; i < NKS * 64; i += 256) whT[i] = src[i];
+    }
+    __syncthreads();
+    const int j = g, u0 = w * 32 + 8 * j + 4 * h;
+    float4 dcc_reg = make_float4(0.f, 0.f, 0.f, 0.f);  // c cotangent into the step (its units)
+    for (int t = bptt - 1; t >= -1; --t) {
+        const bool cell = t >= 0, prod = t + 1 < bptt;
+        const int64_t fs = (int64_t)t * mb + m;
+        bool cut = true;
+        float4 dho, gi, gf, gg, go, c4, ci;
+        if (cell) {
+            cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
+            const T* gts = (const T*)lw.gates + fs * 4 * H;
+            dho = load4((const T*)lw.dhout + fs * H + u0);
+            gi = load4(gts + u0);
+            gf = load4(gts + H + u0);
+            gg = load4(gts + 2 * H + u0);
+            go = load4(gts + 3 * H + u0);
+            c4 = load4((const T*)lw.cout + fs * H + u0);
+            ci = load4((const T*)lw.cin + fs * H + u0);
+        }
+        f32x16 acc[2];
+        zero_acc<2>(acc);
+        if (prod) {
+            // dG_{t+1} rows of every unit block of the tile (written last iteration)
+            int n = 0;
+            while (__hip_atomic_load(ctr + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                       NU * (bptt - 1 - t) &&
+                   ++n < kScanSpinLimit)
+                __builtin_amdgcn_s_sleep(1);
+            const T* brow = (const T*)lw.dg + (fs + mb) * 4 * H + g * H;
+            const T* img = (const T*)R.w_bwd + ((int64_t)w * NKS + g * NQ) * 64 * E;
+            const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
+            constexpr int FB = 64 * E * (int)sizeof(T);
+            const int voff = lane * E * (int)sizeof(T);
+#pragma unroll
+            for (int s = 0; s < NQ; ++s) {
+                const frag b = sc1_row<T>(brow, s, h);
+                acc[0] = MT<T>::mma(img_load<T>(rs, voff, s * FB), b, acc[0]);
+                acc[1] = MT<T>::mma(whT[(g * NQ + s) * 64 + lane], b, acc[1]);
+            }
+        }
+        float dhh[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[1][q];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = 4 * j + e;
+            dhh[e] = ((part[0][q][lane] + part[1][q][lane]) + part[2][q][lane]) + part[3][q][lane];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
+        __syncthreads();
+        if (prod) {
+            float d[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = 4 * j + e;
+                d[e] = ((part[0][q][lane] + part[1][q][lane]) + part[2][q][lane]) + part[3][q][lane];
+            }
+            store4((T*)lw.dfeat + (fs + mb) * H + u0, d[0], d[1], d[2], d[3]);
+        }
+        __syncthreads();  // part is rewritten next iteration
+        if (!cell) break;
+        const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : dcc_reg;
+        float dpi[4], dpf[4], dpg[4], dpo[4], dco[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
+            const float dh = f4get(dho, e) + (cut ? 0.f : dhh[e]);
+            const float tc = tanh_fast(f4get(c4, e));
+            const float dout = dh * tc;
+            const float dc = f4get(dcin, e) + dh * o_ * (1.f - tc * tc);
+            dpi[e] = rnd<T>((dc * g_) * i_ * (1.f - i_));
+            dpf[e] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
+            dpg[e] = rnd<T>((dc * i_) * (1.f - g_ * g_));
+            dpo[e] = rnd<T>(dout * o_ * (1.f - o_));
+            dco[e] = dc * f_;
+        }
+        dcc_reg = make_float4(dco[0], dco[1], dco[2], dco[3]);
+        T* dgs = (T*)lw.dg + fs * 4 * H;
+        sc1_store4<T>(dgs + u0, dpi[0], dpi[1], dpi[2], dpi[3]);
+        sc1_store4<T>(dgs + H + u0, dpf[0], dpf[1], dpf[2], dpf[3]);
+        sc1_store4<T>(dgs + 2 * H + u0, dpg[0], dpg[1], dpg[2], dpg[3]);
+        sc1_store4<T>(dgs + 3 * H + u0, dpo[0], dpo[1], dpo[2], dpo[3]);
+        float* cp = colpart + (int64_t)(((int64_t)t * mb + m0) / 32) * CP + cp0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float si = half_sum32(dpi[e]), sf = half_sum32(dpf[e]);
+            const float sg = half_sum32(dpg[e]), so = half_sum32(dpo[e]);
+            if (r == 0) {
+                cp[u0 + e] = si;
+                cp[H + u0 + e] = sf;
+                cp[2 * H + u0 + e] = sg;
+                cp[3 * H + u0 + e] = so;
+            }
+        }
+        // this workgroup's dG rows of step t complete (every wave), then the
+        // tile's counter (iterations t - 1 .. -1 read them)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

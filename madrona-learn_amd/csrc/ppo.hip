@@ -1700,6 +1700,23 @@ template <typename T, int H> static bool lstm_scan_resident(int mb) {
     return (int64_t)per_cu * cus >= (int64_t)(mb / 32) * (H / 32);
 }
 
+template <typename T, int H> static bool lstm_bscan_resident(int mb) {
+    static int per_cu = -1, cus = 0;
+    if (per_cu < 0) {
+        auto k = lstm_bwd_scan_kernel<T, H>;
+        int dev = 0;
+        per_cu = 0;
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lstm_bscan_lds<T, H>()) != hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256,
+                                                         lstm_bscan_lds<T, H>()) != hipSuccess)
+            per_cu = 0;
+    }
+    return (int64_t)per_cu * cus >= (int64_t)(mb / 32) * (H / 32);
+}
+
 template <typename T, int H>
 static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& lstm,
                                  const mlearn_rollout_view& ro, const void* start_h,
@@ -1761,9 +1778,16 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     step(std::integral_constant<int, kHeads>{});
     // reverse scan: dh_t and dF_{t+1} per step, then dF_0 from dG_0
     const int cp0 = L * 2 * H + head_cols(p);
-    for (int t = bptt - 1; t >= -1; --t)
-        hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
-                           RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+    if (!h.lstm_step_launches && lstm_bscan_resident<T, H>(mb)) {
+        (void)hipMemsetAsync(lw.ctr, 0, (size_t)(mb / 32) * sizeof(int), s);
+        const size_t lds = lstm_bscan_lds<T, H>();
+        hipLaunchKernelGGL((lstm_bwd_scan_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), lds, s,
+                           RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, lw.ctr);
+    } else {
+        for (int t = bptt - 1; t >= -1; --t)
+            hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
+                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
+    }
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});
     // weight gradients: trunk, head (from the LSTM outputs), Wi, Wh
