@@ -348,10 +348,11 @@ typedef struct mlearn_ppo_hparams {
                                               per-action-group means (ppo.py:221-239) are
                                               obj_weight[j] = K / K_g and entropy_coef[j] =
                                               c_g K / K_g for the group g holding j. */
-    int32_t lstm_step_launches;            /* recurrent policies: 1 runs the forward LSTM scan
-                                              as one launch per step; 0 as one persistent
-                                              launch when its grid fits the device at once
-                                              (the same bits either way) */
+    int32_t lstm_scan;                     /* recurrent policies, the LSTM scans (forward and
+                                              reverse): 1 one launch per time step; 2 one
+                                              persistent launch per direction when its grid
+                                              fits the device at once (else 1); 0 the
+                                              library's choice.  The same bits either way. */
     double* grad_sumsq_out;                /* may be NULL: per-64-parameter partial sums of
                                               grad^2 (mlearn_grad_sumsq_parts entries),
                                               written by the gradient reduction; the next

@@ -1679,6 +1679,13 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 // ---------------------------------------------------------------------------
 #include "lstm_scan.h"
 
+// mlearn_ppo_hparams.lstm_scan: 1 per-step launches, 2 persistent scans; 0
+// picks kLstmScanDefault.
+constexpr int kLstmScanDefault = 1;
+static inline int lstm_scan_mode(const mlearn_ppo_hparams& h) {
+    return h.lstm_scan == 1 || h.lstm_scan == 2 ? h.lstm_scan : kLstmScanDefault;
+}
+
 // The persistent forward scan needs every workgroup of its grid resident at
 // once (its steps wait on each other): the occupancy API's answer for its
 // LDS (the unit block's Wh image) x the CU count (once per instantiation,
@@ -1764,7 +1771,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // forward scan: one persistent launch when its whole grid is resident
     // (lstm_fwd_scan_kernel), else one launch per step over (mb / 32) x
     // (H / 32) one-wave workgroups (the input product F_t Wi inside each step)
-    if (!h.lstm_step_launches && lstm_scan_resident<T, H>(mb)) {
+    if (lstm_scan_mode(h) == 2 && lstm_scan_resident<T, H>(mb)) {
         (void)hipMemsetAsync(lw.ctr, 0, (size_t)(mb / 32) * sizeof(int), s);
         const size_t lds = lstm_scan_lds<T, H>();
         hipLaunchKernelGGL((lstm_fwd_scan_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), lds, s, RK,
@@ -1778,7 +1785,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     step(std::integral_constant<int, kHeads>{});
     // reverse scan: dh_t and dF_{t+1} per step, then dF_0 from dG_0
     const int cp0 = L * 2 * H + head_cols(p);
-    if (!h.lstm_step_launches && lstm_bscan_resident<T, H>(mb)) {
+    if (lstm_scan_mode(h) == 2 && lstm_bscan_resident<T, H>(mb)) {
         (void)hipMemsetAsync(lw.ctr, 0, (size_t)(mb / 32) * sizeof(int), s);
         const size_t lds = lstm_bscan_lds<T, H>();
         hipLaunchKernelGGL((lstm_bwd_scan_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), lds, s,

@@ -66,7 +66,7 @@ class PPOHparams(Structure):
                 ("entropy_coef", c_float * MAX_GROUPS), ("normalize_advantages", c_int32),
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
                 ("loss_scale", c_float), ("normalize_values", c_int32),
-                ("obj_weight", c_float * MAX_GROUPS), ("lstm_step_launches", c_int32),
+                ("obj_weight", c_float * MAX_GROUPS), ("lstm_scan", c_int32),
                 ("grad_sumsq_out", c_void_p)]
 
 

@@ -427,9 +427,9 @@ def test_lstm_scan_launch_forms_bit_identical(gpu, dtype, H, N, mb, bptt):
     """The forward LSTM scan as one persistent launch (lstm_fwd_scan_kernel:
     Wh resident in LDS, carries handed between the tile's unit-block
     workgroups through write-through rows and a counter) vs one launch per
-    step (mlearn_ppo_hparams.lstm_step_launches = 1): same gradient, same
-    loss metrics, bit for bit (the persistent form runs whenever the device
-    holds its whole grid, as at config L's production grid)."""
+    step (mlearn_ppo_hparams.lstm_scan = 2 vs 1): same gradient, same loss
+    metrics, bit for bit (the persistent form runs whenever the device holds
+    its whole grid, as at config L's production grid)."""
     from madrona_learn import _native as nat
     D, L, T = 64, 2, 32
     ps = make_policy_state(gpu, D, H, L, dtype, seed=H + 3)
@@ -445,9 +445,9 @@ def test_lstm_scan_launch_forms_bit_identical(gpu, dtype, H, N, mb, bptt):
     L_ = nat.lib()
     sq = torch.from_numpy(seqs).to(gpu)
     outs = []
-    for per_step in (0, 1):
+    for mode in (2, 1):
         hp = _hp(nat)
-        hp.lstm_step_launches = per_step
+        hp.lstm_scan = mode
         ws = torch.zeros(int(L_.mlearn_lstm_ppo_workspace_bytes(ps.desc, ps.lstm_desc, M, mb)),
                          dtype=torch.uint8, device=gpu)
         grad = torch.zeros(ps.layout["total"], dtype=torch.float32, device=gpu)

@@ -19,7 +19,7 @@ run() {
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider"
 run t_scan 240 $PYT tests/test_gpu_lstm.py -k "launch_forms"
 run t_lstm 400 $PYT tests/test_gpu_lstm.py tests/test_gpu_configs.py
-run bench_lstm 200 python bench.py --config lstm --steps 5 --warmup 2 --no-cpu-baseline --no-separate-sim-line
-run bench_lstm_ps 200 python bench.py --config lstm --steps 5 --warmup 2 --no-cpu-baseline --no-separate-sim-line --lstm-step-launches
+run bench_lstm 200 python bench.py --config lstm --lstm-scan 2 --steps 5 --warmup 2 --no-cpu-baseline --no-separate-sim-line
+run bench_lstm_ps 200 python bench.py --config lstm --steps 5 --warmup 2 --no-cpu-baseline --no-separate-sim-line --lstm-scan 1
 run t_all 1000 $PYT tests -m gpu
 exit 0
