@@ -352,9 +352,6 @@ def main():
                          "launches (as a user sim plugin runs) instead of fused into them")
     ap.add_argument("--critic", choices=["scalar", "twohot"], default="scalar",
                     help="DenseLayerCritic (SURVEY B1) or DreamerV3Critic (63-bin two-hot)")
-    ap.add_argument("--lstm-scan", type=int, default=0, choices=[0, 1, 2],
-                    help="config lstm: mlearn_ppo_hparams.lstm_scan (1 per-step launches, "
-                         "2 persistent scans, 0 the library's choice)")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="one process, one GPU: time rank 0's share of a W-rank headline job "
                          "(65536/W envs, minibatch slices of 2048/W seqs, every minibatch's "
@@ -387,9 +384,6 @@ def main():
     mgr = make(dev, total, rank * n_rank, n_rank, use_graph=not args.no_graph,
                config=args.config, chunks=args.bptt_chunks, critic=args.critic,
                fused_sim=not args.separate_sim)
-    if args.lstm_scan:
-        for a in getattr(mgr, "algos", [mgr.algo]):
-            a.hp.lstm_scan = args.lstm_scan
     for _ in range(args.warmup):
         mgr.update_iter()
     torch.cuda.synchronize()

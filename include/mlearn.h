@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 15
+#define MLEARN_ABI_VERSION 16
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -348,11 +348,6 @@ typedef struct mlearn_ppo_hparams {
                                               per-action-group means (ppo.py:221-239) are
                                               obj_weight[j] = K / K_g and entropy_coef[j] =
                                               c_g K / K_g for the group g holding j. */
-    int32_t lstm_scan;                     /* recurrent policies, the LSTM scans (forward and
-                                              reverse): 1 one launch per time step; 2 one
-                                              persistent launch per direction when its grid
-                                              fits the device at once (else 1); 0 the
-                                              library's choice.  The same bits either way. */
     double* grad_sumsq_out;                /* may be NULL: per-64-parameter partial sums of
                                               grad^2 (mlearn_grad_sumsq_parts entries),
                                               written by the gradient reduction; the next

@@ -11,10 +11,12 @@
 // cotangent into step t is dcc [Mp][H] f32 written by step t + 1.  B
 // fragments are read straight from the natural-order rows (RT<T>::row).
 //   lstm_fwd_step_kernel   gates_t = F_t Wi + h_{t-1} Wh + bias -> cell
-//   lstm_fwd_scan_kernel   the same steps in ONE launch (below)
 //   lstm_bwd_step4_kernel  dh_t = dG_{t+1} Wh^T and dF_{t+1} = dG_{t+1} Wi^T
 //                          from one stream of the dG rows -> cell backward
-//   lstm_bwd_scan_kernel   the same reverse steps in ONE launch (at the end)
+// (Both scans as one persistent launch per direction -- unit-block slices of
+// Wh / Wh^T resident in LDS, carries handed between a tile's workgroups
+// through write-through rows and counters -- were bit-identical and slower:
+// 13.82 vs 10.40 ms per config-L update, profiles/r04_lstm_scan_ab.txt.)
 #pragma once
 
 // k-steps of weight fragments in flight per wave in the per-step scans
@@ -114,163 +116,6 @@ __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
         if (more) {
             store4((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
             store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
-        }
-    }
-}
-
-// The forward scan as one launch.  Workgroup (tile, w) runs every step of its
-// (32 sequences, 32-unit block) with its Wh slice (4 gates x K, 64 KB bf16)
-// resident in LDS; the c carry stays in registers (its own units); the h
-// carry of ALL units is the hin rows the tile's 8 unit-block workgroups wrote
-// for this step.  Hand-off (MI355X_MICROARCH.md, sc1 hand-off table row 1):
-// every hin store is a write-through (sc1) store, the wave waits for its
-// stores (vmcnt 0), then one agent-scope atomic add on the tile's counter;
-// a consumer polls the counter with sc1 loads and reads the rows with sc1
-// loads only.  Each step's input product F_t Wi (streamed from L2) does not
-// depend on the carry and runs before the wait.  Same arithmetic, same
-// order, same stores as T launches of lstm_fwd_step_kernel (bit-identical).
-// The host launches it only when the whole grid is resident at once (the
-// occupancy API); the wait is bounded, so a miscount ends with wrong rows,
-// not a hung queue.
-constexpr int kScanSpinLimit = 1 << 22;
-template <typename T> __device__ inline void sc1_store4(T* p, float a, float b, float c, float d);
-template <> __device__ inline void sc1_store4<bf16>(bf16* p, float a, float b, float c, float d) {
-    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-    const b4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
-    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-template <> __device__ inline void sc1_store4<float>(float* p, float a, float b, float c, float d) {
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, f2v{a, b}), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((uint64_t*)(p + 2), __builtin_bit_cast(uint64_t, f2v{c, d}),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// RT<T>::row through sc1 loads (8 bytes each)
-template <typename T> __device__ inline typename RT<T>::frag sc1_row(const T* p, int s, int h);
-template <> __device__ inline bf16x8 sc1_row<bf16>(const bf16* p, int s, int h) {
-    const uint64_t* q = (const uint64_t*)(p + 16 * s + 8 * h);
-    typedef __attribute__((ext_vector_type(2))) uint64_t u2;
-    const u2 v = {__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                  __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-    return __builtin_bit_cast(bf16x8, v);
-}
-template <> __device__ inline float sc1_row<float>(const float* p, int s, int h) {
-    return __hip_atomic_load(p + 2 * s + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <typename T, int H> constexpr size_t lstm_scan_lds() {
-    return (size_t)4 * (H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag);
-}
-
-template <typename T, int H>
-__global__ __launch_bounds__(64) void lstm_fwd_scan_kernel(
-    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
-    const T* __restrict__ sh, const T* __restrict__ sc, LstmWsK lw, const T* __restrict__ feat,
-    int* __restrict__ ctr) {
-    typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, NU = H / 32;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    frag* whl = (frag*)smem;  // [gate][k-step][lane]: this unit block's Wh image
-    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    const int tile = blockIdx.x, w = blockIdx.y;
-    const int m = tile * 32 + r;
-    {
-        const frag* src = (const frag*)((const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E);
-        for (int i = lane; i < 4 * KSH * 64; i += 64) whl[i] = src[i];
-    }
-    float bz[4][16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) bz[g][4 * j + e] = R.bias[g * H + w * 32 + 8 * j + 4 * h + e];
-    // carries into step 0: the sequence's rnn_start_states (rollouts.py:533-537),
-    // also written out as step 0's hin / cin rows (backward, weight gradient)
-    const int64_t seq = mb_seq[m];
-    const int64_t sc0 = seq / ro.N, sb0 = seq - sc0 * ro.N;
-    const T* hrow0 = sh + (sc0 * ro.ld + sb0) * H;
-    float cc[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u0 = w * 32 + 8 * j + 4 * h;
-        const float4 cv = load4(sc + (sc0 * ro.ld + sb0) * H + u0);
-        const float4 hv = load4(hrow0 + u0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cc[4 * j + e] = f4get(cv, e);
-        store4((T*)lw.hin + (int64_t)m * H + u0, hv.x, hv.y, hv.z, hv.w);
-        store4((T*)lw.cin + (int64_t)m * H + u0, cv.x, cv.y, cv.z, cv.w);
-    }
-    __syncthreads();  // the Wh slice staged
-    for (int t = 0; t < ro.bptt; ++t) {
-        const int64_t f = (int64_t)t * mb + m;
-        f32x16 acc[4];
-        {
-            frag fb[KSH];
-#pragma unroll
-            for (int s = 0; s < KSH; ++s) fb[s] = RT<T>::row(feat + f * H, s, h);
-            zero_acc<4>(acc);
-            gemm_ring<T, 4, KSH, kLstmFwdDepth>(acc, fb, KSH,
-                                                (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
-        }
-        const bool more = t + 1 < ro.bptt;
-        const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
-        frag hb[KSH];
-        if (t == 0) {
-#pragma unroll
-            for (int s = 0; s < KSH; ++s) hb[s] = RT<T>::row(hrow0, s, h);
-        } else {
-            // every unit block of the tile has written its hin rows of step t
-            int n = 0;
-            while (__hip_atomic_load(ctr + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < NU * t &&
-                   ++n < kScanSpinLimit)
-                __builtin_amdgcn_s_sleep(1);
-            const T* hrow = (const T*)lw.hin + f * H;
-#pragma unroll
-            for (int s = 0; s < KSH; ++s) hb[s] = sc1_row<T>(hrow, s, h);
-        }
-#pragma unroll
-        for (int s = 0; s < KSH; ++s)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) acc[g] = MT<T>::mma(whl[(g * KSH + s) * 64 + lane], hb[s], acc[g]);
-        const float keep = done ? 0.f : 1.f;
-        T* gts = (T*)lw.gates + f * 4 * H;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int u0 = w * 32 + 8 * j + 4 * h;
-            float gi[4], gf[4], gg[4], go[4], cn[4], hn[4], hc[4], ck[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int q = 4 * j + e;
-                const CellOut o = lstm_cell_fwd<T>(acc[0][q] + bz[0][q], acc[1][q] + bz[1][q],
-                                                   acc[2][q] + bz[2][q], acc[3][q] + bz[3][q], cc[q]);
-                gi[e] = o.i;
-                gf[e] = o.f;
-                gg[e] = o.g;
-                go[e] = o.o;
-                cn[e] = o.c;
-                hn[e] = o.h;
-                ck[e] = keep * o.c;
-                hc[e] = keep * o.h;
-                cc[q] = rnd<T>(ck[e]);  // the cin row step t + 1 reads back
-            }
-            store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
-            store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
-            store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
-            store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
-            store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
-            store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
-            if (more) {
-                sc1_store4<T>((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
-                store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
-            }
-        }
-        if (more) {
-            // this wave's stores complete, then the tile's counter (one add)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -385,138 +230,3 @@ __global__ __launch_bounds__(256) void lstm_bwd_step4_kernel(
     }
 }
 
-// The reverse scan as one launch (the forward's scheme): workgroup (tile, w)
-// runs every reverse step of its (32 sequences, 32-unit block) with the
-// Wh^T rows of its units (the dh half of w_bwd, 4H deep) resident in LDS;
-// the Wi^T rows (dF, off the recurrence) stream from L2 as in the per-step
-// kernel; the c cotangent stays in registers; the dG_{t+1} rows of ALL units
-// come from the tile's 8 unit-block workgroups through write-through (sc1)
-// stores, a per-tile counter and sc1 loads.  Partials reduced in the same
-// fixed order as lstm_bwd_step4_kernel (bit-identical); one 16 KB partial
-// buffer serves dh then dF.
-template <typename T, int H> constexpr size_t lstm_bscan_lds() {
-    return (size_t)(4 * H / RT<T>::KS) * 64 * sizeof(typename RT<T>::frag) + 4 * 16 * 64 * sizeof(float);
-}
-
-template <typename T, int H>
-__global__ __launch_bounds__(256) void lstm_bwd_scan_kernel(
-    LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, LstmWsK lw,
-    float* colpart, int CP, int cp0, int* __restrict__ ctr) {
-    typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, NKS = 4 * H / KS, NQ = NKS / 4, NU = H / 32;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    frag* whT = (frag*)smem;                                   // [k-step][lane], the dh rows
-    float (*part)[16][64] = (float (*)[16][64])(whT + NKS * 64);  // [K quarter][register][lane]
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // K quarter (product) / register quad (cell)
-    const int tile = blockIdx.x, w = blockIdx.y;
-    const int m0 = tile * 32, m = m0 + r;
-    const int bptt = ro.bptt;
-    {
-        const frag* src = (const frag*)((const T*)R.w_bwd + (int64_t)(NU + w) * NKS * 64 * E);
-        for (int i = tid; i < NKS * 64; i += 256) whT[i] = src[i];
-    }
-    __syncthreads();
-    const int j = g, u0 = w * 32 + 8 * j + 4 * h;
-    float4 dcc_reg = make_float4(0.f, 0.f, 0.f, 0.f);  // c cotangent into the step (its units)
-    for (int t = bptt - 1; t >= -1; --t) {
-        const bool cell = t >= 0, prod = t + 1 < bptt;
-        const int64_t fs = (int64_t)t * mb + m;
-        bool cut = true;
-        float4 dho, gi, gf, gg, go, c4, ci;
-        if (cell) {
-            cut = t + 1 == bptt || ro.dones[store_row(ro, mb_seq, mb, fs)] != 0;
-            const T* gts = (const T*)lw.gates + fs * 4 * H;
-            dho = load4((const T*)lw.dhout + fs * H + u0);
-            gi = load4(gts + u0);
-            gf = load4(gts + H + u0);
-            gg = load4(gts + 2 * H + u0);
-            go = load4(gts + 3 * H + u0);
-            c4 = load4((const T*)lw.cout + fs * H + u0);
-            ci = load4((const T*)lw.cin + fs * H + u0);
-        }
-        f32x16 acc[2];
-        zero_acc<2>(acc);
-        if (prod) {
-            // dG_{t+1} rows of every unit block of the tile (written last iteration)
-            int n = 0;
-            while (__hip_atomic_load(ctr + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                       NU * (bptt - 1 - t) &&
-                   ++n < kScanSpinLimit)
-                __builtin_amdgcn_s_sleep(1);
-            const T* brow = (const T*)lw.dg + (fs + mb) * 4 * H + g * H;
-            const T* img = (const T*)R.w_bwd + ((int64_t)w * NKS + g * NQ) * 64 * E;
-            const __amdgpu_buffer_rsrc_t rs = img_rsrc(img);
-            constexpr int FB = 64 * E * (int)sizeof(T);
-            const int voff = lane * E * (int)sizeof(T);
-#pragma unroll
-            for (int s = 0; s < NQ; ++s) {
-                const frag b = sc1_row<T>(brow, s, h);
-                acc[0] = MT<T>::mma(img_load<T>(rs, voff, s * FB), b, acc[0]);
-                acc[1] = MT<T>::mma(whT[(g * NQ + s) * 64 + lane], b, acc[1]);
-            }
-        }
-        float dhh[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[1][q];
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int q = 4 * j + e;
-            dhh[e] = ((part[0][q][lane] + part[1][q][lane]) + part[2][q][lane]) + part[3][q][lane];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 16; ++q) part[g][q][lane] = acc[0][q];
-        __syncthreads();
-        if (prod) {
-            float d[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int q = 4 * j + e;
-                d[e] = ((part[0][q][lane] + part[1][q][lane]) + part[2][q][lane]) + part[3][q][lane];
-            }
-            store4((T*)lw.dfeat + (fs + mb) * H + u0, d[0], d[1], d[2], d[3]);
-        }
-        __syncthreads();  // part is rewritten next iteration
-        if (!cell) break;
-        const float4 dcin = cut ? make_float4(0.f, 0.f, 0.f, 0.f) : dcc_reg;
-        float dpi[4], dpf[4], dpg[4], dpo[4], dco[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float i_ = f4get(gi, e), f_ = f4get(gf, e), g_ = f4get(gg, e), o_ = f4get(go, e);
-            const float dh = f4get(dho, e) + (cut ? 0.f : dhh[e]);
-            const float tc = tanh_fast(f4get(c4, e));
-            const float dout = dh * tc;
-            const float dc = f4get(dcin, e) + dh * o_ * (1.f - tc * tc);
-            dpi[e] = rnd<T>((dc * g_) * i_ * (1.f - i_));
-            dpf[e] = rnd<T>((dc * f4get(ci, e)) * f_ * (1.f - f_));
-            dpg[e] = rnd<T>((dc * i_) * (1.f - g_ * g_));
-            dpo[e] = rnd<T>(dout * o_ * (1.f - o_));
-            dco[e] = dc * f_;
-        }
-        dcc_reg = make_float4(dco[0], dco[1], dco[2], dco[3]);
-        T* dgs = (T*)lw.dg + fs * 4 * H;
-        sc1_store4<T>(dgs + u0, dpi[0], dpi[1], dpi[2], dpi[3]);
-        sc1_store4<T>(dgs + H + u0, dpf[0], dpf[1], dpf[2], dpf[3]);
-        sc1_store4<T>(dgs + 2 * H + u0, dpg[0], dpg[1], dpg[2], dpg[3]);
-        sc1_store4<T>(dgs + 3 * H + u0, dpo[0], dpo[1], dpo[2], dpo[3]);
-        float* cp = colpart + (int64_t)(((int64_t)t * mb + m0) / 32) * CP + cp0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float si = half_sum32(dpi[e]), sf = half_sum32(dpf[e]);
-            const float sg = half_sum32(dpg[e]), so = half_sum32(dpo[e]);
-            if (r == 0) {
-                cp[u0 + e] = si;
-                cp[H + u0 + e] = sf;
-                cp[2 * H + u0 + e] = sg;
-                cp[3 * H + u0 + e] = so;
-            }
-        }
-        // this workgroup's dG rows of step t complete (every wave), then the
-        // tile's counter (iterations t - 1 .. -1 read them)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}

@@ -79,7 +79,6 @@ struct LstmWsK {
     void* dhout;  // [Mp][H]  d loss / d h_t from the heads
     void* dfeat;  // [Mp][H]  d loss / d trunk output
     float* dcc;   // [Mp][H] f32  c cotangent into step t (per-step reverse scan)
-    int* ctr;     // [mb / 32] forward-scan hand-off counters (lstm_fwd_scan_kernel)
 };
 
 struct WsK {
@@ -200,7 +199,6 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         lw.dhout = take(Mp * H * es);
         lw.dfeat = take(Mp * H * es);
         lw.dcc = (float*)take(Mp * H * sizeof(float));
-        lw.ctr = (int*)take(((mb + 31) / 32) * sizeof(int));
         if (LW) *LW = lw;
     }
     if (W) *W = w;
@@ -1679,51 +1677,6 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
 // ---------------------------------------------------------------------------
 #include "lstm_scan.h"
 
-// mlearn_ppo_hparams.lstm_scan: 1 per-step launches, 2 persistent scans; 0
-// picks kLstmScanDefault.
-constexpr int kLstmScanDefault = 1;
-static inline int lstm_scan_mode(const mlearn_ppo_hparams& h) {
-    return h.lstm_scan == 1 || h.lstm_scan == 2 ? h.lstm_scan : kLstmScanDefault;
-}
-
-// The persistent forward scan needs every workgroup of its grid resident at
-// once (its steps wait on each other): the occupancy API's answer for its
-// LDS (the unit block's Wh image) x the CU count (once per instantiation,
-// outside graph capture).
-template <typename T, int H> static bool lstm_scan_resident(int mb) {
-    static int per_cu = -1, cus = 0;
-    if (per_cu < 0) {
-        auto k = lstm_fwd_scan_kernel<T, H>;
-        int dev = 0;
-        per_cu = 0;
-        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lstm_scan_lds<T, H>()) != hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 64,
-                                                         lstm_scan_lds<T, H>()) != hipSuccess)
-            per_cu = 0;
-    }
-    return (int64_t)per_cu * cus >= (int64_t)(mb / 32) * (H / 32);
-}
-
-template <typename T, int H> static bool lstm_bscan_resident(int mb) {
-    static int per_cu = -1, cus = 0;
-    if (per_cu < 0) {
-        auto k = lstm_bwd_scan_kernel<T, H>;
-        int dev = 0;
-        per_cu = 0;
-        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lstm_bscan_lds<T, H>()) != hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256,
-                                                         lstm_bscan_lds<T, H>()) != hipSuccess)
-            per_cu = 0;
-    }
-    return (int64_t)per_cu * cus >= (int64_t)(mb / 32) * (H / 32);
-}
-
 template <typename T, int H>
 static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& lstm,
                                  const mlearn_rollout_view& ro, const void* start_h,
@@ -1768,33 +1721,18 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // trunk forward over every row (the LSTM input F = A_{L-1})
     step(std::integral_constant<int, kTrunkFwd>{});
     const T* feat = (const T*)ws.a[L - 1];
-    // forward scan: one persistent launch when its whole grid is resident
-    // (lstm_fwd_scan_kernel), else one launch per step over (mb / 32) x
-    // (H / 32) one-wave workgroups (the input product F_t Wi inside each step)
-    if (lstm_scan_mode(h) == 2 && lstm_scan_resident<T, H>(mb)) {
-        (void)hipMemsetAsync(lw.ctr, 0, (size_t)(mb / 32) * sizeof(int), s);
-        const size_t lds = lstm_scan_lds<T, H>();
-        hipLaunchKernelGGL((lstm_fwd_scan_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), lds, s, RK,
-                           R, mb_seq, mb, (const T*)start_h, (const T*)start_c, lw, feat, lw.ctr);
-    } else {
-        for (int t = 0; t < bptt; ++t)
-            hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s,
-                               RK, R, mb_seq, mb, (const T*)start_h, (const T*)start_c, lw, t, feat);
-    }
+    // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
+    // workgroups (the input product F_t Wi inside each step)
+    for (int t = 0; t < bptt; ++t)
+        hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s, RK,
+                           R, mb_seq, mb, (const T*)start_h, (const T*)start_c, lw, t, feat);
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});
     // reverse scan: dh_t and dF_{t+1} per step, then dF_0 from dG_0
     const int cp0 = L * 2 * H + head_cols(p);
-    if (lstm_scan_mode(h) == 2 && lstm_bscan_resident<T, H>(mb)) {
-        (void)hipMemsetAsync(lw.ctr, 0, (size_t)(mb / 32) * sizeof(int), s);
-        const size_t lds = lstm_bscan_lds<T, H>();
-        hipLaunchKernelGGL((lstm_bwd_scan_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), lds, s,
-                           RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, lw.ctr);
-    } else {
-        for (int t = bptt - 1; t >= -1; --t)
-            hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
-                               RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
-    }
+    for (int t = bptt - 1; t >= -1; --t)
+        hipLaunchKernelGGL((lstm_bwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s,
+                           RK, R, mb_seq, mb, lw, ws.colpart, ws.CP, cp0, t);
     // trunk backward from d features
     step(std::integral_constant<int, kTrunkBwd>{});
     // weight gradients: trunk, head (from the LSTM outputs), Wi, Wh

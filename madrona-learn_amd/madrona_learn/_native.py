@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -66,7 +66,7 @@ class PPOHparams(Structure):
                 ("entropy_coef", c_float * MAX_GROUPS), ("normalize_advantages", c_int32),
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
                 ("loss_scale", c_float), ("normalize_values", c_int32),
-                ("obj_weight", c_float * MAX_GROUPS), ("lstm_scan", c_int32),
+                ("obj_weight", c_float * MAX_GROUPS),
                 ("grad_sumsq_out", c_void_p)]
 
 

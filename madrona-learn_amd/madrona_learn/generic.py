@@ -442,9 +442,8 @@ class TorchRollout:
             # the carry entering every BPTT chunk (rnn_start_states,
             # rollouts.py:528-537), one [C][N][...] tensor per state leaf
             rollout_state.rnn_states = _to_device(rollout_state.rnn_states, ps.device)
-            bptt = m.T // m.cfg.num_bptt_chunks
+            bptt, C = m.bptt, m.C
             if getattr(s, "torch_start", None) is None:
-                C = m.cfg.num_bptt_chunks
                 s.torch_start = _map_leaves(
                     lambda x: torch.zeros((C, *x.shape), dtype=x.dtype, device=x.device),
                     rollout_state.rnn_states)

@@ -418,46 +418,3 @@ def test_lstm_graph_replay_matches_eager(gpu):
     assert torch.equal(eager.rollout_mgr.store.actions, graph.rollout_mgr.store.actions)
     assert torch.equal(eager.rollout.rnn_states[1][0], graph.rollout.rnn_states[1][0])
 
-
-@pytest.mark.parametrize("dtype,H,N,mb,bptt", [
-    (torch.bfloat16, 256, 96, 64, 32), (torch.bfloat16, 128, 96, 64, 16),
-    (torch.float32, 64, 96, 64, 32),
-    (torch.bfloat16, 256, 2048, 2048, 32)])  # config L's grid: 64 x 8 = 512 workgroups
-def test_lstm_scan_launch_forms_bit_identical(gpu, dtype, H, N, mb, bptt):
-    """The forward LSTM scan as one persistent launch (lstm_fwd_scan_kernel:
-    Wh resident in LDS, carries handed between the tile's unit-block
-    workgroups through write-through rows and a counter) vs one launch per
-    step (mlearn_ppo_hparams.lstm_scan = 2 vs 1): same gradient, same loss
-    metrics, bit for bit (the persistent form runs whenever the device holds
-    its whole grid, as at config L's production grid)."""
-    from madrona_learn import _native as nat
-    D, L, T = 64, 2, 32
-    ps = make_policy_state(gpu, D, H, L, dtype, seed=H + 3)
-    perturb(ps, 5, scale=0.2)
-    C = T // bptt
-    rng = np.random.default_rng(21)
-    st = _random_store(rng, T, N, D, H, C, ps, "bf16" if dtype == torch.bfloat16 else "f32")
-    s = _device_store(gpu, st, dtype, C)
-    seqs = rng.permutation(C * N)[:mb].astype(np.int32)
-    view = s.view(bptt)
-    stats = torch.tensor([0.1, 1.3], dtype=torch.float32, device=gpu)
-    M = mb * bptt
-    L_ = nat.lib()
-    sq = torch.from_numpy(seqs).to(gpu)
-    outs = []
-    for mode in (2, 1):
-        hp = _hp(nat)
-        hp.lstm_scan = mode
-        ws = torch.zeros(int(L_.mlearn_lstm_ppo_workspace_bytes(ps.desc, ps.lstm_desc, M, mb)),
-                         dtype=torch.uint8, device=gpu)
-        grad = torch.zeros(ps.layout["total"], dtype=torch.float32, device=gpu)
-        out = torch.zeros(25, dtype=torch.float32, device=gpu)
-        nat.check(L_.mlearn_lstm_ppo_minibatch_grad(
-            ps.desc, ps.lstm_desc, view, nat.ptr(s.start_h), nat.ptr(s.start_c), nat.ptr(sq), mb,
-            nat.ptr(stats), hp, nat.ptr(grad), nat.ptr(out), nat.ptr(ws), nat.stream_handle()),
-            "lstm minibatch grad")
-        torch.cuda.synchronize()
-        outs.append((grad.clone(), out.clone()))
-    assert torch.isfinite(outs[0][0]).all()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
