@@ -62,6 +62,7 @@ constexpr int kWgTile = 128;     // weight-gradient output tile (rows and cols)
 template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_CHUNK : 32; }
 static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
 constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number of 32-row tiles)
+
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif
@@ -457,21 +458,19 @@ struct RecK {
     const void* head_t_nat;  // head image, natural k order (kHeads)
 };
 
-// 16-byte stores of a wave's NBW 32-feature blocks (bf16): lane (r, h) holds
-// features {4h..4h+3, 8+4h..8+4h+3} of each 16-feature half s (Pk words
-// 4s .. 4s+3); one v_permlane32_swap per word pair trades half h = 0's
-// second quad for half h = 1's first, after which lane (r, h) holds the
-// natural features 16s + 8h .. 16s + 8h + 7.  Two stores per block instead
-// of four 8-byte row pieces, to one of two layouts:
-//   rows (TILED = false): row-major [Mp][H] rows (p = the lane's row);
-//   tiled (TILED = true, ML_TILED_SPILL): the 32-row tile's block b as
-//     2 x 1 KB, the lane's 16 bytes of half s at [s][lane] (p = the spill
-//     buffer): each store instruction writes 1 KB contiguously; wgrad_tile
-//     reads it (xtile / ytile).
-// In place (the swap is an involution: RESTORE swaps back for a caller that
-// reads the words again; no temporaries at the register peak).
-template <int NBW, bool RESTORE, bool TILED>
-__device__ inline void store16(bf16* p, int tile, int H, int w, uint32_t (&wd)[NBW][8], int lane) {
+// Row-major stores of a wave's NBW 32-feature blocks of its row (bf16), 16
+// bytes per lane: lane (r, h) holds features {4h..4h+3, 8+4h..8+4h+3} of
+// each 16-feature half s (Pk words 4s .. 4s+3); one v_permlane32_swap per
+// word pair trades half h = 0's second quad for half h = 1's first, after
+// which lane (r, h) holds the natural features 16s + 8h .. 16s + 8h + 7: two
+// 16-byte stores per block instead of four 8-byte row pieces (the A_l / dZ_l
+// spill is the step kernel's largest store stream; a tile-native layout with
+// 1 KB per store instruction made the step faster and the weight-gradient
+// read slower: profiles/r04_spill_layout_ab.txt).  In place (the swap is an
+// involution: RESTORE swaps back for a caller that reads the words again; no
+// temporaries at the register peak).
+template <int NBW, bool RESTORE>
+__device__ inline void store_rows16(bf16* rowp, int w, uint32_t (&wd)[NBW][8], int h) {
     typedef __attribute__((ext_vector_type(4))) uint32_t u4;
     auto swap = [&](int i, int s) {
 #pragma unroll
@@ -487,17 +486,13 @@ __device__ inline void store16(bf16* p, int tile, int H, int w, uint32_t (&wd)[N
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             swap(i, s);
-            bf16* dst = TILED ? p + (((int64_t)tile * (H >> 5) + w * NBW + i) * 2 + s) * 512 + lane * 8
-                              : p + (w * NBW + i) * 32 + 16 * s + 8 * (lane >> 5);
-            *(u4*)dst = u4{wd[i][4 * s], wd[i][4 * s + 1], wd[i][4 * s + 2], wd[i][4 * s + 3]};
+            *(u4*)(rowp + (w * NBW + i) * 32 + 16 * s + 8 * h) =
+                u4{wd[i][4 * s], wd[i][4 * s + 1], wd[i][4 * s + 2], wd[i][4 * s + 3]};
             if (RESTORE) swap(i, s);
         }
 }
-template <int NBW, bool RESTORE, bool TILED>
-__device__ inline void store16(float*, int, int, int, f2 (&)[NBW][8], int) {}
-#ifndef ML_TILED_SPILL
-#define ML_TILED_SPILL 0  // 1: tiled A / dZ spill (step 73 vs 84 us, wgrad +17 us: profiles/r04_spill_layout_ab.txt)
-#endif
+template <int NBW, bool RESTORE>
+__device__ inline void store_rows16(float*, int, f2 (&)[NBW][8], int) {}
 
 // RTW row tiles of 32 rows per workgroup (kFused): waves w and w + W * rt own
 // the same features of different rows, released by the same barriers, so
@@ -509,10 +504,6 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
     constexpr bool kFwd = MODE != kHeads;                     // runs the trunk forward
     constexpr bool kLoss = MODE == kFused || MODE == kHeads;  // heads + loss
     constexpr bool kBwd = MODE == kFused || MODE == kTrunkBwd;  // trunk backward
-    // A_l / dZ_l spill layout (store16): tiled only for the feed-forward step
-    // (whose only reader is wgrad_tile); rows for the recurrent modes (the
-    // LSTM kernels read A_{L-1} and the d-feature rows)
-    constexpr bool kTiledSpill = ML_TILED_SPILL && MODE == kFused && std::is_same<T, bf16>::value;
     typedef typename RT<T>::frag frag;
     typedef StepCfg<H> C;
     constexpr int NBW = C::NBW, W = C::W, THREADS = 64 * W;
@@ -601,10 +592,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
         if (MODE == kTrunkBwd) return;
         T* arow = (T*)ws.a[l] + row * H;
         if constexpr (std::is_same<T, bf16>::value) {
-            if constexpr (kTiledSpill)
-                store16<NBW, decltype(keep)::value, true>((T*)ws.a[l], tile, H, w, aw, lane);
-            else
-                store16<NBW, decltype(keep)::value, false>(arow, tile, H, w, aw, lane);
+            store_rows16<NBW, decltype(keep)::value>(arow, w, aw, h);
             return;
         }
 #pragma unroll
@@ -1007,10 +995,7 @@ __global__ __launch_bounds__(64 * StepCfg<H>::W * RTW) __attribute__((amdgpu_wav
             }
         auto store_dz = [&]() {
             if constexpr (std::is_same<T, bf16>::value) {
-                if constexpr (kTiledSpill)
-                    store16<NBW, false, true>((T*)ws.dz[l], tile, H, w, dzw, lane);
-                else
-                    store16<NBW, false, false>(dzrow, tile, H, w, dzw, lane);
+                store_rows16<NBW, false>(dzrow, w, dzw, h);
                 return;
             }
 #pragma unroll
@@ -1104,7 +1089,6 @@ struct WgJob {
     float* out;
     int64_t rps;
     int I, J, ti, tj, splits, wg0;
-    int xtile, ytile;  // operand in the step kernel's tiled spill layout (store16, bf16)
 };
 struct WgJobs {
     WgJob job[kMaxJobs];
@@ -1121,32 +1105,16 @@ template <typename T> struct WgCfg {
 
 typedef short short4v __attribute__((ext_vector_type(4)));
 
-// LDS column of element (row k, column c) of a bf16 staging tile with the
-// tiled spill (ML_TILED_SPILL): the 8-element group index XOR (k >> 2) & 3.
-// Staging stores of one row's 16 groups and of one group's 16 rows (the
-// tiled spill's 16-lane pass) then both cover all 64 banks; the transposed
-// reads see one XOR per half wave (their 4 rows share k >> 2), i.e. a
-// permutation of the unswizzled banks.
-__device__ inline int wg_col(int k, int c) {
-    return ML_TILED_SPILL ? ((((c >> 3) ^ ((k >> 2) & 3)) << 3) | (c & 7)) : c;
-}
-
 template <typename T> struct WgFrag;
 template <> struct WgFrag<bf16> {
     typedef bf16x8 frag;
     // lane (r, h): tile[k = 16 ks + 8 h + e][c0 + r], e = 0..7
     __device__ static frag load(const bf16* tile, int ks, int c0, int lane) {
         const int g = lane >> 4, hh = g >> 1, cc = g & 1, q = (lane >> 2) & 3, p = lane & 3;
-        const int k = 16 * ks + 8 * hh + q;
-        constexpr int LD = WgCfg<bf16>::LD;
-        // wg_col(k, c0 + 16 cc + 4 p) with c0 a multiple of 32: (k >> 2) & 3 is
-        // 2 hh for rows k and 2 hh + 1 for rows k + 4, whatever ks
-        const int glo = 2 * cc + (p >> 1), ce = 4 * (p & 1);
-        const int sw = ML_TILED_SPILL ? 2 * hh : 0, sw4 = ML_TILED_SPILL ? 2 * hh + 1 : 0;
-        const int clo = c0 + ((glo ^ sw) << 3) + ce, chi = c0 + ((glo ^ sw4) << 3) + ce;
+        const bf16* base = tile + (16 * ks + 8 * hh + q) * WgCfg<bf16>::LD + c0 + 16 * cc + 4 * p;
         typedef __attribute__((address_space(3))) short4v* lp;
-        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(tile + k * LD + clo));
-        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(tile + (k + 4) * LD + chi));
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base + 4 * WgCfg<bf16>::LD));
         typedef short short8v __attribute__((ext_vector_type(8)));
         short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(frag, v);
@@ -1202,25 +1170,6 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
     // two register sets of staged rows: chunk c + 2 is in flight while chunk c
     // is multiplied out of LDS and chunk c + 1 is written to the other buffer
     u4 rx[2][PER], ry[2][PER];
-    constexpr bool kBf = std::is_same<T, bf16>::value;
-    const bool xtile = ML_TILED_SPILL && kBf && J.xtile, ytile = ML_TILED_SPILL && kBf && J.ytile;
-    // tiled operands (store16): the tile row's 128 columns (4 blocks x 2
-    // halves x 64 lanes x 16 B) are 8 KB contiguous, piece q = idx -> row
-    // lane & 31, columns 32 (q >> 7) + 16 ((q >> 6) & 1) + 8 (lane >> 5)
-    auto tile_src = [&](const T* P, int NBk, int c0, int64_t mb0, int idx, bool& in) {
-        const int tt = idx >> 9, q = idx & 511;
-        in = (c0 >> 5) + (q >> 7) < NBk;
-        return P + ((((mb0 >> 5) + tt) * NBk + (c0 >> 5)) * 2) * 512 + (int64_t)q * 8;
-    };
-    auto lds_at = [&](int idx, bool tiled) {
-        if (tiled) {
-            const int tt = idx >> 9, q = idx & 511, ln = q & 63, k = tt * 32 + (ln & 31);
-            const int c = 32 * (q >> 7) + 16 * ((q >> 6) & 1) + 8 * (ln >> 5);
-            return k * LD + (kBf ? wg_col(k, c) : c);
-        }
-        const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
-        return rr * LD + (kBf ? wg_col(rr, cc) : cc);
-    };
     auto gload = [&](int c, int set) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
@@ -1228,19 +1177,8 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
             const int idx = tid + 256 * u;
             const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
             const u4 zero = {0u, 0u, 0u, 0u};
-            bool in;
-            if (xtile) {
-                const T* src = tile_src(X, J.I >> 5, i0, mb0, idx, in);
-                rx[set][u] = in ? *(const u4*)src : zero;
-            } else {
-                rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
-            }
-            if (ytile) {
-                const T* src = tile_src(Y, J.J >> 5, j0, mb0, idx, in);
-                ry[set][u] = in ? *(const u4*)src : zero;
-            } else {
-                ry[set][u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
-            }
+            rx[set][u] = i0 + cc < J.I ? *(const u4*)(X + (mb0 + rr) * J.I + i0 + cc) : zero;
+            ry[set][u] = j0 + cc < J.J ? *(const u4*)(Y + (mb0 + rr) * J.J + j0 + cc) : zero;
         }
     };
     auto sstore = [&](int stage, int set) {
@@ -1249,8 +1187,9 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = tid + 256 * u;
-            *(u4*)(xs + lds_at(idx, xtile)) = rx[set][u];
-            *(u4*)(ys + lds_at(idx, ytile)) = ry[set][u];
+            const int rr = idx / CPR, cc = (idx - rr * CPR) * VPC;
+            *(u4*)(xs + rr * LD + cc) = rx[set][u];
+            *(u4*)(ys + rr * LD + cc) = ry[set][u];
         }
     };
     f32x16 acc[2][2];
@@ -1651,9 +1590,6 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
         J.J = l == L ? head_cols(p) : H;
         J.X = l == 0 ? ws.x0 : ws.a[l - 1];
         J.Y = l == L ? ws.dhead : ws.dz[l];
-        // (ML_TILED_SPILL: the feed-forward step spills A_l and dZ_l tiled in bf16)
-        J.xtile = l > 0;
-        J.ytile = l < L;
         J.out = ws.slab + ws.slab_off[l];
         J.rps = ws.rps[l];
         J.ti = (J.I + kWgTile - 1) / kWgTile;
