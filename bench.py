@@ -126,7 +126,7 @@ def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
     return fwd, bwd_dx, wgrad
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r03.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r04.json")
 
 
 def pmc_traffic(kernel_key):
