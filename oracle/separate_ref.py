@@ -78,9 +78,15 @@ def project(named, init_norms, L):
 
 def ppo_update(named, order, store, hp, buckets, L, init_norms, *, num_epochs, minibatch_size,
                bptt, key, epoch_base, mode, lr, max_grad_norm, ad=np.float64):
-    """_ppo (ppo.py:366-488), one rank: the same minibatch plan as
-    ppo_ref.ppo_update; the optimizer runs over the flat vector in `order`
-    (the parameter names in the torch arena's order)."""
+    """_ppo (ppo.py:366-488): the same minibatch plan as ppo_ref.ppo_update;
+    the optimizer runs over the flat vector in `order` (the parameter names in
+    the torch arena's order).  `store` is one rank's [T][N] store or a list of
+    them (data parallelism: each optimizer step over the union of the ranks'
+    minibatches -- union advantage statistics, gradient = sum over ranks of
+    the rank-local gradients of the loss scaled by 1 / world)."""
+    stores = store if isinstance(store, (list, tuple)) else [store]
+    world = len(stores)
+    store = stores[0]
     T, N = store["rewards"].shape
     nseq = (T // bptt) * N
     nmb = nseq // minibatch_size
@@ -99,14 +105,21 @@ def ppo_update(named, order, store, hp, buckets, L, init_norms, *, num_epochs, m
     count = 0
     met = None
     for e in range(num_epochs):
-        perm = ref.epoch_permutation(key[0], key[1], epoch_base + e, 0, nseq)
+        perms = [ref.epoch_permutation(key[0], key[1], epoch_base + e, r, nseq)
+                 for r in range(world)]
         for i in range(nmb):
-            ids = perm[i * minibatch_size:(i + 1) * minibatch_size]
-            b = ref.gather_minibatch(store, ref.minibatch_rows(ids, N, bptt))
-            adv = np.asarray(b[ref.objective_key(hp)], np.float64)
-            _, G, met = loss_grads(unflat(flat), b, hp, buckets, L, mode, (adv.mean(), adv.var()),
-                                   ad)
-            g = np.concatenate([np.asarray(G[k], ad).reshape(-1) for k in order])
+            bs = [ref.gather_minibatch(stores[r], ref.minibatch_rows(
+                perms[r][i * minibatch_size:(i + 1) * minibatch_size], N, bptt))
+                for r in range(world)]
+            adv = np.concatenate([np.asarray(b[ref.objective_key(hp)], np.float64) for b in bs])
+            g = None
+            for r, b in enumerate(bs):
+                _, G, m_r = loss_grads(unflat(flat), b, hp, buckets, L, mode,
+                                       (adv.mean(), adv.var()), ad)
+                gr = np.concatenate([np.asarray(G[k], ad).reshape(-1) for k in order]) / world
+                g = gr if g is None else g + gr
+                if r == 0:
+                    met = m_r
             g, _ = ref.clip_by_global_norm(g, max_grad_norm)
             flat, m, v = ref.adam_step(flat, g, m, v, count, lr)
             count += 1
