@@ -736,12 +736,14 @@ static int64_t rollout_grid(int L, int64_t N, int max_wg) {
     int64_t slots = (int64_t)per_cu * cus;
     if (max_wg < 0 || slots <= 0) return -1;
     if (max_wg > 0 && max_wg < slots) slots = max_wg;
-    // ceil(tiles / slots) tiles per workgroup in series (headline: 2 048
-    // tiles, 768 slots, 3 per workgroup; 1.648 ms vs 33 per-step launches
-    // ~1.65-1.70 ms, +1 % on the update; the W = 8 share: one tile per
-    // workgroup, 3.91 vs 3.99 ms)
-    const int64_t per = (tiles + slots - 1) / slots;
-    return (tiles + per - 1) / per;
+    // one workgroup per resident slot, tiles dealt round-robin (tile =
+    // blockIdx + k * grid): at the headline's 2 048 tiles on 768 slots every
+    // CU holds workgroups b, b + 256, b + 512 with 3 + 3 + 2 = 8 tiles, the
+    // chip's mean.  The earlier grid of ceil(tiles / 3) = 683 workgroups left
+    // CUs with 9 or 6 tiles: 1.66 -> 1.45 ms per rollout, 10.01 -> 9.80 ms
+    // per update (profiles/r04_rollout_grid_ab.txt).  The W = 8 share (256
+    // tiles) keeps one tile per workgroup.
+    return tiles < slots ? tiles : slots;
 }
 
 // The whole rollout as one launch (every env tile gets a resident workgroup,
