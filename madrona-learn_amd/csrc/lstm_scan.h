@@ -10,7 +10,7 @@
 // hin / cin written by step t - 1 (cleared where dones[t - 1]), the c
 // cotangent into step t is dcc [Mp][H] f32 written by step t + 1.  B
 // fragments are read straight from the natural-order rows (RT<T>::row).
-//   lstm_fwd_step_kernel   gates_t = F_t Wi + h_{t-1} Wh + bias -> cell
+//   lstm_fwd_step4_kernel  gates_t = F_t Wi + h_{t-1} Wh + bias -> cell
 //   lstm_bwd_step4_kernel  dh_t = dG_{t+1} Wh^T and dF_{t+1} = dG_{t+1} Wi^T
 //                          from one stream of the dG rows -> cell backward
 // (Both scans as one persistent launch per direction -- unit-block slices of
@@ -20,23 +20,32 @@
 #pragma once
 
 // k-steps of weight fragments in flight per wave in the per-step scans
-// (DEPTH > k-steps: the whole product's loads issued up front)
+// (DEPTH >= k-steps: the whole product's loads issued up front)
 constexpr int kLstmFwdDepth = 8, kLstmBwdDepth = 8;
 
+// Forward step t with four waves per (32 sequences, 32-unit block): wave g
+// computes k-half (g & 1) of the input product F_t Wi (g < 2) or of the
+// hidden product h_{t-1} Wh (g >= 2) for all four gate blocks; the four
+// partials meet in LDS and are summed in fixed order ((p0 + p1) + p2) + p3;
+// wave j then runs the cell update for register quad j (as the reverse step).
+// The carry rows into step t: the sequence's rnn_start_states (rollouts.py:
+// 533-537) at step 0 (also written out as the step's hin / cin rows for the
+// backward and the weight gradient), else the rows step t - 1 wrote.
+// (One wave per workgroup doing both whole products: 11.13 vs 10.84 us per
+// step, 10.26 vs 10.14 ms per config-L update, profiles/r04_lstm_fwd4_ab.txt.)
 template <typename T, int H>
-__global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
+__global__ __launch_bounds__(256) void lstm_fwd_step4_kernel(
     LstmK R, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb,
     const T* __restrict__ sh, const T* __restrict__ sc, LstmWsK lw, int t,
     const T* __restrict__ feat) {
     typedef typename RT<T>::frag frag;
-    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS;
-    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    constexpr int KS = RT<T>::KS, E = RT<T>::E, KSH = H / KS, KH = KSH / 2;
+    __shared__ float part[4][4][16][64];  // wave g, gate block, accumulator register q, lane
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = blockIdx.x, w = blockIdx.y;
     const int m = tile * 32 + r;
     const int64_t f = (int64_t)t * mb + m;
-    // carry rows into step t: the sequence's rnn_start_states (rollouts.py:
-    // 533-537) at step 0 (also written out as the step's hin / cin rows for
-    // the backward and the weight gradient), else the rows step t - 1 wrote
     const T *hrow, *crow;
     if (t == 0) {
         const int64_t seq = mb_seq[m];
@@ -47,76 +56,65 @@ __global__ __launch_bounds__(64) void lstm_fwd_step_kernel(
         hrow = (const T*)lw.hin + f * H;
         crow = (const T*)lw.cin + f * H;
     }
-    frag hb[KSH];
+    const int k0 = (g & 1) * KH;
+    const T* brow = g < 2 ? feat + f * H : hrow;
+    frag bf[KH];
 #pragma unroll
-    for (int s = 0; s < KSH; ++s) hb[s] = RT<T>::row(hrow, s, h);
-    float cc[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u0 = w * 32 + 8 * j + 4 * h;
-        const float4 cv = load4(crow + u0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cc[4 * j + e] = f4get(cv, e);
-        if (t == 0) {
-            const float4 hv = load4(hrow + u0);
-            store4((T*)lw.hin + f * H + u0, hv.x, hv.y, hv.z, hv.w);
-            store4((T*)lw.cin + f * H + u0, cv.x, cv.y, cv.z, cv.w);
-        }
-    }
-    // the input product F_t Wi (F = the step's trunk output rows), then the
-    // hidden product into the same accumulators
-    f32x16 acc[4];
-    {
-        frag fb[KSH];
-#pragma unroll
-        for (int s = 0; s < KSH; ++s) fb[s] = RT<T>::row(feat + f * H, s, h);
-        zero_acc<4>(acc);
-        gemm_ring<T, 4, KSH, kLstmFwdDepth>(acc, fb, KSH,
-                                            (const T*)R.wi_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
-    }
-    // the cell's other operands (done flag: two dependent loads; the biases)
-    // in flight under the product: gemm_ring's scheduling fences would
-    // otherwise leave their round trips after the last MFMA
+    for (int s = 0; s < KH; ++s) bf[s] = RT<T>::row(brow, k0 + s, h);
+    // cell operands of register quad j = g in flight under the product
+    const int j = g, u0 = w * 32 + 8 * j + 4 * h;
+    const float4 cv = load4(crow + u0);
     const bool more = t + 1 < ro.bptt;
     const bool done = more && ro.dones[store_row(ro, mb_seq, mb, f)] != 0;
-    float bz[4][16];
+    float bz[4][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int gt = 0; gt < 4; ++gt) bz[gt][e] = R.bias[gt * H + u0 + e];
+    if (t == 0) {
+        const float4 hv = load4(hrow + u0);
+        store4((T*)lw.hin + f * H + u0, hv.x, hv.y, hv.z, hv.w);
+        store4((T*)lw.cin + f * H + u0, cv.x, cv.y, cv.z, cv.w);
+    }
+    f32x16 acc[4];
+    zero_acc<4>(acc);
+    const T* img = (const T*)(g < 2 ? R.wi_nat : R.wh_nat) + ((int64_t)w * 4 * KSH + k0) * 64 * E;
+    gemm_ring<T, 4, KH, (kLstmFwdDepth < KH ? kLstmFwdDepth : KH)>(acc, bf, KH, img, lane, KSH);
 #pragma unroll
-            for (int g = 0; g < 4; ++g) bz[g][4 * j + e] = R.bias[g * H + w * 32 + 8 * j + 4 * h + e];
-    gemm_ring<T, 4, KSH, kLstmFwdDepth>(acc, hb, KSH, (const T*)R.wh_nat + (int64_t)w * 4 * KSH * 64 * E, lane);
+    for (int gt = 0; gt < 4; ++gt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) part[g][gt][q][lane] = acc[gt][q];
+    __syncthreads();
     const float keep = done ? 0.f : 1.f;
     T* gts = (T*)lw.gates + f * 4 * H;
+    float gi[4], gf[4], gg[4], go[4], cn[4], hn[4], hc[4], ck[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u0 = w * 32 + 8 * j + 4 * h;
-        float gi[4], gf[4], gg[4], go[4], cn[4], hn[4], hc[4], ck[4];
+    for (int e = 0; e < 4; ++e) {
+        const int q = 4 * j + e;
+        float z[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int q = 4 * j + e, u = u0 + e;
-            const CellOut o = lstm_cell_fwd<T>(acc[0][q] + bz[0][q], acc[1][q] + bz[1][q],
-                                               acc[2][q] + bz[2][q], acc[3][q] + bz[3][q], cc[q]);
-            gi[e] = o.i;
-            gf[e] = o.f;
-            gg[e] = o.g;
-            go[e] = o.o;
-            cn[e] = o.c;
-            hn[e] = o.h;
-            ck[e] = keep * o.c;
-            hc[e] = keep * o.h;
-        }
-        store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
-        store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
-        store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
-        store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
-        store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
-        store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
-        if (more) {
-            store4((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
-            store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
-        }
+        for (int gt = 0; gt < 4; ++gt)
+            z[gt] = (((part[0][gt][q][lane] + part[1][gt][q][lane]) + part[2][gt][q][lane]) +
+                     part[3][gt][q][lane]) + bz[gt][e];
+        const CellOut o = lstm_cell_fwd<T>(z[0], z[1], z[2], z[3], f4get(cv, e));
+        gi[e] = o.i;
+        gf[e] = o.f;
+        gg[e] = o.g;
+        go[e] = o.o;
+        cn[e] = o.c;
+        hn[e] = o.h;
+        ck[e] = keep * o.c;
+        hc[e] = keep * o.h;
+    }
+    store4(gts + u0, gi[0], gi[1], gi[2], gi[3]);
+    store4(gts + H + u0, gf[0], gf[1], gf[2], gf[3]);
+    store4(gts + 2 * H + u0, gg[0], gg[1], gg[2], gg[3]);
+    store4(gts + 3 * H + u0, go[0], go[1], go[2], go[3]);
+    store4((T*)lw.cout + f * H + u0, cn[0], cn[1], cn[2], cn[3]);
+    store4((T*)lw.hout + f * H + u0, hn[0], hn[1], hn[2], hn[3]);
+    if (more) {
+        store4((T*)lw.hin + (f + mb) * H + u0, hc[0], hc[1], hc[2], hc[3]);
+        store4((T*)lw.cin + (f + mb) * H + u0, ck[0], ck[1], ck[2], ck[3]);
     }
 }
 

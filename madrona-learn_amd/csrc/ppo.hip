@@ -1657,10 +1657,10 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     // trunk forward over every row (the LSTM input F = A_{L-1})
     step(std::integral_constant<int, kTrunkFwd>{});
     const T* feat = (const T*)ws.a[L - 1];
-    // forward scan: one launch per step over (mb / 32) x (H / 32) one-wave
+    // forward scan: one launch per step over (mb / 32) x (H / 32) four-wave
     // workgroups (the input product F_t Wi inside each step)
     for (int t = 0; t < bptt; ++t)
-        hipLaunchKernelGGL((lstm_fwd_step_kernel<T, H>), dim3(mb / 32, H / 32), dim3(64), 0, s, RK,
+        hipLaunchKernelGGL((lstm_fwd_step4_kernel<T, H>), dim3(mb / 32, H / 32), dim3(256), 0, s, RK,
                            R, mb_seq, mb, (const T*)start_h, (const T*)start_c, lw, t, feat);
     // heads + loss from the LSTM outputs
     step(std::integral_constant<int, kHeads>{});

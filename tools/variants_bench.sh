@@ -12,5 +12,5 @@ for v in ${VARIANTS}; do
   export MADRONA_LEARN_LIB=$PWD/$lib
   timeout -k 10 240 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/var_$v.json 2> gpurun_out/var_$v.err
   rc=$?; if [ $rc -ne 0 ]; then echo "$v bench rc=$rc"; tail -5 gpurun_out/var_$v.err; exit $rc; fi
-  python -c "import json,sys; d=json.load(open('gpurun_out/var_$v.json')); k=d.get('kernels',{}); print('$v', round(d['ms_per_step'],4), 'ms step_us', round(d.get('roofline',{}).get('avg_launch_us'),2), 'rollout_us', round(k.get('policy_rollout',{}).get('avg_launch_us'),2), 'minibatch', k.get('minibatch'))"
+  python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); k=d.get('kernels',{}); r=d.get('roofline',{}); print('$v', round(d['ms_per_step'],4), 'ms', r.get('kernel'), r.get('avg_launch_us'), 'rollout_us', k.get('policy_rollout',{}).get('avg_launch_us'), 'minibatch', k.get('minibatch'))"
 done
