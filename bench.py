@@ -357,7 +357,13 @@ def main():
                          "(65536/W envs, minibatch slices of 2048/W seqs, every minibatch's "
                          "gradient all-reduce a real RCCL call on a one-rank communicator) and "
                          "the N=1 headline, and print the implied 1->W strong scaling")
+    ap.add_argument("--per-policy-rollouts", action="store_true",
+                    help="config pbt: one whole-rollout launch per policy instead of the "
+                         "population launch (RolloutManager.population_launch = False)")
     args = ap.parse_args()
+    if args.per_policy_rollouts:
+        from madrona_learn.rollouts import RolloutManager
+        RolloutManager.population_launch = False
     if args.emulate_world > 1:
         return emulate_world(args)
 

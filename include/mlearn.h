@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 16
+#define MLEARN_ABI_VERSION 17
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -634,16 +634,39 @@ typedef struct mlearn_rollout_out {
     int64_t ld;
     float gamma;
     int32_t max_workgroups;     /* 0: one workgroup per resident slot (every CU busy; with
-                                   more 32-env tiles than slots each workgroup runs
-                                   ceil(tiles / slots) tiles in series); > 0: at most this
-                                   many workgroups (tiles in series); < 0: T + 1 per-step
-                                   launches of the same body (same bits either way) */
+                                   more 32-env tiles than slots the tiles are dealt
+                                   round-robin, 2-3 in series per workgroup at the headline);
+                                   > 0: at most this many workgroups (tiles in series);
+                                   < 0: T + 1 per-step launches of the same body (same bits
+                                   either way) */
 } mlearn_rollout_out;
 int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                               const mlearn_lstm_carry* carry, const float* obs, int64_t N,
                               const mlearn_rollout_out* out, uint32_t k0, uint32_t k1,
                               const uint64_t* step_ctr, uint32_t env_offset,
                               const mlearn_dummy_env* env, mlearn_stream_t stream);
+/* A population's whole rollouts as ONE launch (replaces the P launches of
+ * mlearn_policy_rollout_env a PBT population issues, one per policy's env
+ * columns, rollouts.py:501-577 run per policy by the reference's
+ * rollout_loop over its policy_assignments): policy p's arguments -- exactly
+ * those of its own mlearn_policy_rollout_env call, N envs each, every policy
+ * of the same shape, max_workgroups 0 -- are written once into a device
+ * buffer of mlearn_policy_pop_bytes(P) bytes by mlearn_policy_pop_prepare
+ * (synchronous copy; call it outside stream capture, again whenever one of
+ * the pointers changes); mlearn_policy_rollout_env_pop then launches the
+ * P * ceil(N / 32) env tiles over one workgroup per resident slot (capture-
+ * safe).  Same bits as the P separate launches.  lstms / carries: arrays of
+ * P, or both null for feed-forward policies. */
+int64_t mlearn_policy_pop_bytes(int32_t num_policies);
+int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies, const mlearn_lstm* lstms,
+                              const mlearn_lstm_carry* carries, const float* const* obs,
+                              int64_t N, const mlearn_rollout_out* outs,
+                              const uint32_t* env_offsets, const mlearn_dummy_env* envs,
+                              int32_t num_policies, void* pop);
+int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0, const mlearn_lstm* lstm0,
+                                  const void* pop, int32_t num_policies, int64_t N,
+                                  uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
+                                  mlearn_stream_t stream);
 /* Workgroups mlearn_policy_rollout_env launches for N envs under
  * max_workgroups (0 = the launch it would issue per-step: -1 means per-step
  * launches are used, i.e. the occupancy query failed or max_workgroups < 0);

@@ -9,6 +9,8 @@
 //   rounded to the compute dtype; heads: rnd(rnd(x.W) + rnd(b)); critic and
 //   logits upcast to f32 (dists.py:22, models.py:154).
 
+#include <vector>
+
 #include "common.h"
 #include "dists.h"
 #include "env.h"
@@ -613,65 +615,115 @@ struct RollK {
     int max_wg;          // mlearn_rollout_out.max_workgroups
 };
 
+// LayerNorm / head-bias parameters, LSTM bias, critic bins of policy P
+// staged in LDS for every step of a tile (the body's first statistics
+// barrier orders them)
+template <typename T, int H, bool RNN, int HC>
+__device__ inline void rollout_stage(const PolicyK& P, const LstmK& R) {
+    constexpr int THREADS = pol_threads<H, RNN>();
+    constexpr int KSH = H / RT<T>::KS;
+    constexpr int LGS = HC + 1;
+    constexpr int W = THREADS / 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* gb = (float*)((typename RT<T>::frag*)smem + KSH * 64);
+    float* hbias = gb + P.L * 2 * H;
+    float* rbias = hbias + HC + W * 64 + head_parts<HC, W>() * 32 * LGS + 32 * LGS;
+    float* bins = rbias + (RNN ? 4 * H : 0);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < P.L * 2 * H + HC; i += THREADS) {
+        float v;
+        if (i < P.L * 2 * H) {
+            const int l = i / (2 * H), c = i - l * 2 * H;
+            v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
+        } else {
+            v = P.head_b[i - P.L * 2 * H];
+        }
+        gb[i] = v;
+    }
+    if constexpr (RNN)
+        for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
+    if (P.CB > 1)
+        for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
+}
+
+// All T steps + the bootstrap of one 32-env tile (first: the workgroup's
+// first tile, whose step 0 needs no leading barrier; RESTAGE: a later tile
+// may belong to another policy, whose parameters are staged after that
+// barrier).
+template <typename T, int H, bool RNN, int HC, bool RESTAGE>
+__device__ inline void rollout_tile(const PolicyK& P, const float* __restrict__ obs, int64_t N,
+                                    const RollK& rk, uint32_t k0, uint32_t k1,
+                                    const uint64_t* step_ctr, uint32_t eoff, const LstmK& R,
+                                    const CarryK& cy0, const EnvK& env, int tile, bool first) {
+#pragma clang loop unroll(disable)
+    for (int t = 0; t <= rk.T; ++t) {
+        // the previous step's LDS reads (and its env outputs, read by this
+        // step's post-step and first product) are ordered by the barrier
+        if (t > 0 || !first) __syncthreads();
+        if (RESTAGE && t == 0 && !first) rollout_stage<T, H, RNN, HC>(P, R);
+        const bool act = t < rk.T;
+        const int64_t so = (int64_t)t * rk.ld;
+        PostK post{};
+        if (t > 0)
+            post = PostK{env.rew, env.done, rk.rewards + so - rk.ld, rk.dones + so - rk.ld,
+                         rk.env_returns, rk.trace ? rk.trace + so - rk.ld : nullptr, rk.gamma};
+        CarryK cy = cy0;
+        if constexpr (RNN) {
+            const bool cs = act && t % rk.bptt == 0;
+            const int64_t co = (int64_t)(t / rk.bptt) * rk.ld * H;
+            cy.sh = cs ? (void*)((T*)rk.start_h + co) : nullptr;
+            cy.sc = cs ? (void*)((T*)rk.start_c + co) : nullptr;
+            cy.commit = act ? 1 : 0;
+        }
+        policy_step_body<T, H, RNN, HC, pol_maxw<RNN>(), true>(
+            P, obs, N, (act && rk.obs) ? (T*)rk.obs + so * P.D : nullptr,
+            act ? rk.actions + so * P.K : nullptr, act ? rk.logp + so * P.K : nullptr,
+            act ? rk.values + so : rk.bootstrap, k0, k1, step_ctr, (uint64_t)t, eoff, 1, post,
+            R, cy, EvalK{}, act ? env : EnvK{}, tile);
+    }
+}
+
 template <typename T, int H, bool RNN, int HC>
 __global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_waves_per_eu(RNN ? ML_ROLL_RNN_WAVES : ML_ROLL_MLP_WAVES, 8))) void policy_rollout_kernel(
     PolicyK P, const float* __restrict__ obs, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
     const uint64_t* step_ctr, uint32_t eoff, LstmK R, CarryK cy0, EnvK env) {
     const int ntiles = (int)((N + 31) / 32);
-    {
-        // LayerNorm / head-bias parameters, LSTM bias, critic bins: staged
-        // once for every step (the body's first statistics barrier orders them)
-        constexpr int THREADS = pol_threads<H, RNN>();
-        constexpr int KSH = H / RT<T>::KS;
-        constexpr int LGS = HC + 1;
-        constexpr int W = THREADS / 64;
-        extern __shared__ __attribute__((aligned(16))) char smem[];
-        float* gb = (float*)((typename RT<T>::frag*)smem + KSH * 64);
-        float* hbias = gb + P.L * 2 * H;
-        float* rbias = hbias + HC + W * 64 + head_parts<HC, W>() * 32 * LGS + 32 * LGS;
-        float* bins = rbias + (RNN ? 4 * H : 0);
-        const int tid = threadIdx.x;
-        for (int i = tid; i < P.L * 2 * H + HC; i += THREADS) {
-            float v;
-            if (i < P.L * 2 * H) {
-                const int l = i / (2 * H), c = i - l * 2 * H;
-                v = c < H ? P.lns[l][c] : P.lnb[l][c - H];
-            } else {
-                v = P.head_b[i - P.L * 2 * H];
-            }
-            gb[i] = v;
-        }
-        if constexpr (RNN)
-            for (int i = tid; i < 4 * H; i += THREADS) rbias[i] = R.bias[i];
-        if (P.CB > 1)
-            for (int i = tid; i < P.CB; i += THREADS) bins[i] = twohot_bin(i, P.CB);
-    }
-    for (int tile = blockIdx.x; tile < ntiles; tile += (int)gridDim.x) {
-#pragma clang loop unroll(disable)
-        for (int t = 0; t <= rk.T; ++t) {
-            // the previous step's LDS reads (and its env outputs, read by this
-            // step's post-step and first product) are ordered by the barrier
-            if (t > 0 || tile != (int)blockIdx.x) __syncthreads();
-            const bool act = t < rk.T;
-            const int64_t so = (int64_t)t * rk.ld;
-            PostK post{};
-            if (t > 0)
-                post = PostK{env.rew, env.done, rk.rewards + so - rk.ld, rk.dones + so - rk.ld,
-                             rk.env_returns, rk.trace ? rk.trace + so - rk.ld : nullptr, rk.gamma};
-            CarryK cy = cy0;
-            if constexpr (RNN) {
-                const bool cs = act && t % rk.bptt == 0;
-                const int64_t co = (int64_t)(t / rk.bptt) * rk.ld * H;
-                cy.sh = cs ? (void*)((T*)rk.start_h + co) : nullptr;
-                cy.sc = cs ? (void*)((T*)rk.start_c + co) : nullptr;
-                cy.commit = act ? 1 : 0;
-            }
-            policy_step_body<T, H, RNN, HC, pol_maxw<RNN>(), true>(
-                P, obs, N, (act && rk.obs) ? (T*)rk.obs + so * P.D : nullptr,
-                act ? rk.actions + so * P.K : nullptr, act ? rk.logp + so * P.K : nullptr,
-                act ? rk.values + so : rk.bootstrap, k0, k1, step_ctr, (uint64_t)t, eoff, 1, post,
-                R, cy, EvalK{}, act ? env : EnvK{}, tile);
-        }
+    rollout_stage<T, H, RNN, HC>(P, R);  // once: every tile has the same policy
+    for (int tile = blockIdx.x; tile < ntiles; tile += (int)gridDim.x)
+        rollout_tile<T, H, RNN, HC, false>(P, obs, N, rk, k0, k1, step_ctr, eoff, R, cy0, env,
+                                           tile, tile == (int)blockIdx.x);
+}
+
+// A population's whole rollouts in one launch (mlearn_policy_rollout_env_pop):
+// policy p's launch arguments are entry p of a device array written once by
+// mlearn_policy_pop_prepare; global tile g is tile g % tpp of policy g / tpp,
+// dealt round-robin over one workgroup per resident slot like the
+// single-policy launch, so P launches of B / 32 workgroups become one launch
+// that fills the chip.  Per tile the same body and arguments as policy p's own
+// launch: the same bits.
+struct PopEntry {
+    PolicyK P;
+    const float* obs;
+    RollK rk;
+    uint32_t eoff;
+    LstmK R;
+    CarryK cy;
+    EnvK env;
+};
+
+template <typename T, int H, bool RNN, int HC>
+__global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_waves_per_eu(RNN ? ML_ROLL_RNN_WAVES : ML_ROLL_MLP_WAVES, 8))) void policy_rollout_pop_kernel(
+    const PopEntry* __restrict__ pop, int npol, int64_t N, uint32_t k0, uint32_t k1,
+    const uint64_t* step_ctr) {
+    const int tpp = (int)((N + 31) / 32);
+    const int ntiles = npol * tpp;
+    for (int g = blockIdx.x; g < ntiles; g += (int)gridDim.x) {
+        const int p = __builtin_amdgcn_readfirstlane(g / tpp);
+        const PopEntry& e = pop[p];
+        const bool first = g == (int)blockIdx.x;
+        if (first) rollout_stage<T, H, RNN, HC>(e.P, e.R);
+        rollout_tile<T, H, RNN, HC, true>(e.P, e.obs, N, e.rk, k0, k1, step_ctr, e.eoff, e.R,
+                                          e.cy, e.env, g - p * tpp, first);
     }
 }
 
@@ -788,6 +840,43 @@ static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, 
     return MLEARN_OK;
 }
 
+// Workgroups of the population launch: one per resident slot of the
+// population kernel, at most one per tile.
+template <typename T, int H, bool RNN, int HC>
+static int64_t rollout_pop_grid(int L, int64_t tiles) {
+    constexpr int NT = pol_threads<H, RNN>();
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(L);
+    auto kern = policy_rollout_pop_kernel<T, H, RNN, HC>;
+    static bool attr_set = false;
+    static int per_cu = 0, cus = 0;
+    if (!attr_set) {  // once per instantiation (kept out of graph capture)
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  128 * 1024);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NT, lds) !=
+                hipSuccess)
+            per_cu = cus = 0;
+        attr_set = true;
+    }
+    const int64_t slots = (int64_t)per_cu * cus;
+    if (slots <= 0) return -1;
+    return tiles < slots ? tiles : slots;
+}
+
+template <typename T, int H, bool RNN, int HC>
+static int launch_policy_rollout_pop(int L, const PopEntry* pop, int npol, int64_t N, uint32_t k0,
+                                     uint32_t k1, const uint64_t* step_ctr, hipStream_t s) {
+    constexpr int NT = pol_threads<H, RNN>();
+    const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(L);
+    const int64_t grid = rollout_pop_grid<T, H, RNN, HC>(L, (int64_t)npol * ((N + 31) / 32));
+    ML_REQUIRE(grid > 0, "policy_rollout_env_pop: no occupancy answer for the population kernel");
+    hipLaunchKernelGGL((policy_rollout_pop_kernel<T, H, RNN, HC>), dim3((unsigned)grid), dim3(NT),
+                       lds, s, pop, npol, N, k0, k1, step_ctr);
+    return check_launch("policy_rollout_env_pop");
+}
+
 static int rollout_step_entry(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                               const mlearn_lstm_carry* carry, const float* obs, int64_t N,
                               void* obs_store, int32_t* actions, float* log_probs, float* values,
@@ -883,16 +972,15 @@ extern "C" int mlearn_policy_rollout_step(const mlearn_mlp_policy* policy, const
                               values, k0, k1, step_ctr, step, env_offset, sample, post, stream);
 }
 
-extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
-                                         const mlearn_lstm_carry* carry, const float* obs,
-                                         int64_t N, const mlearn_rollout_out* out, uint32_t k0,
-                                         uint32_t k1, const uint64_t* step_ctr,
-                                         uint32_t env_offset, const mlearn_dummy_env* denv,
-                                         mlearn_stream_t stream) {
+// Validated launch arguments of one policy's whole rollout
+// (mlearn_policy_rollout_env / one entry of a population).
+static int rollout_env_args(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                            const mlearn_lstm_carry* carry, const float* obs, int64_t N,
+                            const mlearn_rollout_out* out, uint32_t env_offset,
+                            const mlearn_dummy_env* denv, PopEntry* e) {
     int rc = lstm ? validate_lstm(policy, lstm) : validate_policy(policy);
     if (rc) return rc;
     ML_REQUIRE(N >= 0, "policy_rollout_env: N < 0");
-    if (N == 0) return MLEARN_OK;
     ML_REQUIRE(obs && out && denv, "policy_rollout_env: null obs / out / env");
     ML_REQUIRE(out->T >= 1 && out->bptt_len >= 1 && out->T % out->bptt_len == 0 && out->ld >= N,
                "policy_rollout_env: bad T / bptt / ld");
@@ -907,20 +995,39 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
     ML_REQUIRE(!policy->obs_stats || policy->obs_stats_tiles >= (N + 31) / 32,
                "policy_rollout_env: obs_stats_tiles %lld < ceil(N / 32)",
                (long long)policy->obs_stats_tiles);
-    LstmK R{};
-    CarryK cy{};
+    *e = PopEntry{};
     if (lstm) {
         ML_REQUIRE(carry && carry->h && carry->c && out->start_h && out->start_c,
                    "lstm rollout: null carry / start states");
-        R = make_lstm_k(*lstm);
-        cy = CarryK{carry->h, carry->c, nullptr, nullptr, 1, nullptr};
+        e->R = make_lstm_k(*lstm);
+        e->cy = CarryK{carry->h, carry->c, nullptr, nullptr, 1, nullptr};
     }
-    RollK rk{out->obs, out->actions, out->log_probs, out->values, out->rewards, out->dones,
-             out->env_returns_trace, out->bootstrap, out->env_returns, out->start_h, out->start_c,
-             out->T, out->bptt_len, out->ld, out->gamma, out->max_workgroups};
-    EnvK ek{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
-            denv->env_offset};
-    PolicyK P = make_policy_k(*policy);
+    e->rk = RollK{out->obs, out->actions, out->log_probs, out->values, out->rewards, out->dones,
+                  out->env_returns_trace, out->bootstrap, out->env_returns, out->start_h,
+                  out->start_c, out->T, out->bptt_len, out->ld, out->gamma, out->max_workgroups};
+    e->env = EnvK{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
+                  denv->env_offset};
+    e->P = make_policy_k(*policy);
+    e->obs = obs;
+    e->eoff = env_offset;
+    return MLEARN_OK;
+}
+
+extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                         const mlearn_lstm_carry* carry, const float* obs,
+                                         int64_t N, const mlearn_rollout_out* out, uint32_t k0,
+                                         uint32_t k1, const uint64_t* step_ctr,
+                                         uint32_t env_offset, const mlearn_dummy_env* denv,
+                                         mlearn_stream_t stream) {
+    PopEntry e;
+    const int rc = rollout_env_args(policy, lstm, carry, obs, N, out, env_offset, denv, &e);
+    if (rc) return rc;
+    if (N == 0) return MLEARN_OK;
+    const PolicyK& P = e.P;
+    const LstmK& R = e.R;
+    const CarryK& cy = e.cy;
+    const RollK& rk = e.rk;
+    const EnvK& ek = e.env;
     hipStream_t s = S(stream);
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \
     (lstm ? launch_policy_rollout<T, HH, true, HC>(P, obs, N, rk, k0, k1, step_ctr, env_offset, R, \
@@ -943,6 +1050,79 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
 #undef ML_DISPATCH
 #undef ML_LAUNCH
 #undef ML_LAUNCH_HC
+}
+
+
+extern "C" int64_t mlearn_policy_pop_bytes(int32_t num_policies) {
+    return num_policies > 0 ? (int64_t)num_policies * (int64_t)sizeof(PopEntry) : 0;
+}
+
+extern "C" int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies,
+                                         const mlearn_lstm* lstms,
+                                         const mlearn_lstm_carry* carries,
+                                         const float* const* obs, int64_t N,
+                                         const mlearn_rollout_out* outs,
+                                         const uint32_t* env_offsets,
+                                         const mlearn_dummy_env* envs, int32_t num_policies,
+                                         void* pop) {
+    ML_REQUIRE(num_policies >= 1 && policies && obs && outs && env_offsets && envs && pop,
+               "policy_pop_prepare: null argument or no policies");
+    ML_REQUIRE(N >= 1, "policy_pop_prepare: N < 1");
+    std::vector<PopEntry> h((size_t)num_policies);
+    for (int p = 0; p < num_policies; ++p) {
+        const mlearn_mlp_policy& a = policies[p];
+        const mlearn_mlp_policy& b = policies[0];
+        ML_REQUIRE(a.dtype == b.dtype && a.hidden == b.hidden && a.num_layers == b.num_layers &&
+                       a.obs_dim == b.obs_dim && head_cols(a) == head_cols(b),
+                   "policy_pop_prepare: policy %d's shape differs from policy 0's", p);
+        ML_REQUIRE(!lstms == !carries, "policy_pop_prepare: lstms and carries go together");
+        const int rc = rollout_env_args(&a, lstms ? &lstms[p] : nullptr,
+                                        carries ? &carries[p] : nullptr, obs[p], N, &outs[p],
+                                        env_offsets[p], &envs[p], &h[(size_t)p]);
+        if (rc) return rc;
+        ML_REQUIRE(outs[p].max_workgroups == 0,
+                   "policy_pop_prepare: the population launch has its own grid (max_workgroups 0)");
+    }
+    const hipError_t err = hipMemcpy(pop, h.data(), h.size() * sizeof(PopEntry),
+                                     hipMemcpyHostToDevice);
+    if (err != hipSuccess) {
+        set_error("policy_pop_prepare: hipMemcpy: %s", hipGetErrorString(err));
+        return MLEARN_EHIP;
+    }
+    return MLEARN_OK;
+}
+
+extern "C" int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0,
+                                             const mlearn_lstm* lstm0, const void* pop,
+                                             int32_t num_policies, int64_t N, uint32_t k0,
+                                             uint32_t k1, const uint64_t* step_ctr,
+                                             mlearn_stream_t stream) {
+    int rc = lstm0 ? validate_lstm(policy0, lstm0) : validate_policy(policy0);
+    if (rc) return rc;
+    ML_REQUIRE(pop && num_policies >= 1 && N >= 1 && step_ctr,
+               "policy_rollout_env_pop: null pop / step counter, or no work");
+    const int L = policy0->num_layers, HC = head_cols(*policy0);
+    const PopEntry* e = (const PopEntry*)pop;
+    hipStream_t s = S(stream);
+#define ML_POP_HC(T, HH, HCC)                                                                   \
+    (lstm0 ? launch_policy_rollout_pop<T, HH, true, HCC>(L, e, num_policies, N, k0, k1, step_ctr, s) \
+           : launch_policy_rollout_pop<T, HH, false, HCC>(L, e, num_policies, N, k0, k1, step_ctr, s))
+#define ML_POP(T, HH) \
+    (HC == MLEARN_HEAD_COLS ? ML_POP_HC(T, HH, MLEARN_HEAD_COLS) : ML_POP_HC(T, HH, MLEARN_HEAD_COLS_MAX))
+#define ML_DISPATCH(T)                   \
+    switch (policy0->hidden) {           \
+        case 64: return ML_POP(T, 64);   \
+        case 128: return ML_POP(T, 128); \
+        default: return ML_POP(T, 256);  \
+    }
+    if (policy0->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
+#undef ML_POP
+#undef ML_POP_HC
 }
 
 extern "C" int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* policy,

@@ -232,10 +232,15 @@ class RolloutManager:  # rollouts.py:373-826
     rollout_step_env call per step from the host.  ``rollout_workgroups`` is
     that launch's mlearn_rollout_out.max_workgroups: 0 one workgroup per
     resident slot, > 0 at most that many (env tiles in series), < 0 the
-    entry's own per-step launches."""
+    entry's own per-step launches.  ``population_launch`` (default True): a
+    population's whole rollouts go out as ONE launch over every policy's env
+    tiles (mlearn_policy_rollout_env_pop), so P launches of B / 32 workgroups
+    each become one that fills the chip; False issues one launch per policy.
+    Same bits either way."""
 
     whole_rollout = True
     rollout_workgroups = 0
+    population_launch = True
 
     def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_states, env_offset=0):
         self.train_cfg = train_cfg
@@ -417,12 +422,14 @@ class RolloutManager:  # rollouts.py:373-826
         sim = rollout_state.native_step
         obs0 = self.prep_obs(rollout_state.cur_obs)
         if sim is not None and obs0.data_ptr() == sim.obs.data_ptr() and self.whole_rollout:
-            # the built-in sim: every step + the bootstrap in one launch per policy
-            for p, ps in enumerate(self.policies):
-                c = slice(p * B, (p + 1) * B)
-                ps.rollout_all(obs0[c], self._rollout_out(rollout_state, p, gamma), key, step_ctr,
-                               self.env_offset + p * B, self._env_desc(sim, p),
-                               carry=self._carry(rollout_state, p, 0) if self.R else None)
+            # the built-in sim: every step + the bootstrap in one launch per
+            # policy, or one launch for the whole population
+            if not self._population_rollout(rollout_state, obs0, sim, key, step_ctr, gamma):
+                for p, ps in enumerate(self.policies):
+                    c = slice(p * B, (p + 1) * B)
+                    ps.rollout_all(obs0[c], self._rollout_out(rollout_state, p, gamma), key,
+                                   step_ctr, self.env_offset + p * B, self._env_desc(sim, p),
+                                   carry=self._carry(rollout_state, p, 0) if self.R else None)
             out = sim.native_outputs()
             rollout_state.sim_state = out["state"]
             rollout_state.cur_obs = out["obs"]
@@ -476,6 +483,43 @@ class RolloutManager:  # rollouts.py:373-826
             ps.critic_only(obs[c], s.bootstrap[c], post=posts[p],
                            carry=self._carry(rollout_state, p, self.T) if self.R else None)
         return self._finish(train_state_mgr, rollout_state, metrics, user_hooks)
+
+    def _population_rollout(self, rollout_state, obs0, sim, key, step_ctr, gamma):
+        """mlearn_policy_rollout_env_pop over every policy's env columns; False
+        when the per-policy launches must run instead (one policy, the
+        population launch switched off, a max_workgroups cap, or the launch
+        arguments changed while a graph is being captured)."""
+        if self.P < 2 or not self.population_launch or int(self.rollout_workgroups) != 0:
+            return False
+        B, P = self.B, self.P
+        outs = [self._rollout_out(rollout_state, p, gamma) for p in range(P)]
+        envs = [self._env_desc(sim, p) for p in range(P)]
+        descs = [ps.desc for ps in self.policies]
+        lstms = [ps.lstm_desc for ps in self.policies] if self.R else None
+        carries = [self._carry(rollout_state, p, 0) for p in range(P)] if self.R else None
+        obs = [obs0[p * B:(p + 1) * B].data_ptr() for p in range(P)]
+        offs = [self.env_offset + p * B for p in range(P)]
+        parts = descs + outs + envs + (lstms or []) + (carries or [])
+        sig = b"".join(bytes(x) for x in parts) + repr((obs, offs)).encode()
+        L = nat.lib()
+        if getattr(self, "_pop_sig", None) != sig:
+            if torch.cuda.is_current_stream_capturing():
+                return False  # (the prepare copy cannot run inside a capture)
+            if getattr(self, "_pop_buf", None) is None:
+                self._pop_buf = torch.empty(int(L.mlearn_policy_pop_bytes(P)), dtype=torch.uint8,
+                                            device=self.policy_state.device)
+            arr = lambda T, xs: (T * P)(*xs)  # noqa: E731
+            nat.check(L.mlearn_policy_pop_prepare(
+                arr(nat.MlpPolicy, descs), arr(nat.Lstm, lstms) if lstms else None,
+                arr(nat.LstmCarry, carries) if carries else None, (nat.c_void_p * P)(*obs), B,
+                arr(nat.RolloutOut, outs), (nat.c_uint32 * P)(*offs), arr(nat.DummyEnv, envs), P,
+                nat.ptr(self._pop_buf)), "policy_pop_prepare")
+            self._pop_sig = sig
+        nat.check(L.mlearn_policy_rollout_env_pop(
+            self.policy_state.desc, self.policy_state.lstm_desc if self.R else None,
+            nat.ptr(self._pop_buf), P, B, key[0], key[1], nat.ptr(step_ctr),
+            nat.stream_handle()), "policy_rollout_env_pop")
+        return True
 
     def _rollout_out(self, rollout_state, p, gamma):
         """nat.RolloutOut of policy p's store columns (cached)."""

@@ -48,12 +48,15 @@ def _manager(gpu, fused, dtype, N, H, mb, P=1, lstm=False, use_graph=False):
 @pytest.mark.parametrize("dtype,N,H,mb,P,lstm,graph", [
     (torch.float32, 80, 64, 16, 1, False, False),    # partial last workgroup (80 = 2.5 x 32)
     (torch.bfloat16, 1024, 256, 256, 1, False, True),
-    (torch.float32, 128, 64, 16, 2, False, True),     # population: one launch per policy
+    (torch.float32, 128, 64, 16, 2, False, True),     # population: one launch for both policies
+    (torch.bfloat16, 384, 256, 32, 3, False, True),   # 3 policies x 4 tiles in one launch
+    (torch.float32, 128, 64, 32, 2, True, True),      # population of LSTM policies
     (torch.bfloat16, 128, 256, 32, 1, True, False),   # LSTM H = 256: carry, start states, clears
     (torch.float32, 64, 64, 32, 1, True, False)])     # LSTM carry + done clears
 def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, graph):
-    """one_launch: the whole rollout + bootstrap in one launch per policy
-    (mlearn_policy_rollout_env, one workgroup per env tile here);
+    """one_launch: the whole rollout + bootstrap in one launch
+    (mlearn_policy_rollout_env, one workgroup per env tile here; a
+    population: mlearn_policy_rollout_env_pop over every policy's tiles);
     multi_tile: the same launch capped at 2 workgroups (1 for a 2-tile
     policy; mlearn_rollout_out.max_workgroups), so every workgroup runs several
     env tiles in series with the parameters it staged in LDS once (the
@@ -78,6 +81,10 @@ def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, gr
         assert grid == -1
     elif mode == "one_launch":
         assert grid == tiles
+        if P > 1:  # the population launch ran (its arguments were prepared)
+            a.update_iter()
+            assert getattr(rm, "_pop_sig", None) is not None
+            b.update_iter()
     assert RolloutManager.rollout_workgroups == 0  # instance setting only
     for _ in range(2):
         a.update_iter()
@@ -96,7 +103,8 @@ def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, gr
     for x, y in zip(pa, pb):
         assert torch.equal(x.params, y.params)
     # the fused run issued no sim launch: its env buffers moved anyway
-    assert int(env_a.state[:, 1].min().item()) == 64
+    iters = 3 if (mode == "one_launch" and P > 1) else 2
+    assert int(env_a.state[:, 1].min().item()) == 32 * iters
 
 
 def test_fused_env_rejects_foreign_obs(gpu):
