@@ -125,6 +125,12 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 #ifndef ML_WG_CPW
 #define ML_WG_CPW 32  // > 0: split every weight into splits of this many chunks (balanced per-WG work)
 #endif
+#ifndef ML_WG_SMALL_CHUNKS
+#define ML_WG_SMALL_CHUNKS 512  // slices of at most this many chunks take at most ML_WG_SMALL_SPLITS splits
+#endif
+#ifndef ML_WG_SMALL_SPLITS
+#define ML_WG_SMALL_SPLITS 32
+#endif
 #ifndef ML_WG_TARGET_LSTM
 #define ML_WG_TARGET_LSTM 512  // the LSTM gate weights' (Wi, Wh) workgroup target (config L: 10.94 / 10.60 / 10.47 ms at 128 / 256 / 512)
 #endif
@@ -142,6 +148,13 @@ static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int
         if (b > 8) b = (b + 7) / 8 * 8;  // multiples of 8 keep the XCD-aware tile mapping
         if (b > s) s = b < 2 * s ? b : 2 * s;
     }
+    // small minibatch slices (the data-parallel ranks' 8 192 / 16 384 rows
+    // = 256 / 512 chunks at W = 8 / 4): at most ML_WG_SMALL_SPLITS splits
+    // per weight instead of 64 for W0 and the head, so the f32 slabs
+    // (splits x I x J, written here and read by reduce_grads) do not
+    // outweigh the operands (emulated rank shares 3.70 -> 3.66 ms at W = 8,
+    // 4.35 -> 4.23 ms at W = 4; profiles/r04_wgrad_small_slices_ab.txt)
+    if (chunks <= ML_WG_SMALL_CHUNKS && s > ML_WG_SMALL_SPLITS) s = ML_WG_SMALL_SPLITS;
     if (s < 1) s = 1;
     if (s > chunks) s = chunks;
     int64_t per = (chunks + s - 1) / s;
