@@ -192,6 +192,13 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
         "traffic_source": (f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc_name})"
                            if traffic is not None else None),
         "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
+        # achieved / frac use avg_launch_us: HIP events on the stream the
+        # kernel is launched on, around `iters` back-to-back launches of the
+        # step-only entry (metrics off); the committed rocprofv3 stats of the
+        # same kernel (profiles/) average every launch of the
+        # update, metrics-on minibatches included
+        "timing_source": f"hip_events: {iters} launches of mlearn_ppo_minibatch_fwd_bwd on "
+                         f"its own stream",
         "units_per_launch": M, "flop_per_unit": fwd + bwd,
         "algorithmic_bytes_per_launch": 184 * M,
         # the measured traffic is dominated by the weight-gradient operands the
@@ -308,6 +315,15 @@ def cpu_baseline(iters=2):
     env = onat.Env(n_env, OBS, 1, 2)
     env.reset()
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01}
+    # every host core this process may run on (the whole host,
+    # not the OMP_NUM_THREADS default), set on the BLAS pools the NumPy
+    # restatement runs its products in; the thread count reported is what the
+    # pools report back while the timed region runs
+    from threadpoolctl import threadpool_info, threadpool_limits
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        (os.cpu_count() or 1)
+    limiter = threadpool_limits(limits=cores)
+    used = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
     norms = np.ones(LAYERS)
     pf = p.astype(np.float64)
     opt = (np.zeros(lay["total"]), np.zeros(lay["total"]), 0)
@@ -325,9 +341,12 @@ def cpu_baseline(iters=2):
                                     epoch_base=it * EPOCHS, mode="f32", lr=3e-4,
                                     max_grad_norm=0.5, ad=np.float32)
     sec = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": threads,
+    limiter.restore_original_limits()
+    return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": used,
             "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cores_available": cores,
+            "threads_note": "cores = BLAS pool threads during the timed region "
+                            "(threadpoolctl), set to every CPU in this process's affinity mask",
             "sample": f"{iters} full PPO iterations on a {n_env}-env shard ({n_env} envs x "
                       f"T={T}, 2 epochs x {n_env // mb} minibatches of {mb} seqs; same work per "
                       f"env-step as the 65536-env workload), NumPy fp32 oracle restatement, "

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 17
+#define MLEARN_ABI_VERSION 18
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -355,6 +355,18 @@ typedef struct mlearn_ppo_hparams {
                                               grad_sumsq_part instead of re-reading grads
                                               (only valid when grads are not all-reduced
                                               in between) */
+    int32_t step_kernel;                   /* forward / loss / backward kernel of the MLP
+                                              step: 0 = the library's choice (the row-split
+                                              kernel where it applies: bf16, hidden 256,
+                                              2 layers, scalar critic, head width 32,
+                                              obs_dim 64, rows a
+                                              multiple of 256 and >= 65536; else the
+                                              feature-split kernel), 1 = the feature-split
+                                              kernel, 2 = the row-split kernel (EINVAL
+                                              where it does not apply).  Same inputs and
+                                              outputs; results within the compute dtype's
+                                              rounding of each other (summation orders) */
+    int32_t pad;
 } mlearn_ppo_hparams;
 
 /* Number of partials mlearn_ppo_hparams.grad_sumsq_out receives: one per 64
@@ -435,8 +447,13 @@ int mlearn_optim_step(const mlearn_mlp_policy* policy, const mlearn_optim_state*
  * together so |scale|^2 + |bias|^2 = features).  groups: DEVICE array. */
 typedef struct mlearn_flat_group {
     int64_t offset, count;    /* kernel / LayerNorm scale: [offset, offset + count) */
-    int64_t offset2, count2;  /* LayerNorm bias (count2 = 0 for a kernel) */
-    int32_t kind;             /* 1: kernel, 2: LayerNorm */
+    int64_t offset2, count2;  /* LayerNorm bias (count2 = 0 for a kernel); kind 3: offset2 =
+                                 row stride, count2 = rows */
+    int32_t kind;             /* 1: kernel, 2: LayerNorm, 3: kernel held as a column block
+                                 of a row-major matrix -- elements offset + r * offset2 + c,
+                                 r < count2, c < count (one gate's kernel of an LSTM layer's
+                                 concatenated [in][4H] weights: flax OptimizedLSTMCell keeps
+                                 each gate's Dense kernel as its own leaf, rnn.py:30-36) */
     int32_t features;         /* LayerNorm: F */
     float init_norm;          /* kernel: its Frobenius norm at initialisation */
     int32_t pad;
@@ -652,21 +669,32 @@ int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm
  * those of its own mlearn_policy_rollout_env call, N envs each, every policy
  * of the same shape, max_workgroups 0 -- are written once into a device
  * buffer of mlearn_policy_pop_bytes(P) bytes by mlearn_policy_pop_prepare
- * (synchronous copy; call it outside stream capture, again whenever one of
+ * (a copy on `stream`, ordered after the work already queued there -- e.g. a
+ * previous population launch still reading the buffer -- and complete when
+ * the call returns; call it outside stream capture, again whenever one of
  * the pointers changes); mlearn_policy_rollout_env_pop then launches the
- * P * ceil(N / 32) env tiles over one workgroup per resident slot (capture-
- * safe).  Same bits as the P separate launches.  lstms / carries: arrays of
- * P, or both null for feed-forward policies. */
+ * P * ceil(N / 32) env tiles (global tile g = tile g % ceil(N / 32) of
+ * policy g / ceil(N / 32)) dealt round-robin over one workgroup per resident
+ * slot, or over at most max_workgroups (> 0) workgroups; a workgroup whose
+ * next tile belongs to another policy restages that policy's parameters
+ * (capture-safe).  Same bits as the P separate launches.  lstms / carries:
+ * arrays of P, or both null for feed-forward policies. */
 int64_t mlearn_policy_pop_bytes(int32_t num_policies);
 int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies, const mlearn_lstm* lstms,
                               const mlearn_lstm_carry* carries, const float* const* obs,
                               int64_t N, const mlearn_rollout_out* outs,
                               const uint32_t* env_offsets, const mlearn_dummy_env* envs,
-                              int32_t num_policies, void* pop);
+                              int32_t num_policies, void* pop, mlearn_stream_t stream);
 int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0, const mlearn_lstm* lstm0,
                                   const void* pop, int32_t num_policies, int64_t N,
                                   uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
-                                  mlearn_stream_t stream);
+                                  int32_t max_workgroups, mlearn_stream_t stream);
+/* Workgroups mlearn_policy_rollout_env_pop launches for num_policies x N envs
+ * under max_workgroups (>= 0); -1 on a bad argument or a failed occupancy
+ * query.  P * ceil(N / 32) > the result means tiles run in series. */
+int64_t mlearn_policy_rollout_pop_workgroups(const mlearn_mlp_policy* policy,
+                                             const mlearn_lstm* lstm, int64_t N,
+                                             int32_t num_policies, int32_t max_workgroups);
 /* Workgroups mlearn_policy_rollout_env launches for N envs under
  * max_workgroups (0 = the launch it would issue per-step: -1 means per-step
  * launches are used, i.e. the occupancy query failed or max_workgroups < 0);

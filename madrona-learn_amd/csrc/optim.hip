@@ -411,14 +411,21 @@ __global__ __launch_bounds__(256) void flat_project_kernel(float* __restrict__ p
     }
     if ((int)blockIdx.x >= ngroups) return;
     const mlearn_flat_group gr = groups[blockIdx.x];
-    const bool on = gr.kind == 1 ? norm_params != 0 : norm_ln != 0;
+    const bool on = gr.kind != 2 ? norm_params != 0 : norm_ln != 0;
     if (!on) return;
+    // kind 3: a column block (count columns of count2 rows, row stride offset2)
+    const bool blk = gr.kind == 3;
+    const int64_t nel = blk ? gr.count * gr.count2 : gr.count;
+    auto at = [&](int64_t i) -> float& {
+        return blk ? params[gr.offset + (i / gr.count) * gr.offset2 + i % gr.count]
+                   : params[gr.offset + i];
+    };
     double t = 0.0;
-    for (int64_t i = threadIdx.x; i < gr.count; i += 256) {
-        const double x = params[gr.offset + i];
+    for (int64_t i = threadIdx.x; i < nel; i += 256) {
+        const double x = at(i);
         t += x * x;
     }
-    for (int64_t i = threadIdx.x; i < gr.count2; i += 256) {
+    for (int64_t i = threadIdx.x; !blk && i < gr.count2; i += 256) {
         const double x = params[gr.offset2 + i];
         t += x * x;
     }
@@ -427,10 +434,10 @@ __global__ __launch_bounds__(256) void flat_project_kernel(float* __restrict__ p
     __syncthreads();
     if (threadIdx.x == 0) sq = (float)(((red[0] + red[1]) + red[2]) + red[3]);
     __syncthreads();
-    if (gr.kind == 1) {  // ppo.py:307: init_norm * W / |W|
-        for (int64_t i = threadIdx.x; i < gr.count; i += 256) {
-            float* q = params + gr.offset + i;
-            *q = (gr.init_norm * *q) / sqrtf(sq);
+    if (gr.kind == 1 || blk) {  // ppo.py:307: init_norm * W / |W|
+        for (int64_t i = threadIdx.x; i < nel; i += 256) {
+            float& q = at(i);
+            q = (gr.init_norm * q) / sqrtf(sq);
         }
     } else {  // ppo.py:324-325: sqrt(F / (b.b + s.s)) * (s, b)
         const float f = sqrtf((float)gr.features / sq);

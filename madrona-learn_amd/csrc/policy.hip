@@ -843,7 +843,7 @@ static int launch_policy_rollout(const PolicyK& P, const float* obs, int64_t N, 
 // Workgroups of the population launch: one per resident slot of the
 // population kernel, at most one per tile.
 template <typename T, int H, bool RNN, int HC>
-static int64_t rollout_pop_grid(int L, int64_t tiles) {
+static int64_t rollout_pop_grid(int L, int64_t tiles, int max_wg) {
     constexpr int NT = pol_threads<H, RNN>();
     const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(L);
     auto kern = policy_rollout_pop_kernel<T, H, RNN, HC>;
@@ -860,17 +860,22 @@ static int64_t rollout_pop_grid(int L, int64_t tiles) {
             per_cu = cus = 0;
         attr_set = true;
     }
-    const int64_t slots = (int64_t)per_cu * cus;
+    int64_t slots = (int64_t)per_cu * cus;
     if (slots <= 0) return -1;
+    // max_wg > 0 caps the grid (tiles of several policies in series per
+    // workgroup, each move to another policy's tile restaging its parameters)
+    if (max_wg > 0 && max_wg < slots) slots = max_wg;
     return tiles < slots ? tiles : slots;
 }
 
 template <typename T, int H, bool RNN, int HC>
 static int launch_policy_rollout_pop(int L, const PopEntry* pop, int npol, int64_t N, uint32_t k0,
-                                     uint32_t k1, const uint64_t* step_ctr, hipStream_t s) {
+                                     uint32_t k1, const uint64_t* step_ctr, int max_wg,
+                                     hipStream_t s) {
     constexpr int NT = pol_threads<H, RNN>();
     const size_t lds = policy_step_lds<T, H, RNN, HC, pol_maxw<RNN>()>(L);
-    const int64_t grid = rollout_pop_grid<T, H, RNN, HC>(L, (int64_t)npol * ((N + 31) / 32));
+    const int64_t grid =
+        rollout_pop_grid<T, H, RNN, HC>(L, (int64_t)npol * ((N + 31) / 32), max_wg);
     ML_REQUIRE(grid > 0, "policy_rollout_env_pop: no occupancy answer for the population kernel");
     hipLaunchKernelGGL((policy_rollout_pop_kernel<T, H, RNN, HC>), dim3((unsigned)grid), dim3(NT),
                        lds, s, pop, npol, N, k0, k1, step_ctr);
@@ -1064,7 +1069,7 @@ extern "C" int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies,
                                          const mlearn_rollout_out* outs,
                                          const uint32_t* env_offsets,
                                          const mlearn_dummy_env* envs, int32_t num_policies,
-                                         void* pop) {
+                                         void* pop, mlearn_stream_t stream) {
     ML_REQUIRE(num_policies >= 1 && policies && obs && outs && env_offsets && envs && pop,
                "policy_pop_prepare: null argument or no policies");
     ML_REQUIRE(N >= 1, "policy_pop_prepare: N < 1");
@@ -1083,8 +1088,12 @@ extern "C" int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies,
         ML_REQUIRE(outs[p].max_workgroups == 0,
                    "policy_pop_prepare: the population launch has its own grid (max_workgroups 0)");
     }
-    const hipError_t err = hipMemcpy(pop, h.data(), h.size() * sizeof(PopEntry),
-                                     hipMemcpyHostToDevice);
+    // ordered after the caller's earlier work on its stream (a previous
+    // population launch may still read the buffer), and complete on return
+    // (the host staging vector dies with this call)
+    hipError_t err = hipMemcpyAsync(pop, h.data(), h.size() * sizeof(PopEntry),
+                                    hipMemcpyHostToDevice, S(stream));
+    if (err == hipSuccess) err = hipStreamSynchronize(S(stream));
     if (err != hipSuccess) {
         set_error("policy_pop_prepare: hipMemcpy: %s", hipGetErrorString(err));
         return MLEARN_EHIP;
@@ -1096,17 +1105,20 @@ extern "C" int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0,
                                              const mlearn_lstm* lstm0, const void* pop,
                                              int32_t num_policies, int64_t N, uint32_t k0,
                                              uint32_t k1, const uint64_t* step_ctr,
-                                             mlearn_stream_t stream) {
+                                             int32_t max_workgroups, mlearn_stream_t stream) {
     int rc = lstm0 ? validate_lstm(policy0, lstm0) : validate_policy(policy0);
     if (rc) return rc;
     ML_REQUIRE(pop && num_policies >= 1 && N >= 1 && step_ctr,
                "policy_rollout_env_pop: null pop / step counter, or no work");
+    ML_REQUIRE(max_workgroups >= 0, "policy_rollout_env_pop: max_workgroups < 0");
     const int L = policy0->num_layers, HC = head_cols(*policy0);
     const PopEntry* e = (const PopEntry*)pop;
     hipStream_t s = S(stream);
 #define ML_POP_HC(T, HH, HCC)                                                                   \
-    (lstm0 ? launch_policy_rollout_pop<T, HH, true, HCC>(L, e, num_policies, N, k0, k1, step_ctr, s) \
-           : launch_policy_rollout_pop<T, HH, false, HCC>(L, e, num_policies, N, k0, k1, step_ctr, s))
+    (lstm0 ? launch_policy_rollout_pop<T, HH, true, HCC>(L, e, num_policies, N, k0, k1, step_ctr, \
+                                                       max_workgroups, s)                     \
+           : launch_policy_rollout_pop<T, HH, false, HCC>(L, e, num_policies, N, k0, k1, step_ctr, \
+                                                        max_workgroups, s))
 #define ML_POP(T, HH) \
     (HC == MLEARN_HEAD_COLS ? ML_POP_HC(T, HH, MLEARN_HEAD_COLS) : ML_POP_HC(T, HH, MLEARN_HEAD_COLS_MAX))
 #define ML_DISPATCH(T)                   \
@@ -1123,6 +1135,36 @@ extern "C" int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0,
 #undef ML_DISPATCH
 #undef ML_POP
 #undef ML_POP_HC
+}
+
+extern "C" int64_t mlearn_policy_rollout_pop_workgroups(const mlearn_mlp_policy* policy,
+                                                        const mlearn_lstm* lstm, int64_t N,
+                                                        int32_t num_policies,
+                                                        int32_t max_workgroups) {
+    if ((lstm ? validate_lstm(policy, lstm) : validate_policy(policy)) || N < 1 ||
+        num_policies < 1 || max_workgroups < 0)
+        return -1;
+    const int HC = head_cols(*policy), L = policy->num_layers;
+    const int64_t tiles = (int64_t)num_policies * ((N + 31) / 32);
+#define ML_GRID_HC(T, HH, HCC) \
+    (lstm ? rollout_pop_grid<T, HH, true, HCC>(L, tiles, max_workgroups) \
+          : rollout_pop_grid<T, HH, false, HCC>(L, tiles, max_workgroups))
+#define ML_GRID(T, HH) \
+    (HC == MLEARN_HEAD_COLS ? ML_GRID_HC(T, HH, MLEARN_HEAD_COLS) : ML_GRID_HC(T, HH, MLEARN_HEAD_COLS_MAX))
+#define ML_DISPATCH(T)                    \
+    switch (policy->hidden) {             \
+        case 64: return ML_GRID(T, 64);   \
+        case 128: return ML_GRID(T, 128); \
+        default: return ML_GRID(T, 256);  \
+    }
+    if (policy->dtype == MLEARN_DTYPE_BF16) {
+        ML_DISPATCH(bf16)
+    } else {
+        ML_DISPATCH(float)
+    }
+#undef ML_DISPATCH
+#undef ML_GRID
+#undef ML_GRID_HC
 }
 
 extern "C" int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* policy,

@@ -1,0 +1,678 @@
+// Row-split minibatch step (ppo.py:109-364 up to the weight-gradient
+// operands) for the headline policy shape: bf16, H = 256, two trunk layers,
+// scalar critic, head width 32.  Included by ppo.hip after ppo_step_kernel;
+// same inputs, outputs and workspace layout (X_0, A_l, dZ_l, d head rows;
+// per-32-row column and loss partials), so wgrad_kernel / reduce_grads_kernel
+// consume either kernel's output unchanged.
+//
+// Why a second kernel.  ppo_step_kernel gives each 32-row tile a workgroup
+// whose 8 waves split the 256 features: every layer ends in a LayerNorm whose
+// row statistics cross the waves (a barrier) and an LDS exchange of the next
+// product's operand (another barrier), and every tile streams its 16 KB-per-
+// wave slice of W1 from L2 twice.  The tile's chain of ~12 latency-bound
+// phases sets the kernel's time.  Here:
+//   * one workgroup of 8 waves per CU stages W1 (128 KB) and the head weights
+//     (16 KB) in LDS once, plus the LayerNorm / head-bias parameters;
+//   * a wave owns whole rows -- two 16-row tiles, v_mfma_f32_16x16x32_bf16 --
+//     so LayerNorm statistics are lane-local sums plus two cross-lane adds,
+//     every product's activation operand comes straight from the previous
+//     accumulators, and no barrier follows the prologue;
+//   * the forward product reads W1 by row (two ds_read_b64 per fragment), the
+//     backward product reads the same image transposed (ds_read_b64_tr_b16);
+//   * the layer-0 weights (K = obs_dim) stream from L2 per tile.
+// Orientation as rowtile.h: Z^T = W^T X^T, features on the MFMA M axis, the
+// 16 rows of a tile on N (lane & 15); lane l holds features 16b + 4(l>>4) + i
+// (i < 4) of accumulator block b.  k-step s of a product over hidden
+// features takes blocks 2s, 2s+1, so its k-slot 8g + j is feature
+// 32s + 16(j>>2) + 4g + (j&3) (g = lane >> 4) -- the A operand is read in
+// that order.
+
+#pragma once
+
+// (included inside namespace ml by ppo.hip)
+
+constexpr int kR16Waves = 8;     // waves per workgroup
+constexpr int kR16Tiles = 2;     // 16-row tiles per wave: 32 rows = one partials row
+constexpr int kR16H = 256;
+constexpr int kR16NB = kR16H / 16;   // 16-feature accumulator blocks
+constexpr int kR16KS = kR16H / 32;   // k-steps over the hidden features
+constexpr int kR16HC = MLEARN_HEAD_COLS;
+constexpr int kR16D = 64;            // observation width (the first layer's K)
+constexpr int kR16LGS = 40;          // logits scratch row stride (bf16; 80-B rows)
+constexpr int kR16Ring = 6;          // LDS A fragments in flight per product
+// LDS: W1 image [256 rows = out][512 B], head image [32 rows = col][512 B],
+// LayerNorm scale/bias [2][2][256] f32, head bias [32] f32, per-wave logits
+// scratch [8][16][kR16LGS] bf16, the action groups' logit offsets, entropy
+// coefficients and objective weights (read per lane by the loss tasks: from
+// the kernel arguments a lane-dependent index would copy the arrays into
+// registers)
+constexpr size_t kR16OffW1 = 0;
+constexpr size_t kR16OffWh = kR16OffW1 + (size_t)kR16H * 512;
+constexpr size_t kR16OffGb = kR16OffWh + (size_t)kR16HC * 512;
+constexpr size_t kR16OffHb = kR16OffGb + (size_t)2 * 2 * kR16H * 4;
+constexpr size_t kR16OffLg = kR16OffHb + (size_t)kR16HC * 4;
+constexpr size_t kR16OffTab = kR16OffLg + (size_t)kR16Waves * 16 * kR16LGS * 2;
+constexpr int kR16TabN = 3 * (MLEARN_MAX_GROUPS + 1);  // group offsets, entropy coefs, obj weights
+constexpr size_t kR16Lds = kR16OffTab + (size_t)kR16TabN * 4;
+static_assert(kR16Lds <= 160 * 1024, "row-split step LDS budget");
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef short short4r __attribute__((ext_vector_type(4)));
+typedef __attribute__((ext_vector_type(4))) uint32_t u4r;
+typedef __attribute__((ext_vector_type(2))) uint32_t u2r;
+
+// 8-byte unit u (4 consecutive bf16 of a 512-B image row) of row n, XOR-
+// swizzled so that the row reads (16 rows x units {8s + g, 8s + 4 + g}) and
+// the transposed reads (8 rows x 4 units) of a 32-lane half hit 32 distinct
+// bank pairs.
+__device__ inline uint32_t r16_off(int n, int u) {
+    const int sw = ((n & 7) << 2) | (((n >> 3) & 1) << 1);
+    return (uint32_t)(n * 512 + ((u ^ sw) << 3));
+}
+
+// An opaque copy of a value (its uses cannot be computed before this point:
+// the row-derived store addresses would otherwise be formed at the tile's
+// start and held live across it).
+template <typename V> __device__ inline V r16_late(V v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ inline f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// A fragment of a forward product from an LDS image: rows n = output feature,
+// k-slots 8g + j = input features 32s + 16(j>>2) + 4g + (j&3): units 8s + g
+// and 8s + 4 + g of row n.
+__device__ inline bf16x8 r16_row_frag(const char* img, int n, int s, int g) {
+    const u2r lo = *(const u2r*)(img + r16_off(n, 8 * s + g));
+    const u2r hi = *(const u2r*)(img + r16_off(n, 8 * s + 4 + g));
+    const u4r v = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// A fragment of a backward product from the same image read transposed: M =
+// image column (input feature 16b + (lane & 15)), k-slots 8g + j = image rows
+// r0 + 4g + j (j < 4) and r0 + 16 + 4g + (j - 4) with r0 = 32s (hidden
+// operands), or rows 8g + j with `step8` (the head's 32 columns, one k-step).
+__device__ inline bf16x8 r16_tr_frag(const char* img, int rlo, int rhi, int b, int lane) {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    typedef __attribute__((address_space(3))) short4r* lp;
+    const short4r lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lp)(img + r16_off(rlo + q, 4 * b + p)));
+    const short4r hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lp)(img + r16_off(rhi + q, 4 * b + p)));
+    typedef short short8r __attribute__((ext_vector_type(8)));
+    const short8r v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ inline uint32_t pk_bf16(float a, float b) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 v = {(bf16)a, (bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ inline f2v up_bf16(uint32_t w) {
+    return f2v{__builtin_bit_cast(float, w << 16), __builtin_bit_cast(float, w & 0xffff0000u)};
+}
+// k-step s B fragment from packed words of blocks 2s, 2s+1 (the acc layout)
+__device__ inline bf16x8 r16_bfrag(const uint32_t (&w)[kR16NB][2], int s) {
+    const u4r v = {w[2 * s][0], w[2 * s][1], w[2 * s + 1][0], w[2 * s + 1][1]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// acc[j] += sum_s A(j, s) B(s) over NBO output blocks and NS k-steps, A
+// fragments from `lda(j, s)` through a ring of RING fragments in flight
+// (sched_barrier fences keep the compiler from hoisting every read of the
+// product ahead of its MFMAs, which would hold them all in registers).
+template <int NBO, int NS, int RING, typename LDA, typename BF>
+__device__ inline void r16_mm(f32x4 (&acc)[NBO], LDA lda, BF bfrag) {
+    constexpr int N = NS * NBO;
+    constexpr int RG = RING < N ? RING : N;
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 ra[RG];
+#pragma unroll
+    for (int i = 0; i < RG; ++i) ra[i] = lda(i % NBO, i / NBO);
+    bf16x8 bfr = bfrag(0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bf16x8 a = ra[i % RG];
+        if (i + RG < N) ra[i % RG] = lda((i + RG) % NBO, (i + RG) / NBO);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[i % NBO] = mma16(a, bfr, acc[i % NBO]);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((i + 1) % NBO == 0 && i + 1 < N) bfr = bfrag((i + 1) / NBO);
+    }
+}
+
+// A forward layer's product Z^T = W^T X^T in two halves of 8 output blocks
+// (32 accumulator registers at a time instead of 64), each half rounded to
+// the compute dtype as it completes (flax Dense output dtype) and packed into
+// zw; returns the LayerNorm statistics of the rows (f32 sums of the rounded
+// values, fast variance, eps 1e-6; models.py:46-56).
+template <int NS, int RING, typename LDA, typename BF>
+__device__ inline void r16_fwd_layer(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2], float& mean_o,
+                                     float& rstd_o) {
+    f2v s2 = {0.f, 0.f}, q2 = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f32x4 acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        r16_mm<8, NS, RING>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                zw[8 * h + j][k] = pk_bf16(acc[j][2 * k], acc[j][2 * k + 1]);
+                const f2v x = up_bf16(zw[8 * h + j][k]);
+                s2 += x;
+                q2 = x * x + q2;
+            }
+    }
+    float sum = s2.x + s2.y, sq = q2.x + q2.y;
+    sum = add_xor32(add_xor16(sum));
+    sq = add_xor32(add_xor16(sq));
+    const float invH = 1.0f / (float)kR16H;
+    const float mean = sum * invH;
+    const float var = fmaxf(sq * invH - mean * mean, 0.f);
+    mean_o = mean;
+    rstd_o = rsqrtf(var + 1e-6f);
+}
+
+// Row-major store of a [16 rows][256] bf16 operand held as packed words (lane
+// (r, g): features 16b + 4g .. 4g+3 of every block b): one v_permlane16_swap
+// per word pair leaves lane g with 8 consecutive features of block 2c + (g&1)
+// (features 8(g>>1) .. +7), one 16-byte store per block pair.  In place.
+__device__ inline void r16_store_rows(bf16* rowp, uint32_t (&w)[kR16NB][2], int g) {
+#pragma unroll
+    for (int c = 0; c < kR16NB / 2; ++c) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const auto v = __builtin_amdgcn_permlane16_swap(w[2 * c][k], w[2 * c + 1][k], false,
+                                                            false);
+            w[2 * c][k] = v[0];
+            w[2 * c + 1][k] = v[1];
+        }
+        const int blk = 2 * c + (g & 1);
+        *(u4r*)(rowp + 16 * blk + 8 * (g >> 1)) =
+            u4r{w[2 * c][0], w[2 * c][1], w[2 * c + 1][0], w[2 * c + 1][1]};
+    }
+}
+
+// Sum of 16 values over the 16 lanes of a DPP row (the 16 rows of a tile):
+// recursive halving (partners lane ^ 1, ^ 2, ^ 8, ^ 4); lane returns the total
+// of value col_sum16_index(lane & 15).
+__device__ inline float r16_rowsum16(float (&v)[16], int lane) {
+    bfly<1, 16>(v, lane);
+    bfly<2, 8>(v, lane);
+    bfly<8, 4>(v, lane);
+    const bool hi = (lane & 4) != 0;
+    const float a = v[0], b = v[1];
+    const float keep = hi ? b : a, send = hi ? a : b;
+    const float r4 = ML_DPP(send, 0x124), r12 = ML_DPP(send, 0x12C);
+    return keep + (hi ? r4 : r12);
+}
+
+// LayerNorm apply + ReLU, rounded to the compute dtype: packed Z -> packed
+// A (the next product's operand).
+__device__ inline void r16_ln_apply(const uint32_t (&zw)[kR16NB][2], float mean, float rstd,
+                                    const float* gm, int g, uint32_t (&aw)[kR16NB][2]) {
+    const f2v m2 = {mean, mean}, r2 = {rstd, rstd};
+#pragma unroll
+    for (int b = 0; b < kR16NB; ++b) {
+        // (one block's scale / bias in flight at a time: without the fence the
+        // scheduler issues all 32 LDS reads first and holds 128 registers)
+        __builtin_amdgcn_sched_barrier(0);
+        // (an opaque feature index per block: the LDS reads of all 16 blocks'
+        // scale / bias are otherwise issued up front, 128 registers)
+        const int f0 = r16_late(16 * b + 4 * g);
+        const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
+        // (words read through opaque copies: the statistics pass's unpacked
+        // values would otherwise be CSE'd into this one and held live, 64
+        // registers across the layer's whole product)
+        const f2v y0 = __builtin_elementwise_fma(up_bf16(r16_late(zw[b][0])) - m2,
+                                                 r2 * f2v{G.x, G.y}, f2v{B.x, B.y});
+        const f2v y1 = __builtin_elementwise_fma(up_bf16(r16_late(zw[b][1])) - m2,
+                                                 r2 * f2v{G.z, G.w}, f2v{B.z, B.w});
+        aw[b][0] = pk_bf16(fmaxf(y0.x, 0.f), fmaxf(y0.y, 0.f));
+        aw[b][1] = pk_bf16(fmaxf(y1.x, 0.f), fmaxf(y1.y, 0.f));
+    }
+}
+
+// LayerNorm + ReLU backward element (models.py:46-56 under jax.value_and_grad,
+// f32 inside the LayerNorm): d loss / d A -> dy (ReLU' from the rounded
+// output: rnd(y) > 0 <=> y > thr; padding rows carry no gradient), x_hat.
+__device__ inline float r16_dy(float z, float mean, float rstd, float gam, float bet, float da,
+                               bool live, float& xh) {
+    const float zc = z - mean;
+    xh = zc * rstd;
+    const float y = __builtin_fmaf(zc, rstd * gam, bet);
+    return ((y > relu_thr<bf16>()) & live) ? da : 0.f;
+}
+
+// Column sums of one block quad's LayerNorm bias (dy) / scale (dy x_hat)
+// gradients over the tile's 16 rows, and the row sums su (u = dy gamma) and
+// sv (u x_hat) over its 16 features per lane; u kept in acc when STORE_U.
+template <bool STORE_U>
+__device__ inline void r16_bwd_quad(f32x4* acc4, const uint32_t (&zw)[kR16NB][2], int qd,
+                                    float mean, float rstd, const float* gm, int g, int lane,
+                                    bool live, float& su, float& sv, float& cbq, float& cgq) {
+    float pb[16], pg[16];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int b = 4 * qd + bb;
+        const int f0 = r16_late(16 * b + 4 * g);
+        const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
+        const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float xh;
+            const float z = up_bf16(r16_late(zw[b][i >> 1]))[i & 1];
+            const float dy = r16_dy(z, mean, rstd, gv[i], bv[i], acc4[bb][i], live, xh);
+            const float u = dy * gv[i];
+            su += u;
+            sv = __builtin_fmaf(u, xh, sv);
+            if (STORE_U) acc4[bb][i] = u;
+            pb[4 * bb + i] = dy;
+            pg[4 * bb + i] = dy * xh;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    cbq += r16_rowsum16(pb, lane);
+    cgq += r16_rowsum16(pg, lane);
+}
+
+// dZ = rstd (u - mean(u) - x_hat mean(u x_hat)) of one block from u
+__device__ inline void r16_dz_block(const f32x4& u, const uint32_t (&zwb)[2], float mean,
+                                    float rstd, float ca, float cbc, uint32_t (&dzb)[2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const f2v zc = up_bf16(r16_late(zwb[k])) - f2v{mean, mean};
+        const f2v d = f2v{rstd, rstd} * f2v{u[2 * k], u[2 * k + 1]} +
+                      (f2v{ca, ca} * zc + f2v{cbc, cbc});
+        dzb[k] = pk_bf16(d.x, d.y);
+    }
+}
+
+// Layer backward with d loss / d A held in full (acc, 64 registers): one pass.
+__device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], const uint32_t (&zw)[kR16NB][2],
+                                  float mean, float rstd, const float* gm, int g, int lane,
+                                  bool live, uint32_t (&dzw)[kR16NB][2], float (&cb)[4],
+                                  float (&cg)[4]) {
+    // opaque copies (of the statistics and of every Z word read): the
+    // forward's unpacked Z values / (z - mean) pairs are otherwise CSE'd into
+    // this pass and held live from the forward LayerNorm
+    mean = r16_late(mean);
+    rstd = r16_late(rstd);
+    float su = 0.f, sv = 0.f;
+#pragma unroll
+    for (int qd = 0; qd < kR16NB / 4; ++qd)
+        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cb[qd],
+                           cg[qd]);
+    su = add_xor32(add_xor16(su));
+    sv = add_xor32(add_xor16(sv));
+    const float invH = 1.0f / (float)kR16H;
+    const float ca = -(rstd * rstd) * (sv * invH), cbc = -rstd * (su * invH);
+#pragma unroll
+    for (int b = 0; b < kR16NB; ++b) r16_dz_block(acc[b], zw[b], mean, rstd, ca, cbc, dzw[b]);
+}
+
+// Layer backward whose d loss / d A comes from a short product (the head
+// backward, K = 32): two passes over two halves of 8 blocks, the half's
+// product run again in the second pass (same MFMAs, same bits) instead of
+// holding all 64 values.
+template <int NS, typename LDA, typename BF>
+__device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, const uint32_t (&zw)[kR16NB][2], float mean,
+                                   float rstd, const float* gm, int g, int lane, bool live,
+                                   uint32_t (&dzw)[kR16NB][2], float (&cb)[4], float (&cg)[4]) {
+    mean = r16_late(mean);
+    rstd = r16_late(rstd);
+    float su = 0.f, sv = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f32x4 acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        r16_mm<8, NS, kR16Ring>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+            r16_bwd_quad<false>(acc + 4 * qh, zw, 2 * h + qh, mean, rstd, gm, g, lane, live, su,
+                                sv, cb[2 * h + qh], cg[2 * h + qh]);
+    }
+    su = add_xor32(add_xor16(su));
+    sv = add_xor32(add_xor16(sv));
+    const float invH = 1.0f / (float)kR16H;
+    const float ca = -(rstd * rstd) * (sv * invH), cbc = -rstd * (su * invH);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f32x4 acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        r16_mm<8, NS, kR16Ring>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int b = 8 * h + j;
+            const int f0 = r16_late(16 * b + 4 * g);
+            const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
+            const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
+            f32x4 u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float xh;
+                const float z = up_bf16(r16_late(zw[b][i >> 1]))[i & 1];
+                u[i] = r16_dy(z, mean, rstd, gv[i], bv[i], acc[j][i], live, xh) * gv[i];
+            }
+            r16_dz_block(u, zw[b], mean, rstd, ca, cbc, dzw[b]);
+        }
+    }
+}
+
+template <bool METRICS>
+__global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void ppo_rows16_kernel(
+    PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
+    const float* __restrict__ adv_st, HpK hp, WsK ws) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* w1img = smem + kR16OffW1;
+    char* whimg = smem + kR16OffWh;
+    float* gb = (float*)(smem + kR16OffGb);
+    float* hb = (float*)(smem + kR16OffHb);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
+    const int K = P.K;
+    constexpr int D = kR16D, DS = D / 32;  // the first layer's k-steps
+
+    // ---- prologue: W1 and head images (P.wt[1], P.head_t: fragment order,
+    // permuted k, K = 256) re-laid as [out row][512 B] with swizzled 8-byte
+    // units; LayerNorm scale / bias, head bias, the loss tasks' group tables
+    {
+        const u4r* src1 = (const u4r*)P.wt[1];
+        const u4r* srch = (const u4r*)P.head_t;
+        constexpr int N1 = kR16H * kR16H * 2 / 16 / (64 * kR16Waves);  // 16 per thread
+        u4r v1[N1], vh[2];
+#pragma unroll
+        for (int i = 0; i < N1; ++i) v1[i] = src1[tid + i * 64 * kR16Waves];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) vh[i] = srch[tid + i * 64 * kR16Waves];
+        float pv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int j = tid + i * 64 * kR16Waves, l = j >> 9, c = j & 511;
+            pv[i] = c < kR16H ? P.lns[l][c] : P.lnb[l][c - kR16H];
+        }
+        const float hbv = tid < kR16HC ? P.head_b[tid] : 0.f;
+        // 16-byte unit U of a (K = 256, perm) image: n = ((U >> 10) << 5) | (U & 31),
+        // h = (U >> 5) & 1, s16 = (U >> 6) & 15; its halves hold inputs
+        // 16 s16 + 4h .. +3 and 16 s16 + 8 + 4h .. +3 (units 4 s16 + h, 4 s16 + 2 + h)
+        auto put = [&](char* img, int U, u4r v) {
+            const int n = ((U >> 10) << 5) | (U & 31), h = (U >> 5) & 1, s16 = (U >> 6) & 15;
+            *(u2r*)(img + r16_off(n, 4 * s16 + h)) = u2r{v[0], v[1]};
+            *(u2r*)(img + r16_off(n, 4 * s16 + 2 + h)) = u2r{v[2], v[3]};
+        };
+#pragma unroll
+        for (int i = 0; i < N1; ++i) put(w1img, tid + i * 64 * kR16Waves, v1[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) put(whimg, tid + i * 64 * kR16Waves, vh[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) gb[tid + i * 64 * kR16Waves] = pv[i];
+        if (tid < kR16HC) hb[tid] = hbv;
+        int* tab = (int*)(smem + kR16OffTab);
+        if (tid <= MLEARN_MAX_GROUPS) {
+            tab[tid] = P.off[tid];
+            ((float*)tab)[MLEARN_MAX_GROUPS + 1 + tid] = tid < MLEARN_MAX_GROUPS ? hp.ecoef[tid] : 0.f;
+            ((float*)tab)[2 * (MLEARN_MAX_GROUPS + 1) + tid] =
+                tid < MLEARN_MAX_GROUPS ? hp.objw[tid] : 0.f;
+        }
+    }
+    __syncthreads();
+    const int* t_off = (const int*)(smem + kR16OffTab);
+    const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
+    const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
+
+    const int ptile = (int)blockIdx.x * kR16Waves + wave;  // 32-row partials row (= ppo_step tile)
+    const float as0 = adv_st[0], as1 = adv_st[1];
+    const float* vn = hp.norm_vals ? adv_st + 2 : nullptr;
+    LossAcc m;
+    bool did = false;
+    float cb[2][4] = {}, cg[2][4] = {};  // LayerNorm bias / scale column sums, per layer
+    float hbsum = 0.f;                   // head-bias column sum (lane = column < 32)
+    uint32_t dz0w[kR16NB][2];            // layer-0 dZ of the previous tile (stored late)
+    int64_t prev_row = -1;
+    const int ntask = 16 * (K + 1);
+
+#pragma clang loop unroll(disable)
+    for (int tt = 0; tt < kR16Tiles; ++tt) {
+        // the lane index through an opaque copy per tile: otherwise every
+        // lane-derived LDS / weight address of the body is hoisted out of the
+        // tile loop and held live across it (rollout kernel)
+        const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
+        const int64_t row0 = (int64_t)ptile * 32 + 16 * tt;
+        const int64_t row = row0 + r;
+        const bool live = row < M;
+        const int64_t sr = live ? store_row(ro, mb_seq, mb, row) : 0;
+        // ---- layer 0: X_0 rows from the store (natural k order), W_0 from its
+        // fragment-order image in L2 (P.wt[0], K = D, natural k): element
+        // (n, k = 32s + 8g) at ((n/32 * D/16 + 2s + g/2) * 64 + n%32 + 32(g&1)) * 8
+        bf16x8 xf[DS];
+        const bf16* orow = (const bf16*)ro.obs + sr * D;
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+            xf[s] = live ? *(const bf16x8*)(orow + 32 * s + 8 * g) : RT<bf16>::zero();
+        // (each use of the first layer takes its own opaque copy of the lane: the
+        // forward's 16 fragment addresses are otherwise CSE'd into the
+        // backward's recompute and held live across the tile)
+        auto lda0 = [&](int ln) {
+            const bf16* w0 = (const bf16*)P.wt[0];
+            const int rr = ln & 15, gg = ln >> 4;
+            return [=](int b, int s) {
+                const int n = 16 * b + rr;
+                const int64_t idx = ((int64_t)(((n >> 5) * (D >> 4) + 2 * s + (gg >> 1)) * 64 +
+                                               (n & 31) + 32 * (gg & 1))) * 8;
+                return *(const bf16x8*)(w0 + idx);
+            };
+        };
+        auto bf0 = [&](int s) { return xf[s]; };
+        uint32_t zw[kR16NB][2], aw[kR16NB][2];
+        float mean, rstd;
+        r16_fwd_layer<DS, 8>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
+        // X_0 rows for the weight gradient (16 bytes per lane and k-step)
+        {
+            bf16* xrow = (bf16*)ws.x0 + r16_late(row) * D;
+#pragma unroll
+            for (int s = 0; s < DS; ++s) *(bf16x8*)(xrow + 32 * s + 8 * g) = xf[s];
+        }
+        // the previous tile's layer-0 dZ rows go out behind this tile's loads
+        if (tt > 0) r16_store_rows((bf16*)ws.dz[0] + r16_late(prev_row) * kR16H, dz0w, g);
+        r16_ln_apply(zw, mean, rstd, gb, g, aw);
+        // this lane's first two loss tasks (row task & 15, group task >> 4;
+        // group K = the value), in flight under the layer-1 product
+        int t_act[2] = {0, 0};
+        float t_lp[2] = {0.f, 0.f}, t_adv[2] = {0.f, 0.f}, t_ret[2] = {0.f, 0.f},
+              t_val[2] = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int task = lane + 64 * u;
+            const int64_t f = row0 + (task & 15);
+            const int grp = task >> 4;
+            if (task < ntask && f < M) {
+                const int64_t q = store_row(ro, mb_seq, mb, f);
+                t_adv[u] = ro.adv[q];
+                if (grp < K) {
+                    t_act[u] = ro.actions[q * K + grp];
+                    t_lp[u] = ro.logp[q * K + grp];
+                } else {
+                    t_ret[u] = ret_at(ro, q);
+                    if (ro.values) t_val[u] = ro.values[q];
+                }
+            }
+        }
+        // ---- layer 1 (W1 from LDS)
+        r16_fwd_layer<kR16KS, kR16Ring>(
+            [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
+            [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
+        r16_store_rows((bf16*)ws.a[0] + r16_late(row) * kR16H, aw, g);  // A_0 rows
+        r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
+        // ---- heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
+        f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        r16_mm<2, kR16KS, 4>(ha, [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
+                             [&](int s) { return r16_bfrag(aw, s); });
+        r16_store_rows((bf16*)ws.a[1] + r16_late(row) * kR16H, aw, g);  // A_1 rows
+        {
+            bf16* lr = lgs + r * kR16LGS;
+#pragma unroll
+            for (int cbk = 0; cbk < 2; ++cbk) {
+                const int c0 = 16 * cbk + 4 * g;
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = rnd<bf16>(rnd<bf16>(ha[cbk][i]) + rnd<bf16>(hb[c0 + i]));
+                *(u2r*)(lr + c0) = u2r{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
+            }
+        }
+        wave_lds_sync();
+        // ---- loss: one (row, group | value) task per lane and pass (ppo.py:129-262),
+        // d loss / d logits written over the logits (bf16: every consumer rounds them)
+        for (int task = lane, u = 0; task < ntask; task += 64, ++u) {
+            const int rr = task & 15, grp = task >> 4;
+            did = true;
+            bf16* lr = lgs + rr * kR16LGS;
+            const int64_t f = row0 + rr;
+            if (f >= M) {  // padding row: zero its d logits
+                if (grp < K)
+                    for (int j = t_off[grp]; j < t_off[grp + 1]; ++j) lr[j] = (bf16)0.f;
+                else
+                    for (int j = P.A; j < kR16HC; ++j) lr[j] = (bf16)0.f;
+                continue;
+            }
+            int act;
+            float olp, adv, ret, oval;
+            if (u < 2) {
+                act = u == 0 ? t_act[0] : t_act[1];
+                olp = u == 0 ? t_lp[0] : t_lp[1];
+                adv = u == 0 ? t_adv[0] : t_adv[1];
+                ret = u == 0 ? t_ret[0] : t_ret[1];
+                oval = u == 0 ? t_val[0] : t_val[1];
+            } else {
+                const int64_t q = store_row(ro, mb_seq, mb, f);
+                adv = ro.adv[q];
+                act = grp < K ? ro.actions[q * K + grp] : 0;
+                olp = grp < K ? ro.logp[q * K + grp] : 0.f;
+                ret = grp < K ? 0.f : ret_at(ro, q);
+                oval = (grp < K || !ro.values) ? 0.f : ro.values[q];
+            }
+            if (grp < K) {
+                if (hp.norm_adv) adv = (adv - as0) * as1;
+                const int o0 = t_off[grp];
+                loss_group(hp, lr + o0, t_off[grp + 1] - o0, act, olp, adv, t_ec[grp], t_ow[grp],
+                           m);
+            } else {
+                loss_value(hp, lr, P.A, kR16HC, ret, oval, m, vn);
+            }
+        }
+        wave_lds_sync();
+        // ---- d head: B operand of the head backward (cols 8g .. 8g+7 of row r),
+        // row-major store, head-bias column sums
+        const bf16x8 dh = *(const bf16x8*)(lgs + r * kR16LGS + 8 * g);
+        *(bf16x8*)((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g) = dh;
+        if (lane < kR16HC) {
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) hbsum += to_f32(lgs[rr * kR16LGS + lane]);
+        }
+        // ---- layer 1 backward: dA_1^T = Wh dHead^T (M = hidden unit = image
+        // column, K = head column), recomputed per half in the LayerNorm's
+        // second pass
+        uint32_t dzw[kR16NB][2];
+        r16_ln_bwd2<1>([&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
+                       [&](int) { return dh; }, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw,
+                       cb[1], cg[1]);
+        // dA_0^T = W1 dZ_1^T: M = input feature (image column), K = output feature
+        // (image rows 32s + 4g + j, 32s + 16 + 4g + j)
+        f32x4 acc[kR16NB];
+#pragma unroll
+        for (int b = 0; b < kR16NB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        r16_mm<kR16NB, kR16KS, kR16Ring>(
+            acc,
+            [&](int b, int s) {
+                return r16_tr_frag(w1img, 32 * s + 4 * g, 32 * s + 16 + 4 * g, b, lane);
+            },
+            [&](int s) { return r16_bfrag(dzw, s); });
+        r16_store_rows((bf16*)ws.dz[1] + r16_late(row) * kR16H, dzw, g);  // dZ_1 rows
+        // ---- layer 0 backward: Z_0 and its statistics again (the same MFMAs in
+        // the same order: the same bits; holding Z_0 across the tile would cost
+        // 32 registers at its peak), then the LayerNorm / ReLU backward
+        r16_fwd_layer<DS, 8>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
+        r16_ln_bwd(acc, zw, mean, rstd, gb, g, lane, live, dz0w, cb[0], cg[0]);
+        prev_row = row;
+    }
+    const int lane = tid & 63, r = lane & 15, g = lane >> 4;
+    r16_store_rows((bf16*)ws.dz[0] + prev_row * kR16H, dz0w, g);
+
+    // ---- column partials of this wave's 32 rows: LayerNorm bias / scale
+    // (value index col_sum16_index(r) of block quad qd), head bias
+    {
+        float* cp = ws.colpart + (int64_t)ptile * ws.CP;
+        const int vi = col_sum16_index(r);
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int f = 16 * (4 * qd + (vi >> 2)) + 4 * g + (vi & 3);
+                cp[l * 2 * kR16H + f] = cb[l][qd];
+                cp[l * 2 * kR16H + kR16H + f] = cg[l][qd];
+            }
+        if (lane < kR16HC) cp[2 * 2 * kR16H + lane] = hbsum;
+    }
+    // ---- loss metrics of this wave's rows (only the minibatch whose metrics survive)
+    if (METRICS) {
+        const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
+                                        m.mxvl, m.serr, m.qerr, m.mnerr, m.mxerr, m.sent, m.qent,
+                                        m.mnent, m.mxent, m.sentw, m.sobjw, 0.f, 0.f};
+        constexpr int kUsed = 18;
+        double* lp = ws.loss_part + (int64_t)ptile * kLossSlots;
+        if (__any(did)) {
+#pragma unroll
+            for (int s = 0; s < kUsed; ++s) {
+                const int kind = (s < 16) ? (s & 3) : 0;
+                float v = vals[s];
+                v = kind == 2 ? wave_reduce<2>(v) : (kind == 3 ? wave_reduce<3>(v) : wave_reduce<0>(v));
+                if (lane == 0) lp[s] = v;
+            }
+            if (lane >= kUsed && lane < kLossSlots) lp[lane] = 0.0;
+        } else if (lane < kLossSlots) {
+            const int kind = (lane < 16) ? (lane & 3) : 0;
+            lp[lane] = kind == 2 ? 3.4e38 : (kind == 3 ? -3.4e38 : 0.0);
+        }
+    }
+}
+
+// The row-split kernel runs the bf16, H = 256, two-layer, scalar-critic step
+// when every CU gets at least one workgroup (one workgroup = 256 rows).
+static bool rows16_eligible(const PolicyK& P, int64_t Mp, int HC, int L, int H, bool bf) {
+    return bf && H == kR16H && L == 2 && HC == kR16HC && P.CB == 1 && P.D == kR16D &&
+           P.K + 1 <= 16 && Mp % (32 * kR16Waves) == 0 &&
+           Mp / (32 * kR16Waves) >= 256;
+}
+
+static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                          int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                          hipStream_t s) {
+    static bool attr_set = false;  // once (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        attr_set = true;
+    }
+    const int grid = (int)(ws.Mp / (32 * kR16Waves));
+    if (hp.metrics)
+        hipLaunchKernelGGL(ppo_rows16_kernel<true>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s, P,
+                           R, mb_seq, mb, M, adv_st, hp, ws);
+    else
+        hipLaunchKernelGGL(ppo_rows16_kernel<false>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s,
+                           P, R, mb_seq, mb, M, adv_st, hp, ws);
+}
+

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -67,7 +67,7 @@ class PPOHparams(Structure):
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
                 ("loss_scale", c_float), ("normalize_values", c_int32),
                 ("obj_weight", c_float * MAX_GROUPS),
-                ("grad_sumsq_out", c_void_p)]
+                ("grad_sumsq_out", c_void_p), ("step_kernel", c_int32), ("pad", c_int32)]
 
 
 class FlatGroup(Structure):  # mlearn_flat_group
@@ -169,9 +169,11 @@ _SIGNATURES = {
     "mlearn_policy_pop_bytes": (c_int64, [c_int32]),
     "mlearn_policy_pop_prepare": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                             _P, c_int64, POINTER(RolloutOut), _P,
-                                            POINTER(DummyEnv), c_int32, _P]),
+                                            POINTER(DummyEnv), c_int32, _P, _S]),
     "mlearn_policy_rollout_env_pop": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), _P, c_int32,
-                                                c_int64, c_uint32, c_uint32, _P, _S]),
+                                                c_int64, c_uint32, c_uint32, _P, c_int32, _S]),
+    "mlearn_policy_rollout_pop_workgroups": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm),
+                                                       c_int64, c_int32, c_int32]),
     "mlearn_policy_evaluate": (c_int32, [POINTER(MlpPolicy), _P, c_int64, _P, _P, _P, _P, _S]),
     "mlearn_lstm_policy_evaluate": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                               _P, c_int64, _P, _P, _P, _P, _S]),

@@ -31,8 +31,13 @@ reference's rules: every Dense kernel (``_Dense.kernel``, or a torch
 goes back to its initial Frobenius norm (ppo.py:303-310,
 train_state.py:413-423), every LayerNorm's (scale, bias) to |s|^2 + |b|^2 =
 features (ppo.py:312-338; ``models.LayerNorm`` or torch ``nn.LayerNorm``).
-This path runs eagerly (no HIP-graph capture) and does not support
-recurrent trees or the value normaliser: those raise.
+An LSTM layer's weights (rnn.MultiLayerLSTMCell ``wi`` / ``wh``, gates
+concatenated along the output axis) project per gate, each of the 8 gate
+kernels to its own initial norm, as flax's separate per-gate Dense leaves do
+(rnn.py:30-36; the fused optimizer's per-gate slots).
+Recurrent trees (a user's recurrent backbone, multi-layer LSTMs) train here
+with the rollout carry and per-chunk start states.  This path runs eagerly
+(no HIP-graph capture); the value normaliser and populations raise.
 """
 
 import ctypes
@@ -99,12 +104,23 @@ class ObsCodec:
 def _projection_groups(ac):
     """[(kind, params...)] in module order: kind 1 = a Dense kernel outside
     the top-level actor / critic (train_state.py:413-423 gives only those an
-    initial norm), kind 2 = a LayerNorm (anywhere, ppo.py:312-338)."""
+    initial norm), kind 2 = a LayerNorm (anywhere, ppo.py:312-338), kind 3 =
+    one gate's kernel of an LSTM layer (weight, gate): flax OptimizedLSTMCell
+    keeps the 8 gate kernels (ii, if, ig, io without bias, hi, hf, hg, ho
+    with bias; rnn.py:30-36) as separate Dense leaves, each projected to its
+    own initial norm -- the same per-gate slots as the fused optimizer
+    (optim.hip proj_slot)."""
     from .models import LayerNorm, _Dense
+    from .rnn import MultiLayerLSTMCell
     groups = []
     for name, m in ac.named_modules():
         top = name.split(".", 1)[0]
-        if isinstance(m, _Dense) and m.kernel is not None and top not in ("actor", "critic"):
+        if isinstance(m, MultiLayerLSTMCell) and top not in ("actor", "critic"):
+            for l in range(len(m.wi)):
+                for w in (m.wi[l], m.wh[l]):
+                    for gate in range(4):
+                        groups.append((3, w, gate))
+        elif isinstance(m, _Dense) and m.kernel is not None and top not in ("actor", "critic"):
             groups.append((1, m.kernel))
         elif isinstance(m, nn.Linear) and top not in ("actor", "critic"):
             groups.append((1, m.weight))
@@ -351,6 +367,12 @@ class TorchTrainState:
                 w = g[1]
                 rows.append((off[w.data_ptr()], w.numel(), 0, 0, 1, 0,
                              float(torch.linalg.vector_norm(w.detach().float()).item())))
+            elif g[0] == 3:  # gate column block of a row-major [in][4R] LSTM weight
+                w, gate = g[1], g[2]
+                R = w.shape[1] // 4
+                blk = w.detach()[:, gate * R:(gate + 1) * R]
+                rows.append((off[w.data_ptr()] + gate * R, R, w.shape[1], w.shape[0], 3, 0,
+                             float(torch.linalg.vector_norm(blk.float()).item())))
             else:
                 s, b = g[1], g[2]
                 rows.append((off[s.data_ptr()], s.numel(), off[b.data_ptr()], b.numel(), 2,
@@ -362,7 +384,7 @@ class TorchTrainState:
             gt[i].kind, gt[i].features, gt[i].init_norm = r[4], r[5], r[6]
         raw = bytes(gt)
         self.groups = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-        self.init_norms = torch.tensor([r[6] for r in rows if r[4] == 1], dtype=torch.float32)
+        self.init_norms = torch.tensor([r[6] for r in rows if r[4] != 2], dtype=torch.float32)
         self.ws = torch.zeros(int(nat.lib().mlearn_flat_optim_workspace_bytes(n, self.num_groups)),
                               dtype=torch.uint8, device=dev)
         d = nat.FlatOptim()
@@ -395,6 +417,9 @@ class TorchTrainState:
               "update_prng_key": list(self.update_prng_key)}
         if self.scaler is not None:
             sd["scaler"] = self.scaler.state_dict()
+        if self.value_norm_est is not None:
+            sd["value_norm_est"] = self.value_norm_est.cpu()
+            sd["value_norm_count"] = self.value_norm_count.cpu()
         return sd
 
     def load_state_dict(self, sd):
@@ -404,6 +429,9 @@ class TorchTrainState:
         self.update_prng_key = tuple(sd["update_prng_key"])
         if self.scaler is not None and "scaler" in sd:
             self.scaler.load_state_dict(sd["scaler"])
+        if self.value_norm_est is not None and "value_norm_est" in sd:
+            self.value_norm_est.copy_(sd["value_norm_est"])
+            self.value_norm_count.copy_(sd["value_norm_count"])
 
 
 def _critic_value(crit):
@@ -515,8 +543,6 @@ class TorchPPO:
         from .models import action_groups
         b = self.base
         algo = cfg.algo
-        if cfg.normalize_values:
-            raise NotImplementedError("normalize_values on the torch path (use a fused tree)")
         if cfg.filter_advantages or cfg.importance_sample_trajectories:
             raise NotImplementedError("filter_advantages / importance_sample_trajectories")
         C = cfg.num_bptt_chunks
@@ -540,7 +566,19 @@ class TorchPPO:
         b.policy_idx = policy_idx
         b.dp = dp
         b.count = float(b.mb * dp.world_size * b.bptt)
-        b.vnorm = False
+        # value normaliser (normalize_values, ppo.py:190-211): the same
+        # per-minibatch return sums and estimate chain as the fused path
+        # (mlearn_return_stats / mlearn_value_norm_chain); the loss reads
+        # record m = {adv mean, adv rstd, mu', inv_sigma' after minibatch m's
+        # update, mu, sigma before it}
+        b.vnorm = bool(cfg.normalize_values)
+        if b.vnorm:
+            b.vn_est = ts.value_norm_est
+            b.vn_count = ts.value_norm_count
+            b.vn_decay = float(cfg.value_normalizer_decay)
+            b.ret_part = torch.zeros_like(b.adv_part)
+            b.vn_rec = torch.zeros((b.E, b.num_mb, 8), dtype=torch.float32, device=dev)
+            b.adv_sums = torch.zeros((b.E, 4 * b.num_mb), dtype=torch.float64, device=dev)
         self.groups = action_groups(cfg.actions)
         if tuple(x for _, g in self.groups for x in g) != tuple(ps.arch.buckets):
             raise ValueError(f"TrainConfig.actions {self.groups} does not match the actor's "
@@ -615,16 +653,25 @@ class TorchPPO:
             entropy_term = entropy_term + c * ent[..., off:off + k].mean()
             off += k
         R = mbd["returns"].float()
+        verr = None
         if isinstance(crit, SymExpTwoHotDistribution):
             vl = crit.two_hot_cross_entropy_loss(R.reshape(-1, 1)).reshape(T, M)
             V = crit.mean().reshape(T, M)
         else:
             V = crit.float().reshape(T, M)
             vpred = V
+            tgt = R
+            if self.base.vnorm:
+                # ppo.py:190-211: errors of the critic inverted with the estimates
+                # before this minibatch; the target = the returns normalised with
+                # the estimates after normalize_and_update_estimates
+                with torch.no_grad():
+                    verr = (V.detach() * adv_stats[5] + adv_stats[4] - R).abs()
+                tgt = (R - adv_stats[2]) * adv_stats[3]
             if self.clip_vl:  # ppo.py:197-203: jnp.clip(V, ov - clip, ov + clip)
                 ov = mbd["values"].float()
                 vpred = torch.minimum(torch.maximum(V, ov - self.clip), ov + self.clip)
-            e = vpred - R
+            e = vpred - tgt
             if self.huber:  # optax.huber_loss (delta 1)
                 ae = e.abs()
                 q = torch.clamp(ae, max=1.0)
@@ -635,7 +682,8 @@ class TorchPPO:
         loss = -action_obj + self.vcoef * value_loss - entropy_term
         with torch.no_grad():
             met = {"Loss": loss.detach(), "Action Obj": obj.detach(), "Value Loss": vl.detach(),
-                   "Value Errors": (V.detach() - R).abs(), "Entropy": ent.detach()}
+                   "Value Errors": (V.detach() - R).abs() if verr is None else verr,
+                   "Entropy": ent.detach()}
         return loss, met
 
     def update_program(self, cfg, policy_state, train_state, rollout_data, user_metrics_cb,
@@ -649,23 +697,36 @@ class TorchPPO:
                                               b.num_seq, nat.ptr(b.perm[e]), strm), "perm")
             nat.check(L.mlearn_adv_stats(b.view, nat.ptr(b.perm[e]), b.num_mb, b.mb,
                                          nat.ptr(b.adv_part[e]), strm), "adv_stats")
+            if b.vnorm:
+                nat.check(L.mlearn_return_stats(b.view, nat.ptr(b.perm[e]), b.num_mb, b.mb,
+                                                nat.ptr(b.ret_part[e]), strm), "return_stats")
         n2 = 2 * b.num_mb
         if b.dp.world_size > 1:
             for e in range(b.E):
                 b.adv_sums[e, :n2].copy_(b.adv_part[e, :n2])
+                if b.vnorm:
+                    b.adv_sums[e, n2:2 * n2].copy_(b.ret_part[e, :n2])
             yield ("allreduce", b.adv_sums)
             for e in range(b.E):
                 b.adv_part[e, :n2].copy_(b.adv_sums[e, :n2])
+                if b.vnorm:
+                    b.ret_part[e, :n2].copy_(b.adv_sums[e, n2:2 * n2])
         for e in range(b.E):
             nat.check(L.mlearn_adv_stats_finish(nat.ptr(b.adv_part[e]), b.num_mb, b.count,
                                                 nat.ptr(b.adv_stats[e]), strm), "adv_stats_finish")
+        if b.vnorm:  # the estimates move minibatch by minibatch, epochs in order (ppo.py:346)
+            for e in range(b.E):
+                nat.check(L.mlearn_value_norm_chain(
+                    nat.ptr(b.ret_part[e]), nat.ptr(b.adv_stats[e]), b.num_mb, b.count,
+                    b.vn_decay, 1e-5, nat.ptr(b.vn_est), nat.ptr(b.vn_count),
+                    nat.ptr(b.vn_rec[e]), strm), "value_norm_chain")
         ps, ts = policy_state, train_state
         for e in range(b.E):
             for m in range(b.num_mb):
                 seqs = b.perm[e, m * b.mb:(m + 1) * b.mb]
                 mbd = self._minibatch(seqs)
                 ps.grads.zero_()
-                loss, met = self._loss(ps, mbd, b.adv_stats[e, m])
+                loss, met = self._loss(ps, mbd, b.vn_rec[e, m] if b.vnorm else b.adv_stats[e, m])
                 sc = ts.scaler
                 if sc is None:
                     (loss * self.loss_scale).backward()

@@ -236,7 +236,8 @@ class RolloutManager:  # rollouts.py:373-826
     population's whole rollouts go out as ONE launch over every policy's env
     tiles (mlearn_policy_rollout_env_pop), so P launches of B / 32 workgroups
     each become one that fills the chip; False issues one launch per policy.
-    Same bits either way."""
+    A ``rollout_workgroups`` cap > 0 caps that launch too (tiles of several
+    policies in series per workgroup).  Same bits either way."""
 
     whole_rollout = True
     rollout_workgroups = 0
@@ -487,12 +488,16 @@ class RolloutManager:  # rollouts.py:373-826
     def _population_rollout(self, rollout_state, obs0, sim, key, step_ctr, gamma):
         """mlearn_policy_rollout_env_pop over every policy's env columns; False
         when the per-policy launches must run instead (one policy, the
-        population launch switched off, a max_workgroups cap, or the launch
-        arguments changed while a graph is being captured)."""
-        if self.P < 2 or not self.population_launch or int(self.rollout_workgroups) != 0:
+        population launch switched off, per-step launches asked for
+        (rollout_workgroups < 0), or the launch arguments changed while a
+        graph is being captured)."""
+        cap = int(self.rollout_workgroups)
+        if self.P < 2 or not self.population_launch or cap < 0:
             return False
         B, P = self.B, self.P
         outs = [self._rollout_out(rollout_state, p, gamma) for p in range(P)]
+        for o in outs:  # the population launch takes its cap as an argument
+            o.max_workgroups = 0
         envs = [self._env_desc(sim, p) for p in range(P)]
         descs = [ps.desc for ps in self.policies]
         lstms = [ps.lstm_desc for ps in self.policies] if self.R else None
@@ -513,11 +518,11 @@ class RolloutManager:  # rollouts.py:373-826
                 arr(nat.MlpPolicy, descs), arr(nat.Lstm, lstms) if lstms else None,
                 arr(nat.LstmCarry, carries) if carries else None, (nat.c_void_p * P)(*obs), B,
                 arr(nat.RolloutOut, outs), (nat.c_uint32 * P)(*offs), arr(nat.DummyEnv, envs), P,
-                nat.ptr(self._pop_buf)), "policy_pop_prepare")
+                nat.ptr(self._pop_buf), nat.stream_handle()), "policy_pop_prepare")
             self._pop_sig = sig
         nat.check(L.mlearn_policy_rollout_env_pop(
             self.policy_state.desc, self.policy_state.lstm_desc if self.R else None,
-            nat.ptr(self._pop_buf), P, B, key[0], key[1], nat.ptr(step_ctr),
+            nat.ptr(self._pop_buf), P, B, key[0], key[1], nat.ptr(step_ctr), cap,
             nat.stream_handle()), "policy_rollout_env_pop")
         return True
 

@@ -306,11 +306,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         preprocess.fused_cast_dtype(cfg.compute_dtype)
         from .observations import ObservationsEMANormalizer
         if isinstance(preprocess, ObservationsEMANormalizer):
-            from .actor_critic import _identity_prefix
-            if prefix is not _identity_prefix:
-                raise NotImplementedError(
-                    "ObservationsEMANormalizer with a BackboneShared prefix: the fused path "
-                    "applies the prefix before the normaliser")
+            # (with a prefix, _fused_tree_problem sent the policy to the torch path)
             o = rollout_state.cur_obs
             obs_key = next(iter(o)) if isinstance(o, dict) else None
     # one PolicyState / PolicyTrainState per train policy (_make_policies,
@@ -384,19 +380,37 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
 
 def _fused_tree_problem(policy, rollout_state, sim_batch, cfg):
     """None when the fused kernels implement the policy (tree and
-    preprocess), else why not (the torch path then trains it)."""
+    preprocess), else why not (the torch path then trains it).  Only the
+    fused path's own limits route a policy to the torch path (an fp16
+    compute dtype, a tree or preprocess it does not implement, the
+    normaliser-before-prefix order); any other error -- e.g. an even
+    DreamerV3Critic num_bins, or a bug inside a user's prefix -- propagates."""
     from .rollouts import obs_to_matrix
     ac = policy.actor_critic
+    if cfg.compute_dtype == torch.float16:
+        return "fp16 compute dtype (DynamicScale, ppo.py:276-291)"
+    bb = getattr(ac, "backbone", None)
+    prefix = getattr(bb, "prefix", None)
+    if prefix is None:
+        return f"{type(bb).__name__} has no shared prefix (actor_critic.py:247-303)"
+    x = prefix(rollout_state.cur_obs, train=False)
+    if isinstance(x, dict) and len(x) != 1:
+        return f"the prefix returns {len(x)} observations (the fused kernels take one matrix)"
+    obs0 = obs_to_matrix(x, sim_batch)
     try:
-        from . import _native as nat
-        nat.dtype_code(cfg.compute_dtype)  # fp16: torch path with DynamicScale
-        prefix = ac.backbone.prefix
-        obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
         compile_arch(ac, obs0.shape[1], cfg.compute_dtype)
         if policy.obs_preprocess is not None:
             policy.obs_preprocess.fused_cast_dtype(cfg.compute_dtype)
-    except (NotImplementedError, AttributeError, ValueError) as e:
-        return f"{type(e).__name__}: {e}"
+    except NotImplementedError as e:
+        return f"NotImplementedError: {e}"
+    from .actor_critic import _identity_prefix
+    from .observations import ObservationsEMANormalizer
+    if isinstance(policy.obs_preprocess, ObservationsEMANormalizer) and \
+            prefix is not _identity_prefix:
+        # the reference normalises the raw observations and runs the prefix on
+        # the result (rollouts.py:838-840, actor_critic.py:226-229); the fused
+        # rollout kernel normalises the prefix's output
+        return "ObservationsEMANormalizer with a BackboneShared prefix (normaliser before prefix)"
     return None
 
 
@@ -411,8 +425,6 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
     from .models import action_groups
     if num_policies != 1:
         raise NotImplementedError(f"populations need a fused policy tree ({why})")
-    if cfg.normalize_values:
-        raise NotImplementedError(f"normalize_values needs a fused policy tree ({why})")
     print(f"[madrona_learn] policy tree outside the fused kernels ({why}): training it with "
           "torch autograd (HIP sampling / GAE / statistics / optimizer)", file=sys.stderr)
     buckets = [b for _, g in action_groups(cfg.actions) for b in g]
@@ -425,8 +437,17 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
     algo = TorchPPO(cfg.algo.setup())
     ts = TorchTrainState(cfg, algo.init_hyperparams(cfg), ps, _split_seed(cfg.seed, 2))
     ts.policy_id = 0
+    value_norm = None
+    if cfg.normalize_values:
+        # EMANormalizer.init_estimates (moving_avg.py:56-76), the fused path's
+        # record layout: mu 0, inv_sigma 1, sigma 1, biased sums 0, N 0
+        value_norm = torch.zeros((1, 8), dtype=torch.float32, device=device)
+        value_norm[:, 1] = 1.0
+        value_norm[:, 2] = 1.0
+        ts.value_norm_est = value_norm[0]
+        ts.value_norm_count = torch.zeros(1, dtype=torch.int32, device=device)
     tsm = TrainStateManager(policy_states=ps, train_states=ts, pbt_rng=None,
-                            user_state=user_hooks.init_user_state(), value_norm=None)
+                            user_state=user_hooks.init_user_state(), value_norm=value_norm)
     start = 0
     if restore_ckpt is not None:
         path = _ckpt_file(restore_ckpt, rank, W)

@@ -31,18 +31,39 @@ ADAM_B1, ADAM_B2, ADAM_EPS = 0.9, 0.999, 1e-8  # optax.adam defaults (optax 0.1.
 def round_bf16(x):
     """float32 -> bfloat16 (round to nearest even) -> float32."""
     x = np.asarray(x, dtype=np.float32)
-    u = x.view(np.uint32).astype(np.uint64)
-    r = (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32)
+    u = x.view(np.uint32)
+    # uint32 arithmetic: only NaN patterns can wrap, and those are kept as is
+    r = (u + (np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1)))) & np.uint32(0xFFFF0000)
     out = r.view(np.float32)
     return np.where(np.isnan(x), x, out)
 
 
+def round_fp16_significand(x):
+    """float32 -> the float16 significand (10 bits, round to nearest even)
+    with float32's exponent range.  The fp16 compute dtype trains under
+    DynamicScale (ppo.py:276-291): the loss is scaled by 2^k before the
+    backward, which keeps the backward's cotangents inside fp16's normal
+    range, where rounding to fp16 and back equals rounding the significand
+    (a power-of-two scale commutes with it); the forward's values are O(1).
+    So the fp16 rounding points are emulated without fp16's range limits
+    (the scale's own overflow handling is oracle/dynamic_scale_ref.py's)."""
+    x = np.asarray(x, dtype=np.float32)
+    u = x.view(np.uint32)
+    r = (u + (np.uint32(0xFFF) + ((u >> np.uint32(13)) & np.uint32(1)))) & np.uint32(0xFFFFE000)
+    out = r.view(np.float32)
+    return np.where(np.isfinite(x), out, x)
+
+
 def rnd(x, mode, ad=np.float64):
+    """Round to the compute dtype of `mode` ("f64": none; "f32"; "bf16";
+    "fp16": round_fp16_significand) and return in the arithmetic dtype ad."""
     if mode == "f64":
         return np.asarray(x, dtype=ad)
     x32 = np.asarray(x, dtype=np.float32)
     if mode == "bf16":
         x32 = round_bf16(x32)
+    elif mode == "fp16":
+        x32 = round_fp16_significand(x32)
     return x32.astype(ad)
 
 

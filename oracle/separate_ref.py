@@ -77,13 +77,17 @@ def project(named, init_norms, L):
 
 
 def ppo_update(named, order, store, hp, buckets, L, init_norms, *, num_epochs, minibatch_size,
-               bptt, key, epoch_base, mode, lr, max_grad_norm, ad=np.float64):
+               bptt, key, epoch_base, mode, lr, max_grad_norm, ad=np.float64, value_norm=None,
+               value_norm_decay=0.99999):
     """_ppo (ppo.py:366-488): the same minibatch plan as ppo_ref.ppo_update;
     the optimizer runs over the flat vector in `order` (the parameter names in
     the torch arena's order).  `store` is one rank's [T][N] store or a list of
     them (data parallelism: each optimizer step over the union of the ranks'
     minibatches -- union advantage statistics, gradient = sum over ranks of
-    the rank-local gradients of the loss scaled by 1 / world)."""
+    the rank-local gradients of the loss scaled by 1 / world).  value_norm
+    (normalize_values, ppo.py:190-211): the EMANormalizer estimates
+    (ppo_ref.ema_init), moved minibatch by minibatch as in
+    ppo_ref.ppo_update."""
     stores = store if isinstance(store, (list, tuple)) else [store]
     world = len(stores)
     store = stores[0]
@@ -112,9 +116,19 @@ def ppo_update(named, order, store, hp, buckets, L, init_norms, *, num_epochs, m
                 perms[r][i * minibatch_size:(i + 1) * minibatch_size], N, bptt))
                 for r in range(world)]
             adv = np.concatenate([np.asarray(b[ref.objective_key(hp)], np.float64) for b in bs])
+            hp_mb = hp
+            if value_norm is not None:  # as ppo_ref.ppo_update (ppo.py:209-211, 346)
+                allret = np.concatenate([np.asarray(b["returns"], np.float64) for b in bs])
+                z = np.zeros(1, np.float32)
+                new = ref.ema_update_estimates(value_norm, ref.ema_update_input_stats(
+                    (z, z), 0, allret[:, None]), value_norm_decay, 1e-5)
+                hp_mb = dict(hp, value_norm=(float(new["mu"][0]), float(new["inv_sigma"][0]),
+                                             float(value_norm["mu"][0]),
+                                             float(value_norm["sigma"][0])))
+                value_norm.update(new)
             g = None
             for r, b in enumerate(bs):
-                _, G, m_r = loss_grads(unflat(flat), b, hp, buckets, L, mode,
+                _, G, m_r = loss_grads(unflat(flat), b, hp_mb, buckets, L, mode,
                                        (adv.mean(), adv.var()), ad)
                 gr = np.concatenate([np.asarray(G[k], ad).reshape(-1) for k in order]) / world
                 g = gr if g is None else g + gr

@@ -9,10 +9,12 @@ within the oracle's own bf16-vs-f32 distance, per tensor).
     of the update runs at its production grid ((2048 / 32) x (256 / 32)
     workgroups), one epoch (one 65,536-row minibatch: the oracle's BPTT
     costs ~15 s on the host).
-  * P: two train policies of 8192 envs each (the 8-policy
-    population's per-policy column block), minibatches of 2048 sequences,
-    one epoch (4 optimizer steps per policy); the oracle replays policy 1's
-    8192 env columns and its 4 minibatches.
+  * L at its stated 8192 envs: oracle column windows of the whole-rollout
+    launch and the whole first update (4 minibatches of 2048 sequences).
+  * P at its stated size: 8 train policies x 8192 envs, the
+    population rollout launch with tiles of several policies in series per
+    workgroup (the parameter-restage branch), oracle windows of restaged
+    tiles and one restaged policy's whole update (4 optimizer steps).
 The rollout data are checked as in tests/test_gpu_train.py (obs / rewards /
 dones / GAE bit-exact, values / log-probs within the bf16 tolerance)."""
 
@@ -106,44 +108,162 @@ def test_lstm_update_production_grid(gpu):
     assert int(ts.step.item()) == 1
 
 
-def test_population_policy_block_8192(gpu):
+def _restage_tiles(grid, tpp, ntiles):
+    """Tiles of the second and third rounds of the population launch whose
+    workgroup's previous tile belonged to another policy (the restage branch
+    of policy_rollout_pop_kernel): tile g runs on workgroup g % grid after
+    tile g - grid."""
+    out = []
+    for k in (1, 2):
+        for g in range(k * grid, min((k + 1) * grid, ntiles)):
+            if (g - grid) // tpp != g // tpp:
+                out.append(g)
+                break
+        for g in range(min((k + 1) * grid, ntiles) - 1, k * grid - 1, -1):
+            if (g - grid) // tpp != g // tpp:
+                out.append(g)
+                break
+    return sorted(set(out))
+
+
+def _check_window(s, mgr, env, p0, lay, e0, cfg):
+    """Replay the 32 envs [e0, e0 + 32) on the oracle env + policy."""
+    c = slice(e0, e0 + 32)
+    oenv = onat.Env(32, D, env.k0, env.k1, e0)
+    oenv.reset()
+    acts = s.actions[:, c].cpu().numpy()
+    ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="bf16",
+                        gamma=cfg.gamma, actions_override=acts)
+    _check_store(s, ro, c)
+    gum = np.stack([onat.gumbel_table(*mgr.rollout.prng_key, t, e0, 32, 26) for t in range(T)])
+    noisy = ro["logits"] + gum
+    off = 0
+    for g, nb in enumerate(BUCKETS):
+        sl = noisy[..., off:off + nb]
+        srt = np.sort(sl, -1)
+        clear = (srt[..., -1] - srt[..., -2]) > 1e-2
+        assert np.array_equal(np.argmax(sl, -1)[clear], acts[..., g][clear]), (e0, g)
+        off += nb
+
+
+@pytest.mark.timeout(600)
+def test_population_8x8192(gpu):
+    """Config P at its stated size: 8 train policies x 8192 envs (65,536 envs)
+    on one GPU, the population's rollouts as ONE launch
+    (mlearn_policy_rollout_env_pop) whose 2048 env tiles outnumber the
+    resident workgroups, so workgroups take tiles of several policies in
+    series and restage the LayerNorm / head parameters on each move.  Env
+    tiles of rounds 2 and 3 whose workgroup's previous tile belonged to
+    another policy are replayed on the oracle with their own policy's
+    parameters (obs / rewards / dones / GAE bit-exact, values / log-probs
+    within the bf16 tolerance, sampled actions where the Gumbel margin is
+    clear); then one restaged policy's whole update (4 minibatches) against
+    the oracle under the per-tensor bf16 bound."""
+    from madrona_learn import _native as nat
     from madrona_learn.envs import DummyVecEnv
     import madrona_learn as ml
     from tests.test_gpu_train import make_policy
-    P, B, mb = 2, 8192, 2048
+    P, B, mb = 8, 8192, 2048
     N = P * B
     env = DummyVecEnv(N, D, 6, seed=3, device=gpu)
     cfg = _cfg(N, mb, pbt_policies=P, seed=9)
     mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.bfloat16, H),
                            use_graph=False)
     pss, tss = mgr.state.policy_list, mgr.state.train_list
-    assert mgr.rollout_mgr.B == B
-    p0 = pss[1].params.cpu().numpy().astype(np.float64)
-    oenv = onat.Env(B, env.D, env.k0, env.k1, B)  # policy 1's env columns only
-    oenv.reset()
+    rm = mgr.rollout_mgr
+    assert rm.B == B and rm.P == P
+    tpp = B // 32
+    grid = nat.lib().mlearn_policy_rollout_pop_workgroups(pss[0].desc, None, B, P, 0)
+    assert 0 < grid < P * tpp, grid
+    picks = _restage_tiles(grid, tpp, P * tpp)
+    assert len(picks) >= 2, (grid, picks)
+    p0s = [ps.params.cpu().numpy().astype(np.float64) for ps in pss]
+    assert not np.array_equal(p0s[0], p0s[1])  # each policy its own initialisation
     mgr.update_iter()
     torch.cuda.synchronize()
-    s = mgr.rollout_mgr.store
-    c = slice(B, 2 * B)
+    assert getattr(rm, "_pop_sig", None) is not None  # the population launch ran
+    s = rm.store
     lay = ref.param_layout(D, H, 2, 26)
-    ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="bf16",
-                        gamma=cfg.gamma, actions_override=s.actions[:, c].cpu().numpy())
-    _check_store(s, ro, c)
+    for g in picks:
+        p = g // tpp
+        _check_window(s, mgr, env, p0s[p], lay, g * 32, cfg)
+    # the whole update of the policy owning the first restaged tile
+    q = picks[0] // tpp
+    c = slice(q * B, (q + 1) * B)
     full = {k: (v.float() if v.dtype == torch.bfloat16 else v).cpu().numpy()
             for k, v in s.as_dict().items()}
     store = {k: (v[:, c] if v.ndim >= 2 else v[c]) for k, v in full.items()}
-    z = np.zeros_like(p0)
-    upd = dict(num_epochs=1, minibatch_size=mb, bptt=T, key=tss[1].update_prng_key,
+    adv, _ = ref.gae_f32(store["rewards"], store["values"], store["dones"],
+                         s.bootstrap[c].cpu().numpy(), 0.99, 0.95)
+    assert np.array_equal(store["advantages"], adv)
+    z = np.zeros_like(p0s[q])
+    upd = dict(num_epochs=1, minibatch_size=mb, bptt=T, key=tss[q].update_prng_key,
                epoch_base=0, lr=3e-4, max_grad_norm=0.5)
-    norms = pss[1].init_norms.cpu().numpy().astype(np.float64)
-    pb, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), [store], HP, BUCKETS, lay, norms,
+    norms = pss[q].init_norms.cpu().numpy().astype(np.float64)
+    pb, _, _ = ref.ppo_update(p0s[q], (z, z.copy(), 0), [store], HP, BUCKETS, lay, norms,
                               mode="bf16", **upd)
-    pf, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), [store], HP, BUCKETS, lay, norms,
+    pf, _, _ = ref.ppo_update(p0s[q], (z, z.copy(), 0), [store], HP, BUCKETS, lay, norms,
                               mode="f32", **upd)
-    check_bf16_update("config_P_policy1_8192", pss[1].params.cpu().numpy(), p0, pb, pf, lay)
-    assert int(tss[1].step.item()) == B // mb
-    last = mgr.metrics.last(policy=1)
+    check_bf16_update(f"config_P_8x8192_policy{q}", pss[q].params.cpu().numpy(), p0s[q], pb, pf,
+                      lay)
+    assert int(tss[q].step.item()) == B // mb
+    last = mgr.metrics.last(policy=q)
     np.testing.assert_allclose(last["Rewards"].mean, store["rewards"].mean(), rtol=1e-5)
+
+
+@pytest.mark.timeout(600)
+def test_lstm_8192_rollout_and_update(gpu):
+    """Config L at its stated size: RecurrentBackboneEncoder(MLP[256,256],
+    LSTM(256)) over 8192 envs, bf16, minibatches of 2048 sequences (one
+    epoch = 4 optimizer steps).  The whole-rollout launch (carry, start
+    states, done clears) is checked on oracle column windows spread over the
+    env tiles; the update against the oracle's BPTT update of the same store
+    under the per-tensor bf16 bound."""
+    import madrona_learn as ml
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    from tests.test_gpu_lstm import make_actor_critic
+    N, mb = 8192, 2048
+    env = DummyVecEnv(N, D, 6, seed=7, device=gpu)
+    cfg = _cfg(N, mb, seed=21)
+    pol = ml.Policy(actor_critic=make_actor_critic(H, 2, torch.bfloat16),
+                    obs_preprocess=ml.ObservationsCaster.create(torch.bfloat16))
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), pol, use_graph=False)
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    grid = nat.lib().mlearn_policy_rollout_workgroups(ps.desc, ps.lstm_desc, N, 0)
+    assert grid > 0  # the whole rollout as one launch
+    a = ps.arch
+    lay = lref.param_layout(a.obs_dim, a.hidden, a.num_layers, a.num_logits, a.critic_bins)
+    p0 = ps.params.cpu().numpy().astype(np.float64)
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    tiles = N // 32
+    z32 = np.zeros((32, H))
+    for tile in sorted({0, grid - 1, min(grid, tiles - 1), tiles // 2 + 1, tiles - 1}):
+        e0 = tile * 32
+        c = slice(e0, e0 + 32)
+        oenv = onat.Env(32, D, env.k0, env.k1, e0)
+        oenv.reset()
+        ro, _, _ = lref.rollout(p0, lay, oenv, T, T, BUCKETS, mgr.rollout.prng_key, 0,
+                                (z32, z32), mode="bf16", gamma=cfg.gamma,
+                                actions_override=s.actions[:, c].cpu().numpy())
+        _check_store(s, ro, c)
+    store = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+             for k, v in s.as_dict().items()}
+    store["start_h"] = s.start_h.float().cpu().numpy()
+    store["start_c"] = s.start_c.float().cpu().numpy()
+    assert not store["start_h"].any()  # the first rollout starts from zero carries
+    zeros = np.zeros_like(p0)
+    upd = dict(num_epochs=1, minibatch_size=mb, bptt=T, key=ts.update_prng_key, epoch_base=0,
+               lr=3e-4, max_grad_norm=0.5)
+    norms = ps.init_norms.cpu().numpy().astype(np.float64)
+    pb, _, _ = lref.ppo_update(p0, (zeros, zeros.copy(), 0), [store], HP, BUCKETS, lay, norms,
+                               mode="bf16", **upd)
+    pf, _, _ = lref.ppo_update(p0, (zeros, zeros.copy(), 0), [store], HP, BUCKETS, lay, norms,
+                               mode="f32", **upd)
+    check_bf16_update("config_L_8192", ps.params.cpu().numpy(), p0, pb, pf, lay)
+    assert int(ts.step.item()) == N // mb
 
 
 def test_headline_rollout_tiles_in_series(gpu):

@@ -64,9 +64,10 @@ def _device_store(gpu, st, dtype):
     return s
 
 
-def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats):
+def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats, step_kernel=0):
     from madrona_learn import _native as nat
     hp = nat.PPOHparams()
+    hp.step_kernel = step_kernel
     hp.clip_coef, hp.value_loss_coef = hpd["clip_coef"], hpd["value_loss_coef"]
     for k in range(6):
         hp.entropy_coef[k] = hpd["entropy_coef"]
@@ -203,3 +204,49 @@ def test_value_loss_variants(gpu, mode, dtype, clip_vl, huber, ties):
         ob, _ = ps.layout["hb"]
         np.testing.assert_allclose(g[ob + A], gflat[ob + A], rtol=1e-5 if mode == "f32" else 2e-2,
                                    atol=1e-7)
+
+
+@pytest.mark.parametrize("mb,bptt", [(2048, 32), (4095, 16)])
+def test_row_split_step_kernel(gpu, mb, bptt):
+    """The row-split step kernel (the bf16 default at >= 65,536 rows: W1 held
+    in LDS, one wave per 16-row tile, 16x16x32 MFMAs) against the oracle and
+    against the feature-split kernel (step_kernel 1) on the same minibatch;
+    (4095, 16) leaves 16 padding rows in the last workgroup.  The two kernels
+    sum in different orders (f32 accumulation of the same bf16 products), so
+    they agree to the bf16 bound, not bitwise."""
+    T, N, D, H, L = 32, 8192, 64, 256, 2
+    ps = make_policy_state(gpu, D, H, L, torch.bfloat16, seed=41)
+    perturb(ps, 42, scale=0.2)
+    rng = np.random.default_rng(43)
+    nseq = (T // bptt) * N
+    seqs = rng.permutation(nseq)[:mb].astype(np.int32)
+    st, rows = _minibatch_store(rng, ps, T, N, D, "bf16", seqs, bptt)
+    s = _device_store(gpu, st, torch.bfloat16)
+    batch = ref.gather_minibatch(st, rows)
+    adv = batch["advantages"].astype(np.float64)
+    stats = (adv.mean(), adv.var())
+    g2, o2 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, step_kernel=2)
+    g1, o1 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, step_kernel=1)
+    g0, o0 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
+    assert np.array_equal(g0, g2) and np.array_equal(o0, o2), "auto must pick the row split"
+    scale = np.abs(g1).max()
+    assert np.abs(g2 - g1).max() / scale < 1e-2
+    assert g2 @ g1 / (np.linalg.norm(g2) * np.linalg.norm(g1)) > 0.9999
+    np.testing.assert_allclose(o2[[0, 10, 15, 20]], o1[[0, 10, 15, 20]], rtol=2e-3)
+    assert o2[14] == mb * bptt and o2[24] == mb * bptt * 6
+    P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
+    loss, G, met, _ = ref.ppo_loss_grads(P, batch, HP, BUCKETS, "bf16", adv_stats=stats)
+    _check("bf16", g2, o2, loss, ref.flatten(G, oracle_layout(ps)), met, mb * bptt)
+
+
+def test_row_split_rejects_ineligible(gpu):
+    """step_kernel 2 on a minibatch the row split cannot take is EINVAL."""
+    from madrona_learn import _native as nat
+    T, N, D, H, L, mb, bptt = 16, 96, 64, 128, 2, 40, 16
+    ps = make_policy_state(gpu, D, H, L, torch.bfloat16, seed=51)
+    rng = np.random.default_rng(52)
+    seqs = rng.permutation(N)[:mb].astype(np.int32)
+    st, _ = _minibatch_store(rng, ps, T, N, D, "bf16", seqs, bptt)
+    s = _device_store(gpu, st, torch.bfloat16)
+    with pytest.raises(RuntimeError, match="step_kernel"):
+        _run_grad(gpu, ps, s, seqs, mb, bptt, HP, (0.0, 1.0), step_kernel=2)

@@ -60,7 +60,10 @@ def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, gr
     multi_tile: the same launch capped at 2 workgroups (1 for a 2-tile
     policy; mlearn_rollout_out.max_workgroups), so every workgroup runs several
     env tiles in series with the parameters it staged in LDS once (the
-    headline's 2048 tiles on 768 resident workgroups take this branch);
+    headline's 2048 tiles on 768 resident workgroups take this branch); a
+    population's launch under the same cap deals tiles of every policy to
+    each workgroup, which restages the parameters when its next tile belongs
+    to another policy (config P's 2048 tiles on 768 slots take that branch);
     c_per_step: the same entry's per-step launches (max_workgroups = -1);
     py_per_step: one rollout_step_env call per step from the host."""
     from madrona_learn import _native as nat
@@ -77,14 +80,21 @@ def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, gr
                                                       rm.rollout_workgroups)
     if mode == "multi_tile":
         assert grid == cap and tiles > grid, (grid, tiles)
+        if P > 1:
+            pg = nat.lib().mlearn_policy_rollout_pop_workgroups(ps.desc, ps.lstm_desc, rm.B, P,
+                                                                cap)
+            assert pg == cap
+            # workgroup 0's tiles 0, cap, 2 cap, ... span more than one policy
+            assert len({g // tiles for g in range(0, P * tiles, pg)}) > 1
     elif mode == "c_per_step":
         assert grid == -1
     elif mode == "one_launch":
         assert grid == tiles
-        if P > 1:  # the population launch ran (its arguments were prepared)
-            a.update_iter()
-            assert getattr(rm, "_pop_sig", None) is not None
-            b.update_iter()
+    if P > 1 and mode in ("one_launch", "multi_tile"):
+        # the population launch ran (its arguments were prepared)
+        a.update_iter()
+        assert getattr(rm, "_pop_sig", None) is not None
+        b.update_iter()
     assert RolloutManager.rollout_workgroups == 0  # instance setting only
     for _ in range(2):
         a.update_iter()
@@ -103,7 +113,7 @@ def test_fused_env_step_is_bit_identical(gpu, mode, dtype, N, H, mb, P, lstm, gr
     for x, y in zip(pa, pb):
         assert torch.equal(x.params, y.params)
     # the fused run issued no sim launch: its env buffers moved anyway
-    iters = 3 if (mode == "one_launch" and P > 1) else 2
+    iters = 3 if (mode in ("one_launch", "multi_tile") and P > 1) else 2
     assert int(env_a.state[:, 1].min().item()) == 32 * iters
 
 

@@ -263,6 +263,10 @@ def test_multilayer_lstm_trains_on_torch_path(gpu):
     mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac))
     ps = mgr.state.policy_states
     assert getattr(ps, "generic", False) and ps.recurrent
+    cell0 = ac.backbone.encoder.rnn.cell
+    wi0 = [w.detach().clone() for w in cell0.wi]
+    wh0 = [w.detach().clone() for w in cell0.wh]
+    assert mgr.state.train_states.num_groups == 2 * 8 + 2  # 8 gate kernels per layer + W0, LN0
     for it in range(2):
         p_roll = ps.params.clone()
         mgr.update_iter()
@@ -289,3 +293,139 @@ def test_multilayer_lstm_trains_on_torch_path(gpu):
                                            s.log_probs[c * bp:(c + 1) * bp], rtol=1e-4, atol=1e-5)
                 torch.testing.assert_close(v, s.values[c * bp:(c + 1) * bp], rtol=1e-4, atol=1e-5)
         ps.params.copy_(p_now)
+        # every gate kernel of every layer stayed at its initial norm (flax's
+        # separate per-gate Dense leaves, each projected, ppo.py:303-310)
+        cell = ac.backbone.encoder.rnn.cell
+        for l in range(2):
+            for w, w0 in ((cell.wi[l], wi0[l]), (cell.wh[l], wh0[l])):
+                for g in range(4):
+                    blk = w.detach()[:, g * 64:(g + 1) * 64]
+                    torch.testing.assert_close(torch.linalg.vector_norm(blk),
+                                               torch.linalg.vector_norm(w0[:, g * 64:(g + 1) * 64]),
+                                               rtol=1e-5, atol=0)
+
+
+def _shared_mlp_flat(ps, D, H, L):
+    """The torch arena of a BackboneShared(BackboneEncoder(MLP)) tree with
+    DenseLayerDiscreteActor / DenseLayerCritic as oracle/ppo_ref's flat
+    layout (trunk W / LayerNorm per layer, head W = [actor | critic] columns)."""
+    named = _named(ps)
+    pre = "backbone.encoder.net"
+    lay = ref.param_layout(D, H, L, sum(BUCKETS))
+    P = {"W": [named[f"{pre}.dense.{l}.kernel"] for l in range(L)],
+         "s": [named[f"{pre}.norms.{l}.scale"] for l in range(L)],
+         "b": [named[f"{pre}.norms.{l}.bias"] for l in range(L)],
+         "Wh": np.concatenate([named["actor.impl.kernel"], named["critic.impl.kernel"]], 1),
+         "bh": np.concatenate([named["actor.impl.bias"], named["critic.impl.bias"]])}
+    return ref.flatten(P, lay), lay
+
+
+def test_fp16_update_matches_oracle(gpu):
+    """compute_dtype fp16 (train_state.py:402-403) on the torch path, one
+    update of 2 epochs x 4 minibatches under DynamicScale (ppo.py:276-291),
+    against the oracle's fp16 mode (oracle/ppo_ref.py rnd 'fp16': the fp16
+    significand at every compute-dtype rounding point) under the per-tensor
+    bound of tests/bf16_bound.py: the GPU's distance to the fp16 oracle
+    within the oracle's own fp16-vs-f32 distance per tensor.  Rollout: the
+    stored fp16 observations bit-exact, values / log-probs within fp16
+    tolerance of the oracle forward."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from tests.bf16_bound import check_bf16_update
+    from tests.test_gpu_train import make_policy
+    N, H, L, mb, T = 64, 64, 2, 16, 32
+    env = DummyVecEnv(N, 64, 6, seed=12, device=gpu)
+    cfg = _cfg(N, mb, epochs=2, dtype=torch.float16)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.float16, H))
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    assert getattr(ps, "generic", False) and ts.scaler is not None
+    p0, lay = _shared_mlp_flat(ps, 64, H, L)
+    oenv = onat.Env(N, 64, env.k0, env.k1, 0)
+    oenv.reset()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert int(ts.scaler.fin_steps.item()) == 2 * (N // mb)  # no skipped step
+    s = mgr.rollout_mgr.store
+    acts = s.actions.cpu().numpy()
+    obs = s.obs.float().cpu().numpy()
+    for t in range(T):
+        assert np.array_equal(obs[t], oenv.obs.astype(np.float16).astype(np.float32)), t
+        oenv.step(acts[t])
+    logits, V, _ = ref.forward(ref.unflatten(p0, lay), obs.reshape(T * N, 64), "fp16")
+    lp, _ = ref.action_stats(logits, BUCKETS, acts.reshape(T * N, 6))
+    np.testing.assert_allclose(s.values.cpu().numpy().reshape(-1), V, rtol=1e-2, atol=1e-2)
+    np.testing.assert_allclose(s.log_probs.cpu().numpy().reshape(-1, 6), lp, rtol=1e-2,
+                               atol=1e-2)
+    store = {k: v.float().cpu().numpy() if v.dtype != torch.uint8 and v.is_floating_point()
+             else v.cpu().numpy() for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    norms = np.array([np.sqrt((w ** 2).sum()) for w in ref.unflatten(p0, lay)["W"]])
+    z = np.zeros_like(p0)
+    upd = dict(num_epochs=2, minibatch_size=mb, bptt=T, key=ts.update_prng_key, epoch_base=0,
+               lr=3e-4, max_grad_norm=0.5)
+    ph, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), [store], hp, BUCKETS, lay, norms,
+                              mode="fp16", **upd)
+    pf, _, _ = ref.ppo_update(p0, (z, z.copy(), 0), [store], hp, BUCKETS, lay, norms,
+                              mode="f32", **upd)
+    got, _ = _shared_mlp_flat(ps, 64, H, L)
+    check_bf16_update("torch_fp16_update", got, p0, ph, pf, lay)
+
+
+def test_value_norm_on_torch_path_matches_oracle(gpu):
+    """normalize_values (ppo.py:190-211) with a tree outside the fused
+    kernels (BackboneSeparate, f32): the GAE inverts the stored values, the
+    per-minibatch return statistics move the estimates minibatch by
+    minibatch (mlearn_return_stats / mlearn_value_norm_chain, as the fused
+    path), the value loss targets the normalised returns; one update against
+    oracle/separate_ref.py with the value normaliser (ppo_ref's rule)."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    N, H, L, mb, T = 64, 64, 2, 16, 32
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=13, device=gpu)
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneSeparate(actor_encoder=ml.BackboneEncoder(net=MLP(H, L, dt)),
+                                     critic_encoder=ml.BackboneEncoder(net=MLP(H, L, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DenseLayerCritic(dt))
+    cfg = dataclasses.replace(_cfg(N, mb), normalize_values=True, value_normalizer_decay=0.99)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac))
+    ps, ts = mgr.state.policy_states, mgr.state.train_states
+    assert getattr(ps, "generic", False) and ts.value_norm_est is not None
+    order = [n for n, _, _ in ps.layout["params"]]
+    p0 = _named(ps)
+    init_norms = {k: float(np.sqrt((v * v).sum())) for k, v in p0.items() if k.endswith("kernel")
+                  and k.startswith("backbone.")}
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    # the initial estimates (mu 0, sigma 1) invert to the stored values exactly
+    adv, _ = ref.gae_f32(s.rewards.cpu().numpy(), s.values.cpu().numpy(), s.dones.cpu().numpy(),
+                         s.bootstrap.cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+    assert np.array_equal(s.advantages.cpu().numpy(), adv)
+    store = {k: v.cpu().numpy() for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    est = ref.ema_init(1)
+    want, met = sref.ppo_update(dict(p0), order, store, hp, BUCKETS, L, init_norms, num_epochs=2,
+                                minibatch_size=mb, bptt=T, key=ts.update_prng_key, epoch_base=0,
+                                mode="f32", lr=3e-4, max_grad_norm=0.5, value_norm=est,
+                                value_norm_decay=0.99)
+    assert est["N"] == 2 * (N // mb)
+    vn = ts.value_norm_est.cpu().numpy()
+    np.testing.assert_allclose(vn[0], est["mu"][0], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(vn[2], est["sigma"][0], rtol=1e-5)
+    assert int(ts.value_norm_count.item()) == est["N"]
+    got = _named(ps)
+    g = np.concatenate([got[k].reshape(-1) for k in order])
+    w = np.concatenate([want[k].reshape(-1) for k in order])
+    np.testing.assert_allclose(g, w, rtol=0, atol=1e-4)
+    close = np.abs(g - w) <= 2e-5 + 1e-4 * np.abs(w)
+    assert close.mean() >= 0.999, close.mean()
+    # the last minibatch's value errors use the critic inverted with the
+    # estimates before that minibatch
+    last = mgr.metrics.last()
+    np.testing.assert_allclose(last["Value Errors"].mean, np.mean(met["Value Errors"]), rtol=1e-4)

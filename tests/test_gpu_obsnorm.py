@@ -148,3 +148,60 @@ def test_obs_stats_kernel_partial_tiles(gpu):
     for i, k in enumerate(("mu", "inv_sigma", "sigma", "mu_biased", "sigma_sq_biased")):
         np.testing.assert_allclose(e[i], exp[k], rtol=2e-5, atol=1e-6, err_msg=k)
     assert int(count.item()) == 1
+
+
+def test_obs_normalizer_before_prefix_on_torch_path(gpu):
+    """ObservationsEMANormalizer with a BackboneShared prefix: the reference
+    normalises the raw observations and runs the prefix on the result
+    (rollouts.py:838-840, actor_critic.py:226-229).  The fused rollout kernel
+    normalises what it multiplies (the prefix's output), so init_training
+    routes this policy to the torch path, which keeps the reference's order.
+    Two updates against the oracle: the stored observations are the
+    normalised RAW observations (bit-exact given the estimates), the
+    estimates follow ppo_ref.ema_* (1e-5 relative), and the stored values
+    are the critic of prefix(normalised observations) (oracle forward)."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from tests.test_gpu_generic import _shared_mlp_flat
+    decay, N, H, T = 0.99, 64, 64, 32
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=14, device=gpu)
+    halve = lambda x, train=False: x * 0.5  # noqa: E731
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneShared(prefix=halve, encoder=ml.BackboneEncoder(net=MLP(H, 2, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DenseLayerCritic(dt))
+    pol = ml.Policy(actor_critic=ac, obs_preprocess=ml.ObservationsEMANormalizer.create(decay, dt))
+    cfg = make_cfg(dt, N=N, H=H)
+    mgr = ml.init_training(gpu, cfg, AffineEnv(env).sim_fns(), pol, use_graph=False)
+    ps = mgr.state.policy_states
+    assert getattr(ps, "generic", False)
+    oenv = onat.Env(env.N, env.D, env.k0, env.k1, 0)
+    oenv.reset()
+    oenv.obs = (oenv.obs * np.float32(SCALE) + np.float32(SHIFT)).astype(np.float32)
+    est = ref.ema_init(64)
+    for it in range(2):
+        p0, lay = _shared_mlp_flat(ps, 64, H, 2)
+        mgr.update_iter()
+        torch.cuda.synchronize()
+        s = mgr.rollout_mgr.store
+        step = oenv.step
+
+        def affine_step(a, _step=step):
+            o, r, d = _step(a)
+            o = (o * np.float32(SCALE) + np.float32(SHIFT)).astype(np.float32)
+            oenv.obs = o
+            return o, r, d
+        oenv.step = affine_step
+        ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, it * T, mode="f32",
+                            gamma=cfg.gamma, actions_override=s.actions.cpu().numpy(),
+                            obs_norm=(est, decay, 1e-5))
+        oenv.step = step
+        assert np.array_equal(s.obs.float().cpu().numpy(), ro["obs"]), f"update {it}"
+        _, V, _ = ref.forward(ref.unflatten(p0, lay), ro["obs"].reshape(T * N, 64) * 0.5, "f32")
+        np.testing.assert_allclose(s.values.cpu().numpy().reshape(-1), V, rtol=1e-4, atol=1e-4)
+        est = ro["obs_est"]
+        got = ps.obs_pre_state
+        for k in ("mu", "sigma"):
+            np.testing.assert_allclose(got[k].cpu().numpy(), est[k], rtol=1e-5, atol=1e-6)
