@@ -359,8 +359,8 @@ typedef struct mlearn_ppo_hparams {
                                               step: 0 = the library's choice (the row-split
                                               kernel where it applies: bf16, hidden 256,
                                               2 layers, scalar critic, head width 32,
-                                              obs_dim 64, rows a
-                                              multiple of 256 and >= 65536; else the
+                                              obs_dim 64, at most 7 action groups,
+                                              rows a multiple of 256 and >= 65536; else the
                                               feature-split kernel), 1 = the feature-split
                                               kernel, 2 = the row-split kernel (EINVAL
                                               where it does not apply).  Same inputs and

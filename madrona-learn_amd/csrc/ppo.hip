@@ -904,10 +904,10 @@ __device__ inline void colsum_block(const WsK& ws, int bx, int c) {
     if (col >= ws.CP) return;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int t = c;
-    for (; t + 7 * kColChunks < ws.ntiles; t += 8 * kColChunks)
+    for (; t + 7 * kColChunks < ws.ncp; t += 8 * kColChunks)
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc[u] += ws.colpart[(int64_t)(t + u * kColChunks) * ws.CP + col];
-    for (int u = 0; t < ws.ntiles; t += kColChunks, ++u) acc[u] += ws.colpart[(int64_t)t * ws.CP + col];
+    for (int u = 0; t < ws.ncp; t += kColChunks, ++u) acc[u] += ws.colpart[(int64_t)t * ws.CP + col];
     ws.colpart2[(int64_t)c * ws.CP + col] =
         ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
@@ -1201,8 +1201,9 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     ML_REQUIRE(h.step_kernel >= 0 && h.step_kernel <= 2, "ppo: step_kernel %d", h.step_kernel);
     ML_REQUIRE(h.step_kernel != 2 || rows16,
                "ppo: step_kernel 2 (row-split) needs bf16, hidden 256, 2 layers, a scalar critic, "
-               "head width 32, obs_dim 64 and >= 65536 rows in multiples of 256");
+               "head width 32, obs_dim 64, <= 7 action groups and >= 65536 rows in multiples of 256");
     if (rows16 && h.step_kernel != 1) {
+        ws.ncp = 2 * ws.ntiles;  // one column-partials row per 16-row tile
         launch_rows16(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
     } else {
         switch (p.num_layers) {

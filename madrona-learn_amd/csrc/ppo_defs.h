@@ -80,6 +80,7 @@ struct WsK {
     int64_t rps[kMaxJobs];  // rows per split
     int64_t Mp;
     int ntiles;                         // Mp / 32
+    int ncp;                            // colpart rows written: ntiles, 2 ntiles (row-split step)
     int CP;                             // L*2*H + 32
     uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
@@ -163,6 +164,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     WsK w{};
     w.Mp = Mp;
     w.ntiles = (int)tiles;
+    w.ncp = (int)tiles;
     // column partials: LayerNorm [L][2][H], head bias [32], (LSTM) bias [4H]
     const int HC = head_cols(p);
     w.CP = L * 2 * H + HC + (lstm ? 4 * H : 0);
@@ -172,7 +174,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
         w.dz[l] = take(Mp * H * es);
     }
     w.dhead = take(Mp * HC * es);
-    w.colpart = (float*)take(tiles * w.CP * sizeof(float));
+    w.colpart = (float*)take(2 * tiles * w.CP * sizeof(float));  // (16-row tiles: row-split)
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
     w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
     int64_t so = 0;
@@ -311,12 +313,28 @@ __device__ inline void loss_group(const HpK& hp, S* lg, int nb, int a, float old
 // zeroes columns A+1..HC-1.
 // vn (normalize_values, may be null) = {mu', inv_sigma'} after this
 // minibatch's update and {mu, sigma} before it (mlearn_value_norm_chain).
+// The value normaliser's four values held by the caller (von = vn != null).
+struct VnVals {
+    bool on;
+    float v[4];
+};
+template <typename S>
+__device__ inline void loss_value(const HpK& hp, S* lg, int A, int HC, float R, float ov,
+                                  LossAcc& m, const VnVals& vn);
 template <typename S>
 __device__ inline void loss_value(const HpK& hp, S* lg, int A, int HC, float R, float ov,
                                   LossAcc& m, const float* vn) {
+    VnVals w{vn != nullptr, {0.f, 0.f, 0.f, 0.f}};
+    if (vn)
+        for (int i = 0; i < 4; ++i) w.v[i] = vn[i];
+    loss_value(hp, lg, A, HC, R, ov, m, w);
+}
+template <typename S>
+__device__ inline void loss_value(const HpK& hp, S* lg, int A, int HC, float R, float ov,
+                                  LossAcc& m, const VnVals& vn) {
     const float V = to_f32(lg[A]);
     // target: the return normalised with the updated estimates (ppo.py:209-211)
-    const float tgt = vn ? (R - vn[0]) * vn[1] : R;
+    const float tgt = vn.on ? (R - vn.v[0]) * vn.v[1] : R;
     float vpred = V, dvp = 1.f;
     if (hp.clip_vl) {  // ppo.py:197-203
         const float vlo = ov - hp.clip, vhi = ov + hp.clip;
@@ -338,7 +356,7 @@ __device__ inline void loss_value(const HpK& hp, S* lg, int A, int HC, float R, 
     lg[A] = cvt<S>(hp.vcoef * hp.inv_s * dvl * dvp * hp.loss_scale);
     for (int j = A + 1; j < HC; ++j) lg[j] = cvt<S>(0.f);
     // value error: the critic inverted with the previous estimates (ppo.py:193-195)
-    const float verr = fabsf((vn ? V * vn[3] + vn[2] : V) - R);
+    const float verr = fabsf((vn.on ? V * vn.v[3] + vn.v[2] : V) - R);
     m.svl += vl;
     m.qvl += vl * vl;
     m.mnvl = fminf(m.mnvl, vl);

@@ -40,6 +40,7 @@ constexpr int kR16HC = MLEARN_HEAD_COLS;
 constexpr int kR16D = 64;            // observation width (the first layer's K)
 constexpr int kR16LGS = 40;          // logits scratch row stride (bf16; 80-B rows)
 constexpr int kR16Ring = 6;          // LDS A fragments in flight per product
+constexpr int kR16Ring0 = 16;        // first-layer (L2) A fragments in flight
 // LDS: W1 image [256 rows = out][512 B], head image [32 rows = col][512 B],
 // LayerNorm scale/bias [2][2][256] f32, head bias [32] f32, per-wave logits
 // scratch [8][16][kR16LGS] bf16, the action groups' logit offsets, entropy
@@ -97,12 +98,15 @@ __device__ inline bf16x8 r16_row_frag(const char* img, int n, int s, int g) {
 // r0 + 4g + j (j < 4) and r0 + 16 + 4g + (j - 4) with r0 = 32s (hidden
 // operands), or rows 8g + j with `step8` (the head's 32 columns, one k-step).
 __device__ inline bf16x8 r16_tr_frag(const char* img, int rlo, int rhi, int b, int lane) {
+    // (rlo, rhi split into a multiple of 16 rows, an instruction offset, and
+    // a lane part that alone sets the swizzle: one block-dependent address
+    // per lane and block)
     const int q = (lane >> 2) & 3, p = lane & 3;
     typedef __attribute__((address_space(3))) short4r* lp;
     const short4r lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lp)(img + r16_off(rlo + q, 4 * b + p)));
+        (lp)(img + (rlo & ~15) * 512 + r16_off((rlo & 15) + q, 4 * b + p)));
     const short4r hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lp)(img + r16_off(rhi + q, 4 * b + p)));
+        (lp)(img + (rhi & ~15) * 512 + r16_off((rhi & 15) + q, 4 * b + p)));
     typedef short short8r __attribute__((ext_vector_type(8)));
     const short8r v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
@@ -143,6 +147,32 @@ __device__ inline void r16_mm(f32x4 (&acc)[NBO], LDA lda, BF bfrag) {
         acc[i % NBO] = mma16(a, bfr, acc[i % NBO]);
         __builtin_amdgcn_sched_barrier(0);
         if ((i + 1) % NBO == 0 && i + 1 < N) bfr = bfrag((i + 1) / NBO);
+    }
+}
+
+// As r16_mm, but block-pair-major: blocks 2p, 2p+1 take all NS k-steps
+// (alternating, two independent accumulator chains) before the next pair, so
+// a fragment address that depends on the block (the transposed reads) is
+// formed once per block instead of once per (block, k-step); B fragments
+// come from registers.
+template <int NBO, int NS, int RING, typename LDA, typename BF>
+__device__ inline void r16_mm_bm(f32x4 (&acc)[NBO], LDA lda, BF bfrag) {
+    static_assert(NBO % 2 == 0, "block pairs");
+    constexpr int N = NS * NBO;
+    constexpr int RG = RING < N ? RING : N;
+    auto jof = [](int i) { return 2 * (i / (2 * NS)) + (i & 1); };
+    auto sof = [](int i) { return (i >> 1) % NS; };
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 ra[RG];
+#pragma unroll
+    for (int i = 0; i < RG; ++i) ra[i] = lda(jof(i), sof(i));
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bf16x8 a = ra[i % RG];
+        if (i + RG < N) ra[i % RG] = lda(jof(i + RG), sof(i + RG));
+        __builtin_amdgcn_sched_barrier(0);
+        acc[jof(i)] = mma16(a, bfrag(sof(i)), acc[jof(i)]);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -196,28 +226,59 @@ __device__ inline void r16_store_rows(bf16* rowp, uint32_t (&w)[kR16NB][2], int 
             w[2 * c + 1][k] = v[1];
         }
         const int blk = 2 * c + (g & 1);
+#ifdef R16_ABL_NOSTORE
+        if ((uintptr_t)rowp == 1)
+#endif
         *(u4r*)(rowp + 16 * blk + 8 * (g >> 1)) =
             u4r{w[2 * c][0], w[2 * c][1], w[2 * c + 1][0], w[2 * c + 1][1]};
     }
 }
 
-// Sum of 16 values over the 16 lanes of a DPP row (the 16 rows of a tile):
-// recursive halving (partners lane ^ 1, ^ 2, ^ 8, ^ 4); lane returns the total
-// of value col_sum16_index(lane & 15).
-__device__ inline float r16_rowsum16(float (&v)[16], int lane) {
-    bfly<1, 16>(v, lane);
-    bfly<2, 8>(v, lane);
-    bfly<8, 4>(v, lane);
-    const bool hi = (lane & 4) != 0;
-    const float a = v[0], b = v[1];
-    const float keep = hi ? b : a, send = hi ? a : b;
-    const float r4 = ML_DPP(send, 0x124), r12 = ML_DPP(send, 0x12C);
-    return keep + (hi ? r4 : r12);
+// One transpose-reduce level at lane distance D = 8 or 4 within a DPP row:
+// lanes with bit D clear return a + (partner's a), the others b + (partner's
+// b) -- two bank-masked v_add_f32_dpp writing complementary lane sets (no
+// selects).  row_ror:N reads lane i - N of the row, so distance-4 lanes with
+// bit 2 clear (banks 0, 2) read through ror:12 (= i + 4).
+template <int D> __device__ inline float r16_pair_dpp(float a, float b) {
+    float r;
+    if constexpr (D == 8)
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+            "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+            : "=&v"(r)
+            : "v"(a), "v"(b));
+    else
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_add_f32_dpp %0, %1, %1 row_ror:12 row_mask:0xf bank_mask:0x5\n\t"
+            "v_add_f32_dpp %0, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xa"
+            : "=&v"(r)
+            : "v"(a), "v"(b));
+    return r;
+}
+
+// Sum of 16 values v over the 16 lanes of a DPP row (the 16 rows of a tile)
+// by recursive halving, partners lane ^ 8 (done by the caller:
+// w[i] = r16_pair_dpp<8>(v[i], v[i + 8])), ^ 4 (bank-masked), then ^ 2, ^ 1
+// (select + DPP add); lane r returns the total of value index r.
+__device__ inline float r16_rowsum8(const float (&w)[8], int lane) {
+    float x[4], y[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = r16_pair_dpp<4>(w[i], w[i + 4]);
+    const bool h1 = (lane & 2) != 0, h0 = (lane & 1) != 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float keep = h1 ? x[i + 2] : x[i], send = h1 ? x[i] : x[i + 2];
+        y[i] = keep + xlane<2>(send);
+    }
+    const float keep = h0 ? y[1] : y[0], send = h0 ? y[0] : y[1];
+    return keep + xlane<1>(send);
 }
 
 // LayerNorm apply + ReLU, rounded to the compute dtype: packed Z -> packed
 // A (the next product's operand).
-__device__ inline void r16_ln_apply(const uint32_t (&zw)[kR16NB][2], float mean, float rstd,
+__device__ inline void r16_ln_apply(uint32_t (&zw)[kR16NB][2], float mean, float rstd,
                                     const float* gm, int g, uint32_t (&aw)[kR16NB][2]) {
     const f2v m2 = {mean, mean}, r2 = {rstd, rstd};
 #pragma unroll
@@ -229,13 +290,15 @@ __device__ inline void r16_ln_apply(const uint32_t (&zw)[kR16NB][2], float mean,
         // scale / bias are otherwise issued up front, 128 registers)
         const int f0 = r16_late(16 * b + 4 * g);
         const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
-        // (words read through opaque copies: the statistics pass's unpacked
-        // values would otherwise be CSE'd into this one and held live, 64
-        // registers across the layer's whole product)
-        const f2v y0 = __builtin_elementwise_fma(up_bf16(r16_late(zw[b][0])) - m2,
-                                                 r2 * f2v{G.x, G.y}, f2v{B.x, B.y});
-        const f2v y1 = __builtin_elementwise_fma(up_bf16(r16_late(zw[b][1])) - m2,
-                                                 r2 * f2v{G.z, G.w}, f2v{B.z, B.w});
+        // (words made opaque in place: the statistics pass's unpacked values
+        // would otherwise be CSE'd into this one and held live, 64 registers
+        // across the layer's whole product)
+        zw[b][0] = r16_late(zw[b][0]);
+        zw[b][1] = r16_late(zw[b][1]);
+        const f2v y0 = __builtin_elementwise_fma(up_bf16(zw[b][0]) - m2, r2 * f2v{G.x, G.y},
+                                                 f2v{B.x, B.y});
+        const f2v y1 = __builtin_elementwise_fma(up_bf16(zw[b][1]) - m2, r2 * f2v{G.z, G.w},
+                                                 f2v{B.z, B.w});
         aw[b][0] = pk_bf16(fmaxf(y0.x, 0.f), fmaxf(y0.y, 0.f));
         aw[b][1] = pk_bf16(fmaxf(y1.x, 0.f), fmaxf(y1.y, 0.f));
     }
@@ -256,41 +319,59 @@ __device__ inline float r16_dy(float z, float mean, float rstd, float gam, float
 // gradients over the tile's 16 rows, and the row sums su (u = dy gamma) and
 // sv (u x_hat) over its 16 features per lane; u kept in acc when STORE_U.
 template <bool STORE_U>
-__device__ inline void r16_bwd_quad(f32x4* acc4, const uint32_t (&zw)[kR16NB][2], int qd,
+__device__ inline void r16_bwd_quad(f32x4* acc4, uint32_t (&zw)[kR16NB][2], int qd,
                                     float mean, float rstd, const float* gm, int g, int lane,
-                                    bool live, float& su, float& sv, float& cbq, float& cgq) {
-    float pb[16], pg[16];
+                                    bool live, float& su, float& sv, float* cpl) {
+    // blocks in the order 0, 2, 1, 3: the first transpose-reduce level pairs
+    // value j (block j / 4) with j + 8, so it runs after each block pair and
+    // 8 instead of 16 values per sum are live at a time
+    float wb[8], wg[8];
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
+    for (int hp = 0; hp < 2; ++hp) {
+        float pb[8], pg[8];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int bb = hp + 2 * k;
+            __builtin_amdgcn_sched_barrier(0);
+            const int b = 4 * qd + bb;
+            const int f0 = r16_late(16 * b + 4 * g);
+            const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
+            const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
+            zw[b][0] = r16_late(zw[b][0]);
+            zw[b][1] = r16_late(zw[b][1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float xh;
+                const float z = up_bf16(zw[b][i >> 1])[i & 1];
+                const float dy = r16_dy(z, mean, rstd, gv[i], bv[i], acc4[bb][i], live, xh);
+                const float u = dy * gv[i];
+                su += u;
+                sv = __builtin_fmaf(u, xh, sv);
+                if (STORE_U) acc4[bb][i] = u;
+                pb[4 * k + i] = dy;
+                pg[4 * k + i] = dy * xh;
+            }
+        }
         __builtin_amdgcn_sched_barrier(0);
-        const int b = 4 * qd + bb;
-        const int f0 = r16_late(16 * b + 4 * g);
-        const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
-        const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float xh;
-            const float z = up_bf16(r16_late(zw[b][i >> 1]))[i & 1];
-            const float dy = r16_dy(z, mean, rstd, gv[i], bv[i], acc4[bb][i], live, xh);
-            const float u = dy * gv[i];
-            su += u;
-            sv = __builtin_fmaf(u, xh, sv);
-            if (STORE_U) acc4[bb][i] = u;
-            pb[4 * bb + i] = dy;
-            pg[4 * bb + i] = dy * xh;
+            wb[4 * hp + i] = r16_pair_dpp<8>(pb[i], pb[4 + i]);
+            wg[4 * hp + i] = r16_pair_dpp<8>(pg[i], pg[4 + i]);
         }
     }
-    __builtin_amdgcn_sched_barrier(0);
-    cbq += r16_rowsum16(pb, lane);
-    cgq += r16_rowsum16(pg, lane);
+    // lane (r, g) holds the column total of feature 16 (4 qd + r / 4) + 4g + r % 4
+    const int r = lane & 15, f = 16 * (4 * qd + (r >> 2)) + 4 * g + (r & 3);
+    cpl[f] = r16_rowsum8(wb, lane);
+    cpl[kR16H + f] = r16_rowsum8(wg, lane);
 }
 
 // dZ = rstd (u - mean(u) - x_hat mean(u x_hat)) of one block from u
-__device__ inline void r16_dz_block(const f32x4& u, const uint32_t (&zwb)[2], float mean,
+__device__ inline void r16_dz_block(const f32x4& u, uint32_t (&zwb)[2], float mean,
                                     float rstd, float ca, float cbc, uint32_t (&dzb)[2]) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const f2v zc = up_bf16(r16_late(zwb[k])) - f2v{mean, mean};
+        zwb[k] = r16_late(zwb[k]);
+        const f2v zc = up_bf16(zwb[k]) - f2v{mean, mean};
         const f2v d = f2v{rstd, rstd} * f2v{u[2 * k], u[2 * k + 1]} +
                       (f2v{ca, ca} * zc + f2v{cbc, cbc});
         dzb[k] = pk_bf16(d.x, d.y);
@@ -298,10 +379,9 @@ __device__ inline void r16_dz_block(const f32x4& u, const uint32_t (&zwb)[2], fl
 }
 
 // Layer backward with d loss / d A held in full (acc, 64 registers): one pass.
-__device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], const uint32_t (&zw)[kR16NB][2],
+__device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2],
                                   float mean, float rstd, const float* gm, int g, int lane,
-                                  bool live, uint32_t (&dzw)[kR16NB][2], float (&cb)[4],
-                                  float (&cg)[4]) {
+                                  bool live, uint32_t (&dzw)[kR16NB][2], float* cpl) {
     // opaque copies (of the statistics and of every Z word read): the
     // forward's unpacked Z values / (z - mean) pairs are otherwise CSE'd into
     // this pass and held live from the forward LayerNorm
@@ -310,8 +390,7 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], const uint32_t (&zw)[kR1
     float su = 0.f, sv = 0.f;
 #pragma unroll
     for (int qd = 0; qd < kR16NB / 4; ++qd)
-        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cb[qd],
-                           cg[qd]);
+        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cpl);
     su = add_xor32(add_xor16(su));
     sv = add_xor32(add_xor16(sv));
     const float invH = 1.0f / (float)kR16H;
@@ -325,9 +404,9 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], const uint32_t (&zw)[kR1
 // product run again in the second pass (same MFMAs, same bits) instead of
 // holding all 64 values.
 template <int NS, typename LDA, typename BF>
-__device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, const uint32_t (&zw)[kR16NB][2], float mean,
+__device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2], float mean,
                                    float rstd, const float* gm, int g, int lane, bool live,
-                                   uint32_t (&dzw)[kR16NB][2], float (&cb)[4], float (&cg)[4]) {
+                                   uint32_t (&dzw)[kR16NB][2], float* cpl) {
     mean = r16_late(mean);
     rstd = r16_late(rstd);
     float su = 0.f, sv = 0.f;
@@ -340,7 +419,7 @@ __device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, const uint32_t (&zw)[kR16N
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
             r16_bwd_quad<false>(acc + 4 * qh, zw, 2 * h + qh, mean, rstd, gm, g, lane, live, su,
-                                sv, cb[2 * h + qh], cg[2 * h + qh]);
+                                sv, cpl);
     }
     su = add_xor32(add_xor16(su));
     sv = add_xor32(add_xor16(sv));
@@ -360,10 +439,12 @@ __device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, const uint32_t (&zw)[kR16N
             const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
             const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
             f32x4 u;
+            zw[b][0] = r16_late(zw[b][0]);
+            zw[b][1] = r16_late(zw[b][1]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float xh;
-                const float z = up_bf16(r16_late(zw[b][i >> 1]))[i & 1];
+                const float z = up_bf16(zw[b][i >> 1])[i & 1];
                 u[i] = r16_dy(z, mean, rstd, gv[i], bv[i], acc[j][i], live, xh) * gv[i];
             }
             r16_dz_block(u, zw[b], mean, rstd, ca, cbc, dzw[b]);
@@ -371,10 +452,40 @@ __device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, const uint32_t (&zw)[kR16N
     }
 }
 
+// Division by a launch constant d (rows by the minibatch's sequence count,
+// sequence ids by the policy's env count): q = (mulhi(n, mag) + n) >> sh,
+// exact for n < 2^31 (magic from r16_magic on the host).
+struct R16Div {
+    uint32_t mb_mag, n_mag;
+    int mb_sh, n_sh;
+};
+__device__ inline uint32_t r16_udiv(uint32_t n, uint32_t mag, int sh) {
+    return (__umulhi(n, mag) + n) >> sh;
+}
+
+// diagnostic builds only (ML_STAMPS): s_memtime per phase held in SGPRs and
+// written once per tile, so the stamps leave the VGPR allocation alone
+#ifdef ML_STAMPS
+#define R16_STAMP(i) (r16_st[i] = __builtin_amdgcn_s_memtime())
+#define R16_STAMPS_OUT()                                                              \
+    do {                                                                              \
+        if (ws.stamps && (tid & 63) == 0)                                             \
+            for (int i_ = 0; i_ < 13; ++i_)                                           \
+                ws.stamps[((int64_t)ptile * kR16Tiles + tt) * 16 + i_] = r16_st[i_]; \
+    } while (0)
+#else
+#define R16_STAMP(i) \
+    do {             \
+    } while (0)
+#define R16_STAMPS_OUT() \
+    do {                 \
+    } while (0)
+#endif
+
 template <bool METRICS>
 __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void ppo_rows16_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
-    const float* __restrict__ adv_st, HpK hp, WsK ws) {
+    const float* __restrict__ adv_st, HpK hp, WsK ws, R16Div dv) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* w1img = smem + kR16OffW1;
     char* whimg = smem + kR16OffWh;
@@ -433,27 +544,69 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
     const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
 
+#ifdef R16_PRIO
+    if (wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef R16_STAGGER
+    if (wave >= kR16Waves / 2)
+        for (int i = 0; i < R16_STAGGER; ++i) __builtin_amdgcn_s_sleep(32);
+#endif
     const int ptile = (int)blockIdx.x * kR16Waves + wave;  // 32-row partials row (= ppo_step tile)
     const float as0 = adv_st[0], as1 = adv_st[1];
-    const float* vn = hp.norm_vals ? adv_st + 2 : nullptr;
+    // value normaliser values, loaded once (a load in the loss loop waits on
+    // the tile's stores)
+    VnVals vn{hp.norm_vals != 0, {0.f, 0.f, 0.f, 0.f}};
+    if (hp.norm_vals)
+        for (int i = 0; i < 4; ++i) vn.v[i] = adv_st[2 + i];
     LossAcc m;
     bool did = false;
-    float cb[2][4] = {}, cg[2][4] = {};  // LayerNorm bias / scale column sums, per layer
-    float hbsum = 0.f;                   // head-bias column sum (lane = column < 32)
     uint32_t dz0w[kR16NB][2];            // layer-0 dZ of the previous tile (stored late)
     int64_t prev_row = -1;
     const int ntask = 16 * (K + 1);
+    // minibatch row -> (time step, sequence slot); the slot's sequence id is
+    // loaded one tile ahead (issued before, and waited on before, the tile's
+    // stores: a load issued behind stores waits for them, vmcnt being in order)
+    auto slot_of = [&](int64_t rw, uint32_t& tl) {
+        const uint32_t f = (uint32_t)rw;
+        tl = r16_udiv(f, dv.mb_mag, dv.mb_sh);
+        return f - tl * (uint32_t)mb;
+    };
+    // store row of minibatch row rw from its slot's sequence id (store_row,
+    // ppo_defs.h); padding rows (rw >= M) get row 0 (loaded, never used)
+    auto srow_of = [&](int64_t rw, uint32_t seq) -> int64_t {
+        uint32_t tl;
+        (void)slot_of(rw, tl);
+        const uint32_t c = r16_udiv(seq, dv.n_mag, dv.n_sh), b = seq - c * (uint32_t)ro.N;
+        return rw < M ? ((int64_t)c * ro.bptt + tl) * ro.ld + b : 0;
+    };
+    int64_t sr_n;  // store row of this lane's row in the next tile
+    {
+        uint32_t tl;
+        const int64_t rw = (int64_t)ptile * 32 + (tid & 15);
+        sr_n = srow_of(rw, (uint32_t)mb_seq[slot_of(rw, tl)]);
+    }
 
 #pragma clang loop unroll(disable)
     for (int tt = 0; tt < kR16Tiles; ++tt) {
         // the lane index through an opaque copy per tile: otherwise every
         // lane-derived LDS / weight address of the body is hoisted out of the
         // tile loop and held live across it (rollout kernel)
+#ifdef ML_STAMPS
+        uint64_t r16_st[13];
+#endif
+        R16_STAMP(0);
         const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
         const int64_t row0 = (int64_t)ptile * 32 + 16 * tt;
         const int64_t row = row0 + r;
         const bool live = row < M;
-        const int64_t sr = live ? store_row(ro, mb_seq, mb, row) : 0;
+        // (sr_n is VALU-written: reading it here needs no vmcnt wait, which the
+        // loop header would otherwise take in full, stores included)
+        const int64_t sr = sr_n;
+        uint32_t seq_n = 0;
+        if (tt + 1 < kR16Tiles) {
+            uint32_t tl;
+            seq_n = (uint32_t)mb_seq[slot_of(row + 16, tl)];
+        }
         // ---- layer 0: X_0 rows from the store (natural k order), W_0 from its
         // fragment-order image in L2 (P.wt[0], K = D, natural k): element
         // (n, k = 32s + 8g) at ((n/32 * D/16 + 2s + g/2) * 64 + n%32 + 32(g&1)) * 8
@@ -461,7 +614,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         const bf16* orow = (const bf16*)ro.obs + sr * D;
 #pragma unroll
         for (int s = 0; s < DS; ++s)
-            xf[s] = live ? *(const bf16x8*)(orow + 32 * s + 8 * g) : RT<bf16>::zero();
+            xf[s] = *(const bf16x8*)(orow + 32 * s + 8 * g);  // (padding rows: row 0)
         // (each use of the first layer takes its own opaque copy of the lane: the
         // forward's 16 fragment addresses are otherwise CSE'd into the
         // backward's recompute and held live across the tile)
@@ -475,47 +628,69 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
                 return *(const bf16x8*)(w0 + idx);
             };
         };
+        // this lane's first two loss tasks (row r, group (lane + 64u) >> 4; group
+        // K = the value): raw inputs loaded here, straight-line from valid
+        // addresses (sr = 0 on padding rows), and combined after the first
+        // layer (a branch or an early use here would wait on the previous
+        // tile's stores, vmcnt being in order)
+        const bool has_ret = ro.ret != nullptr, has_val = ro.values != nullptr;
+        float t_adv = ro.adv[sr];
+        float rv = (has_ret ? ro.ret : ro.adv)[sr], vv = (has_val ? ro.values : ro.adv)[sr];
+        int ract[2];
+        float rlp[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int grp = (lane + 64 * u) >> 4;
+            const int ga = grp < K ? grp : K - 1;
+            ract[u] = ro.actions[sr * K + ga];
+            rlp[u] = ro.logp[sr * K + ga];
+        }
         auto bf0 = [&](int s) { return xf[s]; };
-        uint32_t zw[kR16NB][2], aw[kR16NB][2];
-        float mean, rstd;
-        r16_fwd_layer<DS, 8>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
+        // Z_0 (packed) and its statistics stay live to the layer-0 backward
+        uint32_t zw0[kR16NB][2], zw[kR16NB][2], aw[kR16NB][2];
+        float mean0, rstd0, mean, rstd;
+        r16_fwd_layer<DS, kR16Ring0>(lda0(r16_late(lane)), bf0, zw0, mean0, rstd0);
+        // (the tile's loads are consumed here, ahead of its first stores)
+        sr_n = srow_of(row + 16, r16_late(seq_n));
+        // (action | return bits, old log-prob | old value) per task
+        uint32_t t_a[2];
+        float t_b[2];
+        {
+            t_adv = r16_late(t_adv);
+            rv = r16_late(rv);
+            vv = r16_late(vv);
+            const float retv = has_ret ? rv : t_adv + vv;  // ret_at (ppo_defs.h)
+            const float ov = has_val ? vv : 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int grp = (lane + 64 * u) >> 4;
+                t_a[u] = grp < K ? (uint32_t)r16_late(ract[u]) : __builtin_bit_cast(uint32_t, retv);
+                t_b[u] = grp < K ? r16_late(rlp[u]) : ov;
+            }
+        }
+        R16_STAMP(1);
         // X_0 rows for the weight gradient (16 bytes per lane and k-step)
         {
             bf16* xrow = (bf16*)ws.x0 + r16_late(row) * D;
 #pragma unroll
-            for (int s = 0; s < DS; ++s) *(bf16x8*)(xrow + 32 * s + 8 * g) = xf[s];
+            for (int s = 0; s < DS; ++s)
+#ifdef R16_ABL_NOSTORE
+                if ((uintptr_t)xrow == 1)
+#endif
+                *(bf16x8*)(xrow + 32 * s + 8 * g) = xf[s];
         }
         // the previous tile's layer-0 dZ rows go out behind this tile's loads
         if (tt > 0) r16_store_rows((bf16*)ws.dz[0] + r16_late(prev_row) * kR16H, dz0w, g);
-        r16_ln_apply(zw, mean, rstd, gb, g, aw);
-        // this lane's first two loss tasks (row task & 15, group task >> 4;
-        // group K = the value), in flight under the layer-1 product
-        int t_act[2] = {0, 0};
-        float t_lp[2] = {0.f, 0.f}, t_adv[2] = {0.f, 0.f}, t_ret[2] = {0.f, 0.f},
-              t_val[2] = {0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int task = lane + 64 * u;
-            const int64_t f = row0 + (task & 15);
-            const int grp = task >> 4;
-            if (task < ntask && f < M) {
-                const int64_t q = store_row(ro, mb_seq, mb, f);
-                t_adv[u] = ro.adv[q];
-                if (grp < K) {
-                    t_act[u] = ro.actions[q * K + grp];
-                    t_lp[u] = ro.logp[q * K + grp];
-                } else {
-                    t_ret[u] = ret_at(ro, q);
-                    if (ro.values) t_val[u] = ro.values[q];
-                }
-            }
-        }
+        r16_ln_apply(zw0, mean0, rstd0, gb, g, aw);
+        R16_STAMP(2);
         // ---- layer 1 (W1 from LDS)
         r16_fwd_layer<kR16KS, kR16Ring>(
             [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
             [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
+        R16_STAMP(3);
         r16_store_rows((bf16*)ws.a[0] + r16_late(row) * kR16H, aw, g);  // A_0 rows
         r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
+        R16_STAMP(4);
         // ---- heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
         f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
         r16_mm<2, kR16KS, 4>(ha, [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
@@ -533,35 +708,19 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
             }
         }
         wave_lds_sync();
+        R16_STAMP(5);
         // ---- loss: one (row, group | value) task per lane and pass (ppo.py:129-262),
         // d loss / d logits written over the logits (bf16: every consumer rounds them)
-        for (int task = lane, u = 0; task < ntask; task += 64, ++u) {
+        // one task: padding rows get zero d logits
+        auto loss_task = [&](int task, int act, float olp, float adv, float ret, float oval) {
             const int rr = task & 15, grp = task >> 4;
-            did = true;
             bf16* lr = lgs + rr * kR16LGS;
-            const int64_t f = row0 + rr;
-            if (f >= M) {  // padding row: zero its d logits
+            if (row0 + rr >= M) {
                 if (grp < K)
                     for (int j = t_off[grp]; j < t_off[grp + 1]; ++j) lr[j] = (bf16)0.f;
                 else
                     for (int j = P.A; j < kR16HC; ++j) lr[j] = (bf16)0.f;
-                continue;
-            }
-            int act;
-            float olp, adv, ret, oval;
-            if (u < 2) {
-                act = u == 0 ? t_act[0] : t_act[1];
-                olp = u == 0 ? t_lp[0] : t_lp[1];
-                adv = u == 0 ? t_adv[0] : t_adv[1];
-                ret = u == 0 ? t_ret[0] : t_ret[1];
-                oval = u == 0 ? t_val[0] : t_val[1];
-            } else {
-                const int64_t q = store_row(ro, mb_seq, mb, f);
-                adv = ro.adv[q];
-                act = grp < K ? ro.actions[q * K + grp] : 0;
-                olp = grp < K ? ro.logp[q * K + grp] : 0.f;
-                ret = grp < K ? 0.f : ret_at(ro, q);
-                oval = (grp < K || !ro.values) ? 0.f : ro.values[q];
+                return;
             }
             if (grp < K) {
                 if (hp.norm_adv) adv = (adv - as0) * as1;
@@ -571,60 +730,76 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
             } else {
                 loss_value(hp, lr, P.A, kR16HC, ret, oval, m, vn);
             }
+        };
+#ifdef R16_ABL_NOLOSS
+        if (hp.clip > -1e30f)
+#endif
+        {
+            // the tasks' inputs are registers loaded at the tile's start (K + 1 <= 8
+            // groups: two tasks per lane; no load in this loop, whose waits
+            // would cover the tile's stores)
+#pragma clang loop unroll(disable)
+            for (int task = lane, u = 0; task < ntask; task += 64, ++u) {
+                did = true;
+                const uint32_t a = u == 0 ? t_a[0] : t_a[1];
+                const float b = u == 0 ? t_b[0] : t_b[1];
+                loss_task(task, (int)a, b, t_adv, __builtin_bit_cast(float, a), b);
+            }
         }
         wave_lds_sync();
+        R16_STAMP(6);
         // ---- d head: B operand of the head backward (cols 8g .. 8g+7 of row r),
         // row-major store, head-bias column sums
         const bf16x8 dh = *(const bf16x8*)(lgs + r * kR16LGS + 8 * g);
+#ifdef R16_ABL_NOSTORE
+        if ((uintptr_t)ws.dhead == 1)
+#endif
         *(bf16x8*)((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g) = dh;
+        // column partials of this 16-row tile (colpart row 2 ptile + tt, WsK::ncp):
+        // head bias here, LayerNorm bias / scale in the layer backwards
+        float* cprow = ws.colpart + ((int64_t)ptile * kR16Tiles + tt) * ws.CP;
         if (lane < kR16HC) {
+            float hbs = 0.f;
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) hbsum += to_f32(lgs[rr * kR16LGS + lane]);
+            for (int rr = 0; rr < 16; ++rr) hbs += to_f32(lgs[rr * kR16LGS + lane]);
+            cprow[2 * 2 * kR16H + lane] = hbs;
         }
         // ---- layer 1 backward: dA_1^T = Wh dHead^T (M = hidden unit = image
         // column, K = head column), recomputed per half in the LayerNorm's
         // second pass
+        R16_STAMP(7);
         uint32_t dzw[kR16NB][2];
+#ifdef R16_ABL_NOL1BWD
+        if (hp.clip < -1e30f)
+#endif
         r16_ln_bwd2<1>([&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
                        [&](int) { return dh; }, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw,
-                       cb[1], cg[1]);
+                       cprow + 2 * kR16H);
         // dA_0^T = W1 dZ_1^T: M = input feature (image column), K = output feature
         // (image rows 32s + 4g + j, 32s + 16 + 4g + j)
+        R16_STAMP(8);
         f32x4 acc[kR16NB];
 #pragma unroll
         for (int b = 0; b < kR16NB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-        r16_mm<kR16NB, kR16KS, kR16Ring>(
+        r16_mm_bm<kR16NB, kR16KS, kR16Ring>(
             acc,
             [&](int b, int s) {
                 return r16_tr_frag(w1img, 32 * s + 4 * g, 32 * s + 16 + 4 * g, b, lane);
             },
             [&](int s) { return r16_bfrag(dzw, s); });
+        R16_STAMP(9);
         r16_store_rows((bf16*)ws.dz[1] + r16_late(row) * kR16H, dzw, g);  // dZ_1 rows
-        // ---- layer 0 backward: Z_0 and its statistics again (the same MFMAs in
-        // the same order: the same bits; holding Z_0 across the tile would cost
-        // 32 registers at its peak), then the LayerNorm / ReLU backward
-        r16_fwd_layer<DS, 8>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
-        r16_ln_bwd(acc, zw, mean, rstd, gb, g, lane, live, dz0w, cb[0], cg[0]);
+        R16_STAMP(10);
+        // ---- layer 0 LayerNorm / ReLU backward
+        R16_STAMP(11);
+        r16_ln_bwd(acc, zw0, mean0, rstd0, gb, g, lane, live, dz0w, cprow);
         prev_row = row;
+        R16_STAMP(12);
+        R16_STAMPS_OUT();
     }
     const int lane = tid & 63, r = lane & 15, g = lane >> 4;
     r16_store_rows((bf16*)ws.dz[0] + prev_row * kR16H, dz0w, g);
 
-    // ---- column partials of this wave's 32 rows: LayerNorm bias / scale
-    // (value index col_sum16_index(r) of block quad qd), head bias
-    {
-        float* cp = ws.colpart + (int64_t)ptile * ws.CP;
-        const int vi = col_sum16_index(r);
-#pragma unroll
-        for (int l = 0; l < 2; ++l)
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                const int f = 16 * (4 * qd + (vi >> 2)) + 4 * g + (vi & 3);
-                cp[l * 2 * kR16H + f] = cb[l][qd];
-                cp[l * 2 * kR16H + kR16H + f] = cg[l][qd];
-            }
-        if (lane < kR16HC) cp[2 * 2 * kR16H + lane] = hbsum;
-    }
     // ---- loss metrics of this wave's rows (only the minibatch whose metrics survive)
     if (METRICS) {
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,
@@ -652,13 +827,26 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 // when every CU gets at least one workgroup (one workgroup = 256 rows).
 static bool rows16_eligible(const PolicyK& P, int64_t Mp, int HC, int L, int H, bool bf) {
     return bf && H == kR16H && L == 2 && HC == kR16HC && P.CB == 1 && P.D == kR16D &&
-           P.K + 1 <= 16 && Mp % (32 * kR16Waves) == 0 &&
+           P.K + 1 <= 8 && Mp % (32 * kR16Waves) == 0 &&
            Mp / (32 * kR16Waves) >= 256;
+}
+
+// (mulhi(n, mag) + n) >> sh == n / d for n < 2^31: sh = ceil(log2 d),
+// mag = floor(2^32 (2^sh - d) / d) + 1 (tests/test_gpu_fullsize.py covers
+// d = 4095 and powers of two)
+static void r16_magic(uint32_t d, uint32_t& mag, int& sh) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    mag = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    sh = l;
 }
 
 static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                           int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                           hipStream_t s) {
+    R16Div dv;
+    r16_magic((uint32_t)mb, dv.mb_mag, dv.mb_sh);
+    r16_magic((uint32_t)R.N, dv.n_mag, dv.n_sh);
     static bool attr_set = false;  // once (kept out of graph capture)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<true>,
@@ -670,9 +858,9 @@ static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb
     const int grid = (int)(ws.Mp / (32 * kR16Waves));
     if (hp.metrics)
         hipLaunchKernelGGL(ppo_rows16_kernel<true>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s, P,
-                           R, mb_seq, mb, M, adv_st, hp, ws);
+                           R, mb_seq, mb, M, adv_st, hp, ws, dv);
     else
         hipLaunchKernelGGL(ppo_rows16_kernel<false>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s,
-                           P, R, mb_seq, mb, M, adv_st, hp, ws);
+                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
 }
 

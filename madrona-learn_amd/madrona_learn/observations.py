@@ -17,15 +17,40 @@ from .cfg import canonical_dtype
 from .moving_avg import EMANormalizer
 
 
-def _map_obs(cb, *args):
-    """observations.py:36-57: cb(ob_name, *per-observation args) over the
-    observation names of args[0] (a dict; a bare tensor is one observation
-    named None and maps to a bare result).  The reference's vmap over the
-    policy axis has no counterpart: one policy's state per call."""
-    a0 = args[0]
-    if not isinstance(a0, dict):
-        return cb(None, *args)
-    return {k: cb(k, *[a[k] if isinstance(a, dict) else a for a in args]) for k in a0}
+class _Bare(dict):
+    """The state (or statistics) of a bare, unnamed observation tensor: a dict
+    marked apart from the dict of per-name states a dict of observations
+    keeps, so the state-only hooks know which of the two they were given."""
+
+
+def _wrap(x):
+    return _Bare(x) if isinstance(x, dict) else x
+
+
+def _unwrap(x):
+    return dict(x) if isinstance(x, _Bare) else x
+
+
+def _pick(x, k):
+    return x[k] if isinstance(x, dict) and not isinstance(x, _Bare) else None
+
+
+def _map_obs(cb, obs, *states):
+    """observations.py:36-57: cb(ob_name, ob, *per-observation states) over
+    the names of the observation dict obs; a bare tensor is one observation
+    named None whose states are kept _Bare-marked.  The reference's vmap over
+    the policy axis has no counterpart: one policy's state per call."""
+    if not isinstance(obs, dict):
+        return cb(None, obs, *[_unwrap(s) for s in states])
+    return {k: cb(k, obs[k], *[_pick(s, k) for s in states]) for k in obs}
+
+
+def _map_states(cb, states, *more):
+    """cb(ob_name, state, *more states) over a state structure (a _Bare or
+    None state is the bare observation's); results keep the structure."""
+    if states is None or isinstance(states, _Bare):
+        return _wrap(cb(None, _unwrap(states), *[_unwrap(m) for m in more]))
+    return {k: cb(k, states[k], *[_pick(m, k) for m in more]) for k in states}
 
 
 @dataclass(frozen=True)
@@ -40,22 +65,22 @@ class ObservationsPreprocess:  # observations.py:13-68
     policy's state per call here)."""
 
     def preprocess(self, states, obs, vmap=False):
-        return _map_obs(lambda k, st, ob: self._preprocess(k, st, ob), _states_like(states, obs),
-                        obs)
+        return _map_obs(lambda k, ob, st: self._preprocess(k, st, ob), obs, states)
 
     def init_state(self, obs, vmap=False):
-        return _map_obs(self._init_state, obs)
+        r = _map_obs(lambda k, ob: self._init_state(k, ob), obs)
+        return r if isinstance(obs, dict) else _wrap(r)
 
     def update_state(self, states, o_stats, vmap=False):
-        return _map_obs(self._update_state, states, o_stats)
+        return _map_states(self._update_state, states, o_stats)
 
     def init_obs_stats(self, states, vmap=False):
-        return _map_obs(self._init_obs_stats, states)
+        return _map_states(self._init_obs_stats, states)
 
     def update_obs_stats(self, states, cur_obs_stats, num_prev_updates, obs, vmap=False):
-        return _map_obs(lambda k, st, cs, ob: self._update_obs_stats(k, st, cs, num_prev_updates,
-                                                                    ob),
-                        _states_like(states, obs), _states_like(cur_obs_stats, obs), obs)
+        r = _map_obs(lambda k, ob, st, cs: self._update_obs_stats(k, st, cs, num_prev_updates, ob),
+                     obs, states, cur_obs_stats)
+        return r if isinstance(obs, dict) else _wrap(r)
 
     def _preprocess(self, ob_name, state, ob):
         return ob
@@ -86,13 +111,6 @@ class ObservationsPreprocess:  # observations.py:13-68
         raise NotImplementedError(
             f"{type(self).__name__} is not one of the fused preprocessors (Noop, Caster, "
             "EMANormalizer)")
-
-
-def _states_like(states, obs):
-    """None states for every observation name when a preprocess keeps none."""
-    if states is None and isinstance(obs, dict):
-        return {k: None for k in obs}
-    return states
 
 
 @dataclass(frozen=True)
