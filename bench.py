@@ -126,12 +126,12 @@ def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
     return fwd, bwd_dx, wgrad
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r04.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r05.json")
 
 
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
-    of this round (profiles/pmc_r03.json, tools/pmc_traffic.py): FETCH_SIZE
+    of this round (profiles/pmc_r05.json, tools/pmc_traffic.py): FETCH_SIZE
     doubled (gfx950 reports half the bytes of 16-B streaming reads,
     MI355X_MICROARCH.md HBM) + WRITE_SIZE, with the profiled kernel's name.
     (None, None) when no summary is committed."""
@@ -178,11 +178,18 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     fwd, bwd, _ = flop_per_sample(A1=A1)
     step_flop = (fwd + bwd) * M
     achieved = step_flop / t_step / 1e12
-    # the instantiation launch_minibatch picks for this policy (csrc/ppo.hip)
+    # the step kernel launch_minibatch picks for this policy and minibatch
+    # (mlearn_ppo_step_kernel: 2 = row-split, 1 = feature-split; csrc/ppo.hip)
     HC = 32 if A1 <= 32 else 96
-    kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1>"
-    mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
-    traffic, pmc_name = pmc_traffic("ppo_step")
+    sk = int(L.mlearn_ppo_step_kernel(ps.desc, M, int(algo.hp.step_kernel)))
+    if sk == 2:
+        kname = "ppo_rows16_kernel<false> (row-split)"
+        mangled = ("ppo_rows16_kernelILb0",)
+        traffic, pmc_name = pmc_traffic("ppo_rows16")
+    else:
+        kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1> (feature-split)"
+        mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
+        traffic, pmc_name = pmc_traffic("ppo_step")
     if pmc_name is None or not all(m in pmc_name for m in mangled):
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {

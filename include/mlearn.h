@@ -376,6 +376,11 @@ int64_t mlearn_grad_sumsq_parts(int64_t param_count);
 /* Size of the minibatch workspace (activations + gradient slabs). */
 int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows);
 
+/* The step kernel mlearn_ppo_minibatch_grad runs for this policy and minibatch
+ * row count given mlearn_ppo_hparams.step_kernel = requested: 1 (feature-split)
+ * or 2 (row-split); -1 for an invalid policy / request (host-only, no GPU). */
+int32_t mlearn_ppo_step_kernel(const mlearn_mlp_policy* policy, int64_t rows, int32_t requested);
+
 /* One PPO minibatch step up to the flat gradient: forward (ActorCritic.update,
  * actor_critic.py:98-128), loss (ppo.py:129-262), backward (jax.value_and_grad,
  * ppo.py:276-281) and the reduction of all per-row-tile partials into

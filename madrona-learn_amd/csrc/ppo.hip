@@ -1358,6 +1358,16 @@ int64_t mlearn_ppo_workspace_bytes(const mlearn_mlp_policy* policy, int64_t rows
     return (int64_t)carve(*policy, rows, nullptr, nullptr);
 }
 
+int32_t mlearn_ppo_step_kernel(const mlearn_mlp_policy* policy, int64_t rows, int32_t requested) {
+    if (validate_policy(policy) || rows < 1 || requested < 0 || requested > 2) return -1;
+    const int64_t Mp = (rows + kRowAlign - 1) / kRowAlign * kRowAlign;
+    const PolicyK P = make_policy_k(*policy);
+    const bool rows16 = rows16_eligible(P, Mp, head_cols(*policy), policy->num_layers,
+                                        policy->hidden, policy->dtype == MLEARN_DTYPE_BF16);
+    if (requested == 2 && !rows16) return -1;
+    return rows16 && requested != 1 ? 2 : 1;
+}
+
 static int ppo_entry(const mlearn_mlp_policy* policy, const mlearn_rollout_view* ro,
                      const int32_t* mb_seq, int32_t mb_size, const float* adv_stats,
                      const mlearn_ppo_hparams* hp, float* grad, float* loss_out, void* workspace,

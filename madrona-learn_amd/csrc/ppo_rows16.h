@@ -258,6 +258,39 @@ template <int D> __device__ inline float r16_pair_dpp(float a, float b) {
     return r;
 }
 
+// Feature whose column total lane (r, g) holds after r16_rowsum8 of block quad qd.
+__device__ inline int r16_colf(int qd, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+    return 16 * (4 * qd + (r >> 2)) + 4 * g + (r & 3);
+}
+// Column partials (bias, scale) of one layer's 4 block quads to a colpart row.
+__device__ inline void r16_put_cols(float* cpl, const float (&cb)[4], const float (&cg)[4],
+                                    int lane) {
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+        const int f = r16_colf(qd, lane);
+        cpl[f] = cb[qd];
+        cpl[kR16H + f] = cg[qd];
+    }
+}
+
+// As r16_store_rows, leaving w as it was (the swaps go to temporaries).
+__device__ inline void r16_store_rows_keep(bf16* rowp, const uint32_t (&w)[kR16NB][2], int g) {
+#pragma unroll
+    for (int c = 0; c < kR16NB / 2; ++c) {
+        uint32_t t[2][2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const auto v = __builtin_amdgcn_permlane16_swap(w[2 * c][k], w[2 * c + 1][k], false,
+                                                            false);
+            t[0][k] = v[0];
+            t[1][k] = v[1];
+        }
+        const int blk = 2 * c + (g & 1);
+        *(u4r*)(rowp + 16 * blk + 8 * (g >> 1)) = u4r{t[0][0], t[0][1], t[1][0], t[1][1]};
+    }
+}
+
 // Sum of 16 values v over the 16 lanes of a DPP row (the 16 rows of a tile)
 // by recursive halving, partners lane ^ 8 (done by the caller:
 // w[i] = r16_pair_dpp<8>(v[i], v[i + 8])), ^ 4 (bank-masked), then ^ 2, ^ 1
@@ -321,7 +354,7 @@ __device__ inline float r16_dy(float z, float mean, float rstd, float gam, float
 template <bool STORE_U>
 __device__ inline void r16_bwd_quad(f32x4* acc4, uint32_t (&zw)[kR16NB][2], int qd,
                                     float mean, float rstd, const float* gm, int g, int lane,
-                                    bool live, float& su, float& sv, float* cpl) {
+                                    bool live, float& su, float& sv, float& cbq, float& cgq) {
     // blocks in the order 0, 2, 1, 3: the first transpose-reduce level pairs
     // value j (block j / 4) with j + 8, so it runs after each block pair and
     // 8 instead of 16 values per sum are live at a time
@@ -359,10 +392,9 @@ __device__ inline void r16_bwd_quad(f32x4* acc4, uint32_t (&zw)[kR16NB][2], int 
             wg[4 * hp + i] = r16_pair_dpp<8>(pg[i], pg[4 + i]);
         }
     }
-    // lane (r, g) holds the column total of feature 16 (4 qd + r / 4) + 4g + r % 4
-    const int r = lane & 15, f = 16 * (4 * qd + (r >> 2)) + 4 * g + (r & 3);
-    cpl[f] = r16_rowsum8(wb, lane);
-    cpl[kR16H + f] = r16_rowsum8(wg, lane);
+    // lane (r, g) holds the column total of feature r16_colf(qd, lane)
+    cbq = r16_rowsum8(wb, lane);
+    cgq = r16_rowsum8(wg, lane);
 }
 
 // dZ = rstd (u - mean(u) - x_hat mean(u x_hat)) of one block from u
@@ -381,7 +413,8 @@ __device__ inline void r16_dz_block(const f32x4& u, uint32_t (&zwb)[2], float me
 // Layer backward with d loss / d A held in full (acc, 64 registers): one pass.
 __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2],
                                   float mean, float rstd, const float* gm, int g, int lane,
-                                  bool live, uint32_t (&dzw)[kR16NB][2], float* cpl) {
+                                  bool live, uint32_t (&dzw)[kR16NB][2], float (&cb)[4],
+                                  float (&cg)[4]) {
     // opaque copies (of the statistics and of every Z word read): the
     // forward's unpacked Z values / (z - mean) pairs are otherwise CSE'd into
     // this pass and held live from the forward LayerNorm
@@ -390,7 +423,8 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
     float su = 0.f, sv = 0.f;
 #pragma unroll
     for (int qd = 0; qd < kR16NB / 4; ++qd)
-        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cpl);
+        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cb[qd],
+                           cg[qd]);
     su = add_xor32(add_xor16(su));
     sv = add_xor32(add_xor16(sv));
     const float invH = 1.0f / (float)kR16H;
@@ -406,7 +440,7 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
 template <int NS, typename LDA, typename BF>
 __device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2], float mean,
                                    float rstd, const float* gm, int g, int lane, bool live,
-                                   uint32_t (&dzw)[kR16NB][2], float* cpl) {
+                                   uint32_t (&dzw)[kR16NB][2], float (&cb)[4], float (&cg)[4]) {
     mean = r16_late(mean);
     rstd = r16_late(rstd);
     float su = 0.f, sv = 0.f;
@@ -419,7 +453,7 @@ __device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2],
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
             r16_bwd_quad<false>(acc + 4 * qh, zw, 2 * h + qh, mean, rstd, gm, g, lane, live, su,
-                                sv, cpl);
+                                sv, cb[2 * h + qh], cg[2 * h + qh]);
     }
     su = add_xor32(add_xor16(su));
     sv = add_xor32(add_xor16(sv));
@@ -561,6 +595,8 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     LossAcc m;
     bool did = false;
     uint32_t dz0w[kR16NB][2];            // layer-0 dZ of the previous tile (stored late)
+    float cb0[4], cg0[4];                // its layer-0 column partials (stored with it)
+    float* prev_cp = nullptr;
     int64_t prev_row = -1;
     const int ntask = 16 * (K + 1);
     // minibatch row -> (time step, sequence slot); the slot's sequence id is
@@ -680,7 +716,10 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
                 *(bf16x8*)(xrow + 32 * s + 8 * g) = xf[s];
         }
         // the previous tile's layer-0 dZ rows go out behind this tile's loads
-        if (tt > 0) r16_store_rows((bf16*)ws.dz[0] + r16_late(prev_row) * kR16H, dz0w, g);
+        if (tt > 0) {
+            r16_store_rows((bf16*)ws.dz[0] + r16_late(prev_row) * kR16H, dz0w, g);
+            r16_put_cols(prev_cp, cb0, cg0, lane);
+        }
         r16_ln_apply(zw0, mean0, rstd0, gb, g, aw);
         R16_STAMP(2);
         // ---- layer 1 (W1 from LDS)
@@ -772,11 +811,33 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 #ifdef R16_ABL_NOL1BWD
         if (hp.clip < -1e30f)
 #endif
-        r16_ln_bwd2<1>([&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
-                       [&](int) { return dh; }, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw,
-                       cprow + 2 * kR16H);
+#ifdef R16_L1BWD2
+        {
+            float cb1[4], cg1[4];
+            r16_ln_bwd2<1>(
+                [&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
+                [&](int) { return dh; }, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw, cb1,
+                cg1);
+            r16_put_cols(cprow + 2 * kR16H, cb1, cg1, lane);
+        }
+#else
+        {
+            f32x4 hacc[kR16NB];
+#pragma unroll
+            for (int b = 0; b < kR16NB; ++b) hacc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+            r16_mm<kR16NB, 1, kR16Ring>(
+                hacc, [&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
+                [&](int) { return dh; });
+            float cb1[4], cg1[4];
+            r16_ln_bwd(hacc, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw, cb1, cg1);
+            r16_put_cols(cprow + 2 * kR16H, cb1, cg1, lane);
+        }
+#endif
         // dA_0^T = W1 dZ_1^T: M = input feature (image column), K = output feature
         // (image rows 32s + 4g + j, 32s + 16 + 4g + j)
+        // dZ_1 rows out now, ahead of the W1^T product and the layer-0
+        // backward: the next tile's first loads wait for them (vmcnt in order)
+        r16_store_rows_keep((bf16*)ws.dz[1] + r16_late(row) * kR16H, dzw, g);
         R16_STAMP(8);
         f32x4 acc[kR16NB];
 #pragma unroll
@@ -788,17 +849,18 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
             },
             [&](int s) { return r16_bfrag(dzw, s); });
         R16_STAMP(9);
-        r16_store_rows((bf16*)ws.dz[1] + r16_late(row) * kR16H, dzw, g);  // dZ_1 rows
         R16_STAMP(10);
         // ---- layer 0 LayerNorm / ReLU backward
         R16_STAMP(11);
-        r16_ln_bwd(acc, zw0, mean0, rstd0, gb, g, lane, live, dz0w, cprow);
+        r16_ln_bwd(acc, zw0, mean0, rstd0, gb, g, lane, live, dz0w, cb0, cg0);
         prev_row = row;
+        prev_cp = cprow;
         R16_STAMP(12);
         R16_STAMPS_OUT();
     }
     const int lane = tid & 63, r = lane & 15, g = lane >> 4;
     r16_store_rows((bf16*)ws.dz[0] + prev_row * kR16H, dz0w, g);
+    r16_put_cols(prev_cp, cb0, cg0, lane);
 
     // ---- loss metrics of this wave's rows (only the minibatch whose metrics survive)
     if (METRICS) {

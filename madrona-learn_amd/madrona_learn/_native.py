@@ -188,6 +188,7 @@ _SIGNATURES = {
     "mlearn_value_norm_chain": (c_int32, [_P, _P, c_int32, c_double, c_float, c_float, _P, _P, _P,
                                           _S]),
     "mlearn_ppo_workspace_bytes": (c_int64, [POINTER(MlpPolicy), c_int64]),
+    "mlearn_ppo_step_kernel": (c_int32, [POINTER(MlpPolicy), c_int64, c_int32]),
     "mlearn_ppo_minibatch_grad": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
                                             c_int32, _P, POINTER(PPOHparams), _P, _P, _P, _S]),
     "mlearn_ppo_minibatch_fwd_bwd": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,

@@ -84,6 +84,38 @@ def test_param_count_matches_oracle_layout():
     assert n == ref.param_layout(64, 256, 2, 26)["total"] == 89883
 
 
+def test_step_kernel_selection():
+    """mlearn_ppo_step_kernel: the row-split step kernel exactly where it
+    applies (bf16, H 256, 2 layers, scalar critic, obs 64, <= 7 action
+    groups, >= 65,536 rows in multiples of 256), the feature-split kernel
+    elsewhere; an explicit row-split request elsewhere is -1 (EINVAL)."""
+    from madrona_learn import _native as nat
+    L = nat.lib()
+
+    def desc(dtype=nat.DTYPE_BF16, H=256, layers=2, buckets=(4, 8, 5, 5, 2, 2), bins=1):
+        d = nat.MlpPolicy()
+        d.dtype, d.obs_dim, d.hidden, d.num_layers = dtype, 64, H, layers
+        d.critic_bins = bins
+        d.actions = nat.action_layout(list(buckets))
+        for l in range(layers):
+            d.w_t[l] = d.ln_scale[l] = d.ln_bias[l] = 1
+            d.w[l] = 1
+        d.head_t = d.head = d.head_bias = 1
+        return d
+
+    sel = lambda d, M, req=0: L.mlearn_ppo_step_kernel(ctypes.byref(d), M, req)  # noqa: E731
+    d = desc()
+    assert sel(d, 65536) == 2 and sel(d, 65536, 2) == 2 and sel(d, 65536, 1) == 1
+    assert sel(d, 65520) == 2           # padded to 65,536 rows
+    assert sel(d, 65536 * 4) == 2
+    assert sel(d, 32768) == 1 and sel(d, 32768, 2) == -1   # fewer workgroups than CUs
+    assert sel(d, 65536 + 64) == 1                           # not a multiple of 256
+    for other in (desc(dtype=nat.DTYPE_F32), desc(H=128), desc(layers=3),
+                  desc(buckets=(2,) * 8), desc(bins=9)):
+        assert sel(other, 65536) == 1 and sel(other, 65536, 2) == -1
+    assert sel(d, 65536, 3) == -1 and sel(d, 0) == -1
+
+
 def test_lstm_layout_matches_oracle_and_arch():
     """LSTM parameter segment: native offsets/counts == oracle layout ==
     the product's param_layout; RecurrentBackboneEncoder(MLP, LSTM) compiles."""

@@ -158,7 +158,8 @@ def test_obs_normalizer_before_prefix_on_torch_path(gpu):
     routes this policy to the torch path, which keeps the reference's order.
     Two updates against the oracle: the stored observations are the
     normalised RAW observations (bit-exact given the estimates), the
-    estimates follow ppo_ref.ema_* (1e-5 relative), and the stored values
+    estimates follow ppo_ref.ema_* (1e-5 relative; the observations normalised
+    with updated estimates then agree to 1e-5 as well), and the stored values
     are the critic of prefix(normalised observations) (oracle forward)."""
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
@@ -198,7 +199,15 @@ def test_obs_normalizer_before_prefix_on_torch_path(gpu):
                             gamma=cfg.gamma, actions_override=s.actions.cpu().numpy(),
                             obs_norm=(est, decay, 1e-5))
         oenv.step = step
-        assert np.array_equal(s.obs.float().cpu().numpy(), ro["obs"]), f"update {it}"
+        # bit-exact with the initial estimates; afterwards the torch path's
+        # estimate update (moving_avg.py in torch) differs from the oracle's by
+        # f32 rounding (checked at 1e-5 below), which the normalised
+        # observations inherit
+        if it == 0:
+            assert np.array_equal(s.obs.float().cpu().numpy(), ro["obs"]), f"update {it}"
+        else:
+            np.testing.assert_allclose(s.obs.float().cpu().numpy(), ro["obs"], rtol=1e-5,
+                                       atol=1e-5, err_msg=f"update {it}")
         _, V, _ = ref.forward(ref.unflatten(p0, lay), ro["obs"].reshape(T * N, 64) * 0.5, "f32")
         np.testing.assert_allclose(s.values.cpu().numpy().reshape(-1), V, rtol=1e-4, atol=1e-4)
         est = ro["obs_est"]
