@@ -112,6 +112,15 @@ __device__ inline bf16x8 r16_tr_frag(const char* img, int rlo, int rhi, int b, i
     return __builtin_bit_cast(bf16x8, v);
 }
 
+// 16-byte store of a weight-gradient operand row chunk (R16_NT: nontemporal)
+__device__ inline void r16_st16(void* p, u4r v) {
+#ifdef R16_NT
+    __builtin_nontemporal_store(v, (u4r*)p);
+#else
+    *(u4r*)p = v;
+#endif
+}
+
 __device__ inline uint32_t pk_bf16(float a, float b) {
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
     const bf16x2 v = {(bf16)a, (bf16)b};
@@ -229,8 +238,8 @@ __device__ inline void r16_store_rows(bf16* rowp, uint32_t (&w)[kR16NB][2], int 
 #ifdef R16_ABL_NOSTORE
         if ((uintptr_t)rowp == 1)
 #endif
-        *(u4r*)(rowp + 16 * blk + 8 * (g >> 1)) =
-            u4r{w[2 * c][0], w[2 * c][1], w[2 * c + 1][0], w[2 * c + 1][1]};
+        r16_st16(rowp + 16 * blk + 8 * (g >> 1),
+                 u4r{w[2 * c][0], w[2 * c][1], w[2 * c + 1][0], w[2 * c + 1][1]});
     }
 }
 
@@ -287,7 +296,7 @@ __device__ inline void r16_store_rows_keep(bf16* rowp, const uint32_t (&w)[kR16N
             t[1][k] = v[1];
         }
         const int blk = 2 * c + (g & 1);
-        *(u4r*)(rowp + 16 * blk + 8 * (g >> 1)) = u4r{t[0][0], t[0][1], t[1][0], t[1][1]};
+        r16_st16(rowp + 16 * blk + 8 * (g >> 1), u4r{t[0][0], t[0][1], t[1][0], t[1][1]});
     }
 }
 
@@ -309,20 +318,47 @@ __device__ inline float r16_rowsum8(const float (&w)[8], int lane) {
     return keep + xlane<1>(send);
 }
 
+// A LayerNorm pass's per-block scale / bias reads (features 16b + 4g .. +3,
+// f32, LDS) one block ahead: take(following) hands over the values loaded
+// last and issues block `following`'s reads (< 0: none), so each read has a
+// block's arithmetic to land.  Each take is a scheduling fence and each read
+// index opaque: otherwise the compiler issues all 16 blocks' reads up front
+// (128 registers).
+struct R16GB {
+    const float* gm;
+    int g;
+    float4 G, B;
+    __device__ R16GB(const float* gm_, int g_, int first) : gm(gm_), g(g_) { load(first); }
+    __device__ void load(int b) {
+        const int f0 = r16_late(16 * b + 4 * g);
+        G = *(const float4*)(gm + f0);
+        B = *(const float4*)(gm + kR16H + f0);
+    }
+    // block b's values read now (no read ahead)
+    __device__ void take_now(int b, float4& Go, float4& Bo) {
+        __builtin_amdgcn_sched_barrier(0);
+        load(b);
+        Go = G;
+        Bo = B;
+    }
+    __device__ void take(int following, float4& Go, float4& Bo) {
+        __builtin_amdgcn_sched_barrier(0);
+        Go = G;
+        Bo = B;
+        if (following >= 0) load(following);
+    }
+};
+
 // LayerNorm apply + ReLU, rounded to the compute dtype: packed Z -> packed
 // A (the next product's operand).
 __device__ inline void r16_ln_apply(uint32_t (&zw)[kR16NB][2], float mean, float rstd,
                                     const float* gm, int g, uint32_t (&aw)[kR16NB][2]) {
     const f2v m2 = {mean, mean}, r2 = {rstd, rstd};
+    R16GB gb(gm, g, 0);
 #pragma unroll
     for (int b = 0; b < kR16NB; ++b) {
-        // (one block's scale / bias in flight at a time: without the fence the
-        // scheduler issues all 32 LDS reads first and holds 128 registers)
-        __builtin_amdgcn_sched_barrier(0);
-        // (an opaque feature index per block: the LDS reads of all 16 blocks'
-        // scale / bias are otherwise issued up front, 128 registers)
-        const int f0 = r16_late(16 * b + 4 * g);
-        const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
+        float4 G, B;
+        gb.take(b + 1 < kR16NB ? b + 1 : -1, G, B);
         // (words made opaque in place: the statistics pass's unpacked values
         // would otherwise be CSE'd into this one and held live, 64 registers
         // across the layer's whole product)
@@ -348,55 +384,6 @@ __device__ inline float r16_dy(float z, float mean, float rstd, float gam, float
     return ((y > relu_thr<bf16>()) & live) ? da : 0.f;
 }
 
-// Column sums of one block quad's LayerNorm bias (dy) / scale (dy x_hat)
-// gradients over the tile's 16 rows, and the row sums su (u = dy gamma) and
-// sv (u x_hat) over its 16 features per lane; u kept in acc when STORE_U.
-template <bool STORE_U>
-__device__ inline void r16_bwd_quad(f32x4* acc4, uint32_t (&zw)[kR16NB][2], int qd,
-                                    float mean, float rstd, const float* gm, int g, int lane,
-                                    bool live, float& su, float& sv, float& cbq, float& cgq) {
-    // blocks in the order 0, 2, 1, 3: the first transpose-reduce level pairs
-    // value j (block j / 4) with j + 8, so it runs after each block pair and
-    // 8 instead of 16 values per sum are live at a time
-    float wb[8], wg[8];
-#pragma unroll
-    for (int hp = 0; hp < 2; ++hp) {
-        float pb[8], pg[8];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int bb = hp + 2 * k;
-            __builtin_amdgcn_sched_barrier(0);
-            const int b = 4 * qd + bb;
-            const int f0 = r16_late(16 * b + 4 * g);
-            const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
-            const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
-            zw[b][0] = r16_late(zw[b][0]);
-            zw[b][1] = r16_late(zw[b][1]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float xh;
-                const float z = up_bf16(zw[b][i >> 1])[i & 1];
-                const float dy = r16_dy(z, mean, rstd, gv[i], bv[i], acc4[bb][i], live, xh);
-                const float u = dy * gv[i];
-                su += u;
-                sv = __builtin_fmaf(u, xh, sv);
-                if (STORE_U) acc4[bb][i] = u;
-                pb[4 * k + i] = dy;
-                pg[4 * k + i] = dy * xh;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            wb[4 * hp + i] = r16_pair_dpp<8>(pb[i], pb[4 + i]);
-            wg[4 * hp + i] = r16_pair_dpp<8>(pg[i], pg[4 + i]);
-        }
-    }
-    // lane (r, g) holds the column total of feature r16_colf(qd, lane)
-    cbq = r16_rowsum8(wb, lane);
-    cgq = r16_rowsum8(wg, lane);
-}
-
 // dZ = rstd (u - mean(u) - x_hat mean(u x_hat)) of one block from u
 __device__ inline void r16_dz_block(const f32x4& u, uint32_t (&zwb)[2], float mean,
                                     float rstd, float ca, float cbc, uint32_t (&dzb)[2]) {
@@ -410,7 +397,13 @@ __device__ inline void r16_dz_block(const f32x4& u, uint32_t (&zwb)[2], float me
     }
 }
 
-// Layer backward with d loss / d A held in full (acc, 64 registers): one pass.
+// Layer backward (d loss / d A in acc, 64 registers) in two passes.  Pass 1,
+// per block: dy (r16_dy), u = dy gamma kept in acc, the row sums su (u) and sv
+// (u x_hat), and the column sums of the bias (dy) and scale (dy x_hat)
+// gradients over the tile's 16 rows -- blocks of a quad in the order 0, 2, 1,
+// 3, so the first transpose-reduce level (value j with j + 8) runs after each
+// block pair with 8 values per sum live; lane (r, g) ends with quad qd's total
+// of feature r16_colf(qd, lane).  Pass 2: dZ.
 __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2],
                                   float mean, float rstd, const float* gm, int g, int lane,
                                   bool live, uint32_t (&dzw)[kR16NB][2], float (&cb)[4],
@@ -421,69 +414,58 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
     mean = r16_late(mean);
     rstd = r16_late(rstd);
     float su = 0.f, sv = 0.f;
+    constexpr int ord[4] = {0, 2, 1, 3};
+    R16GB gb(gm, g, 0);
 #pragma unroll
-    for (int qd = 0; qd < kR16NB / 4; ++qd)
-        r16_bwd_quad<true>(acc + 4 * qd, zw, qd, mean, rstd, gm, g, lane, live, su, sv, cb[qd],
-                           cg[qd]);
+    for (int qd = 0; qd < kR16NB / 4; ++qd) {
+        float wb[8], wg[8];
+#pragma unroll
+        for (int hp = 0; hp < 2; ++hp) {
+            float pb[8], pg[8];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int step = 4 * qd + 2 * hp + k;
+                const int b = 4 * qd + ord[2 * hp + k];
+                const int bnext = step + 1 < kR16NB ? 4 * ((step + 1) / 4) + ord[(step + 1) % 4] : -1;
+                float4 G, B;
+#ifdef R16_GB_BWD_AHEAD
+                gb.take(bnext, G, B);
+#else
+                (void)bnext;
+                gb.take_now(b, G, B);
+#endif
+                const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
+                zw[b][0] = r16_late(zw[b][0]);
+                zw[b][1] = r16_late(zw[b][1]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float xh;
+                    const float z = up_bf16(zw[b][i >> 1])[i & 1];
+                    const float dy = r16_dy(z, mean, rstd, gv[i], bv[i], acc[b][i], live, xh);
+                    const float u = dy * gv[i];
+                    su += u;
+                    sv = __builtin_fmaf(u, xh, sv);
+                    acc[b][i] = u;
+                    pb[4 * k + i] = dy;
+                    pg[4 * k + i] = dy * xh;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                wb[4 * hp + i] = r16_pair_dpp<8>(pb[i], pb[4 + i]);
+                wg[4 * hp + i] = r16_pair_dpp<8>(pg[i], pg[4 + i]);
+            }
+        }
+        cb[qd] = r16_rowsum8(wb, lane);
+        cg[qd] = r16_rowsum8(wg, lane);
+    }
     su = add_xor32(add_xor16(su));
     sv = add_xor32(add_xor16(sv));
     const float invH = 1.0f / (float)kR16H;
     const float ca = -(rstd * rstd) * (sv * invH), cbc = -rstd * (su * invH);
 #pragma unroll
     for (int b = 0; b < kR16NB; ++b) r16_dz_block(acc[b], zw[b], mean, rstd, ca, cbc, dzw[b]);
-}
-
-// Layer backward whose d loss / d A comes from a short product (the head
-// backward, K = 32): two passes over two halves of 8 blocks, the half's
-// product run again in the second pass (same MFMAs, same bits) instead of
-// holding all 64 values.
-template <int NS, typename LDA, typename BF>
-__device__ inline void r16_ln_bwd2(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2], float mean,
-                                   float rstd, const float* gm, int g, int lane, bool live,
-                                   uint32_t (&dzw)[kR16NB][2], float (&cb)[4], float (&cg)[4]) {
-    mean = r16_late(mean);
-    rstd = r16_late(rstd);
-    float su = 0.f, sv = 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        f32x4 acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        r16_mm<8, NS, kR16Ring>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh)
-            r16_bwd_quad<false>(acc + 4 * qh, zw, 2 * h + qh, mean, rstd, gm, g, lane, live, su,
-                                sv, cb[2 * h + qh], cg[2 * h + qh]);
-    }
-    su = add_xor32(add_xor16(su));
-    sv = add_xor32(add_xor16(sv));
-    const float invH = 1.0f / (float)kR16H;
-    const float ca = -(rstd * rstd) * (sv * invH), cbc = -rstd * (su * invH);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        f32x4 acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        r16_mm<8, NS, kR16Ring>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int b = 8 * h + j;
-            const int f0 = r16_late(16 * b + 4 * g);
-            const float4 G = *(const float4*)(gm + f0), B = *(const float4*)(gm + kR16H + f0);
-            const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
-            f32x4 u;
-            zw[b][0] = r16_late(zw[b][0]);
-            zw[b][1] = r16_late(zw[b][1]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float xh;
-                const float z = up_bf16(zw[b][i >> 1])[i & 1];
-                u[i] = r16_dy(z, mean, rstd, gv[i], bv[i], acc[j][i], live, xh) * gv[i];
-            }
-            r16_dz_block(u, zw[b], mean, rstd, ca, cbc, dzw[b]);
-        }
-    }
 }
 
 // Division by a launch constant d (rows by the minibatch's sequence count,
@@ -521,6 +503,9 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws, R16Div dv) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef ML_STAMPS
+    const uint64_t r16_t_entry = __builtin_amdgcn_s_memtime();
+#endif
     char* w1img = smem + kR16OffW1;
     char* whimg = smem + kR16OffWh;
     float* gb = (float*)(smem + kR16OffGb);
@@ -574,6 +559,9 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         }
     }
     __syncthreads();
+#ifdef ML_STAMPS
+    const uint64_t r16_t_pro = __builtin_amdgcn_s_memtime();
+#endif
     const int* t_off = (const int*)(smem + kR16OffTab);
     const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
     const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
@@ -627,6 +615,9 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         // the lane index through an opaque copy per tile: otherwise every
         // lane-derived LDS / weight address of the body is hoisted out of the
         // tile loop and held live across it (rollout kernel)
+#ifdef R16_PRIO2
+        if (tt == R16_PRIO2 && wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef ML_STAMPS
         uint64_t r16_st[13];
 #endif
@@ -713,7 +704,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 #ifdef R16_ABL_NOSTORE
                 if ((uintptr_t)xrow == 1)
 #endif
-                *(bf16x8*)(xrow + 32 * s + 8 * g) = xf[s];
+                r16_st16(xrow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
         }
         // the previous tile's layer-0 dZ rows go out behind this tile's loads
         if (tt > 0) {
@@ -793,7 +784,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 #ifdef R16_ABL_NOSTORE
         if ((uintptr_t)ws.dhead == 1)
 #endif
-        *(bf16x8*)((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g) = dh;
+        r16_st16((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g, __builtin_bit_cast(u4r, dh));
         // column partials of this 16-row tile (colpart row 2 ptile + tt, WsK::ncp):
         // head bias here, LayerNorm bias / scale in the layer backwards
         float* cprow = ws.colpart + ((int64_t)ptile * kR16Tiles + tt) * ws.CP;
@@ -811,16 +802,6 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 #ifdef R16_ABL_NOL1BWD
         if (hp.clip < -1e30f)
 #endif
-#ifdef R16_L1BWD2
-        {
-            float cb1[4], cg1[4];
-            r16_ln_bwd2<1>(
-                [&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
-                [&](int) { return dh; }, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw, cb1,
-                cg1);
-            r16_put_cols(cprow + 2 * kR16H, cb1, cg1, lane);
-        }
-#else
         {
             f32x4 hacc[kR16NB];
 #pragma unroll
@@ -832,7 +813,6 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
             r16_ln_bwd(hacc, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw, cb1, cg1);
             r16_put_cols(cprow + 2 * kR16H, cb1, cg1, lane);
         }
-#endif
         // dA_0^T = W1 dZ_1^T: M = input feature (image column), K = output feature
         // (image rows 32s + 4g + j, 32s + 16 + 4g + j)
         // dZ_1 rows out now, ahead of the W1^T product and the layer-0
@@ -862,6 +842,18 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     r16_store_rows((bf16*)ws.dz[0] + prev_row * kR16H, dz0w, g);
     r16_put_cols(prev_cp, cb0, cg0, lane);
 
+#ifdef ML_STAMPS
+    {  // entry, after the prologue, end (last stores completed), in tile 0's row
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        if (ws.stamps && (tid & 63) == 0) {
+            uint64_t* st = ws.stamps + (int64_t)ptile * kR16Tiles * 16;
+            st[13] = r16_t_entry;
+            st[14] = r16_t_pro;
+            st[15] = t_end;
+        }
+    }
+#endif
     // ---- loss metrics of this wave's rows (only the minibatch whose metrics survive)
     if (METRICS) {
         const float vals[kLossSlots] = {m.sobj, m.qobj, m.mnobj, m.mxobj, m.svl, m.qvl, m.mnvl,

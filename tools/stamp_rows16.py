@@ -40,6 +40,22 @@ for it in range(3):
                                           nat.stream_handle()))
     torch.cuda.synchronize()
 st = buf.cpu().numpy().astype(np.int64)
+w0 = st[0::2]  # tile 0 rows of each wave: [13] entry, [14] after prologue, [15] end
+print("per wave (cycles, median / max): prologue", np.median(w0[:, 14] - w0[:, 13]),
+      (w0[:, 14] - w0[:, 13]).max(), "| tiles", np.median(st[1::2, 12] - w0[:, 0]),
+      "| epilogue (last stores done)", np.median(w0[:, 15] - st[1::2, 12]),
+      (w0[:, 15] - st[1::2, 12]).max(), "| entry..end", np.median(w0[:, 15] - w0[:, 13]),
+      (w0[:, 15] - w0[:, 13]).max())
+# per workgroup (8 waves, one CU): wave time entry..end by wave index, and the
+# spread inside a workgroup vs across workgroups
+tw = (w0[:, 15] - w0[:, 13]).reshape(-1, 8)
+print("wave time by wave index (median over WGs):", [int(x) for x in np.median(tw, 0)])
+print("WG max/min ratio median", float(np.median(tw.max(1) / tw.min(1))),
+      "| WG max: median", float(np.median(tw.max(1))), "max", int(tw.max()),
+      "| WG mean: min", float(tw.mean(1).min()), "max", float(tw.mean(1).max()))
+end_rel = (w0[:, 15] - w0[:, 13].reshape(-1, 8).min(1).repeat(8)).reshape(-1, 8)
+print("WG finish (from its first wave's entry): median", float(np.median(end_rel.max(1))),
+      "max", int(end_rel.max()))
 ok = st[:, 12] != 0
 st = st[ok]
 print("tiles stamped", int(ok.sum()), "of", tiles, "- cycles per phase (median / mean / max):")
