@@ -566,13 +566,6 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
     const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
 
-#ifdef R16_PRIO
-    if (wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef R16_STAGGER
-    if (wave >= kR16Waves / 2)
-        for (int i = 0; i < R16_STAGGER; ++i) __builtin_amdgcn_s_sleep(32);
-#endif
     const int ptile = (int)blockIdx.x * kR16Waves + wave;  // 32-row partials row (= ppo_step tile)
     const float as0 = adv_st[0], as1 = adv_st[1];
     // value normaliser values, loaded once (a load in the loss loop waits on
@@ -615,9 +608,10 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         // the lane index through an opaque copy per tile: otherwise every
         // lane-derived LDS / weight address of the body is hoisted out of the
         // tile loop and held live across it (rollout kernel)
-#ifdef R16_PRIO2
-        if (tt == R16_PRIO2 && wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
-#endif
+        // the second wave of each SIMD (waves 4..7) loses issue arbitration to
+        // the first throughout (tile 0 ends ~24 % later); it takes priority for
+        // its last tile so the two finish closer together (-1..2 % kernel time)
+        if (tt == kR16Tiles - 1 && wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef ML_STAMPS
         uint64_t r16_st[13];
 #endif
