@@ -231,10 +231,19 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
 
         t_roll = time_call(roll, 5, rstream)
         roll_flop = fwd * rm.B * (T + 1)
-        grid = int(L.mlearn_policy_rollout_workgroups(ps.desc, None, rm.B, rm.rollout_workgroups))
+        rk = int(L.mlearn_policy_rollout_kernel(ps.desc, None, rm.B, rm.rollout_workgroups,
+                                                int(rm.rollout_kernel)))
+        if rk == 2:  # row split: one 8-wave workgroup per CU, 16-env tiles per wave
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            kname, grid, tiles = "rollout16_kernel (row-split)", min(cus, rm.B // 128), rm.B // 16
+        else:
+            kname = "policy_rollout_kernel (feature-split)"
+            grid = int(L.mlearn_policy_rollout_workgroups(ps.desc, None, rm.B,
+                                                          rm.rollout_workgroups))
+            tiles = -(-rm.B // 32)
         extra["policy_rollout"] = {
-            "kernel": "policy_rollout_kernel (mlearn_policy_rollout_env)", "bound": "mfma",
-            "envs": rm.B, "steps": T + 1, "workgroups": grid, "env_tiles": -(-rm.B // 32),
+            "kernel": f"{kname} (mlearn_policy_rollout_env)", "bound": "mfma",
+            "envs": rm.B, "steps": T + 1, "workgroups": grid, "env_tiles": tiles,
             "avg_launch_us": t_roll * 1e6, "us_per_step": t_roll * 1e6 / (T + 1),
             "achieved": roll_flop / t_roll / 1e12, "unit": "TFLOP/s",
             "frac": roll_flop / t_roll / 1e12 / BF16_PEAK_TFS}

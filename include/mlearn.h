@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 18
+#define MLEARN_ABI_VERSION 19
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -661,6 +661,15 @@ typedef struct mlearn_rollout_out {
                                    > 0: at most this many workgroups (tiles in series);
                                    < 0: T + 1 per-step launches of the same body (same bits
                                    either way) */
+    int32_t policy_kernel;      /* 0: the library's choice (the row-split rollout where it
+                                   applies: the row-split step's policy shape, <= 8 action
+                                   groups, no observation normaliser, max_workgroups 0,
+                                   N a multiple of 256 and >= 65536; else the feature-split
+                                   kernel), 1: the feature-split kernel (the per-step
+                                   launches' body), 2: the row-split kernel (EINVAL where it
+                                   does not apply).  The row split accumulates the trunk and
+                                   heads in another order: logits within a bf16 ulp of the
+                                   feature split's */
 } mlearn_rollout_out;
 int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                               const mlearn_lstm_carry* carry, const float* obs, int64_t N,
@@ -706,6 +715,13 @@ int64_t mlearn_policy_rollout_pop_workgroups(const mlearn_mlp_policy* policy,
  * tiles = ceil(N / 32) > the result means tiles run in series. */
 int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                                          int64_t N, int32_t max_workgroups);
+/* The rollout kernel mlearn_policy_rollout_env runs for this policy, N and
+ * max_workgroups given mlearn_rollout_out.policy_kernel = requested: 1
+ * (feature split; its grid is mlearn_policy_rollout_workgroups) or 2 (row
+ * split: one 8-wave workgroup per CU, 16-env tiles in series per wave); -1
+ * for an invalid request (host-only). */
+int32_t mlearn_policy_rollout_kernel(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                     int64_t N, int32_t max_workgroups, int32_t requested);
 int mlearn_lstm_policy_rollout_step_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                                         const mlearn_lstm_carry* carry, const float* obs,
                                         int64_t N, void* obs_store, int32_t* actions,

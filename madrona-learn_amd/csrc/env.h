@@ -43,8 +43,9 @@ __device__ inline void env_obs_quad(float* o, int D, uint32_t k0, uint32_t k1, u
 
 // One env's reward / done / state advance (its counter {env, 2^31, step});
 // a0 = the env's first action.
-__device__ inline void env_advance_a0(int4* state, int64_t n, uint32_t g, uint32_t k0, uint32_t k1,
-                                      float a0, float* rew, uint8_t* done, int4 st) {
+// The values of that advance: reward, done, next state word.
+__device__ inline int4 env_advance_vals(uint32_t g, uint32_t k0, uint32_t k1, float a0, int4 st,
+                                        float& rew, bool& done) {
 #pragma clang fp contract(off)
     const uint64_t step = env_step_of(st);
     int s = st.x + 1;
@@ -53,10 +54,19 @@ __device__ inline void env_advance_a0(int4* state, int64_t n, uint32_t g, uint32
     u32x4 r = philox4x32(u32x4{g, 0x80000000u, (uint32_t)step, (uint32_t)(step >> 32)}, k0,
                          k1 ^ 0x5eedu);
     float u = u32_to_unit(r.x);
-    rew[n] = (u * 2.0f - 1.0f) + 0.01f * a0;
-    done[n] = d ? 1 : 0;
+    rew = (u * 2.0f - 1.0f) + 0.01f * a0;
+    done = d;
     const uint64_t ns = step + 1;
-    state[n] = make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
+    return make_int4(d ? 0 : s, (int)(uint32_t)ns, (int)(uint32_t)(ns >> 32), 0);
+}
+__device__ inline void env_advance_a0(int4* state, int64_t n, uint32_t g, uint32_t k0, uint32_t k1,
+                                      float a0, float* rew, uint8_t* done, int4 st) {
+    float r;
+    bool d;
+    const int4 ns = env_advance_vals(g, k0, k1, a0, st, r, d);
+    rew[n] = r;
+    done[n] = d ? 1 : 0;
+    state[n] = ns;
 }
 
 __device__ inline void env_advance(int4* state, const int32_t* actions, int K, int64_t n,

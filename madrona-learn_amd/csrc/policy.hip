@@ -15,6 +15,7 @@
 #include "dists.h"
 #include "env.h"
 #include "rowtile.h"
+#include "r16_common.h"
 
 namespace ml {
 
@@ -615,6 +616,8 @@ struct RollK {
     int max_wg;          // mlearn_rollout_out.max_workgroups
 };
 
+#include "rollout_rows16.h"
+
 // LayerNorm / head-bias parameters, LSTM bias, critic bins of policy P
 // staged in LDS for every step of a tile (the body's first statistics
 // barrier orders them)
@@ -1034,6 +1037,16 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
     const RollK& rk = e.rk;
     const EnvK& ek = e.env;
     hipStream_t s = S(stream);
+    ML_REQUIRE(out->policy_kernel >= 0 && out->policy_kernel <= 2,
+               "policy_rollout_env: policy_kernel %d", out->policy_kernel);
+    const bool r16 = rollout16_eligible(P, N, out->max_workgroups,
+                                        policy->dtype == MLEARN_DTYPE_BF16, lstm != nullptr);
+    ML_REQUIRE(out->policy_kernel != 2 || r16,
+               "policy_rollout_env: policy_kernel 2 (row split) needs the row-split step's policy "
+               "shape, <= 8 action groups, no observation normaliser, max_workgroups 0 and N a "
+               "multiple of 256, >= 65536");
+    if (r16 && out->policy_kernel != 1)
+        return launch_rollout16(P, obs, N, rk, k0, k1, step_ctr, env_offset, ek, s);
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \
     (lstm ? launch_policy_rollout<T, HH, true, HC>(P, obs, N, rk, k0, k1, step_ctr, env_offset, R, \
                                                    cy, ek, s)                                     \
@@ -1191,6 +1204,18 @@ extern "C" int64_t mlearn_policy_rollout_workgroups(const mlearn_mlp_policy* pol
 #undef ML_DISPATCH
 #undef ML_GRID
 #undef ML_GRID_HC
+}
+
+extern "C" int32_t mlearn_policy_rollout_kernel(const mlearn_mlp_policy* policy,
+                                                const mlearn_lstm* lstm, int64_t N,
+                                                int32_t max_workgroups, int32_t requested) {
+    if ((lstm ? validate_lstm(policy, lstm) : validate_policy(policy)) || N < 1 || requested < 0 ||
+        requested > 2)
+        return -1;
+    const bool r16 = rollout16_eligible(make_policy_k(*policy), N, max_workgroups,
+                                        policy->dtype == MLEARN_DTYPE_BF16, lstm != nullptr);
+    if (requested == 2 && !r16) return -1;
+    return r16 && requested != 1 ? 2 : 1;
 }
 
 extern "C" int mlearn_policy_rollout_step_env(const mlearn_mlp_policy* policy, const float* obs,

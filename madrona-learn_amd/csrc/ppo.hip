@@ -20,6 +20,7 @@
 //   store row = (c * bptt + tl) * N + b.
 
 #include "ppo_defs.h"
+#include "r16_common.h"
 
 namespace ml {
 

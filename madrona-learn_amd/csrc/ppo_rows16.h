@@ -31,218 +31,6 @@
 
 // (included inside namespace ml by ppo.hip)
 
-constexpr int kR16Waves = 8;     // waves per workgroup
-constexpr int kR16Tiles = 2;     // 16-row tiles per wave: 32 rows = one partials row
-constexpr int kR16H = 256;
-constexpr int kR16NB = kR16H / 16;   // 16-feature accumulator blocks
-constexpr int kR16KS = kR16H / 32;   // k-steps over the hidden features
-constexpr int kR16HC = MLEARN_HEAD_COLS;
-constexpr int kR16D = 64;            // observation width (the first layer's K)
-constexpr int kR16LGS = 40;          // logits scratch row stride (bf16; 80-B rows)
-constexpr int kR16Ring = 6;          // LDS A fragments in flight per product
-constexpr int kR16Ring0 = 16;        // first-layer (L2) A fragments in flight
-// LDS: W1 image [256 rows = out][512 B], head image [32 rows = col][512 B],
-// LayerNorm scale/bias [2][2][256] f32, head bias [32] f32, per-wave logits
-// scratch [8][16][kR16LGS] bf16, the action groups' logit offsets, entropy
-// coefficients and objective weights (read per lane by the loss tasks: from
-// the kernel arguments a lane-dependent index would copy the arrays into
-// registers)
-constexpr size_t kR16OffW1 = 0;
-constexpr size_t kR16OffWh = kR16OffW1 + (size_t)kR16H * 512;
-constexpr size_t kR16OffGb = kR16OffWh + (size_t)kR16HC * 512;
-constexpr size_t kR16OffHb = kR16OffGb + (size_t)2 * 2 * kR16H * 4;
-constexpr size_t kR16OffLg = kR16OffHb + (size_t)kR16HC * 4;
-constexpr size_t kR16OffTab = kR16OffLg + (size_t)kR16Waves * 16 * kR16LGS * 2;
-constexpr int kR16TabN = 3 * (MLEARN_MAX_GROUPS + 1);  // group offsets, entropy coefs, obj weights
-constexpr size_t kR16Lds = kR16OffTab + (size_t)kR16TabN * 4;
-static_assert(kR16Lds <= 160 * 1024, "row-split step LDS budget");
-
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef short short4r __attribute__((ext_vector_type(4)));
-typedef __attribute__((ext_vector_type(4))) uint32_t u4r;
-typedef __attribute__((ext_vector_type(2))) uint32_t u2r;
-
-// 8-byte unit u (4 consecutive bf16 of a 512-B image row) of row n, XOR-
-// swizzled so that the row reads (16 rows x units {8s + g, 8s + 4 + g}) and
-// the transposed reads (8 rows x 4 units) of a 32-lane half hit 32 distinct
-// bank pairs.
-__device__ inline uint32_t r16_off(int n, int u) {
-    const int sw = ((n & 7) << 2) | (((n >> 3) & 1) << 1);
-    return (uint32_t)(n * 512 + ((u ^ sw) << 3));
-}
-
-// An opaque copy of a value (its uses cannot be computed before this point:
-// the row-derived store addresses would otherwise be formed at the tile's
-// start and held live across it).
-template <typename V> __device__ inline V r16_late(V v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-
-__device__ inline f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// A fragment of a forward product from an LDS image: rows n = output feature,
-// k-slots 8g + j = input features 32s + 16(j>>2) + 4g + (j&3): units 8s + g
-// and 8s + 4 + g of row n.
-__device__ inline bf16x8 r16_row_frag(const char* img, int n, int s, int g) {
-    const u2r lo = *(const u2r*)(img + r16_off(n, 8 * s + g));
-    const u2r hi = *(const u2r*)(img + r16_off(n, 8 * s + 4 + g));
-    const u4r v = {lo[0], lo[1], hi[0], hi[1]};
-    return __builtin_bit_cast(bf16x8, v);
-}
-
-// A fragment of a backward product from the same image read transposed: M =
-// image column (input feature 16b + (lane & 15)), k-slots 8g + j = image rows
-// r0 + 4g + j (j < 4) and r0 + 16 + 4g + (j - 4) with r0 = 32s (hidden
-// operands), or rows 8g + j with `step8` (the head's 32 columns, one k-step).
-__device__ inline bf16x8 r16_tr_frag(const char* img, int rlo, int rhi, int b, int lane) {
-    // (rlo, rhi split into a multiple of 16 rows, an instruction offset, and
-    // a lane part that alone sets the swizzle: one block-dependent address
-    // per lane and block)
-    const int q = (lane >> 2) & 3, p = lane & 3;
-    typedef __attribute__((address_space(3))) short4r* lp;
-    const short4r lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lp)(img + (rlo & ~15) * 512 + r16_off((rlo & 15) + q, 4 * b + p)));
-    const short4r hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lp)(img + (rhi & ~15) * 512 + r16_off((rhi & 15) + q, 4 * b + p)));
-    typedef short short8r __attribute__((ext_vector_type(8)));
-    const short8r v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-}
-
-// 16-byte store of a weight-gradient operand row chunk (R16_NT: nontemporal)
-__device__ inline void r16_st16(void* p, u4r v) {
-#ifdef R16_NT
-    __builtin_nontemporal_store(v, (u4r*)p);
-#else
-    *(u4r*)p = v;
-#endif
-}
-
-__device__ inline uint32_t pk_bf16(float a, float b) {
-    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    const bf16x2 v = {(bf16)a, (bf16)b};
-    return __builtin_bit_cast(uint32_t, v);
-}
-__device__ inline f2v up_bf16(uint32_t w) {
-    return f2v{__builtin_bit_cast(float, w << 16), __builtin_bit_cast(float, w & 0xffff0000u)};
-}
-// k-step s B fragment from packed words of blocks 2s, 2s+1 (the acc layout)
-__device__ inline bf16x8 r16_bfrag(const uint32_t (&w)[kR16NB][2], int s) {
-    const u4r v = {w[2 * s][0], w[2 * s][1], w[2 * s + 1][0], w[2 * s + 1][1]};
-    return __builtin_bit_cast(bf16x8, v);
-}
-
-// acc[j] += sum_s A(j, s) B(s) over NBO output blocks and NS k-steps, A
-// fragments from `lda(j, s)` through a ring of RING fragments in flight
-// (sched_barrier fences keep the compiler from hoisting every read of the
-// product ahead of its MFMAs, which would hold them all in registers).
-template <int NBO, int NS, int RING, typename LDA, typename BF>
-__device__ inline void r16_mm(f32x4 (&acc)[NBO], LDA lda, BF bfrag) {
-    constexpr int N = NS * NBO;
-    constexpr int RG = RING < N ? RING : N;
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 ra[RG];
-#pragma unroll
-    for (int i = 0; i < RG; ++i) ra[i] = lda(i % NBO, i / NBO);
-    bf16x8 bfr = bfrag(0);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const bf16x8 a = ra[i % RG];
-        if (i + RG < N) ra[i % RG] = lda((i + RG) % NBO, (i + RG) / NBO);
-        __builtin_amdgcn_sched_barrier(0);
-        acc[i % NBO] = mma16(a, bfr, acc[i % NBO]);
-        __builtin_amdgcn_sched_barrier(0);
-        if ((i + 1) % NBO == 0 && i + 1 < N) bfr = bfrag((i + 1) / NBO);
-    }
-}
-
-// As r16_mm, but block-pair-major: blocks 2p, 2p+1 take all NS k-steps
-// (alternating, two independent accumulator chains) before the next pair, so
-// a fragment address that depends on the block (the transposed reads) is
-// formed once per block instead of once per (block, k-step); B fragments
-// come from registers.
-template <int NBO, int NS, int RING, typename LDA, typename BF>
-__device__ inline void r16_mm_bm(f32x4 (&acc)[NBO], LDA lda, BF bfrag) {
-    static_assert(NBO % 2 == 0, "block pairs");
-    constexpr int N = NS * NBO;
-    constexpr int RG = RING < N ? RING : N;
-    auto jof = [](int i) { return 2 * (i / (2 * NS)) + (i & 1); };
-    auto sof = [](int i) { return (i >> 1) % NS; };
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 ra[RG];
-#pragma unroll
-    for (int i = 0; i < RG; ++i) ra[i] = lda(jof(i), sof(i));
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const bf16x8 a = ra[i % RG];
-        if (i + RG < N) ra[i % RG] = lda(jof(i + RG), sof(i + RG));
-        __builtin_amdgcn_sched_barrier(0);
-        acc[jof(i)] = mma16(a, bfrag(sof(i)), acc[jof(i)]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// A forward layer's product Z^T = W^T X^T in two halves of 8 output blocks
-// (32 accumulator registers at a time instead of 64), each half rounded to
-// the compute dtype as it completes (flax Dense output dtype) and packed into
-// zw; returns the LayerNorm statistics of the rows (f32 sums of the rounded
-// values, fast variance, eps 1e-6; models.py:46-56).
-template <int NS, int RING, typename LDA, typename BF>
-__device__ inline void r16_fwd_layer(LDA lda, BF bfrag, uint32_t (&zw)[kR16NB][2], float& mean_o,
-                                     float& rstd_o) {
-    f2v s2 = {0.f, 0.f}, q2 = {0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        f32x4 acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        r16_mm<8, NS, RING>(acc, [&](int j, int s) { return lda(8 * h + j, s); }, bfrag);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                zw[8 * h + j][k] = pk_bf16(acc[j][2 * k], acc[j][2 * k + 1]);
-                const f2v x = up_bf16(zw[8 * h + j][k]);
-                s2 += x;
-                q2 = x * x + q2;
-            }
-    }
-    float sum = s2.x + s2.y, sq = q2.x + q2.y;
-    sum = add_xor32(add_xor16(sum));
-    sq = add_xor32(add_xor16(sq));
-    const float invH = 1.0f / (float)kR16H;
-    const float mean = sum * invH;
-    const float var = fmaxf(sq * invH - mean * mean, 0.f);
-    mean_o = mean;
-    rstd_o = rsqrtf(var + 1e-6f);
-}
-
-// Row-major store of a [16 rows][256] bf16 operand held as packed words (lane
-// (r, g): features 16b + 4g .. 4g+3 of every block b): one v_permlane16_swap
-// per word pair leaves lane g with 8 consecutive features of block 2c + (g&1)
-// (features 8(g>>1) .. +7), one 16-byte store per block pair.  In place.
-__device__ inline void r16_store_rows(bf16* rowp, uint32_t (&w)[kR16NB][2], int g) {
-#pragma unroll
-    for (int c = 0; c < kR16NB / 2; ++c) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const auto v = __builtin_amdgcn_permlane16_swap(w[2 * c][k], w[2 * c + 1][k], false,
-                                                            false);
-            w[2 * c][k] = v[0];
-            w[2 * c + 1][k] = v[1];
-        }
-        const int blk = 2 * c + (g & 1);
-#ifdef R16_ABL_NOSTORE
-        if ((uintptr_t)rowp == 1)
-#endif
-        r16_st16(rowp + 16 * blk + 8 * (g >> 1),
-                 u4r{w[2 * c][0], w[2 * c][1], w[2 * c + 1][0], w[2 * c + 1][1]});
-    }
-}
-
 // One transpose-reduce level at lane distance D = 8 or 4 within a DPP row:
 // lanes with bit D clear return a + (partner's a), the others b + (partner's
 // b) -- two bank-masked v_add_f32_dpp writing complementary lane sets (no
@@ -283,23 +71,6 @@ __device__ inline void r16_put_cols(float* cpl, const float (&cb)[4], const floa
     }
 }
 
-// As r16_store_rows, leaving w as it was (the swaps go to temporaries).
-__device__ inline void r16_store_rows_keep(bf16* rowp, const uint32_t (&w)[kR16NB][2], int g) {
-#pragma unroll
-    for (int c = 0; c < kR16NB / 2; ++c) {
-        uint32_t t[2][2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const auto v = __builtin_amdgcn_permlane16_swap(w[2 * c][k], w[2 * c + 1][k], false,
-                                                            false);
-            t[0][k] = v[0];
-            t[1][k] = v[1];
-        }
-        const int blk = 2 * c + (g & 1);
-        r16_st16(rowp + 16 * blk + 8 * (g >> 1), u4r{t[0][0], t[0][1], t[1][0], t[1][1]});
-    }
-}
-
 // Sum of 16 values v over the 16 lanes of a DPP row (the 16 rows of a tile)
 // by recursive halving, partners lane ^ 8 (done by the caller:
 // w[i] = r16_pair_dpp<8>(v[i], v[i + 8])), ^ 4 (bank-masked), then ^ 2, ^ 1
@@ -316,61 +87,6 @@ __device__ inline float r16_rowsum8(const float (&w)[8], int lane) {
     }
     const float keep = h0 ? y[1] : y[0], send = h0 ? y[0] : y[1];
     return keep + xlane<1>(send);
-}
-
-// A LayerNorm pass's per-block scale / bias reads (features 16b + 4g .. +3,
-// f32, LDS) one block ahead: take(following) hands over the values loaded
-// last and issues block `following`'s reads (< 0: none), so each read has a
-// block's arithmetic to land.  Each take is a scheduling fence and each read
-// index opaque: otherwise the compiler issues all 16 blocks' reads up front
-// (128 registers).
-struct R16GB {
-    const float* gm;
-    int g;
-    float4 G, B;
-    __device__ R16GB(const float* gm_, int g_, int first) : gm(gm_), g(g_) { load(first); }
-    __device__ void load(int b) {
-        const int f0 = r16_late(16 * b + 4 * g);
-        G = *(const float4*)(gm + f0);
-        B = *(const float4*)(gm + kR16H + f0);
-    }
-    // block b's values read now (no read ahead)
-    __device__ void take_now(int b, float4& Go, float4& Bo) {
-        __builtin_amdgcn_sched_barrier(0);
-        load(b);
-        Go = G;
-        Bo = B;
-    }
-    __device__ void take(int following, float4& Go, float4& Bo) {
-        __builtin_amdgcn_sched_barrier(0);
-        Go = G;
-        Bo = B;
-        if (following >= 0) load(following);
-    }
-};
-
-// LayerNorm apply + ReLU, rounded to the compute dtype: packed Z -> packed
-// A (the next product's operand).
-__device__ inline void r16_ln_apply(uint32_t (&zw)[kR16NB][2], float mean, float rstd,
-                                    const float* gm, int g, uint32_t (&aw)[kR16NB][2]) {
-    const f2v m2 = {mean, mean}, r2 = {rstd, rstd};
-    R16GB gb(gm, g, 0);
-#pragma unroll
-    for (int b = 0; b < kR16NB; ++b) {
-        float4 G, B;
-        gb.take(b + 1 < kR16NB ? b + 1 : -1, G, B);
-        // (words made opaque in place: the statistics pass's unpacked values
-        // would otherwise be CSE'd into this one and held live, 64 registers
-        // across the layer's whole product)
-        zw[b][0] = r16_late(zw[b][0]);
-        zw[b][1] = r16_late(zw[b][1]);
-        const f2v y0 = __builtin_elementwise_fma(up_bf16(zw[b][0]) - m2, r2 * f2v{G.x, G.y},
-                                                 f2v{B.x, B.y});
-        const f2v y1 = __builtin_elementwise_fma(up_bf16(zw[b][1]) - m2, r2 * f2v{G.z, G.w},
-                                                 f2v{B.z, B.w});
-        aw[b][0] = pk_bf16(fmaxf(y0.x, 0.f), fmaxf(y0.y, 0.f));
-        aw[b][1] = pk_bf16(fmaxf(y1.x, 0.f), fmaxf(y1.y, 0.f));
-    }
 }
 
 // LayerNorm + ReLU backward element (models.py:46-56 under jax.value_and_grad,
@@ -468,17 +184,6 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
     for (int b = 0; b < kR16NB; ++b) r16_dz_block(acc[b], zw[b], mean, rstd, ca, cbc, dzw[b]);
 }
 
-// Division by a launch constant d (rows by the minibatch's sequence count,
-// sequence ids by the policy's env count): q = (mulhi(n, mag) + n) >> sh,
-// exact for n < 2^31 (magic from r16_magic on the host).
-struct R16Div {
-    uint32_t mb_mag, n_mag;
-    int mb_sh, n_sh;
-};
-__device__ inline uint32_t r16_udiv(uint32_t n, uint32_t mag, int sh) {
-    return (__umulhi(n, mag) + n) >> sh;
-}
-
 // diagnostic builds only (ML_STAMPS): s_memtime per phase held in SGPRs and
 // written once per tile, so the stamps leave the VGPR allocation alone
 #ifdef ML_STAMPS
@@ -520,36 +225,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     // permuted k, K = 256) re-laid as [out row][512 B] with swizzled 8-byte
     // units; LayerNorm scale / bias, head bias, the loss tasks' group tables
     {
-        const u4r* src1 = (const u4r*)P.wt[1];
-        const u4r* srch = (const u4r*)P.head_t;
-        constexpr int N1 = kR16H * kR16H * 2 / 16 / (64 * kR16Waves);  // 16 per thread
-        u4r v1[N1], vh[2];
-#pragma unroll
-        for (int i = 0; i < N1; ++i) v1[i] = src1[tid + i * 64 * kR16Waves];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) vh[i] = srch[tid + i * 64 * kR16Waves];
-        float pv[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int j = tid + i * 64 * kR16Waves, l = j >> 9, c = j & 511;
-            pv[i] = c < kR16H ? P.lns[l][c] : P.lnb[l][c - kR16H];
-        }
-        const float hbv = tid < kR16HC ? P.head_b[tid] : 0.f;
-        // 16-byte unit U of a (K = 256, perm) image: n = ((U >> 10) << 5) | (U & 31),
-        // h = (U >> 5) & 1, s16 = (U >> 6) & 15; its halves hold inputs
-        // 16 s16 + 4h .. +3 and 16 s16 + 8 + 4h .. +3 (units 4 s16 + h, 4 s16 + 2 + h)
-        auto put = [&](char* img, int U, u4r v) {
-            const int n = ((U >> 10) << 5) | (U & 31), h = (U >> 5) & 1, s16 = (U >> 6) & 15;
-            *(u2r*)(img + r16_off(n, 4 * s16 + h)) = u2r{v[0], v[1]};
-            *(u2r*)(img + r16_off(n, 4 * s16 + 2 + h)) = u2r{v[2], v[3]};
-        };
-#pragma unroll
-        for (int i = 0; i < N1; ++i) put(w1img, tid + i * 64 * kR16Waves, v1[i]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) put(whimg, tid + i * 64 * kR16Waves, vh[i]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) gb[tid + i * 64 * kR16Waves] = pv[i];
-        if (tid < kR16HC) hb[tid] = hbv;
+        r16_stage(P, smem, tid);
         int* tab = (int*)(smem + kR16OffTab);
         if (tid <= MLEARN_MAX_GROUPS) {
             tab[tid] = P.off[tid];
@@ -877,16 +553,6 @@ static bool rows16_eligible(const PolicyK& P, int64_t Mp, int HC, int L, int H, 
     return bf && H == kR16H && L == 2 && HC == kR16HC && P.CB == 1 && P.D == kR16D &&
            P.K + 1 <= 8 && Mp % (32 * kR16Waves) == 0 &&
            Mp / (32 * kR16Waves) >= 256;
-}
-
-// (mulhi(n, mag) + n) >> sh == n / d for n < 2^31: sh = ceil(log2 d),
-// mag = floor(2^32 (2^sh - d) / d) + 1 (tests/test_gpu_fullsize.py covers
-// d = 4095 and powers of two)
-static void r16_magic(uint32_t d, uint32_t& mag, int& sh) {
-    int l = 0;
-    while ((1ull << l) < d) ++l;
-    mag = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
-    sh = l;
 }
 
 static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,

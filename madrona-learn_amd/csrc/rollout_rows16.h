@@ -1,0 +1,281 @@
+// Whole rollout of the built-in synthetic sim, row split
+// (mlearn_policy_rollout_env, mlearn_rollout_out.policy_kernel = 2, the
+// library's choice at the headline shape): rollout_loop rollouts.py:829-978
+// -- per step the policy (ObservationsCaster -> MLP trunk -> heads,
+// models.py:46-56, 99-154), Gumbel-max sampling (dists.py:26-52), the store
+// writes (_post_inference_cb 637-680), the sim step and _post_step_cb
+// (682-714, bookkeeping 933-973); then the bootstrap critic (607-635).
+// Included by policy.hip inside namespace ml after RollK.
+//
+// Layout as the row-split minibatch step (r16_common.h): one workgroup of 8
+// waves per CU keeps W1 and the head weights in LDS; a wave owns a tile of
+// 16 envs (lane & 15 = env row) for all T + 1 steps, then its next tile.  The
+// sim is per-env, so the next observations never leave the wave: each lane
+// draws exactly the 16 features of its row that its layer-0 B fragment needs
+// (4 Philox blocks), carried in registers to the next step; env.obs is
+// written once, after the tile's last step.  The step's store writes are
+// issued after the next step's first-layer weight loads (vmcnt counts loads
+// and stores in issue order: a load behind stores waits for them).
+// Same counters and arithmetic order as the feature-split rollout kernel for
+// the sim, sampling, post-step and stores; the trunk and heads accumulate in
+// another order (16x16x32 MFMAs), so logits can differ by a bf16 ulp and a
+// sampled action can differ where two perturbed logits tie that closely.
+#pragma once
+
+// Action of one group by Gumbel-max over the bf16 logits of a row in LDS
+// (o0: first logit, nb: group size) with the noise of flattened logit j from
+// Philox {env, j / 4, step} (one block per quad, cached): the values
+// sample_group / pick_group (dists.h) form, bit for bit.
+__device__ inline void r16_pick(const bf16* lr, int o0, int nb, uint32_t ge, uint64_t step,
+                                uint32_t k0, uint32_t k1, int& act, float& lp) {
+#pragma clang fp contract(off)
+    float mx = to_f32(lr[o0]);
+    for (int j = 1; j < nb; ++j) mx = fmaxf(mx, to_f32(lr[o0 + j]));
+    float se = 0.f;
+    for (int j = 0; j < nb; ++j) se += __expf(to_f32(lr[o0 + j]) - mx);
+    const float lse = mx + __logf(se);
+    int best = 0, qc = -1;
+    float bv = 0.f;
+    u32x4 w{0u, 0u, 0u, 0u};
+    for (int j = 0; j < nb; ++j) {
+        const int jj = o0 + j;
+        if ((jj >> 2) != qc) {
+            qc = jj >> 2;
+            w = philox4x32(u32x4{ge, (uint32_t)qc, (uint32_t)step, (uint32_t)(step >> 32)}, k0, k1);
+        }
+        const float v = to_f32(lr[jj]) + det_gumbel(u32_to_unit(u32x4_get(w, jj & 3)));
+        if (j == 0 || v > bv) {
+            bv = v;
+            best = j;
+        }
+    }
+    act = best;
+    lp = to_f32(lr[o0 + best]) - lse;
+}
+
+// The row-split rollout applies to the headline shape on the fused sim: the
+// row-split step's policy shape (rows16_eligible), at most 8 action groups
+// (two sampling tasks per lane), no observation normaliser, a whole-rollout
+// launch (max_workgroups 0) and every wave with a tile (N a multiple of 256,
+// >= 65 536 envs).
+static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf, bool rnn) {
+    return bf && !rnn && P.H == kR16H && P.L == 2 && P.HC == kR16HC && P.CB == 1 &&
+           P.D == kR16D && P.K <= 8 && !P.obs_mu && !P.obs_stats && max_wg == 0 &&
+           N % 256 == 0 && N >= 65536 && N / 16 <= 0x7fffffff;
+}
+
+__global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void rollout16_kernel(
+    PolicyK P, const float* __restrict__ obs0, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
+    const uint64_t* step_ctr, uint32_t eoff, EnvK env) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const char* w1img = smem + kR16OffW1;
+    const char* whimg = smem + kR16OffWh;
+    const float* gb = (const float*)(smem + kR16OffGb);
+    const float* hb = (const float*)(smem + kR16OffHb);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
+    int* tab = (int*)(smem + kR16OffTab);
+    r16_stage(P, smem, tid);
+    if (tid <= MLEARN_MAX_GROUPS) tab[tid] = P.off[tid];
+    __syncthreads();
+    const int* t_off = tab;
+    const int K = P.K, A = P.A;
+    constexpr int D = kR16D, DS = D / 32;
+    const uint64_t step0 = step_ctr ? *step_ctr : 0ull;
+    const int ntile = (int)(N / 16);
+    const int TW = (int)gridDim.x * kR16Waves;
+
+#pragma clang loop unroll(disable)
+    for (int tile = (int)blockIdx.x * kR16Waves + wave; tile < ntile; tile += TW) {
+        // (the lane through an opaque copy per tile: rows16 kernel, ppo_rows16.h)
+        const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
+        const int64_t n = (int64_t)tile * 16 + r;
+        const uint32_t ge = eoff + (uint32_t)n;
+        // this lane's 16 observation features (32s + 8g + j) and its env's state
+        float xo[DS][8];
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+            const float4* src = (const float4*)(obs0 + n * D + 32 * s + 8 * g);
+            const float4 a = src[0], b = src[1];
+            xo[s][0] = a.x; xo[s][1] = a.y; xo[s][2] = a.z; xo[s][3] = a.w;
+            xo[s][4] = b.x; xo[s][5] = b.y; xo[s][6] = b.z; xo[s][7] = b.w;
+        }
+        int4 st = env.state[n];
+        float eret = rk.env_returns[n];
+        // the previous step's store writes (issued behind this step's weight loads)
+        bool pend = false;
+        int pa[2] = {0, 0};
+        float plp[2] = {0.f, 0.f}, pv = 0.f, prew = 0.f, per = 0.f;
+        bool pdone = false;
+        int64_t prow = 0;
+        auto flush = [&]() {
+            if (!pend) return;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int grp = (lane + 64 * u) >> 4;
+                if (grp < K) {
+                    rk.actions[prow * K + grp] = pa[u];
+                    rk.logp[prow * K + grp] = plp[u];
+                }
+            }
+            if (g == 0) {
+                rk.values[prow] = pv;
+                rk.rewards[prow] = prew;
+                rk.dones[prow] = pdone ? 1 : 0;
+                if (rk.trace) rk.trace[prow] = per;
+            }
+            pend = false;
+        };
+#pragma clang loop unroll(disable)
+        for (int t = 0; t <= rk.T; ++t) {
+            const bool act = t < rk.T;
+            const uint64_t step = step0 + (uint64_t)t;
+            const int64_t srow = (int64_t)t * rk.ld + n;  // store row of step t
+            // ObservationsCaster: the compute-dtype cast is layer 0's B operand
+            bf16x8 xf[DS];
+#pragma unroll
+            for (int s = 0; s < DS; ++s) {
+                const u4r v = {pk_bf16(xo[s][0], xo[s][1]), pk_bf16(xo[s][2], xo[s][3]),
+                               pk_bf16(xo[s][4], xo[s][5]), pk_bf16(xo[s][6], xo[s][7])};
+                xf[s] = __builtin_bit_cast(bf16x8, v);
+            }
+            auto lda0 = [&](int ln) {
+                const bf16* w0 = (const bf16*)P.wt[0];
+                const int rr = ln & 15, gg = ln >> 4;
+                return [=](int b, int s) {
+                    const int nn = 16 * b + rr;
+                    const int64_t idx = ((int64_t)(((nn >> 5) * (D >> 4) + 2 * s + (gg >> 1)) * 64 +
+                                                   (nn & 31) + 32 * (gg & 1))) * 8;
+                    return *(const bf16x8*)(w0 + idx);
+                };
+            };
+            auto bf0 = [&](int s) { return xf[s]; };
+            uint32_t zw[kR16NB][2], aw[kR16NB][2];
+            float mean, rstd;
+            r16_fwd_layer<DS, kR16Ring0>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
+            // the store rows of step t - 1 and this step's observations (behind
+            // this step's weight loads)
+            flush();
+            if (act && rk.obs) {
+                bf16* orow = (bf16*)rk.obs + r16_late(srow) * D;
+#pragma unroll
+                for (int s = 0; s < DS; ++s)
+                    r16_st16(orow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
+            }
+            r16_ln_apply(zw, mean, rstd, gb, g, aw);
+            r16_fwd_layer<kR16KS, kR16Ring>(
+                [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
+                [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
+            r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
+            // heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
+            f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            r16_mm<2, kR16KS, 4>(ha,
+                                 [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
+                                 [&](int s) { return r16_bfrag(aw, s); });
+            {
+                bf16* lr = lgs + r * kR16LGS;
+#pragma unroll
+                for (int cbk = 0; cbk < 2; ++cbk) {
+                    const int c0 = 16 * cbk + 4 * g;
+                    float v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        v[i] = rnd<bf16>(rnd<bf16>(ha[cbk][i]) + rnd<bf16>(hb[c0 + i]));
+                    *(u2r*)(lr + c0) = u2r{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
+                }
+            }
+            wave_lds_sync();
+            const float value = to_f32(lgs[r * kR16LGS + A]);
+            if (!act) {  // the bootstrap critic (rollouts.py:607-635)
+                if (g == 0) rk.bootstrap[n] = value;
+                break;
+            }
+            // the sim's next observations: drawn from the state before the
+            // advance (env.h), the quads of this lane's B fragment
+            const uint64_t es = env_step_of(st);
+#pragma unroll
+            for (int s = 0; s < DS; ++s)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const u32x4 w = env_obs_words(env.k0, env.k1, ge, 8 * s + 2 * g + hh, es);
+                    xo[s][4 * hh + 0] = env_obs_word(w.x);
+                    xo[s][4 * hh + 1] = env_obs_word(w.y);
+                    xo[s][4 * hh + 2] = env_obs_word(w.z);
+                    xo[s][4 * hh + 3] = env_obs_word(w.w);
+                }
+            // sampling: task (row r, group (lane + 64u) >> 4)
+            int a0 = 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int grp = (lane + 64 * u) >> 4;
+                pa[u] = 0;
+                plp[u] = 0.f;
+                if (grp < K) {
+                    const int o0 = t_off[grp];
+                    r16_pick(lgs + r * kR16LGS, o0, t_off[grp + 1] - o0, ge, step, k0, k1, pa[u],
+                             plp[u]);
+                }
+                if (u == 0) a0 = pa[0];  // lanes 0..15: group 0 of row r
+            }
+            // the sim step and _post_step_cb of env n (lane g == 0 holds its
+            // first action); every lane advances its copy of the env counter
+            float rew;
+            bool done;
+            const int4 ns = env_advance_vals(ge, env.k0, env.k1, (float)a0, st, rew, done);
+            float er;
+            {
+#pragma clang fp contract(off)
+                er = rew + rk.gamma * eret;
+            }
+            eret = done ? 0.f : er;
+            st = ns;
+            pend = true;
+            pv = value;
+            prew = rew;
+            pdone = done;
+            per = er;
+            prow = srow;
+            wave_lds_sync();  // the logits scratch is rewritten by the next step
+        }
+        flush();
+        // the env's state after the rollout: observations, state, running return
+        {
+            float* orow = env.obs + n * D;
+#pragma unroll
+            for (int s = 0; s < DS; ++s) {
+                float4* dst = (float4*)(orow + 32 * s + 8 * g);
+                dst[0] = make_float4(xo[s][0], xo[s][1], xo[s][2], xo[s][3]);
+                dst[1] = make_float4(xo[s][4], xo[s][5], xo[s][6], xo[s][7]);
+            }
+            if (g == 0) {
+                env.state[n] = st;
+                env.rew[n] = prew;
+                env.done[n] = pdone ? 1 : 0;
+                rk.env_returns[n] = eret;
+            }
+        }
+    }
+}
+
+static int launch_rollout16(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
+                            uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
+                            const EnvK& env, hipStream_t s) {
+    static bool attr_set = false;
+    static int cus = 0;
+    if (!attr_set) {  // once (kept out of graph capture)
+        (void)hipFuncSetAttribute((const void*)rollout16_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        attr_set = true;
+    }
+    const int64_t waves = N / 16;
+    int64_t grid = cus > 0 ? cus : 256;
+    if (grid * kR16Waves > waves) grid = waves / kR16Waves;
+    hipLaunchKernelGGL(rollout16_kernel, dim3((unsigned)grid), dim3(64 * kR16Waves), kR16Lds, s, P,
+                       obs, N, rk, k0, k1, step_ctr, eoff, env);
+    return check_launch("policy_rollout_env (row split)");
+}

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -116,7 +116,7 @@ class RolloutOut(Structure):  # mlearn_rollout_out
                 ("env_returns_trace", c_void_p), ("bootstrap", c_void_p),
                 ("env_returns", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
                 ("T", c_int32), ("bptt_len", c_int32), ("ld", c_int64), ("gamma", c_float),
-                ("max_workgroups", c_int32)]
+                ("max_workgroups", c_int32), ("policy_kernel", c_int32)]
 
 
 _S = c_void_p  # hipStream_t
@@ -166,6 +166,8 @@ _SIGNATURES = {
                                             c_uint32, POINTER(DummyEnv), _S]),
     "mlearn_policy_rollout_workgroups": (c_int64, [POINTER(MlpPolicy), POINTER(Lstm), c_int64,
                                                    c_int32]),
+    "mlearn_policy_rollout_kernel": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), c_int64, c_int32,
+                                               c_int32]),
     "mlearn_policy_pop_bytes": (c_int64, [c_int32]),
     "mlearn_policy_pop_prepare": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), POINTER(LstmCarry),
                                             _P, c_int64, POINTER(RolloutOut), _P,

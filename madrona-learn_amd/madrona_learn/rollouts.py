@@ -237,10 +237,15 @@ class RolloutManager:  # rollouts.py:373-826
     tiles (mlearn_policy_rollout_env_pop), so P launches of B / 32 workgroups
     each become one that fills the chip; False issues one launch per policy.
     A ``rollout_workgroups`` cap > 0 caps that launch too (tiles of several
-    policies in series per workgroup).  Same bits either way."""
+    policies in series per workgroup).  Same bits either way.
+    ``rollout_kernel`` is mlearn_rollout_out.policy_kernel of the whole-rollout
+    launch: 0 the library's choice (the row-split rollout at the headline
+    shape, include/mlearn.h), 1 the feature-split kernel (the per-step
+    launches' body: bit-identical to them), 2 the row-split kernel."""
 
     whole_rollout = True
     rollout_workgroups = 0
+    rollout_kernel = 0
     population_launch = True
 
     def __init__(self, train_cfg, init_rollout_state: RolloutState, policy_states, env_offset=0):
@@ -552,6 +557,7 @@ class RolloutManager:  # rollouts.py:373-826
             o.T, o.bptt_len, o.ld, o.gamma = self.T, self.bptt, self.N, gamma
             self._routs[key] = o
         o.max_workgroups = int(self.rollout_workgroups)
+        o.policy_kernel = int(self.rollout_kernel)
         return o
 
     def _finish(self, train_state_mgr, rollout_state, metrics, user_hooks):

@@ -266,14 +266,21 @@ def test_lstm_8192_rollout_and_update(gpu):
     assert int(ts.step.item()) == N // mb
 
 
-def test_headline_rollout_tiles_in_series(gpu):
-    """The headline (BASELINE metric) rollout: 65,536 envs = 2,048 env tiles
-    on fewer resident workgroups, so mlearn_policy_rollout_env runs several
-    tiles in series per workgroup, reusing the parameters it staged in LDS
-    once.  Env tiles of the second and third rounds (and the last tile) are
-    replayed on the oracle env + policy: obs / rewards / dones / GAE bit-exact,
-    values / log-probs within the bf16 tolerance, sampled actions equal to the
-    oracle's wherever the Gumbel margin is clear."""
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_headline_rollout_tiles_in_series(gpu, kernel):
+    """The headline (BASELINE metric) rollout, 65,536 envs, on both rollout
+    kernels (mlearn_rollout_out.policy_kernel):
+      1 feature split: 2,048 32-env tiles on fewer resident workgroups, so
+        every workgroup runs several tiles in series, reusing the parameters
+        it staged in LDS once;
+      2 row split (the library's choice here): 4,096 16-env tiles over one
+        8-wave workgroup per CU, two in series per wave, the sim's next
+        observations carried in registers and written to the env once.
+    32-env windows of the second tile round (and the last one) are replayed on
+    the oracle env + policy: obs / rewards / dones / GAE bit-exact, values /
+    log-probs within the bf16 tolerance, sampled actions equal to the oracle's
+    wherever the Gumbel margin is clear, and the env's observations, state
+    and rewards after the rollout bit-exact."""
     from madrona_learn import _native as nat
     from madrona_learn.envs import DummyVecEnv
     import madrona_learn as ml
@@ -285,19 +292,28 @@ def test_headline_rollout_tiles_in_series(gpu):
                            use_graph=False)
     ps = mgr.state.policy_states
     rm = mgr.rollout_mgr
-    grid = nat.lib().mlearn_policy_rollout_workgroups(ps.desc, None, N, 0)
-    tiles = N // 32
-    assert 0 < grid < tiles, (grid, tiles)
-    per = -(-tiles // grid)
-    assert per >= 2
+    rm.rollout_kernel = kernel
+    L_ = nat.lib()
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N, 0, 0) == 2  # auto: row split
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N, 0, kernel) == kernel
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N, 2, 2) == -1  # capped: no row split
+    if kernel == 1:
+        grid = L_.mlearn_policy_rollout_workgroups(ps.desc, None, N, 0)
+        tiles = N // 32
+        assert 0 < grid < tiles, (grid, tiles)
+        assert -(-tiles // grid) >= 2
+        picks = [grid + 3, tiles - 1] + ([2 * grid + 5] if 2 * grid + 5 < tiles else [])
+        windows = [t * 32 for t in picks]
+    else:
+        waves = torch.cuda.get_device_properties(gpu).multi_processor_count * 8
+        assert N // 16 >= 2 * waves
+        windows = [(16 * (waves + 7)) // 32 * 32, N - 32, (16 * waves) // 32 * 32 + 32 * 40]
     p0 = ps.params.cpu().numpy().astype(np.float64)
     mgr.update_iter()
     torch.cuda.synchronize()
     s = rm.store
     lay = ref.param_layout(D, H, 2, 26)
-    picks = [grid + 3, tiles - 1] + ([2 * grid + 5] if 2 * grid + 5 < tiles else [])
-    for tile in picks:
-        e0 = tile * 32
+    for e0 in windows:
         c = slice(e0, e0 + 32)
         oenv = onat.Env(32, D, env.k0, env.k1, e0)
         oenv.reset()
@@ -313,5 +329,11 @@ def test_headline_rollout_tiles_in_series(gpu):
             sl = noisy[..., off:off + nb]
             srt = np.sort(sl, -1)
             clear = (srt[..., -1] - srt[..., -2]) > 1e-2
-            assert np.array_equal(np.argmax(sl, -1)[clear], acts[..., g][clear]), (tile, g)
+            assert np.array_equal(np.argmax(sl, -1)[clear], acts[..., g][clear]), (e0, g)
             off += nb
+        # the env after the rollout (the row split writes it once, at the end)
+        assert np.array_equal(env.obs[c].cpu().numpy(), oenv.obs), e0
+        assert np.array_equal(env.state[c].cpu().numpy(), oenv.state), e0
+        assert np.array_equal(env.rewards[c].cpu().numpy().reshape(-1), oenv.rew), e0
+        assert np.array_equal(env.dones[c].cpu().numpy().reshape(-1).astype(np.uint8),
+                              oenv.done), e0
