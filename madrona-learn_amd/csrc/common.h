@@ -53,13 +53,14 @@ __host__ __device__ inline u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
-        uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        // (the full 64-bit products: one v_mad_u64_u32 each instead of a
+        // v_mul_hi_u32 + v_mul_lo_u32 pair, both quarter-rate)
+        const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
         u32x4 n;
-        n.x = hi1 ^ c.y ^ k0;
-        n.y = lo1;
-        n.z = hi0 ^ c.w ^ k1;
-        n.w = lo0;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
         c = n;
         k0 += W0;
         k1 += W1;
