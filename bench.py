@@ -184,13 +184,13 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     sk = int(L.mlearn_ppo_step_kernel(ps.desc, M, int(algo.hp.step_kernel)))
     if sk == 2:
         kname = "ppo_rows16_kernel<false> (row-split)"
-        mangled = ("ppo_rows16_kernelILb0",)
+        mangled = ("ppo_rows16_kernel",)
         traffic, pmc_name = pmc_traffic("ppo_rows16")
     else:
         kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1> (feature-split)"
         mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
         traffic, pmc_name = pmc_traffic("ppo_step")
-    if pmc_name is None or not all(m in pmc_name for m in mangled):
+    if pmc_name is None or not all(m in pmc_name for m in mangled) or "<true>" in pmc_name or "ILb1" in pmc_name:
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {
         "kernel": f"{kname} (mlearn_ppo_minibatch_fwd_bwd)",

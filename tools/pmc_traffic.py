@@ -14,11 +14,11 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/pmc_summary.json"
-KEYS = {"ppo_step": r"ppo_step_kernel", "ppo_rows16": r"ppo_rows16_kernel", "wgrad": r"wgrad_kernel", "policy_step": r"policy_step_kernel", "policy_rollout": r"policy_rollout_kernel",
+KEYS = {"ppo_step": r"ppo_step_kernel", "ppo_rows16": r"ppo_rows16_kernel(<false>|ILb0)", "ppo_rows16_metrics": r"ppo_rows16_kernel(<true>|ILb1)", "wgrad": r"wgrad_kernel", "policy_step": r"policy_step_kernel", "policy_rollout": r"policy_rollout_kernel",
         "gae": r"gae_kernel", "reduce_grads": r"reduce_grads_kernel", "env_step": r"env_step_kernel",
         "adam": r"adam_kernel", "project": r"project_kernel", "sumsq": r"sumsq_partial_kernel",
         "optim": r"optim_fused_kernel", "lstm_fwd_step": r"lstm_fwd_step", "lstm_bwd_step": r"lstm_bwd_step",
-        "lstm_gin": r"lstm_gin_kernel", "lstm_dfeat": r"lstm_dfeat_kernel"}
+        "lstm_gin": r"lstm_gin_kernel", "rollout16": r"rollout16_kernel", "lstm_dfeat": r"lstm_dfeat_kernel"}
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 names = {}
 for f in sorted(glob.glob(f"{root}/p*/*counter_collection.csv")):
