@@ -1043,8 +1043,8 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
                                         policy->dtype == MLEARN_DTYPE_BF16, lstm != nullptr);
     ML_REQUIRE(out->policy_kernel != 2 || r16,
                "policy_rollout_env: policy_kernel 2 (row split) needs the row-split step's policy "
-               "shape, <= 8 action groups, no observation normaliser, max_workgroups 0 and N a "
-               "multiple of 256, >= 65536");
+               "shape, <= 8 action groups, no observation normaliser, max_workgroups 0 and N of "
+               "32768 or a multiple of 256 from 65536");
     if (r16 && out->policy_kernel != 1)
         return launch_rollout16(P, obs, N, rk, k0, k1, step_ctr, env_offset, ek, s);
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \

@@ -1095,7 +1095,7 @@ __device__ inline void loss_block(const WsK& ws, const HpK& hp, int64_t M, int K
         const int kind = (s < 16) ? (s & 3) : 0;
         v[s] = kind == 2 ? 3.4e38 : (kind == 3 ? -3.4e38 : 0.0);
     }
-    for (int t = tid; t < ws.ntiles; t += 256) {
+    for (int t = tid; t < ws.nlp; t += 256) {
 #pragma unroll
         for (int s = 0; s < kLossSlots; ++s) {
             const int kind = (s < 16) ? (s & 3) : 0;
@@ -1202,9 +1202,11 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     ML_REQUIRE(h.step_kernel >= 0 && h.step_kernel <= 2, "ppo: step_kernel %d", h.step_kernel);
     ML_REQUIRE(h.step_kernel != 2 || rows16,
                "ppo: step_kernel 2 (row-split) needs bf16, hidden 256, 2 layers, a scalar critic, "
-               "head width 32, obs_dim 64, <= 7 action groups and >= 65536 rows in multiples of 256");
+               "head width 32, obs_dim 64, <= 7 action groups and (padded) rows of 32768 or a "
+               "multiple of 256 from 65536");
     if (rows16 && h.step_kernel != 1) {
         ws.ncp = 2 * ws.ntiles;  // one column-partials row per 16-row tile
+        if (rows16_cfg(ws.Mp).nt == 1) ws.nlp = 2 * ws.ntiles;  // one loss-partials row per wave
         launch_rows16(P, R, mb_seq, mb, M, adv_st, hp, ws, s);
     } else {
         switch (p.num_layers) {

@@ -73,7 +73,7 @@ struct WsK {
     void* dz[MLEARN_MAX_LAYERS];        // [Mp][H]  d loss / d Dense outputs
     float* colpart;                     // [tiles][CP] per-tile column partials
     float* colpart2;                    // [kColChunks][CP]
-    double* loss_part;                  // [tiles][kLossSlots]
+    double* loss_part;                  // [2 tiles][kLossSlots]
     float* slab;                        // split-K partial weight gradients
     int64_t slab_off[kMaxJobs];         // jobs: W_0..W_{L-1}, head, (LSTM) Wi, Wh
     int splits[kMaxJobs];
@@ -81,6 +81,8 @@ struct WsK {
     int64_t Mp;
     int ntiles;                         // Mp / 32
     int ncp;                            // colpart rows written: ntiles, 2 ntiles (row-split step)
+    int nlp;                            // loss_part rows written: ntiles, 2 ntiles (row-split
+                                        // step with one 16-row tile per wave)
     int CP;                             // L*2*H + 32
     uint64_t* stamps;                   // diagnostic builds only (ML_STAMPS): [tiles][16]
 };
@@ -165,6 +167,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     w.Mp = Mp;
     w.ntiles = (int)tiles;
     w.ncp = (int)tiles;
+    w.nlp = (int)tiles;
     // column partials: LayerNorm [L][2][H], head bias [32], (LSTM) bias [4H]
     const int HC = head_cols(p);
     w.CP = L * 2 * H + HC + (lstm ? 4 * H : 0);
@@ -176,7 +179,7 @@ static size_t carve(const mlearn_mlp_policy& p, int64_t M, char* base, WsK* W,
     w.dhead = take(Mp * HC * es);
     w.colpart = (float*)take(2 * tiles * w.CP * sizeof(float));  // (16-row tiles: row-split)
     w.colpart2 = (float*)take(kColChunks * w.CP * sizeof(float));
-    w.loss_part = (double*)take(tiles * kLossSlots * sizeof(double));
+    w.loss_part = (double*)take(2 * tiles * kLossSlots * sizeof(double));  // (16-row tiles: row-split)
     int64_t so = 0;
     const int njobs = L + 1 + (lstm ? 2 : 0);
     for (int l = 0; l < njobs; ++l) {

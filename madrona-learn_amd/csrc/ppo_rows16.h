@@ -192,7 +192,7 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
     do {                                                                              \
         if (ws.stamps && (tid & 63) == 0)                                             \
             for (int i_ = 0; i_ < 13; ++i_)                                           \
-                ws.stamps[((int64_t)ptile * kR16Tiles + tt) * 16 + i_] = r16_st[i_]; \
+                ws.stamps[((int64_t)ptile * NT + tt) * 16 + i_] = r16_st[i_];        \
     } while (0)
 #else
 #define R16_STAMP(i) \
@@ -203,8 +203,10 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
     } while (0)
 #endif
 
-template <bool METRICS>
-__global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void ppo_rows16_kernel(
+// NW waves per workgroup (8: two per SIMD; 4 or 2: one per SIMD), NT 16-row
+// tiles per wave (rows16_cfg).
+template <bool METRICS, int NW, int NT>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3) / 4, (NW + 3) / 4))) void ppo_rows16_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws, R16Div dv) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -225,6 +227,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     // permuted k, K = 256) re-laid as [out row][512 B] with swizzled 8-byte
     // units; LayerNorm scale / bias, head bias, the loss tasks' group tables
     {
+        static_assert(NW == kR16Waves, "r16_stage stages with kR16Waves waves");
         r16_stage(P, smem, tid);
         int* tab = (int*)(smem + kR16OffTab);
         if (tid <= MLEARN_MAX_GROUPS) {
@@ -242,7 +245,9 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
     const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
 
-    const int ptile = (int)blockIdx.x * kR16Waves + wave;  // 32-row partials row (= ppo_step tile)
+    // this wave's index: rows [16 NT ptile, 16 NT (ptile + 1)), loss-partials
+    // row ptile (32 rows at NT = 2 = a ppo_step tile; 16 rows at NT = 1, WsK::nlp)
+    const int ptile = (int)blockIdx.x * NW + wave;
     const float as0 = adv_st[0], as1 = adv_st[1];
     // value normaliser values, loaded once (a load in the loss loop waits on
     // the tile's stores)
@@ -275,32 +280,33 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     int64_t sr_n;  // store row of this lane's row in the next tile
     {
         uint32_t tl;
-        const int64_t rw = (int64_t)ptile * 32 + (tid & 15);
+        const int64_t rw = (int64_t)ptile * (16 * NT) + (tid & 15);
         sr_n = srow_of(rw, (uint32_t)mb_seq[slot_of(rw, tl)]);
     }
 
 #pragma clang loop unroll(disable)
-    for (int tt = 0; tt < kR16Tiles; ++tt) {
+    for (int tt = 0; tt < NT; ++tt) {
         // the lane index through an opaque copy per tile: otherwise every
         // lane-derived LDS / weight address of the body is hoisted out of the
         // tile loop and held live across it (rollout kernel)
         // the second wave of each SIMD (waves 4..7) loses issue arbitration to
         // the first throughout (tile 0 ends ~24 % later); it takes priority for
         // its last tile so the two finish closer together (-1..2 % kernel time)
-        if (tt == kR16Tiles - 1 && wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
+        // (at NW <= 4 every wave has its SIMD to itself)
+        if (NW > 4 && tt == NT - 1 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef ML_STAMPS
         uint64_t r16_st[13];
 #endif
         R16_STAMP(0);
         const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
-        const int64_t row0 = (int64_t)ptile * 32 + 16 * tt;
+        const int64_t row0 = (int64_t)ptile * (16 * NT) + 16 * tt;
         const int64_t row = row0 + r;
         const bool live = row < M;
         // (sr_n is VALU-written: reading it here needs no vmcnt wait, which the
         // loop header would otherwise take in full, stores included)
         const int64_t sr = sr_n;
         uint32_t seq_n = 0;
-        if (tt + 1 < kR16Tiles) {
+        if (tt + 1 < NT) {
             uint32_t tl;
             seq_n = (uint32_t)mb_seq[slot_of(row + 16, tl)];
         }
@@ -455,9 +461,9 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         if ((uintptr_t)ws.dhead == 1)
 #endif
         r16_st16((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g, __builtin_bit_cast(u4r, dh));
-        // column partials of this 16-row tile (colpart row 2 ptile + tt, WsK::ncp):
+        // column partials of this 16-row tile (colpart row NT ptile + tt, WsK::ncp):
         // head bias here, LayerNorm bias / scale in the layer backwards
-        float* cprow = ws.colpart + ((int64_t)ptile * kR16Tiles + tt) * ws.CP;
+        float* cprow = ws.colpart + ((int64_t)ptile * NT + tt) * ws.CP;
         if (lane < kR16HC) {
             float hbs = 0.f;
 #pragma unroll
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
         __builtin_amdgcn_s_waitcnt(0);
         const uint64_t t_end = __builtin_amdgcn_s_memtime();
         if (ws.stamps && (tid & 63) == 0) {
-            uint64_t* st = ws.stamps + (int64_t)ptile * kR16Tiles * 16;
+            uint64_t* st = ws.stamps + (int64_t)ptile * NT * 16;
             st[13] = r16_t_entry;
             st[14] = r16_t_pro;
             st[15] = t_end;
@@ -548,33 +554,58 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 }
 
 // The row-split kernel runs the bf16, H = 256, two-layer, scalar-critic step
-// when every CU gets at least one workgroup (one workgroup = 256 rows).
+// in a shape that gives every CU one 8-wave workgroup: 2 tiles per wave (256
+// rows per workgroup) from 65 536 rows, 1 tile per wave at exactly 32 768
+// rows (a two-rank data-parallel slice); nw = 0 where it does not apply.
+// (Measured and not kept, profiles/r05_rank_slices_ab.txt: 4 x 1 and 2 x 1
+// waves x tiles at 16 384 / 8 192 rows, one wave per SIMD: 32.4 / 30.3 us
+// against the feature split's 19.6 us at 8 192 rows -- a lone wave exposes
+// its whole tile chain.)
+struct R16Cfg {
+    int nw, nt;
+};
+static R16Cfg rows16_cfg(int64_t Mp) {
+    constexpr int64_t kCUs = 256;  // MI355X
+    if (Mp % 256 == 0 && Mp / 256 >= kCUs) return R16Cfg{8, 2};
+    if (Mp == 128 * kCUs) return R16Cfg{8, 1};  // exactly one round of workgroups
+    return R16Cfg{0, 0};
+}
 static bool rows16_eligible(const PolicyK& P, int64_t Mp, int HC, int L, int H, bool bf) {
     return bf && H == kR16H && L == 2 && HC == kR16HC && P.CB == 1 && P.D == kR16D &&
-           P.K + 1 <= 8 && Mp % (32 * kR16Waves) == 0 &&
-           Mp / (32 * kR16Waves) >= 256;
+           P.K + 1 <= 8 && rows16_cfg(Mp).nw > 0;
 }
 
+template <int NW, int NT>
+static void launch_rows16_cfg(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
+                              int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
+                              const R16Div& dv, hipStream_t s) {
+    static bool attr_set = false;  // once per shape (kept out of graph capture)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<true, NW, NT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<false, NW, NT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        attr_set = true;
+    }
+    const int grid = (int)(ws.Mp / (16 * NW * NT));
+    if (hp.metrics)
+        hipLaunchKernelGGL((ppo_rows16_kernel<true, NW, NT>), dim3(grid), dim3(64 * NW), kR16Lds, s,
+                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
+    else
+        hipLaunchKernelGGL((ppo_rows16_kernel<false, NW, NT>), dim3(grid), dim3(64 * NW), kR16Lds, s,
+                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
+}
+
+// (the caller sets ws.ncp / ws.nlp to the row-split partial-row counts)
 static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                           int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                           hipStream_t s) {
     R16Div dv;
     r16_magic((uint32_t)mb, dv.mb_mag, dv.mb_sh);
     r16_magic((uint32_t)R.N, dv.n_mag, dv.n_sh);
-    static bool attr_set = false;  // once (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        attr_set = true;
-    }
-    const int grid = (int)(ws.Mp / (32 * kR16Waves));
-    if (hp.metrics)
-        hipLaunchKernelGGL(ppo_rows16_kernel<true>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s, P,
-                           R, mb_seq, mb, M, adv_st, hp, ws, dv);
+    const R16Cfg c = rows16_cfg(ws.Mp);
+    if (c.nt == 2)
+        launch_rows16_cfg<8, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
     else
-        hipLaunchKernelGGL(ppo_rows16_kernel<false>, dim3(grid), dim3(64 * kR16Waves), kR16Lds, s,
-                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
+        launch_rows16_cfg<8, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
 }
-

@@ -53,18 +53,31 @@ __device__ inline void r16_pick(const bf16* lr, int o0, int nb, uint32_t ge, uin
     lp = to_f32(lr[o0 + best]) - lse;
 }
 
-// The row-split rollout applies to the headline shape on the fused sim: the
-// row-split step's policy shape (rows16_eligible), at most 8 action groups
-// (two sampling tasks per lane), no observation normaliser, a whole-rollout
-// launch (max_workgroups 0) and every wave with a tile (N a multiple of 256,
-// >= 65 536 envs).
+// Waves per workgroup of the row-split rollout for N envs (one workgroup per
+// CU): 8 from 65 536 envs in multiples of 256 (tiles in series beyond 2 048
+// tiles) and at exactly 32 768 (one 16-env tile per wave: a two-rank
+// data-parallel shard); 0 otherwise.  (4 and 2 waves at 16 384 / 8 192 envs,
+// one wave per SIMD, measured no faster than the feature-split kernel: 363
+// vs 361 us per rollout at 8 192, profiles/r05_rank_slices_ab.txt.)
+static int rollout16_waves(int64_t N) {
+    constexpr int64_t kCUs = 256;  // MI355X
+    if (N % 256 == 0 && N >= 65536 && N / 16 <= 0x7fffffff) return 8;
+    if (N == 16 * 8 * kCUs) return 8;
+    return 0;
+}
+
+// The row-split rollout applies on the fused sim to the row-split step's
+// policy shape (rows16_eligible), at most 8 action groups (two sampling tasks
+// per lane), no observation normaliser, a whole-rollout launch (max_workgroups
+// 0) and the env counts rollout16_waves takes.
 static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf, bool rnn) {
     return bf && !rnn && P.H == kR16H && P.L == 2 && P.HC == kR16HC && P.CB == 1 &&
            P.D == kR16D && P.K <= 8 && !P.obs_mu && !P.obs_stats && max_wg == 0 &&
-           N % 256 == 0 && N >= 65536 && N / 16 <= 0x7fffffff;
+           rollout16_waves(N) > 0;
 }
 
-__global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void rollout16_kernel(
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3) / 4, (NW + 3) / 4))) void rollout16_kernel(
     PolicyK P, const float* __restrict__ obs0, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
     const uint64_t* step_ctr, uint32_t eoff, EnvK env) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -76,6 +89,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
     int* tab = (int*)(smem + kR16OffTab);
+    static_assert(NW == kR16Waves, "r16_stage stages with kR16Waves waves");
     r16_stage(P, smem, tid);
     if (tid <= MLEARN_MAX_GROUPS) tab[tid] = P.off[tid];
     __syncthreads();
@@ -84,10 +98,10 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     constexpr int D = kR16D, DS = D / 32;
     const uint64_t step0 = step_ctr ? *step_ctr : 0ull;
     const int ntile = (int)(N / 16);
-    const int TW = (int)gridDim.x * kR16Waves;
+    const int TW = (int)gridDim.x * NW;
 
 #pragma clang loop unroll(disable)
-    for (int tile = (int)blockIdx.x * kR16Waves + wave; tile < ntile; tile += TW) {
+    for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW) {
         // (the lane through an opaque copy per tile: rows16 kernel, ppo_rows16.h)
         const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
         const int64_t n = (int64_t)tile * 16 + r;
@@ -258,24 +272,33 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
-static int launch_rollout16(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
-                            uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
-                            const EnvK& env, hipStream_t s) {
+template <int NW>
+static void launch_rollout16_nw(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
+                                uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
+                                const EnvK& env, int cus, hipStream_t s) {
     static bool attr_set = false;
-    static int cus = 0;
-    if (!attr_set) {  // once (kept out of graph capture)
-        (void)hipFuncSetAttribute((const void*)rollout16_kernel,
+    if (!attr_set) {  // once per shape (kept out of graph capture)
+        (void)hipFuncSetAttribute((const void*)rollout16_kernel<NW>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
         attr_set = true;
     }
     const int64_t waves = N / 16;
     int64_t grid = cus > 0 ? cus : 256;
-    if (grid * kR16Waves > waves) grid = waves / kR16Waves;
-    hipLaunchKernelGGL(rollout16_kernel, dim3((unsigned)grid), dim3(64 * kR16Waves), kR16Lds, s, P,
+    if (grid * NW > waves) grid = waves / NW;
+    hipLaunchKernelGGL((rollout16_kernel<NW>), dim3((unsigned)grid), dim3(64 * NW), kR16Lds, s, P,
                        obs, N, rk, k0, k1, step_ctr, eoff, env);
+}
+
+static int launch_rollout16(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
+                            uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
+                            const EnvK& env, hipStream_t s) {
+    static int cus = -1;
+    if (cus < 0) {  // once (kept out of graph capture)
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+    }
+    launch_rollout16_nw<8>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, cus, s);
     return check_launch("policy_rollout_env (row split)");
 }

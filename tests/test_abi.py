@@ -87,8 +87,9 @@ def test_param_count_matches_oracle_layout():
 def test_step_kernel_selection():
     """mlearn_ppo_step_kernel: the row-split step kernel exactly where it
     applies (bf16, H 256, 2 layers, scalar critic, obs 64, <= 7 action
-    groups, >= 65,536 rows in multiples of 256), the feature-split kernel
-    elsewhere; an explicit row-split request elsewhere is -1 (EINVAL)."""
+    groups, padded rows of 32,768 or a multiple of 256 from 65,536: one
+    8-wave workgroup per CU), the feature-split kernel elsewhere; an explicit
+    row-split request elsewhere is -1 (EINVAL)."""
     from madrona_learn import _native as nat
     L = nat.lib()
 
@@ -108,7 +109,10 @@ def test_step_kernel_selection():
     assert sel(d, 65536) == 2 and sel(d, 65536, 2) == 2 and sel(d, 65536, 1) == 1
     assert sel(d, 65520) == 2           # padded to 65,536 rows
     assert sel(d, 65536 * 4) == 2
-    assert sel(d, 32768) == 1 and sel(d, 32768, 2) == -1   # fewer workgroups than CUs
+    for rows in (32768, 32740):                              # the two-rank slice
+        assert sel(d, rows) == 2 and sel(d, rows, 1) == 1
+    for rows in (8192, 16384, 24576, 49152):                 # one tile per wave: not kept
+        assert sel(d, rows) == 1 and sel(d, rows, 2) == -1
     assert sel(d, 65536 + 64) == 1                           # not a multiple of 256
     for other in (desc(dtype=nat.DTYPE_F32), desc(H=128), desc(layers=3),
                   desc(buckets=(2,) * 8), desc(bins=9)):

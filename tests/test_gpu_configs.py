@@ -308,6 +308,34 @@ def test_headline_rollout_tiles_in_series(gpu, kernel):
         waves = torch.cuda.get_device_properties(gpu).multi_processor_count * 8
         assert N // 16 >= 2 * waves
         windows = [(16 * (waves + 7)) // 32 * 32, N - 32, (16 * waves) // 32 * 32 + 32 * 40]
+    _replay_windows(mgr, env, cfg, windows)
+
+
+@pytest.mark.parametrize("N", [32768])
+def test_row_split_rollout_rank_sizes(gpu, N):
+    """The row-split rollout at a two-rank data-parallel shard (32,768 envs:
+    one 8-wave workgroup per CU, one 16-env tile per wave), the library's
+    choice there: oracle windows at the start, middle and end as in the
+    headline test."""
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    import madrona_learn as ml
+    from tests.test_gpu_train import make_policy
+    mb = N // 4
+    env = DummyVecEnv(N, D, 6, seed=7, device=gpu)
+    cfg = _cfg(N, mb, seed=17)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.bfloat16, H),
+                           use_graph=False)
+    ps = mgr.state.policy_states
+    L_ = nat.lib()
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N, 0, 0) == 2
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N - 256, 0, 0) == 1
+    _replay_windows(mgr, env, cfg, [0, N // 2 + 32 * 5, N - 32])
+
+
+def _replay_windows(mgr, env, cfg, windows):
+    ps = mgr.state.policy_states
+    rm = mgr.rollout_mgr
     p0 = ps.params.cpu().numpy().astype(np.float64)
     mgr.update_iter()
     torch.cuda.synchronize()

@@ -206,12 +206,14 @@ def test_value_loss_variants(gpu, mode, dtype, clip_vl, huber, ties):
                                    atol=1e-7)
 
 
-@pytest.mark.parametrize("mb,bptt", [(2048, 32), (4095, 16)])
+@pytest.mark.parametrize("mb,bptt", [(2048, 32), (4095, 16), (1024, 32), (1023, 32)])
 def test_row_split_step_kernel(gpu, mb, bptt):
-    """The row-split step kernel (the bf16 default at >= 65,536 rows: W1 held
-    in LDS, one wave per 16-row tile, 16x16x32 MFMAs) against the oracle and
-    against the feature-split kernel (step_kernel 1) on the same minibatch;
-    (4095, 16) leaves 16 padding rows in the last workgroup.  The two kernels
+    """The row-split step kernel (the bf16 default: W1 held in LDS, one wave
+    per 16-row tile, 16x16x32 MFMAs) against the oracle and against the
+    feature-split kernel (step_kernel 1) on the same minibatch, in both of
+    its shapes: 8 waves x 2 tiles per workgroup at 65,536 rows, 8 x 1 at
+    32,768 (a two-rank data-parallel slice); (4095, 16) and (1023, 32) leave
+    padding rows.  The two kernels
     sum in different orders (f32 accumulation of the same bf16 products), so
     they agree to the bf16 bound, not bitwise."""
     T, N, D, H, L = 32, 8192, 64, 256, 2
