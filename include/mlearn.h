@@ -360,8 +360,9 @@ typedef struct mlearn_ppo_hparams {
                                               kernel where it applies: bf16, hidden 256,
                                               2 layers, scalar critic, head width 32,
                                               obs_dim 64, at most 7 action groups,
-                                              rows a multiple of 256 and >= 65536; else the
-                                              feature-split kernel), 1 = the feature-split
+                                              padded rows of exactly 32768 (one 16-row tile
+                                              per wave) or a multiple of 256 and >= 65536;
+                                              else the feature-split kernel), 1 = the feature-split
                                               kernel, 2 = the row-split kernel (EINVAL
                                               where it does not apply).  Same inputs and
                                               outputs; results within the compute dtype's
@@ -664,7 +665,8 @@ typedef struct mlearn_rollout_out {
     int32_t policy_kernel;      /* 0: the library's choice (the row-split rollout where it
                                    applies: the row-split step's policy shape, <= 8 action
                                    groups, no observation normaliser, max_workgroups 0,
-                                   N a multiple of 256 and >= 65536; else the feature-split
+                                   N of exactly 32768 or a multiple of 256 and >= 65536;
+                                   else the feature-split
                                    kernel), 1: the feature-split kernel (the per-step
                                    launches' body), 2: the row-split kernel (EINVAL where it
                                    does not apply).  The row split accumulates the trunk and
