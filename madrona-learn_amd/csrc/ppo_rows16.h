@@ -142,14 +142,8 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
             for (int k = 0; k < 2; ++k) {
                 const int step = 4 * qd + 2 * hp + k;
                 const int b = 4 * qd + ord[2 * hp + k];
-                const int bnext = step + 1 < kR16NB ? 4 * ((step + 1) / 4) + ord[(step + 1) % 4] : -1;
                 float4 G, B;
-#ifdef R16_GB_BWD_AHEAD
-                gb.take(bnext, G, B);
-#else
-                (void)bnext;
-                gb.take_now(b, G, B);
-#endif
+                gb.take_now(b, G, B);  // (read ahead, one block early: slower)
                 const float gv[4] = {G.x, G.y, G.z, G.w}, bv[4] = {B.x, B.y, B.z, B.w};
                 zw[b][0] = r16_late(zw[b][0]);
                 zw[b][1] = r16_late(zw[b][1]);
@@ -377,9 +371,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
             bf16* xrow = (bf16*)ws.x0 + r16_late(row) * D;
 #pragma unroll
             for (int s = 0; s < DS; ++s)
-#ifdef R16_ABL_NOSTORE
-                if ((uintptr_t)xrow == 1)
-#endif
                 r16_st16(xrow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
         }
         // the previous tile's layer-0 dZ rows go out behind this tile's loads
@@ -437,9 +428,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
                 loss_value(hp, lr, P.A, kR16HC, ret, oval, m, vn);
             }
         };
-#ifdef R16_ABL_NOLOSS
-        if (hp.clip > -1e30f)
-#endif
         {
             // the tasks' inputs are registers loaded at the tile's start (K + 1 <= 8
             // groups: two tasks per lane; no load in this loop, whose waits
@@ -457,9 +445,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         // ---- d head: B operand of the head backward (cols 8g .. 8g+7 of row r),
         // row-major store, head-bias column sums
         const bf16x8 dh = *(const bf16x8*)(lgs + r * kR16LGS + 8 * g);
-#ifdef R16_ABL_NOSTORE
-        if ((uintptr_t)ws.dhead == 1)
-#endif
         r16_st16((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g, __builtin_bit_cast(u4r, dh));
         // column partials of this 16-row tile (colpart row NT ptile + tt, WsK::ncp):
         // head bias here, LayerNorm bias / scale in the layer backwards
@@ -475,9 +460,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         // second pass
         R16_STAMP(7);
         uint32_t dzw[kR16NB][2];
-#ifdef R16_ABL_NOL1BWD
-        if (hp.clip < -1e30f)
-#endif
         {
             f32x4 hacc[kR16NB];
 #pragma unroll
