@@ -21,7 +21,13 @@
 
 // k-steps of weight fragments in flight per wave in the per-step scans
 // (DEPTH >= k-steps: the whole product's loads issued up front)
-constexpr int kLstmFwdDepth = 8, kLstmBwdDepth = 8;
+#ifndef ML_LSTM_FWD_DEPTH
+#define ML_LSTM_FWD_DEPTH 4  // (config L, rocprof us per step: 8 -> 11.0, 4 -> 10.5, 3 -> 10.6, 2 -> 10.9, 6 -> 10.8)
+#endif
+#ifndef ML_LSTM_BWD_DEPTH
+#define ML_LSTM_BWD_DEPTH 8  // (2 -> 14.9, 4 -> 14.7, 6 -> 14.6, 8 -> 14.7, 16 -> 16.3)
+#endif
+constexpr int kLstmFwdDepth = ML_LSTM_FWD_DEPTH, kLstmBwdDepth = ML_LSTM_BWD_DEPTH;
 
 // Forward step t with four waves per (32 sequences, 32-unit block): wave g
 // computes k-half (g & 1) of the input product F_t Wi (g < 2) or of the

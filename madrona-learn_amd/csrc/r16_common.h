@@ -23,8 +23,14 @@ constexpr int kR16KS = kR16H / 32;   // k-steps over the hidden features
 constexpr int kR16HC = MLEARN_HEAD_COLS;
 constexpr int kR16D = 64;            // observation width (the first layer's K)
 constexpr int kR16LGS = 40;          // logits scratch row stride (bf16; 80-B rows)
-constexpr int kR16Ring = 6;          // LDS A fragments in flight per product
-constexpr int kR16Ring0 = 16;        // first-layer (L2) A fragments in flight
+#ifndef ML_R16_RING
+#define ML_R16_RING 6
+#endif
+#ifndef ML_R16_RING0
+#define ML_R16_RING0 16
+#endif
+constexpr int kR16Ring = ML_R16_RING;    // LDS A fragments in flight per product
+constexpr int kR16Ring0 = ML_R16_RING0;  // first-layer (L2) A fragments in flight
 // LDS: W1 image [256 rows = out][512 B], head image [32 rows = col][512 B],
 // LayerNorm scale/bias [2][2][256] f32, head bias [32] f32, per-wave logits
 // scratch [8][16][kR16LGS] bf16, the action groups' logit offsets, entropy
