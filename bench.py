@@ -395,10 +395,14 @@ def main():
     ap.add_argument("--per-policy-rollouts", action="store_true",
                     help="config pbt: one whole-rollout launch per policy instead of the "
                          "population launch (RolloutManager.population_launch = False)")
+    ap.add_argument("--rollout-kernel", type=int, choices=[0, 1, 2], default=0,
+                    help="RolloutManager.rollout_kernel: 0 the library's choice, 1 the "
+                         "feature-split rollout kernels, 2 the row-split ones (A/B runs)")
     args = ap.parse_args()
+    from madrona_learn.rollouts import RolloutManager
     if args.per_policy_rollouts:
-        from madrona_learn.rollouts import RolloutManager
         RolloutManager.population_launch = False
+    RolloutManager.rollout_kernel = args.rollout_kernel
     if args.emulate_world > 1:
         return emulate_world(args)
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 19
+#define MLEARN_ABI_VERSION 20
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -705,9 +705,20 @@ int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0, const mlearn
                                   const void* pop, int32_t num_policies, int64_t N,
                                   uint32_t k0, uint32_t k1, const uint64_t* step_ctr,
                                   int32_t max_workgroups, mlearn_stream_t stream);
-/* Workgroups mlearn_policy_rollout_env_pop launches for num_policies x N envs
- * under max_workgroups (>= 0); -1 on a bad argument or a failed occupancy
- * query.  P * ceil(N / 32) > the result means tiles run in series. */
+/* The kernel mlearn_policy_rollout_env_pop runs for num_policies x N envs
+ * under max_workgroups (host-only, v20): 2 = the row-split rollout (the
+ * library's choice when uncapped, the row-split rollout's policy shape --
+ * see mlearn_rollout_out.policy_kernel -- with no observation normaliser, N a
+ * multiple of 128 and >= 2048 16-env tiles in all: 16-env tiles dealt in
+ * rounds of 8 per workgroup, W1 / head / LayerNorm images restaged when a
+ * workgroup's round belongs to another policy), 1 = the feature-split
+ * population kernel (every other case; max_workgroups > 0 selects it); -1 on a
+ * bad argument. */
+int32_t mlearn_policy_rollout_pop_kernel(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                         int64_t N, int32_t num_policies, int32_t max_workgroups);
+/* Workgroups the feature-split population kernel launches for num_policies x
+ * N envs under max_workgroups (>= 0); -1 on a bad argument or a failed
+ * occupancy query.  P * ceil(N / 32) > the result means tiles run in series. */
 int64_t mlearn_policy_rollout_pop_workgroups(const mlearn_mlp_policy* policy,
                                              const mlearn_lstm* lstm, int64_t N,
                                              int32_t num_policies, int32_t max_workgroups);

@@ -730,6 +730,60 @@ __global__ __launch_bounds__((pol_threads<H, RNN>())) __attribute__((amdgpu_wave
     }
 }
 
+// A population's whole rollouts on the row-split kernel (the library's
+// choice where rollout16_pop_eligible): global 16-env tile g is tile g % tpp
+// of policy g / tpp (tpp = N / 16, a multiple of 8), dealt in rounds of 8
+// consecutive tiles per workgroup, so all 8 waves of a workgroup hold tiles of
+// one policy in every round; a workgroup restages that policy's W1 / head /
+// LayerNorm images when its round's policy is not the one staged (the
+// barriers are workgroup-uniform).  Per tile the body and arguments of the
+// policy's own rollout16_kernel launch: the same bits.
+__global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(2, 2))) void rollout16_pop_kernel(
+    const PopEntry* __restrict__ pop, int npol, int64_t N, uint32_t k0, uint32_t k1,
+    const uint64_t* step_ctr) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* tab = (int*)(smem + kR16OffTab);
+    const uint64_t step0 = step_ctr ? *step_ctr : 0ull;
+    const int tpp = (int)(N / 16), ntile = npol * tpp;
+    const int TW = (int)gridDim.x * kR16Waves;
+    int cur = -1;
+#pragma clang loop unroll(disable)
+    for (int t0 = (int)blockIdx.x * kR16Waves; t0 < ntile; t0 += TW) {
+        const int p = __builtin_amdgcn_readfirstlane(t0 / tpp);
+        const PopEntry& e = pop[p];
+        if (p != cur) {
+            if (cur >= 0) __syncthreads();  // every wave is past its reads of the old images
+            r16_stage(e.P, smem, tid);
+            if (tid <= MLEARN_MAX_GROUPS) tab[tid] = e.P.off[tid];
+            __syncthreads();
+            cur = p;
+        }
+        r16_roll_tile(e.P, e.obs, e.rk, k0, k1, step0, e.eoff, e.env, t0 + wave - p * tpp, tid,
+                      smem);
+    }
+}
+
+static int launch_rollout16_pop(const PopEntry* pop, int npol, int64_t N, uint32_t k0, uint32_t k1,
+                                const uint64_t* step_ctr, hipStream_t s) {
+    static int cus = -1;
+    if (cus < 0) {  // once (kept out of graph capture)
+        (void)hipFuncSetAttribute((const void*)rollout16_pop_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+    }
+    const int64_t rounds_of_8 = (int64_t)npol * (N / 16) / kR16Waves;
+    int64_t grid = cus > 0 ? cus : 256;
+    if (grid > rounds_of_8) grid = rounds_of_8;
+    hipLaunchKernelGGL(rollout16_pop_kernel, dim3((unsigned)grid), dim3(64 * kR16Waves), kR16Lds, s,
+                       pop, npol, N, k0, k1, step_ctr);
+    return check_launch("policy_rollout_env_pop (row split)");
+}
+
 template <typename T, int H, bool RNN, int HC, int MAXW = ML_POL_MAXW>
 static size_t policy_step_lds(int L) {
     typedef PolCfg<H, MAXW> C;
@@ -1100,6 +1154,9 @@ extern "C" int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies,
         if (rc) return rc;
         ML_REQUIRE(outs[p].max_workgroups == 0,
                    "policy_pop_prepare: the population launch has its own grid (max_workgroups 0)");
+        ML_REQUIRE(!a.obs_mu == !b.obs_mu && !a.obs_stats == !b.obs_stats,
+                   "policy_pop_prepare: policy %d's observation normaliser differs from policy 0's",
+                   p);
     }
     // ordered after the caller's earlier work on its stream (a previous
     // population launch may still read the buffer), and complete on return
@@ -1127,6 +1184,9 @@ extern "C" int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0,
     const int L = policy0->num_layers, HC = head_cols(*policy0);
     const PopEntry* e = (const PopEntry*)pop;
     hipStream_t s = S(stream);
+    if (rollout16_pop_eligible(make_policy_k(*policy0), N, num_policies, max_workgroups,
+                               policy0->dtype == MLEARN_DTYPE_BF16, lstm0 != nullptr))
+        return launch_rollout16_pop(e, num_policies, N, k0, k1, step_ctr, s);
 #define ML_POP_HC(T, HH, HCC)                                                                   \
     (lstm0 ? launch_policy_rollout_pop<T, HH, true, HCC>(L, e, num_policies, N, k0, k1, step_ctr, \
                                                        max_workgroups, s)                     \
@@ -1148,6 +1208,19 @@ extern "C" int mlearn_policy_rollout_env_pop(const mlearn_mlp_policy* policy0,
 #undef ML_DISPATCH
 #undef ML_POP
 #undef ML_POP_HC
+}
+
+extern "C" int32_t mlearn_policy_rollout_pop_kernel(const mlearn_mlp_policy* policy,
+                                                    const mlearn_lstm* lstm, int64_t N,
+                                                    int32_t num_policies,
+                                                    int32_t max_workgroups) {
+    if ((lstm ? validate_lstm(policy, lstm) : validate_policy(policy)) || N < 1 ||
+        num_policies < 1 || max_workgroups < 0)
+        return -1;
+    return rollout16_pop_eligible(make_policy_k(*policy), N, num_policies, max_workgroups,
+                                  policy->dtype == MLEARN_DTYPE_BF16, lstm != nullptr)
+               ? 2
+               : 1;
 }
 
 extern "C" int64_t mlearn_policy_rollout_pop_workgroups(const mlearn_mlp_policy* policy,

@@ -356,7 +356,7 @@ __device__ inline void r16_stage(const PolicyK& P, char* smem, int tid) {
 // (mulhi(n, mag) + n) >> sh == n / d for n < 2^31: sh = ceil(log2 d),
 // mag = floor(2^32 (2^sh - d) / d) + 1 (tests/test_gpu_fullsize.py covers
 // d = 4095 and powers of two)
-static void r16_magic(uint32_t d, uint32_t& mag, int& sh) {
+static inline void r16_magic(uint32_t d, uint32_t& mag, int& sh) {
     int l = 0;
     while ((1ull << l) < d) ++l;
     mag = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);

@@ -70,10 +70,208 @@ static int rollout16_waves(int64_t N) {
 // policy shape (rows16_eligible), at most 8 action groups (two sampling tasks
 // per lane), no observation normaliser, a whole-rollout launch (max_workgroups
 // 0) and the env counts rollout16_waves takes.
-static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf, bool rnn) {
+static bool rollout16_shape(const PolicyK& P, bool bf, bool rnn) {
     return bf && !rnn && P.H == kR16H && P.L == 2 && P.HC == kR16HC && P.CB == 1 &&
-           P.D == kR16D && P.K <= 8 && !P.obs_mu && !P.obs_stats && max_wg == 0 &&
-           rollout16_waves(N) > 0;
+           P.D == kR16D && P.K <= 8 && !P.obs_mu && !P.obs_stats;
+}
+static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf, bool rnn) {
+    return rollout16_shape(P, bf, rnn) && max_wg == 0 && rollout16_waves(N) > 0;
+}
+// A population's rollouts on the row-split kernel (rollout16_pop_kernel,
+// policy.hip): every policy of that shape (mlearn_policy_pop_prepare checks
+// they agree), uncapped, N a multiple of 128 (so the 8 waves of a workgroup
+// hold tiles of one policy in every round) and every wave of the chip with a
+// tile (>= 2 048 16-env tiles in all).
+static bool rollout16_pop_eligible(const PolicyK& P0, int64_t N, int npol, int max_wg, bool bf,
+                                   bool rnn) {
+    const int64_t tiles = (int64_t)npol * (N / 16);
+    return rollout16_shape(P0, bf, rnn) && max_wg == 0 && N % 128 == 0 && tiles >= 2048 &&
+           tiles <= 0x7fffffff;
+}
+
+// One 16-env tile's whole rollout on one wave: T policy steps with the sim
+// step and post-step fused, then the bootstrap critic; the policy's W1 /
+// head / LayerNorm images and action-group table already staged in smem.
+__device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __restrict__ obs0,
+                                              const RollK& rk, uint32_t k0, uint32_t k1,
+                                              uint64_t step0, uint32_t eoff, const EnvK& env,
+                                              int tile, int tid, char* smem) {
+    const char* w1img = smem + kR16OffW1;
+    const char* whimg = smem + kR16OffWh;
+    const float* gb = (const float*)(smem + kR16OffGb);
+    const float* hb = (const float*)(smem + kR16OffHb);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
+    const int* t_off = (const int*)(smem + kR16OffTab);
+    const int K = P.K, A = P.A;
+    constexpr int D = kR16D, DS = D / 32;
+    // (the lane through an opaque copy per tile: rows16 kernel, ppo_rows16.h)
+    const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
+    const int64_t n = (int64_t)tile * 16 + r;
+    const uint32_t ge = eoff + (uint32_t)n;
+    // this lane's 16 observation features (32s + 8g + j) and its env's state
+    float xo[DS][8];
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+        const float4* src = (const float4*)(obs0 + n * D + 32 * s + 8 * g);
+        const float4 a = src[0], b = src[1];
+        xo[s][0] = a.x; xo[s][1] = a.y; xo[s][2] = a.z; xo[s][3] = a.w;
+        xo[s][4] = b.x; xo[s][5] = b.y; xo[s][6] = b.z; xo[s][7] = b.w;
+    }
+    int4 st = env.state[n];
+    float eret = rk.env_returns[n];
+    // the previous step's store writes (issued behind this step's weight loads)
+    bool pend = false;
+    int pa[2] = {0, 0};
+    float plp[2] = {0.f, 0.f}, pv = 0.f, prew = 0.f, per = 0.f;
+    bool pdone = false;
+    int64_t prow = 0;
+    auto flush = [&]() {
+        if (!pend) return;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int grp = (lane + 64 * u) >> 4;
+            if (grp < K) {
+                rk.actions[prow * K + grp] = pa[u];
+                rk.logp[prow * K + grp] = plp[u];
+            }
+        }
+        if (g == 0) {
+            rk.values[prow] = pv;
+            rk.rewards[prow] = prew;
+            rk.dones[prow] = pdone ? 1 : 0;
+            if (rk.trace) rk.trace[prow] = per;
+        }
+        pend = false;
+    };
+#pragma clang loop unroll(disable)
+    for (int t = 0; t <= rk.T; ++t) {
+        const bool act = t < rk.T;
+        const uint64_t step = step0 + (uint64_t)t;
+        const int64_t srow = (int64_t)t * rk.ld + n;  // store row of step t
+        // ObservationsCaster: the compute-dtype cast is layer 0's B operand
+        bf16x8 xf[DS];
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+            const u4r v = {pk_bf16(xo[s][0], xo[s][1]), pk_bf16(xo[s][2], xo[s][3]),
+                           pk_bf16(xo[s][4], xo[s][5]), pk_bf16(xo[s][6], xo[s][7])};
+            xf[s] = __builtin_bit_cast(bf16x8, v);
+        }
+        auto lda0 = [&](int ln) {
+            const bf16* w0 = (const bf16*)P.wt[0];
+            const int rr = ln & 15, gg = ln >> 4;
+            return [=](int b, int s) {
+                const int nn = 16 * b + rr;
+                const int64_t idx = ((int64_t)(((nn >> 5) * (D >> 4) + 2 * s + (gg >> 1)) * 64 +
+                                               (nn & 31) + 32 * (gg & 1))) * 8;
+                return *(const bf16x8*)(w0 + idx);
+            };
+        };
+        auto bf0 = [&](int s) { return xf[s]; };
+        uint32_t zw[kR16NB][2], aw[kR16NB][2];
+        float mean, rstd;
+        r16_fwd_layer<DS, kR16Ring0>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
+        // the store rows of step t - 1 and this step's observations (behind
+        // this step's weight loads)
+        flush();
+        if (act && rk.obs) {
+            bf16* orow = (bf16*)rk.obs + r16_late(srow) * D;
+#pragma unroll
+            for (int s = 0; s < DS; ++s)
+                r16_st16(orow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
+        }
+        r16_ln_apply(zw, mean, rstd, gb, g, aw);
+        r16_fwd_layer<kR16KS, kR16Ring>(
+            [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
+            [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
+        r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
+        // heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
+        f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        r16_mm<2, kR16KS, 4>(ha,
+                             [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
+                             [&](int s) { return r16_bfrag(aw, s); });
+        {
+            bf16* lr = lgs + r * kR16LGS;
+#pragma unroll
+            for (int cbk = 0; cbk < 2; ++cbk) {
+                const int c0 = 16 * cbk + 4 * g;
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[i] = rnd<bf16>(rnd<bf16>(ha[cbk][i]) + rnd<bf16>(hb[c0 + i]));
+                *(u2r*)(lr + c0) = u2r{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
+            }
+        }
+        wave_lds_sync();
+        const float value = to_f32(lgs[r * kR16LGS + A]);
+        if (!act) {  // the bootstrap critic (rollouts.py:607-635)
+            if (g == 0) rk.bootstrap[n] = value;
+            break;
+        }
+        // the sim's next observations: drawn from the state before the
+        // advance (env.h), the quads of this lane's B fragment
+        const uint64_t es = env_step_of(st);
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const u32x4 w = env_obs_words(env.k0, env.k1, ge, 8 * s + 2 * g + hh, es);
+                xo[s][4 * hh + 0] = env_obs_word(w.x);
+                xo[s][4 * hh + 1] = env_obs_word(w.y);
+                xo[s][4 * hh + 2] = env_obs_word(w.z);
+                xo[s][4 * hh + 3] = env_obs_word(w.w);
+            }
+        // sampling: task (row r, group (lane + 64u) >> 4)
+        int a0 = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int grp = (lane + 64 * u) >> 4;
+            pa[u] = 0;
+            plp[u] = 0.f;
+            if (grp < K) {
+                const int o0 = t_off[grp];
+                r16_pick(lgs + r * kR16LGS, o0, t_off[grp + 1] - o0, ge, step, k0, k1, pa[u],
+                         plp[u]);
+            }
+            if (u == 0) a0 = pa[0];  // lanes 0..15: group 0 of row r
+        }
+        // the sim step and _post_step_cb of env n (lane g == 0 holds its
+        // first action); every lane advances its copy of the env counter
+        float rew;
+        bool done;
+        const int4 ns = env_advance_vals(ge, env.k0, env.k1, (float)a0, st, rew, done);
+        float er;
+        {
+#pragma clang fp contract(off)
+            er = rew + rk.gamma * eret;
+        }
+        eret = done ? 0.f : er;
+        st = ns;
+        pend = true;
+        pv = value;
+        prew = rew;
+        pdone = done;
+        per = er;
+        prow = srow;
+        wave_lds_sync();  // the logits scratch is rewritten by the next step
+    }
+    flush();
+    // the env's state after the rollout: observations, state, running return
+    {
+        float* orow = env.obs + n * D;
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+            float4* dst = (float4*)(orow + 32 * s + 8 * g);
+            dst[0] = make_float4(xo[s][0], xo[s][1], xo[s][2], xo[s][3]);
+            dst[1] = make_float4(xo[s][4], xo[s][5], xo[s][6], xo[s][7]);
+        }
+        if (g == 0) {
+            env.state[n] = st;
+            env.rew[n] = prew;
+            env.done[n] = pdone ? 1 : 0;
+            rk.env_returns[n] = eret;
+        }
+    }
 }
 
 template <int NW>
@@ -81,195 +279,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
     PolicyK P, const float* __restrict__ obs0, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
     const uint64_t* step_ctr, uint32_t eoff, EnvK env) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const char* w1img = smem + kR16OffW1;
-    const char* whimg = smem + kR16OffWh;
-    const float* gb = (const float*)(smem + kR16OffGb);
-    const float* hb = (const float*)(smem + kR16OffHb);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
     int* tab = (int*)(smem + kR16OffTab);
     static_assert(NW == kR16Waves, "r16_stage stages with kR16Waves waves");
     r16_stage(P, smem, tid);
     if (tid <= MLEARN_MAX_GROUPS) tab[tid] = P.off[tid];
     __syncthreads();
-    const int* t_off = tab;
-    const int K = P.K, A = P.A;
-    constexpr int D = kR16D, DS = D / 32;
     const uint64_t step0 = step_ctr ? *step_ctr : 0ull;
     const int ntile = (int)(N / 16);
     const int TW = (int)gridDim.x * NW;
-
 #pragma clang loop unroll(disable)
-    for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW) {
-        // (the lane through an opaque copy per tile: rows16 kernel, ppo_rows16.h)
-        const int lane = r16_late(tid & 63), r = lane & 15, g = lane >> 4;
-        const int64_t n = (int64_t)tile * 16 + r;
-        const uint32_t ge = eoff + (uint32_t)n;
-        // this lane's 16 observation features (32s + 8g + j) and its env's state
-        float xo[DS][8];
-#pragma unroll
-        for (int s = 0; s < DS; ++s) {
-            const float4* src = (const float4*)(obs0 + n * D + 32 * s + 8 * g);
-            const float4 a = src[0], b = src[1];
-            xo[s][0] = a.x; xo[s][1] = a.y; xo[s][2] = a.z; xo[s][3] = a.w;
-            xo[s][4] = b.x; xo[s][5] = b.y; xo[s][6] = b.z; xo[s][7] = b.w;
-        }
-        int4 st = env.state[n];
-        float eret = rk.env_returns[n];
-        // the previous step's store writes (issued behind this step's weight loads)
-        bool pend = false;
-        int pa[2] = {0, 0};
-        float plp[2] = {0.f, 0.f}, pv = 0.f, prew = 0.f, per = 0.f;
-        bool pdone = false;
-        int64_t prow = 0;
-        auto flush = [&]() {
-            if (!pend) return;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int grp = (lane + 64 * u) >> 4;
-                if (grp < K) {
-                    rk.actions[prow * K + grp] = pa[u];
-                    rk.logp[prow * K + grp] = plp[u];
-                }
-            }
-            if (g == 0) {
-                rk.values[prow] = pv;
-                rk.rewards[prow] = prew;
-                rk.dones[prow] = pdone ? 1 : 0;
-                if (rk.trace) rk.trace[prow] = per;
-            }
-            pend = false;
-        };
-#pragma clang loop unroll(disable)
-        for (int t = 0; t <= rk.T; ++t) {
-            const bool act = t < rk.T;
-            const uint64_t step = step0 + (uint64_t)t;
-            const int64_t srow = (int64_t)t * rk.ld + n;  // store row of step t
-            // ObservationsCaster: the compute-dtype cast is layer 0's B operand
-            bf16x8 xf[DS];
-#pragma unroll
-            for (int s = 0; s < DS; ++s) {
-                const u4r v = {pk_bf16(xo[s][0], xo[s][1]), pk_bf16(xo[s][2], xo[s][3]),
-                               pk_bf16(xo[s][4], xo[s][5]), pk_bf16(xo[s][6], xo[s][7])};
-                xf[s] = __builtin_bit_cast(bf16x8, v);
-            }
-            auto lda0 = [&](int ln) {
-                const bf16* w0 = (const bf16*)P.wt[0];
-                const int rr = ln & 15, gg = ln >> 4;
-                return [=](int b, int s) {
-                    const int nn = 16 * b + rr;
-                    const int64_t idx = ((int64_t)(((nn >> 5) * (D >> 4) + 2 * s + (gg >> 1)) * 64 +
-                                                   (nn & 31) + 32 * (gg & 1))) * 8;
-                    return *(const bf16x8*)(w0 + idx);
-                };
-            };
-            auto bf0 = [&](int s) { return xf[s]; };
-            uint32_t zw[kR16NB][2], aw[kR16NB][2];
-            float mean, rstd;
-            r16_fwd_layer<DS, kR16Ring0>(lda0(r16_late(lane)), bf0, zw, mean, rstd);
-            // the store rows of step t - 1 and this step's observations (behind
-            // this step's weight loads)
-            flush();
-            if (act && rk.obs) {
-                bf16* orow = (bf16*)rk.obs + r16_late(srow) * D;
-#pragma unroll
-                for (int s = 0; s < DS; ++s)
-                    r16_st16(orow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
-            }
-            r16_ln_apply(zw, mean, rstd, gb, g, aw);
-            r16_fwd_layer<kR16KS, kR16Ring>(
-                [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
-                [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
-            r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
-            // heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
-            f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-            r16_mm<2, kR16KS, 4>(ha,
-                                 [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
-                                 [&](int s) { return r16_bfrag(aw, s); });
-            {
-                bf16* lr = lgs + r * kR16LGS;
-#pragma unroll
-                for (int cbk = 0; cbk < 2; ++cbk) {
-                    const int c0 = 16 * cbk + 4 * g;
-                    float v[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        v[i] = rnd<bf16>(rnd<bf16>(ha[cbk][i]) + rnd<bf16>(hb[c0 + i]));
-                    *(u2r*)(lr + c0) = u2r{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
-                }
-            }
-            wave_lds_sync();
-            const float value = to_f32(lgs[r * kR16LGS + A]);
-            if (!act) {  // the bootstrap critic (rollouts.py:607-635)
-                if (g == 0) rk.bootstrap[n] = value;
-                break;
-            }
-            // the sim's next observations: drawn from the state before the
-            // advance (env.h), the quads of this lane's B fragment
-            const uint64_t es = env_step_of(st);
-#pragma unroll
-            for (int s = 0; s < DS; ++s)
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const u32x4 w = env_obs_words(env.k0, env.k1, ge, 8 * s + 2 * g + hh, es);
-                    xo[s][4 * hh + 0] = env_obs_word(w.x);
-                    xo[s][4 * hh + 1] = env_obs_word(w.y);
-                    xo[s][4 * hh + 2] = env_obs_word(w.z);
-                    xo[s][4 * hh + 3] = env_obs_word(w.w);
-                }
-            // sampling: task (row r, group (lane + 64u) >> 4)
-            int a0 = 0;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int grp = (lane + 64 * u) >> 4;
-                pa[u] = 0;
-                plp[u] = 0.f;
-                if (grp < K) {
-                    const int o0 = t_off[grp];
-                    r16_pick(lgs + r * kR16LGS, o0, t_off[grp + 1] - o0, ge, step, k0, k1, pa[u],
-                             plp[u]);
-                }
-                if (u == 0) a0 = pa[0];  // lanes 0..15: group 0 of row r
-            }
-            // the sim step and _post_step_cb of env n (lane g == 0 holds its
-            // first action); every lane advances its copy of the env counter
-            float rew;
-            bool done;
-            const int4 ns = env_advance_vals(ge, env.k0, env.k1, (float)a0, st, rew, done);
-            float er;
-            {
-#pragma clang fp contract(off)
-                er = rew + rk.gamma * eret;
-            }
-            eret = done ? 0.f : er;
-            st = ns;
-            pend = true;
-            pv = value;
-            prew = rew;
-            pdone = done;
-            per = er;
-            prow = srow;
-            wave_lds_sync();  // the logits scratch is rewritten by the next step
-        }
-        flush();
-        // the env's state after the rollout: observations, state, running return
-        {
-            float* orow = env.obs + n * D;
-#pragma unroll
-            for (int s = 0; s < DS; ++s) {
-                float4* dst = (float4*)(orow + 32 * s + 8 * g);
-                dst[0] = make_float4(xo[s][0], xo[s][1], xo[s][2], xo[s][3]);
-                dst[1] = make_float4(xo[s][4], xo[s][5], xo[s][6], xo[s][7]);
-            }
-            if (g == 0) {
-                env.state[n] = st;
-                env.rew[n] = prew;
-                env.done[n] = pdone ? 1 : 0;
-                rk.env_returns[n] = eret;
-            }
-        }
-    }
+    for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW)
+        r16_roll_tile(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem);
 }
 
 template <int NW>

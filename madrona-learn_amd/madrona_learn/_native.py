@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -191,6 +191,8 @@ _SIGNATURES = {
                                           _S]),
     "mlearn_ppo_workspace_bytes": (c_int64, [POINTER(MlpPolicy), c_int64]),
     "mlearn_ppo_step_kernel": (c_int32, [POINTER(MlpPolicy), c_int64, c_int32]),
+    "mlearn_policy_rollout_pop_kernel": (c_int32, [POINTER(MlpPolicy), POINTER(Lstm), c_int64,
+                                                   c_int32, c_int32]),
     "mlearn_ppo_minibatch_grad": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,
                                             c_int32, _P, POINTER(PPOHparams), _P, _P, _P, _S]),
     "mlearn_ppo_minibatch_fwd_bwd": (c_int32, [POINTER(MlpPolicy), POINTER(RolloutView), _P,

@@ -241,7 +241,10 @@ class RolloutManager:  # rollouts.py:373-826
     ``rollout_kernel`` is mlearn_rollout_out.policy_kernel of the whole-rollout
     launch: 0 the library's choice (the row-split rollout at the headline
     shape, include/mlearn.h), 1 the feature-split kernel (the per-step
-    launches' body: bit-identical to them), 2 the row-split kernel."""
+    launches' body: bit-identical to them), 2 the row-split kernel.  The
+    population launch follows it too (mlearn_policy_rollout_pop_kernel: the
+    row split uncapped where it applies; 1 runs the feature split on its own
+    grid, 2 raises where the row split does not apply)."""
 
     whole_rollout = True
     rollout_workgroups = 0
@@ -525,10 +528,17 @@ class RolloutManager:  # rollouts.py:373-826
                 arr(nat.RolloutOut, outs), (nat.c_uint32 * P)(*offs), arr(nat.DummyEnv, envs), P,
                 nat.ptr(self._pop_buf), nat.stream_handle()), "policy_pop_prepare")
             self._pop_sig = sig
+        lstm0 = self.policy_state.lstm_desc if self.R else None
+        kern = int(L.mlearn_policy_rollout_pop_kernel(self.policy_state.desc, lstm0, B, P, cap))
+        if self.rollout_kernel == 1 and kern == 2:
+            # the feature split on the grid it takes uncapped
+            cap = int(L.mlearn_policy_rollout_pop_workgroups(self.policy_state.desc, lstm0, B, P, 0))
+        elif self.rollout_kernel == 2 and kern != 2:
+            raise RuntimeError("rollout_kernel 2: the row-split population rollout does not apply "
+                               f"({P} policies x {B} envs, cap {cap})")
         nat.check(L.mlearn_policy_rollout_env_pop(
-            self.policy_state.desc, self.policy_state.lstm_desc if self.R else None,
-            nat.ptr(self._pop_buf), P, B, key[0], key[1], nat.ptr(step_ctr), cap,
-            nat.stream_handle()), "policy_rollout_env_pop")
+            self.policy_state.desc, lstm0, nat.ptr(self._pop_buf), P, B, key[0], key[1],
+            nat.ptr(step_ctr), cap, nat.stream_handle()), "policy_rollout_env_pop")
         return True
 
     def _rollout_out(self, rollout_state, p, gamma):

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from madrona_learn import _native as nat
-    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 19
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 20
     hdr = open(HEADER).read()
     assert f"#define MLEARN_ABI_VERSION {nat.ABI_VERSION}" in hdr
 
@@ -118,6 +118,15 @@ def test_step_kernel_selection():
                   desc(buckets=(2,) * 8), desc(bins=9)):
         assert sel(other, 65536) == 1 and sel(other, 65536, 2) == -1
     assert sel(d, 65536, 3) == -1 and sel(d, 0) == -1
+    # the population launch (mlearn_policy_rollout_pop_kernel): the row split
+    # uncapped over >= 2048 16-env tiles of policies with N a multiple of 128
+    pk = lambda d, N, P, cap=0: L.mlearn_policy_rollout_pop_kernel(ctypes.byref(d), None, N, P, cap)  # noqa: E731
+    assert pk(d, 8192, 8) == 2 and pk(d, 4096, 8) == 2 and pk(d, 65536, 1) == 2
+    assert pk(d, 8192, 8, 64) == 1                            # capped: feature split
+    assert pk(d, 8192, 2) == 1 and pk(d, 8000, 8) == 1        # too few tiles / N % 128
+    for other in (desc(dtype=nat.DTYPE_F32), desc(H=128), desc(bins=9)):
+        assert pk(other, 8192, 8) == 1
+    assert pk(d, 0, 8) == -1 and pk(d, 8192, 0) == -1 and pk(d, 8192, 8, -1) == -1
 
 
 def test_lstm_layout_matches_oracle_and_arch():

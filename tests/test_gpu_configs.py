@@ -172,6 +172,10 @@ def test_population_8x8192(gpu):
     pss, tss = mgr.state.policy_list, mgr.state.train_list
     rm = mgr.rollout_mgr
     assert rm.B == B and rm.P == P
+    # the feature-split population kernel (the row split, the library's choice
+    # here, has its own test below)
+    assert nat.lib().mlearn_policy_rollout_pop_kernel(pss[0].desc, None, B, P, 0) == 2
+    rm.rollout_kernel = 1
     tpp = B // 32
     grid = nat.lib().mlearn_policy_rollout_pop_workgroups(pss[0].desc, None, B, P, 0)
     assert 0 < grid < P * tpp, grid
@@ -212,6 +216,52 @@ def test_population_8x8192(gpu):
 
 
 @pytest.mark.timeout(600)
+def test_population_8x8192_row_split(gpu):
+    """Config P on the row-split population kernel (the library's choice):
+    8 policies x 512 16-env tiles dealt in rounds of 8 consecutive tiles per
+    8-wave workgroup, one workgroup per CU, so every workgroup's second round
+    belongs to another policy and restages its W1 / head / LayerNorm images.
+    32-env windows of second-round tiles of several workgroups (and the last
+    one) are replayed on the oracle with their own policy's parameters, as in
+    the feature-split test above."""
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    import madrona_learn as ml
+    from tests.test_gpu_train import make_policy
+    P, B, mb = 8, 8192, 2048
+    N = P * B
+    env = DummyVecEnv(N, D, 6, seed=4, device=gpu)
+    cfg = _cfg(N, mb, pbt_policies=P, seed=10)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), make_policy(torch.bfloat16, H),
+                           use_graph=False)
+    pss = mgr.state.policy_list
+    rm = mgr.rollout_mgr
+    L_ = nat.lib()
+    assert L_.mlearn_policy_rollout_pop_kernel(pss[0].desc, None, B, P, 0) == 2
+    rm.rollout_kernel = 2
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    tpp, TW = B // 16, cus * 8
+    ntile = P * tpp
+    assert ntile > TW  # rounds in series
+    # second-round tiles of workgroups whose first round was another policy
+    picks = []
+    for wg in (0, cus // 2 - 1, cus - 1):
+        t1 = TW + 8 * wg
+        if t1 < ntile and t1 // tpp != (8 * wg) // tpp:
+            picks.append(t1 + 2 * (wg % 4))
+    picks.append(ntile - 2)
+    assert len(picks) >= 3, picks
+    p0s = [ps.params.cpu().numpy().astype(np.float64) for ps in pss]
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert getattr(rm, "_pop_sig", None) is not None  # the population launch ran
+    s = rm.store
+    lay = ref.param_layout(D, H, 2, 26)
+    for t in picks:
+        e0 = 16 * t  # a 32-env window: tiles t, t + 1 of the same workgroup round
+        _check_window(s, mgr, env, p0s[e0 // B], lay, e0, cfg)
+
+
 def test_lstm_8192_rollout_and_update(gpu):
     """Config L at its stated size: RecurrentBackboneEncoder(MLP[256,256],
     LSTM(256)) over 8192 envs, bf16, minibatches of 2048 sequences (one
