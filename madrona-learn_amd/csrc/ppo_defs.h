@@ -119,7 +119,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 #define ML_WG_SMALL_SPLITS 32
 #endif
 #ifndef ML_WG_TARGET_LSTM
-#define ML_WG_TARGET_LSTM 512  // the LSTM gate weights' (Wi, Wh) workgroup target (config L: 10.94 / 10.60 / 10.47 ms at 128 / 256 / 512)
+#define ML_WG_TARGET_LSTM 512  // the LSTM gate weights' (Wi, Wh) workgroup target (config L: 10.94 / 10.60 / 10.47 ms at 128 / 256 / 512); round 5: 10.27 / 10.33 / 10.51 ms at 512 / 768 / 1024
 #endif
 static void plan_splits(int I, int J, int64_t Mp, int kWgChunk, int* splits, int64_t* rps,
                         int target = ML_WG_TARGET) {
