@@ -760,6 +760,7 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
             __syncthreads();
             cur = p;
         }
+        if (wave >= kR16Waves / 2 && t0 + TW >= ntile) __builtin_amdgcn_s_setprio(1);  // (rollout16_kernel)
         r16_roll_tile(e.P, e.obs, e.rk, k0, k1, step0, e.eoff, e.env, t0 + wave - p * tpp, tid,
                       smem);
     }

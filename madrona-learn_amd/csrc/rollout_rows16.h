@@ -290,8 +290,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
     const int ntile = (int)(N / 16);
     const int TW = (int)gridDim.x * NW;
 #pragma clang loop unroll(disable)
-    for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW)
+    for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW) {
+        // the second wave of each SIMD (waves 4..7) loses issue arbitration
+        // throughout; it takes priority for its last tile (as the row-split
+        // step kernel does; rollout 1075-1104 -> 1058-1083 us at the headline)
+        if (NW > 4 && wave >= NW / 2 && tile + TW >= ntile) __builtin_amdgcn_s_setprio(1);
         r16_roll_tile(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem);
+    }
 }
 
 template <int NW>
