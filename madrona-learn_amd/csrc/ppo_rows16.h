@@ -283,11 +283,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         // the lane index through an opaque copy per tile: otherwise every
         // lane-derived LDS / weight address of the body is hoisted out of the
         // tile loop and held live across it (rollout kernel)
-        // the second wave of each SIMD (waves 4..7) loses issue arbitration to
-        // the first throughout (tile 0 ends ~24 % later); it takes priority for
-        // its last tile so the two finish closer together (-1..2 % kernel time)
-        // (at NW <= 4 every wave has its SIMD to itself)
-        if (NW > 4 && tt == NT - 1 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef ML_STAMPS
         uint64_t r16_st[13];
 #endif
@@ -385,6 +380,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
             [&](int b, int s) { return r16_row_frag(w1img, 16 * b + r, s, g); },
             [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
         R16_STAMP(3);
+        // the second wave of each SIMD (waves 4..7) loses issue arbitration to
+        // the first throughout (tile 0 ends ~24 % later); it takes priority from
+        // its first tile's layer-1 output on, so the two finish closer together
+        // (update 8.43-8.50 -> 8.36-8.38 ms on one box; from the last tile's
+        // start: -1..2 % kernel time; from the kernel's start: slower)
+        if (NW > 4 && tt == 0 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
         r16_store_rows((bf16*)ws.a[0] + r16_late(row) * kR16H, aw, g);  // A_0 rows
         r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
         R16_STAMP(4);
