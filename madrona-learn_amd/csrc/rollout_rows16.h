@@ -95,7 +95,7 @@ static bool rollout16_pop_eligible(const PolicyK& P0, int64_t N, int npol, int m
 __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __restrict__ obs0,
                                               const RollK& rk, uint32_t k0, uint32_t k1,
                                               uint64_t step0, uint32_t eoff, const EnvK& env,
-                                              int tile, int tid, char* smem) {
+                                              int tile, int tid, char* smem, int prio_t = -1) {
     const char* w1img = smem + kR16OffW1;
     const char* whimg = smem + kR16OffWh;
     const float* gb = (const float*)(smem + kR16OffGb);
@@ -147,6 +147,7 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
 #pragma clang loop unroll(disable)
     for (int t = 0; t <= rk.T; ++t) {
         const bool act = t < rk.T;
+        if (t == prio_t) __builtin_amdgcn_s_setprio(1);
         const uint64_t step = step0 + (uint64_t)t;
         const int64_t srow = (int64_t)t * rk.ld + n;  // store row of step t
         // ObservationsCaster: the compute-dtype cast is layer 0's B operand
@@ -274,6 +275,10 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
     }
 }
 
+#ifndef ML_ROLL_PRIO_NUM
+#define ML_ROLL_PRIO_NUM 6  // eighths of T: the step the second wave takes priority
+#endif
+
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3) / 4, (NW + 3) / 4))) void rollout16_kernel(
     PolicyK P, const float* __restrict__ obs0, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
@@ -292,10 +297,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
 #pragma clang loop unroll(disable)
     for (int tile = (int)blockIdx.x * NW + wave; tile < ntile; tile += TW) {
         // the second wave of each SIMD (waves 4..7) loses issue arbitration
-        // throughout; it takes priority for its last tile (as the row-split
-        // step kernel does; rollout 1075-1104 -> 1058-1083 us at the headline)
+        // throughout; it takes priority for its last tile and from step
+        // 6T/8 of the tile before it (rollout 1081-1086 -> 1027-1037 us at the
+        // headline on one box; from the last tile's start only: 1058-1083
+        // against 1075-1104; from step T/2: 1057-1066; from the start: slower)
         if (NW > 4 && wave >= NW / 2 && tile + TW >= ntile) __builtin_amdgcn_s_setprio(1);
-        r16_roll_tile(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem);
+        const int pt = (NW > 4 && wave >= NW / 2 && tile + 2 * TW >= ntile)
+                           ? rk.T * ML_ROLL_PRIO_NUM / 8 : -1;
+        r16_roll_tile(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem, pt);
     }
 }
 
