@@ -24,6 +24,12 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// CU count of the current device, queried once per device id (0 when the
+// query fails, e.g. without a GPU: callers then assume MI355X's 256)
+int device_cus();
+// hipFuncAttributeMaxDynamicSharedMemorySize of fn, set once per (function,
+// device) outside graph capture; MLEARN_EHIP with a message when refused
+int set_lds_attr(const void* fn, int bytes, const char* what);
 
 #define ML_REQUIRE(cond, ...)                                   \
     do {                                                        \

@@ -10,6 +10,11 @@
 #include <stdio.h>
 
 #include "common.h"
+
+#include <atomic>
+#include <mutex>
+#include <set>
+#include <utility>
 #include "dists.h"
 #include "env.h"
 #include "rowtile.h"
@@ -25,12 +30,46 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
+constexpr int kMaxDevices = 64;
+
 int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("%s: %s", what, hipGetErrorString(e));
         return MLEARN_EHIP;
     }
+    return MLEARN_OK;
+}
+
+int device_cus() {
+    static std::atomic<int> cache[kMaxDevices];  // CU count + 1; 0 = not queried yet
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        v = cus + 1;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v - 1;
+}
+
+int set_lds_attr(const void* fn, int bytes, const char* what) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({fn, dev})) return MLEARN_OK;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("%s: %d B of LDS refused (%s)", what, bytes, hipGetErrorString(e));
+        return MLEARN_EHIP;
+    }
+    done.insert({fn, dev});
     return MLEARN_OK;
 }
 

@@ -768,15 +768,10 @@ __global__ __launch_bounds__(64 * kR16Waves) __attribute__((amdgpu_waves_per_eu(
 
 static int launch_rollout16_pop(const PopEntry* pop, int npol, int64_t N, uint32_t k0, uint32_t k1,
                                 const uint64_t* step_ctr, hipStream_t s) {
-    static int cus = -1;
-    if (cus < 0) {  // once (kept out of graph capture)
-        (void)hipFuncSetAttribute((const void*)rollout16_pop_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
-    }
+    // (once per device, kept out of graph capture)
+    if (set_lds_attr((const void*)rollout16_pop_kernel, (int)kR16Lds, "rollout16_pop"))
+        return MLEARN_EHIP;
+    const int cus = device_cus();
     const int64_t rounds_of_8 = (int64_t)npol * (N / 16) / kR16Waves;
     int64_t grid = cus > 0 ? cus : 256;
     if (grid > rounds_of_8) grid = rounds_of_8;

@@ -548,7 +548,8 @@ struct R16Cfg {
     int nw, nt;
 };
 static R16Cfg rows16_cfg(int64_t Mp) {
-    constexpr int64_t kCUs = 256;  // MI355X
+    const int cus = device_cus();
+    const int64_t kCUs = cus > 0 ? cus : 256;  // (256: MI355X, when no device answers)
     if (Mp % 256 == 0 && Mp / 256 >= kCUs) return R16Cfg{8, 2};
     if (Mp == 128 * kCUs) return R16Cfg{8, 1};  // exactly one round of workgroups
     return R16Cfg{0, 0};
@@ -562,14 +563,10 @@ template <int NW, int NT>
 static void launch_rows16_cfg(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                               int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                               const R16Div& dv, hipStream_t s) {
-    static bool attr_set = false;  // once per shape (kept out of graph capture)
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<true, NW, NT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        (void)hipFuncSetAttribute((const void*)ppo_rows16_kernel<false, NW, NT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        attr_set = true;
-    }
+    // (once per shape and device, kept out of graph capture)
+    if (set_lds_attr((const void*)ppo_rows16_kernel<true, NW, NT>, (int)kR16Lds, "ppo_rows16") ||
+        set_lds_attr((const void*)ppo_rows16_kernel<false, NW, NT>, (int)kR16Lds, "ppo_rows16"))
+        return;  // (the caller's check_launch reports a failed launch; the message is set)
     const int grid = (int)(ws.Mp / (16 * NW * NT));
     if (hp.metrics)
         hipLaunchKernelGGL((ppo_rows16_kernel<true, NW, NT>), dim3(grid), dim3(64 * NW), kR16Lds, s,

@@ -60,7 +60,8 @@ __device__ inline void r16_pick(const bf16* lr, int o0, int nb, uint32_t ge, uin
 // one wave per SIMD, measured no faster than the feature-split kernel: 363
 // vs 361 us per rollout at 8 192, profiles/r05_rank_slices_ab.txt.)
 static int rollout16_waves(int64_t N) {
-    constexpr int64_t kCUs = 256;  // MI355X
+    const int cus = device_cus();
+    const int64_t kCUs = cus > 0 ? cus : 256;  // (256: MI355X, when no device answers)
     if (N % 256 == 0 && N >= 65536 && N / 16 <= 0x7fffffff) return 8;
     if (N == 16 * 8 * kCUs) return 8;
     return 0;
@@ -312,12 +313,8 @@ template <int NW>
 static void launch_rollout16_nw(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
                                 uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
                                 const EnvK& env, int cus, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {  // once per shape (kept out of graph capture)
-        (void)hipFuncSetAttribute((const void*)rollout16_kernel<NW>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16Lds);
-        attr_set = true;
-    }
+    // (once per shape and device, kept out of graph capture)
+    if (set_lds_attr((const void*)rollout16_kernel<NW>, (int)kR16Lds, "rollout16")) return;
     const int64_t waves = N / 16;
     int64_t grid = cus > 0 ? cus : 256;
     if (grid * NW > waves) grid = waves / NW;
@@ -328,13 +325,7 @@ static void launch_rollout16_nw(const PolicyK& P, const float* obs, int64_t N, c
 static int launch_rollout16(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
                             uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
                             const EnvK& env, hipStream_t s) {
-    static int cus = -1;
-    if (cus < 0) {  // once (kept out of graph capture)
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
-    }
-    launch_rollout16_nw<8>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, cus, s);
+    if (set_lds_attr((const void*)rollout16_kernel<8>, (int)kR16Lds, "rollout16")) return MLEARN_EHIP;
+    launch_rollout16_nw<8>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, device_cus(), s);
     return check_launch("policy_rollout_env (row split)");
 }

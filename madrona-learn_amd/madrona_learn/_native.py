@@ -324,8 +324,10 @@ def head_cols(num_logits, critic_bins):
         return HEAD_COLS
     if num_logits + critic_bins <= HEAD_COLS_MAX:
         return HEAD_COLS_MAX
-    raise ValueError(f"{num_logits} actor logits + {critic_bins} critic outputs exceed "
-                     f"{HEAD_COLS_MAX} head columns")
+    # NotImplementedError: such a tree is valid (e.g. DreamerV3Critic with
+    # 255 bins) and trains on the torch path (train._fused_tree_problem)
+    raise NotImplementedError(f"{num_logits} actor logits + {critic_bins} critic outputs "
+                              f"exceed the fused kernels' {HEAD_COLS_MAX} head columns")
 
 
 def dtype_code(dtype):

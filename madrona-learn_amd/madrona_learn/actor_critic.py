@@ -219,11 +219,11 @@ class ActorCritic(nn.Module):  # actor_critic.py:38-128
         x = self._obs_matrix(obs)
         try:
             enc = self.backbone.encoder if isinstance(self.backbone, BackboneShared) else None
-            dtype = enc.net.dtype if enc is not None and hasattr(enc.net, "dtype") else None
+            dtype = getattr(getattr(enc, "net", None), "dtype", None)
             if dtype is None:
                 raise NotImplementedError("no MLP trunk")
             arch = compile_arch(self, x.shape[1], dtype)
-        except (NotImplementedError, ValueError, AttributeError, TypeError):
+        except NotImplementedError:
             object.__setattr__(self, "_fast", False)
             return None
         ps = PolicyState(self, arch, None, x.device, np.random.default_rng(0))

@@ -204,6 +204,9 @@ class TorchPolicyState:
         self.compute_dtype = compute_dtype
         self.obs_pre_state = preprocess.init_state(sample_obs, False) \
             if _has_state(preprocess) else None
+        # a bare (unnamed) observation tensor keeps its preprocess state
+        # _Bare-marked; a checkpoint stores plain dicts, so load re-marks it
+        self._bare_obs = not isinstance(sample_obs, dict)
         pre = self.preprocess(sample_obs)
         # materialise the lazily created parameters (the reference's
         # apply_fn init with the 'rollout' method, train_state.py:318-379)
@@ -283,7 +286,11 @@ class TorchPolicyState:
     def load_state_dict(self, sd):
         self.params.copy_(sd["params"])
         if sd.get("obs_pre_state") is not None:
-            self.obs_pre_state = _to_device(sd["obs_pre_state"], self.device)
+            st = _to_device(sd["obs_pre_state"], self.device)
+            if self._bare_obs:
+                from .observations import _wrap
+                st = _wrap(st)
+            self.obs_pre_state = st
 
     def policy_tensors(self):
         return [self.params]
@@ -293,7 +300,8 @@ def _to_device(x, dev):
     if isinstance(x, torch.Tensor):
         return x.to(dev)
     if isinstance(x, dict):
-        return {k: _to_device(v, dev) for k, v in x.items()}
+        r = {k: _to_device(v, dev) for k, v in x.items()}
+        return type(x)(r) if type(x) is not dict else r  # (keeps a _Bare marker)
     if isinstance(x, (list, tuple)):
         return type(x)(_to_device(v, dev) for v in x)
     return x
@@ -572,6 +580,12 @@ class TorchPPO:
         # record m = {adv mean, adv rstd, mu', inv_sigma' after minibatch m's
         # update, mu, sigma before it}
         b.vnorm = bool(cfg.normalize_values)
+        if b.vnorm and ps.critic_bins > 1:
+            # ppo.py:57 asserts not normalize_values for distributional
+            # critics: the two-hot loss ignores the normaliser, yet GAE would
+            # invert the two-hot mean with drifting estimates
+            raise ValueError("normalize_values with a SymExpTwoHotDistribution critic "
+                             "(the reference asserts against it, ppo.py:57)")
         if b.vnorm:
             b.vn_est = ts.value_norm_est
             b.vn_count = ts.value_norm_count

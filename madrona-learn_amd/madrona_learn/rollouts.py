@@ -237,7 +237,15 @@ class RolloutManager:  # rollouts.py:373-826
     tiles (mlearn_policy_rollout_env_pop), so P launches of B / 32 workgroups
     each become one that fills the chip; False issues one launch per policy.
     A ``rollout_workgroups`` cap > 0 caps that launch too (tiles of several
-    policies in series per workgroup).  Same bits either way.
+    policies in series per workgroup).  Same bits either way while both
+    launches run the same kernel: with ``rollout_kernel`` 0 an uncapped
+    population launch may take the row-split kernel where the per-policy
+    launches or a capped population launch take the feature split (the row
+    split needs >= 65 536 envs per launch, the population form >= 2 048 16-env
+    tiles in all), and the two kernels' logits may differ by a bf16 ulp, so
+    a sampled action may differ where two perturbed logits nearly tie; set
+    ``rollout_kernel`` = 1 for bit-identical trajectories across these
+    switches.
     ``rollout_kernel`` is mlearn_rollout_out.policy_kernel of the whole-rollout
     launch: 0 the library's choice (the row-split rollout at the headline
     shape, include/mlearn.h), 1 the feature-split kernel (the per-step

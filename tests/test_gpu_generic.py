@@ -429,3 +429,31 @@ def test_value_norm_on_torch_path_matches_oracle(gpu):
     # estimates before that minibatch
     last = mgr.metrics.last()
     np.testing.assert_allclose(last["Value Errors"].mean, np.mean(met["Value Errors"]), rtol=1e-4)
+
+
+def test_wide_head_routes_to_torch_path(gpu):
+    """A head wider than the fused kernels' 96 columns (DreamerV3Critic with
+    255 bins, the dreamerv3 default the reference's models.py mentions) is a
+    valid tree: init_training trains it on the torch path instead of failing
+    (_native.head_cols raises NotImplementedError)."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerDiscreteActor, DreamerV3Critic
+    N, H = 64, 64
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=5, device=gpu)
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneShared(encoder=ml.BackboneEncoder(net=MLP(H, 2, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DreamerV3Critic(dt, num_bins=255))
+    cfg = _cfg(N, 16, epochs=1)
+    import dataclasses
+    cfg = dataclasses.replace(cfg, dreamer_v3_critic=True)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac))
+    ps = mgr.state.policy_states
+    assert getattr(ps, "generic", False) and ps.critic_bins == 255
+    p0 = ps.params.clone()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
+    assert np.isfinite(mgr.metrics.last()["Loss"].mean)

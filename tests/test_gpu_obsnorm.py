@@ -214,3 +214,52 @@ def test_obs_normalizer_before_prefix_on_torch_path(gpu):
         got = ps.obs_pre_state
         for k in ("mu", "sigma"):
             np.testing.assert_allclose(got[k].cpu().numpy(), est[k], rtol=1e-5, atol=1e-6)
+
+
+def test_bare_obs_normalizer_state_survives_checkpoint(gpu, tmp_path):
+    """A bare (unnamed) observation tensor under ObservationsEMANormalizer on
+    the torch path keeps its normaliser state _Bare-marked; a checkpoint
+    stores plain dicts, so the restore must re-mark it: after
+    save -> load into a fresh manager the state is the same estimates, still
+    read as the bare observation's, and training continues from it (the
+    estimates move on from the restored ones)."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.observations import _Bare
+    decay, N, H = 0.99, 64, 64
+    dt = torch.float32
+
+    def build():
+        env = DummyVecEnv(N, 64, 6, seed=21, device=gpu)
+        halve = lambda x, train=False: x * 0.5  # noqa: E731  (routes to the torch path)
+        ac = ml.ActorCritic(
+            backbone=ml.BackboneShared(prefix=halve,
+                                       encoder=ml.BackboneEncoder(net=MLP(H, 2, dt))),
+            actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+            critic=DenseLayerCritic(dt))
+        pol = ml.Policy(actor_critic=ac,
+                        obs_preprocess=ml.ObservationsEMANormalizer.create(decay, dt))
+        return ml.init_training(gpu, make_cfg(dt, N=N, H=H), AffineEnv(env).sim_fns(), pol,
+                                use_graph=False)
+
+    a = build()
+    assert getattr(a.state.policy_states, "generic", False)
+    a.update_iter()
+    torch.cuda.synchronize()
+    a.save_ckpt(str(tmp_path))
+    b = build()
+    b.load_ckpt(str(tmp_path))
+    sa, sb = a.state.policy_states.obs_pre_state, b.state.policy_states.obs_pre_state
+    assert isinstance(sa, _Bare) and isinstance(sb, _Bare)
+    assert set(sa) == set(sb)
+    for k in sa:
+        assert torch.equal(sa[k].cpu(), sb[k].cpu()), k
+    loaded = {k: v.clone() for k, v in sb.items()}
+    b.update_iter()  # (a crash here was the ADVICE r05 failure: the state read as named obs)
+    torch.cuda.synchronize()
+    sb = b.state.policy_states.obs_pre_state
+    assert isinstance(sb, _Bare) and set(sb) == set(loaded)
+    for k in sb:
+        assert torch.isfinite(sb[k]).all(), k
+    assert not torch.equal(sb["mu"], loaded["mu"])  # the estimates moved on from the restore

@@ -1,6 +1,6 @@
 """Diagnostic: per-phase s_memtime stamps of the row-split step kernel
 (ppo_rows16.h) at the headline shape.  Run with
-MADRONA_LEARN_LIB=madrona-learn_amd/madrona_learn/_lib/libmlearn_stamps.so
+MADRONA_LEARN_LIB=madrona-learn_amd/variants/libmlearn_stamps.so
 (tools/build_stamps.sh)."""
 import ctypes
 import os
