@@ -308,6 +308,26 @@ def gae_roofline(dev, N, iters=50, returns=False):
 
 
 def cpu_baseline(iters=2):
+    """Two timed runs of the oracle's CPU iteration (_cpu_baseline_run): BLAS
+    on every CPU of this process's affinity mask (SURVEY §8(d)'s whole-host
+    reading) and on 16 threads (the box's CPU share per GPU; on a many-socket
+    host the small GEMMs of this workload lose to oversubscription across
+    sockets).  `value` is the faster of the two, both runs are listed."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        (os.cpu_count() or 1)
+    runs = [_cpu_baseline_run(iters, cores)]
+    if cores > 16:
+        runs.append(_cpu_baseline_run(iters, 16))
+    best = max(runs, key=lambda r: r["value"])
+    out = dict(best)
+    out["runs"] = [{"value": r["value"], "cores": r["cores"], "seconds": r["seconds"]}
+                   for r in runs]
+    out["threads_note"] = ("cores = BLAS pool threads during the faster timed run "
+                           "(threadpoolctl); runs = every CPU of the affinity mask and 16")
+    return out
+
+
+def _cpu_baseline_run(iters, threads):
     """The oracle restatement (NumPy fp32 arithmetic, host BLAS threads) of
     `iters` full PPO iterations on an 8192-env shard of the workload: 8192
     envs x T=32 rollout with the synthetic env, GAE, 2 epochs over every
@@ -331,14 +351,14 @@ def cpu_baseline(iters=2):
     env = onat.Env(n_env, OBS, 1, 2)
     env.reset()
     hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01}
-    # every host core this process may run on (the whole host,
-    # not the OMP_NUM_THREADS default), set on the BLAS pools the NumPy
+    # `threads` BLAS threads (the caller runs every host core of the affinity
+    # mask), set on the BLAS pools the NumPy
     # restatement runs its products in; the thread count reported is what the
     # pools report back while the timed region runs
     from threadpoolctl import threadpool_info, threadpool_limits
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
         (os.cpu_count() or 1)
-    limiter = threadpool_limits(limits=cores)
+    limiter = threadpool_limits(limits=threads)
     used = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
     norms = np.ones(LAYERS)
     pf = p.astype(np.float64)
@@ -360,9 +380,7 @@ def cpu_baseline(iters=2):
     limiter.restore_original_limits()
     return {"value": iters * n_env * T / sec, "unit": "env-steps/s", "cores": used,
             "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-            "cores_available": cores,
-            "threads_note": "cores = BLAS pool threads during the timed region "
-                            "(threadpoolctl), set to every CPU in this process's affinity mask",
+            "cores_available": cores, "seconds": sec,
             "sample": f"{iters} full PPO iterations on a {n_env}-env shard ({n_env} envs x "
                       f"T={T}, 2 epochs x {n_env // mb} minibatches of {mb} seqs; same work per "
                       f"env-step as the 65536-env workload), NumPy fp32 oracle restatement, "

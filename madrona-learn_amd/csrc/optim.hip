@@ -313,6 +313,273 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
     write_copies<T>(Lk, C, p, val);
 }
 
+// ---------------------------------------------------------------------------
+// The optimizer chain as ONE launch (round 6): [global-norm partials] ->
+// clip + Adam -> projection + compute images.  The 2-3 launches above each
+// cost a kernel boundary plus a dependent load chain; here the seams are an
+// in-launch grid barrier whose only payload is the per-block partials (a few
+// KB): every workgroup keeps its own parameters in registers from the Adam
+// update to the projection, so no parameter crosses a workgroup.
+//
+// Bit-identical to the split chain: a workgroup of 256 * VB threads runs VB
+// "virtual" adam_kernel blocks (virtual block vb = VB * blockIdx + tid / 256,
+// the same grid-stride parameter mapping over ablk virtual blocks), writes
+// the same per-(virtual block, slot) partials, and its first 256 threads
+// replay global_norm / sumsq_partial_kernel / project_kernel's reductions in
+// their fixed orders.
+//
+// Hand-off protocol (MI355X_MICROARCH.md, hand-off table row 1, "one lane of
+// each storing workgroup ... agent-scope atomic add"): partials are stored
+// with agent-scope (sc1) atomic stores; every wave waits s_waitcnt vmcnt(0);
+// a workgroup barrier; ONE lane adds to a counter shard (blockIdx % 8) with an
+// agent-scope atomic add; one lane polls the 8 shards with sc1 loads until
+// their sum reaches the target, the workgroup barrier releases the other
+// waves, and every load of handed-off partials is an sc1 load.  One workgroup
+// per CU (the launch requests kFusedLds of LDS), grid <= the device's CUs, so
+// every workgroup is resident.  Targets: `base` (arrivals before this launch,
+// stored by workgroup 0 after the last barrier of the previous launch) +
+// k * grid.  Every poll loop is bounded (kSpinCap); an expired poll sets the
+// fail word and proceeds (no hang; results of that step are then invalid).
+// ---------------------------------------------------------------------------
+constexpr int kBarShards = 8, kBarStride = 16;  // one 128-B line per shard
+constexpr int kBarWords = kBarShards * kBarStride + 16;  // shards, base, fail
+constexpr uint32_t kSpinCap = 1u << 22;
+constexpr int kFusedLds = 96 * 1024;  // > half a CU's LDS: one workgroup per CU
+
+struct GridBarK {
+    uint64_t* shard;  // [kBarShards * kBarStride]
+    uint64_t* base;
+    uint64_t* fail;
+};
+
+__device__ inline uint64_t ld_sc1(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double ld_sc1d(const double* p) {
+    return __builtin_bit_cast(double, ld_sc1((const uint64_t*)p));
+}
+__device__ inline void st_sc1d(double* p, double x) {
+    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Arrive and wait until `target` arrivals have been counted.  Every thread
+// of the workgroup calls it (its sc1 partial stores issued before).
+__device__ inline void grid_sync(const GridBarK& gb, uint64_t target) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(gb.shard + kBarStride * (blockIdx.x % kBarShards), (uint64_t)1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t it = 0;; ++it) {
+            uint64_t n = 0;
+#pragma unroll
+            for (int k = 0; k < kBarShards; ++k) n += ld_sc1(gb.shard + kBarStride * k);
+            if (n >= target) break;
+            if (it >= kSpinCap) {
+                __hip_atomic_store(gb.fail, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+template <typename T, int NS, int PRE, int VB, bool NORM>
+__global__ __launch_bounds__(256 * VB) void optim_fused_kernel(
+    LayoutK Lk, CopiesK C, float* __restrict__ params, const float* __restrict__ grads,
+    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ init_norms,
+    int32_t* step, const double* gpart_in, int64_t npart_in, double* gpart, double* ppart, int ablk,
+    float lr, float b1, float b2, float eps, float max_norm, int norm_params, int norm_ln,
+    GridBarK gb) {
+    extern __shared__ char fused_dyn[];  // (unused: sized so that one workgroup fits per CU)
+    __shared__ float sh[VB][4][kMaxSlots];
+    __shared__ double red[4][kMaxSlots];
+    __shared__ float sq[kMaxSlots];
+    __shared__ double gn_red[4];
+    __shared__ float gn_sh;
+    __shared__ uint64_t base_sh;
+    constexpr int nslot = NS;
+    const int tid = threadIdx.x, vt = tid & 255, half = tid >> 8, w = vt >> 6, lane = tid & 63;
+    const int vb = VB * blockIdx.x + half;
+    const uint64_t G = gridDim.x;
+    for (int i = tid; i < VB * 4 * kMaxSlots; i += 256 * VB) (&sh[0][0][0])[i] = 0.f;
+    if (tid == 0) base_sh = ld_sc1(gb.base);
+    (void)fused_dyn;
+
+    // this thread's parameters (adam_kernel's mapping over ablk blocks), in
+    // flight while the norm is formed
+    const int64_t p0 = vb * (int64_t)256 + vt;
+    const int64_t stride = (int64_t)ablk * 256;
+    float gq[PRE], mq[PRE], vq[PRE], qq[PRE];
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+        const int64_t p = p0 + u * stride;
+        gq[u] = mq[u] = vq[u] = qq[u] = 0.f;
+        if (vb < ablk && p < Lk.total) {
+            gq[u] = grads[p];
+            mq[u] = m[p];
+            vq[u] = v[p];
+            qq[u] = params[p];
+        }
+    }
+    const int count = step[0] + 1;
+    __syncthreads();  // base_sh
+    const uint64_t base = base_sh;
+    int nbar = 0;
+
+    const double* gp = gpart_in;
+    int64_t np = npart_in;
+    if (NORM) {
+        // sumsq_partial_kernel's kNormBlocks partials of grads^2 (the
+        // all-reduced gradient), virtual norm block k on the first 256 threads
+        for (int k = blockIdx.x; k < kNormBlocks; k += gridDim.x) {
+            double s = 0;
+            if (tid < 256) {
+                const int64_t st = (int64_t)kNormBlocks * 256;
+                for (int64_t i0 = k * 256 + tid; i0 < Lk.total; i0 += 8 * st) {
+                    float x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = i0 + u * st < Lk.total ? grads[i0 + u * st] : 0.f;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (i0 + u * st < Lk.total) {
+                            const double d = x[u];
+                            s += d * d;
+                        }
+                }
+                s = wave_sum64d(s);
+                if (lane == 0) gn_red[w] = s;
+            }
+            __syncthreads();
+            if (tid == 0) st_sc1d(gpart + k, ((gn_red[0] + gn_red[1]) + gn_red[2]) + gn_red[3]);
+            __syncthreads();
+        }
+        grid_sync(gb, base + (uint64_t)(++nbar) * G);
+        gp = gpart;
+        np = kNormBlocks;
+    }
+    // global_norm's fixed order on the first 256 threads (sc1 loads where
+    // the partials came from this launch)
+    if (tid < 256) {
+        double t = 0.0;
+        for (int64_t i0 = tid; i0 < np; i0 += 8 * 256) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + (int64_t)u * 256;
+                x[u] = i < np ? (NORM ? ld_sc1d(gp + i) : gp[i]) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t += x[u];
+        }
+        t = wave_sum64d(t);
+        if (lane == 0) gn_red[w] = t;
+    }
+    __syncthreads();
+    if (tid == 0) gn_sh = sqrtf((float)((gn_red[0] + gn_red[1]) + (gn_red[2] + gn_red[3])));
+    __syncthreads();
+    const float gn = gn_sh;
+
+    // clip + Adam (adam_kernel's arithmetic), new values kept in registers
+    float nq[PRE];
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+        const int64_t p = p0 + u * stride;
+        nq[u] = qq[u];
+        if (vb >= ablk || p - vt >= Lk.total) continue;  // (uniform per virtual block)
+        float contrib = 0.f;
+        int slot = -2;
+        const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
+        if (p < Lk.total && !pad) {
+            float g = gq[u];
+            if (!(gn < max_norm)) g = (g / gn) * max_norm;
+            const float mm = (1.f - b1) * g + b1 * mq[u];
+            const float vv = (1.f - b2) * (g * g) + b2 * vq[u];
+            const float mhat = mm / (1.f - powf(b1, (float)count));
+            const float vhat = vv / (1.f - powf(b2, (float)count));
+            const float up = mhat / (sqrtf(vhat) + eps);
+            nq[u] = qq[u] + (-lr) * up;
+            m[p] = mm;
+            v[p] = vv;
+            slot = proj_slot(Lk, p);
+            contrib = nq[u] * nq[u];
+        }
+        for (int s2 = 0; s2 < nslot; ++s2) {
+            if (!__any(slot == s2)) continue;
+            float x = slot == s2 ? contrib : 0.f;
+            x = wave_sum64(x);
+            if (lane == 0) sh[half][w][s2] += x;
+        }
+    }
+    __syncthreads();
+    if (vt < nslot && vb < ablk) {
+        const int s2 = vt;
+        st_sc1d(ppart + vb * (int64_t)nslot + s2,
+                ((double)sh[half][0][s2] + sh[half][1][s2]) + ((double)sh[half][2][s2] + sh[half][3][s2]));
+    }
+    grid_sync(gb, base + (uint64_t)(++nbar) * G);
+
+    // project_kernel's per-slot totals (fixed order, first 256 threads)
+    if (tid < 256) {
+        double t[NS];
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) t[sl] = 0;
+        for (int b0 = tid; b0 < ablk; b0 += 512) {
+            double x[2][NS];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int sl = 0; sl < NS; ++sl) {
+                    const int b = b0 + 256 * u;
+                    x[u][sl] = b < ablk ? ld_sc1d(ppart + (int64_t)b * nslot + sl) : 0.0;
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int sl = 0; sl < NS; ++sl)
+                    if (b0 + 256 * u < ablk) t[sl] += x[u][sl];
+        }
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            const double tt = wave_sum64d(t[sl]);
+            if (lane == 0) red[w][sl] = tt;
+        }
+    }
+    __syncthreads();
+    if (tid < nslot) sq[tid] = (float)(((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]);
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) {
+        if (step) step[0] += 1;
+        // arrivals so far, for the next launch's targets (every workgroup has
+        // read base: it arrived at the barriers above after reading it)
+        __hip_atomic_store(gb.base, base + (uint64_t)nbar * G, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // projection (project_kernel's arithmetic) + master params + images
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+        const int64_t p = p0 + u * stride;
+        if (vb >= ablk || p >= Lk.total) continue;
+        const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
+        float val = nq[u];
+        const int slot = proj_slot(Lk, p);
+        if (slot >= 2 * Lk.L) {
+            if (norm_params) val = (init_norms[Lk.L + slot - 2 * Lk.L] * val) / sqrtf(sq[slot]);
+        } else if (slot >= 0) {
+            const int l = slot >> 1;
+            if ((slot & 1) == 0) {
+                if (norm_params) val = (init_norms[l] * val) / sqrtf(sq[slot]);
+            } else if (norm_ln) {
+                val = sqrtf((float)Lk.H / sq[slot]) * val;
+            }
+        }
+        if (!pad) params[p] = val;
+        write_copies<T>(Lk, C, p, val);
+    }
+}
+
 // compute copies from params without any projection; zero the head padding
 template <typename T>
 __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const float* params) {
@@ -330,10 +597,13 @@ __global__ __launch_bounds__(256) void sync_kernel(LayoutK Lk, CopiesK C, const 
     if (p < Lk.total) write_copies<T>(Lk, C, p, params[p]);
 }
 
-static int64_t optim_ws_doubles(const LayoutK& k) {
+// workspace (doubles): norm partials, projection partials, spare, then the
+// fused launch's barrier words on 128-B lines (zeroed by the caller once)
+static int64_t optim_bar_offset(const LayoutK& k) {
     int64_t nblk = (k.total + 255) / 256;
-    return kNormBlocks + nblk * kMaxSlots + 8 + kMaxSlots + 8;
+    return (kNormBlocks + nblk * kMaxSlots + 8 + kMaxSlots + 8 + 15) / 16 * 16;
 }
+static int64_t optim_ws_doubles(const LayoutK& k) { return optim_bar_offset(k) + kBarWords; }
 
 // Projection slot counts with a project_kernel instantiation: 2 L (trunk
 // kernels + LayerNorms, L <= MLEARN_MAX_LAYERS) and 2 L + 8 (the LSTM gate
@@ -446,6 +716,62 @@ __global__ __launch_bounds__(256) void flat_project_kernel(float* __restrict__ p
     }
 }
 
+// The fused launch applies when its grid (ablk / kFusedVB workgroups, one per
+// CU) fits the device's CUs and every thread's parameters fit PRE = 8.
+constexpr int kFusedVB = 4;
+static bool fused_ok(int ablk, int64_t nit) {
+    const int cus = device_cus();
+    const int grid = (ablk + kFusedVB - 1) / kFusedVB;
+    return cus > 0 && grid <= cus && nit <= 8;
+}
+
+template <typename T, int NS, int PRE, bool NORM>
+static int launch_fused_k(const LayoutK& Lk, const CopiesK& C, const mlearn_optim_state* st,
+                          const double* gpart_in, int64_t npart_in, double* gpart, double* ppart,
+                          int ablk, uint64_t* bar, hipStream_t s) {
+    auto kern = optim_fused_kernel<T, NS, PRE, kFusedVB, NORM>;
+    int rc = set_lds_attr((const void*)kern, kFusedLds, "optim_fused");
+    if (rc) return rc;
+    GridBarK gb{bar, bar + kBarShards * kBarStride, bar + kBarShards * kBarStride + 8};
+    const int grid = (ablk + kFusedVB - 1) / kFusedVB;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256 * kFusedVB), kFusedLds, s, Lk, C, st->params,
+                       st->grads, st->adam_m, st->adam_v, st->init_norms, st->step, gpart_in,
+                       npart_in, gpart, ppart, ablk, st->lr, st->b1, st->b2, st->eps,
+                       st->max_grad_norm, st->normalize_params, st->normalize_layernorms, gb);
+    return check_launch("optim_step (fused)");
+}
+
+template <typename T>
+static int launch_fused(int nslot, int64_t nit, int norm, const LayoutK& Lk, const CopiesK& C,
+                        const mlearn_optim_state* st, const double* gpart_in, int64_t npart_in,
+                        double* gpart, double* ppart, int ablk, uint64_t* bar, hipStream_t s) {
+#define ML_FUSED(NS)                                                                              \
+    case NS:                                                                                      \
+        if (nit <= 1)                                                                             \
+            return norm ? launch_fused_k<T, NS, 1, true>(Lk, C, st, gpart_in, npart_in, gpart,    \
+                                                         ppart, ablk, bar, s)                     \
+                        : launch_fused_k<T, NS, 1, false>(Lk, C, st, gpart_in, npart_in, gpart,   \
+                                                          ppart, ablk, bar, s);                   \
+        return norm ? launch_fused_k<T, NS, 8, true>(Lk, C, st, gpart_in, npart_in, gpart, ppart, \
+                                                     ablk, bar, s)                                \
+                    : launch_fused_k<T, NS, 8, false>(Lk, C, st, gpart_in, npart_in, gpart,       \
+                                                      ppart, ablk, bar, s);
+    switch (nslot) {
+        ML_FUSED(2)
+        ML_FUSED(4)
+        ML_FUSED(6)
+        ML_FUSED(8)
+        ML_FUSED(10)
+        ML_FUSED(12)
+        ML_FUSED(14)
+        ML_FUSED(16)
+        default: break;
+    }
+#undef ML_FUSED
+    set_error("optim_step: %d projection slots", nslot);
+    return MLEARN_EINVAL;
+}
+
 }  // namespace ml
 
 using namespace ml;
@@ -501,18 +827,34 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
     double* ppart = gpart + kNormBlocks;
     const double* norm_part = gpart;
     int64_t nparts = kNormBlocks;
+    ML_REQUIRE(st->launch_form >= 0 && st->launch_form <= 2, "optim_step: launch_form %d",
+               st->launch_form);
+    const bool fused_fits =
+        fused_ok(ablk, (Lk.total + (int64_t)ablk * 256 - 1) / ((int64_t)ablk * 256));
+    ML_REQUIRE(st->launch_form != 2 || fused_fits,
+               "optim_step: the fused launch needs %d workgroups (one per CU) on %d CUs",
+               (ablk + kFusedVB - 1) / kFusedVB, device_cus());
+    const bool fused = fused_fits && st->launch_form != 1;
     if (st->grad_sumsq_part) {  // partials from the gradient reduction (no extra launch)
         ML_REQUIRE(st->grad_sumsq_nparts == (Lk.total + 63) / 64,
                    "optim_step: grad_sumsq_nparts %lld != %lld", (long long)st->grad_sumsq_nparts,
                    (long long)((Lk.total + 63) / 64));
         norm_part = st->grad_sumsq_part;
         nparts = st->grad_sumsq_nparts;
-    } else {
+    } else if (!fused) {  // (the fused launch forms the norm partials itself)
         hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, st->grads,
                            Lk.total, gpart);
     }
     const int nslot = 2 * Lk.L + (Lk.lstm_H ? 8 : 0);
     const int64_t nit = (Lk.total + (int64_t)ablk * 256 - 1) / ((int64_t)ablk * 256);
+    if (fused) {
+        const int norm = st->grad_sumsq_part ? 0 : 1;
+        if (dtype == MLEARN_DTYPE_BF16)
+            return launch_fused<bf16>(nslot, nit, norm, Lk, C, st, norm_part, nparts, gpart, ppart,
+                                      ablk, (uint64_t*)(gpart + optim_bar_offset(Lk)), s);
+        return launch_fused<float>(nslot, nit, norm, Lk, C, st, norm_part, nparts, gpart, ppart,
+                                   ablk, (uint64_t*)(gpart + optim_bar_offset(Lk)), s);
+    }
     auto adam = nit <= 1 ? adam_kernel<1> : nit <= 2 ? adam_kernel<2> : nit <= 4 ? adam_kernel<4> : adam_kernel<8>;
     hipLaunchKernelGGL(adam, dim3((unsigned)ablk), dim3(256), 0, s, Lk, st->params,
                        st->grads, st->adam_m, st->adam_v, (const int32_t*)st->step, norm_part,

@@ -792,9 +792,12 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
     const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
     const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
 
-    // two register sets of staged rows: chunk c + 2 is in flight while chunk c
-    // is multiplied out of LDS and chunk c + 1 is written to the other buffer
-    u4 rx[2][PER], ry[2][PER];
+    // NS register sets of staged rows: chunks c + 1 .. c + NS are in flight
+    // while chunk c is multiplied out of LDS (two LDS stages); the chunk loop
+    // is unrolled by lcm(NS, 2) so that every set / stage index is static
+    constexpr int NS = ML_WG_SETS;
+    constexpr int U = NS % 2 ? 2 * NS : NS;
+    u4 rx[NS][PER], ry[NS][PER];
     auto gload = [&](int c, int set) {
         const int64_t mb0 = m0 + (int64_t)c * kWgChunk;
 #pragma unroll
@@ -838,27 +841,24 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
                 for (int b = 0; b < 2; ++b) acc[a][b] = MT<T>::mma(fa[a], fb[b], acc[a][b]);
         }
     };
-    gload(0, 0);
-    if (nchunks > 1) gload(1, 1);
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if (k < nchunks) gload(k, k);
     sstore(0, 0);
-    if (nchunks > 2) gload(2, 0);
+    if (NS < nchunks) gload(NS, 0);
     __syncthreads();
-    for (int c = 0; c < nchunks; c += 2) {
-        // even chunk c: buffer 0; chunk c + 1 waits in set 1
-        compute(0);
-        if (c + 1 < nchunks) {
-            sstore(1, 1);
-            if (c + 3 < nchunks) gload(c + 3, 1);
+    for (int c = 0; c < nchunks; c += U) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            // chunk c + k: LDS stage k % 2; chunk c + k + 1 waits in set (k + 1) % NS
+            if (c + k >= nchunks) break;
+            compute(k % 2);
+            if (c + k + 1 < nchunks) {
+                sstore((k + 1) % 2, (k + 1) % NS);
+                if (c + k + 1 + NS < nchunks) gload(c + k + 1 + NS, (k + 1) % NS);
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (c + 1 >= nchunks) break;
-        // odd chunk c + 1: buffer 1; chunk c + 2 waits in set 0
-        compute(1);
-        if (c + 2 < nchunks) {
-            sstore(0, 0);
-            if (c + 4 < nchunks) gload(c + 4, 0);
-        }
-        __syncthreads();
     }
     if (!wi_on || !wj_on) return;
     float* out = J.out + (int64_t)split * J.I * J.J;

@@ -47,6 +47,9 @@ template <typename T> constexpr int wg_chunk() { return sizeof(T) == 2 ? ML_WG_C
 static inline int wg_chunk_es(size_t es) { return es == 2 ? ML_WG_CHUNK : 32; }
 constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number of 32-row tiles)
 
+#ifndef ML_WG_SETS
+#define ML_WG_SETS 2  // weight-gradient chunks in flight (register sets of staged rows)
+#endif
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif

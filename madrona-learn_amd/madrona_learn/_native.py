@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -90,7 +90,7 @@ class OptimState(Structure):
                 ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float),
                 ("max_grad_norm", c_float), ("normalize_params", c_int32),
                 ("normalize_layernorms", c_int32), ("grad_sumsq_part", c_void_p),
-                ("grad_sumsq_nparts", c_int64)]
+                ("grad_sumsq_nparts", c_int64), ("launch_form", c_int32), ("pad_", c_int32)]
 
 
 class Lstm(Structure):  # mlearn_lstm
