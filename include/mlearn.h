@@ -434,14 +434,15 @@ typedef struct mlearn_optim_state {
                                       by the gradient reduction (grad_sumsq_out); the
                                       clip_by_global_norm norm then comes from them */
     int64_t grad_sumsq_nparts;
-    int32_t launch_form;           /* 0 = the library's choice (one fused launch, ABI 21:
-                                      [norm partials] -> clip + Adam -> projections + images
-                                      with in-launch grid barriers, where its one-workgroup-
-                                      per-CU grid fits the device; else the split launches),
-                                      1 = the split launches (norm partials, Adam, projection),
-                                      2 = the fused launch (MLEARN_EINVAL where it does not
-                                      apply).  Bit-identical results.  The workspace must be
-                                      zeroed once before its first use (barrier counters). */
+    int32_t launch_form;           /* 0 = the library's choice (the split launches: measured
+                                      no slower than the fused one on MI355X), 1 = the split
+                                      launches (norm partials, Adam, projection), 2 = ONE fused
+                                      launch (ABI 21: [norm partials] -> clip + Adam ->
+                                      projections + images with in-launch grid barriers;
+                                      MLEARN_EINVAL where its one-workgroup-per-CU grid does
+                                      not fit the device).  Bit-identical results.  The
+                                      workspace must be zeroed once before its first use
+                                      (the fused launch's barrier counters). */
     int32_t pad_;
 } mlearn_optim_state;
 

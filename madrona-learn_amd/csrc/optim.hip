@@ -51,6 +51,7 @@ static CopiesK make_copies(const mlearn_mlp_policy& p, const mlearn_lstm* r = nu
 
 __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
                                                             double* part) {
+#pragma clang fp contract(off)  // (one rounding per operation: optim_fused_kernel's bits)
     __shared__ double sh[4];
     double s = 0;
     // eight of this thread's strided elements in flight at a time, summed in index order
@@ -123,6 +124,25 @@ __device__ inline float global_norm(const double* gpart, int64_t npart) {
     return gn_sh;
 }
 
+// clip_by_global_norm + one Adam step of one parameter (optax 0.1.9
+// scale_by_adam with bias correction).  Contraction off: one rounding per
+// operation as written, so every kernel that calls this (adam_kernel,
+// optim_fused_kernel) produces the same bits whatever the compiler's
+// vectorisation of the caller (an fma's choice of which product to keep
+// unrounded otherwise differs between the two kernels' schedules).
+__device__ __forceinline__ float adam_param(float g, float m_old, float v_old, float q_old, float gn,
+                                            float max_norm, float b1, float b2, float eps, float lr,
+                                            int count, float& mm, float& vv) {
+#pragma clang fp contract(off)
+    if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
+    mm = (1.f - b1) * g + b1 * m_old;
+    vv = (1.f - b2) * (g * g) + b2 * v_old;
+    const float mhat = mm / (1.f - powf(b1, (float)count));
+    const float vhat = vv / (1.f - powf(b2, (float)count));
+    const float u = mhat / (sqrtf(vhat) + eps);
+    return q_old + (-lr) * u;
+}
+
 template <int PRE>
 __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict__ params,
                                                    const float* __restrict__ grads,
@@ -130,6 +150,7 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
                                                    const int32_t* step, const double* gpart,
                                                    int64_t npart, float lr, float b1, float b2, float eps,
                                                    float max_norm, double* proj_part) {
+#pragma clang fp contract(off)  // (one rounding per operation: optim_fused_kernel's bits)
     // grid-stride over the parameters with at most kAdamBlocks blocks, so the
     // projection reduces a short, fixed list of per-block partials
     __shared__ float sh[4][kMaxSlots];
@@ -164,13 +185,9 @@ __global__ __launch_bounds__(256) void adam_kernel(LayoutK Lk, float* __restrict
         // (recurrent layouts: the alignment padding before the LSTM segment is not a parameter)
         const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
         if (p < Lk.total && !pad) {
-            if (!(gn < max_norm)) g = (g / gn) * max_norm;  // clip_by_global_norm
-            const float mm = (1.f - b1) * g + b1 * m_old;
-            const float vv = (1.f - b2) * (g * g) + b2 * v_old;
-            const float mhat = mm / (1.f - powf(b1, (float)count));
-            const float vhat = vv / (1.f - powf(b2, (float)count));
-            const float u = mhat / (sqrtf(vhat) + eps);
-            const float np = q_old + (-lr) * u;
+            float mm, vv;
+            const float np = adam_param(g, m_old, v_old, q_old, gn, max_norm, b1, b2, eps, lr,
+                                        count, mm, vv);
             m[p] = mm;
             v[p] = vv;
             params[p] = np;
@@ -253,6 +270,7 @@ __global__ __launch_bounds__(256) void project_kernel(LayoutK Lk, CopiesK C, flo
                                                       const float* init_norms, const double* ppart,
                                                       int nblk, int norm_params, int norm_ln,
                                                       int32_t* step) {
+#pragma clang fp contract(off)  // (one rounding per operation: optim_fused_kernel's bits)
     // per-slot sums of squares of the updated tensors (ppo.py:303-338), the
     // same fixed-order tree in every block
     __shared__ double red[4][kMaxSlots];
@@ -380,7 +398,7 @@ __device__ inline void grid_sync(const GridBarK& gb, uint64_t target) {
                 __hip_atomic_store(gb.fail, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
         }
     }
     __syncthreads();
@@ -393,6 +411,7 @@ __global__ __launch_bounds__(256 * VB) void optim_fused_kernel(
     int32_t* step, const double* gpart_in, int64_t npart_in, double* gpart, double* ppart, int ablk,
     float lr, float b1, float b2, float eps, float max_norm, int norm_params, int norm_ln,
     GridBarK gb) {
+#pragma clang fp contract(off)  // (one rounding per operation: the split kernels' bits)
     extern __shared__ char fused_dyn[];  // (unused: sized so that one workgroup fits per CU)
     __shared__ float sh[VB][4][kMaxSlots];
     __shared__ double red[4][kMaxSlots];
@@ -482,7 +501,9 @@ __global__ __launch_bounds__(256 * VB) void optim_fused_kernel(
     __syncthreads();
     const float gn = gn_sh;
 
-    // clip + Adam (adam_kernel's arithmetic), new values kept in registers
+    // clip + Adam (adam_kernel's arithmetic); the new values and moments stay
+    // in registers until after the barrier, so the barrier's vmcnt(0) waits
+    // for the partials' stores only
     float nq[PRE];
 #pragma unroll
     for (int u = 0; u < PRE; ++u) {
@@ -493,16 +514,8 @@ __global__ __launch_bounds__(256 * VB) void optim_fused_kernel(
         int slot = -2;
         const bool pad = Lk.lstm_H && p >= Lk.mlp_total && p < Lk.lstm_off;
         if (p < Lk.total && !pad) {
-            float g = gq[u];
-            if (!(gn < max_norm)) g = (g / gn) * max_norm;
-            const float mm = (1.f - b1) * g + b1 * mq[u];
-            const float vv = (1.f - b2) * (g * g) + b2 * vq[u];
-            const float mhat = mm / (1.f - powf(b1, (float)count));
-            const float vhat = vv / (1.f - powf(b2, (float)count));
-            const float up = mhat / (sqrtf(vhat) + eps);
-            nq[u] = qq[u] + (-lr) * up;
-            m[p] = mm;
-            v[p] = vv;
+            nq[u] = adam_param(gq[u], mq[u], vq[u], qq[u], gn, max_norm, b1, b2, eps, lr, count,
+                               mq[u], vq[u]);
             slot = proj_slot(Lk, p);
             contrib = nq[u] * nq[u];
         }
@@ -575,7 +588,11 @@ __global__ __launch_bounds__(256 * VB) void optim_fused_kernel(
                 val = sqrtf((float)Lk.H / sq[slot]) * val;
             }
         }
-        if (!pad) params[p] = val;
+        if (!pad) {
+            params[p] = val;
+            m[p] = mq[u];
+            v[p] = vq[u];
+        }
         write_copies<T>(Lk, C, p, val);
     }
 }
@@ -834,7 +851,12 @@ static int optim_launch(const LayoutK& Lk, const CopiesK& C, int dtype,
     ML_REQUIRE(st->launch_form != 2 || fused_fits,
                "optim_step: the fused launch needs %d workgroups (one per CU) on %d CUs",
                (ablk + kFusedVB - 1) / kFusedVB, device_cus());
-    const bool fused = fused_fits && st->launch_form != 1;
+    // the library's choice is the split launches: the fused launch measured no
+    // faster at world 1 (9.32 / 9.25 vs 9.26 / 9.26 ms per headline update)
+    // and 2.4 % slower in the emulated world-8 share (3.70 vs 3.61 ms): its
+    // grid barrier costs what the kernel boundary it replaces did
+    // (profiles/r06_optim_fused_ab.txt)
+    const bool fused = fused_fits && st->launch_form == 2;
     if (st->grad_sumsq_part) {  // partials from the gradient reduction (no extra launch)
         ML_REQUIRE(st->grad_sumsq_nparts == (Lk.total + 63) / 64,
                    "optim_step: grad_sumsq_nparts %lld != %lld", (long long)st->grad_sumsq_nparts,

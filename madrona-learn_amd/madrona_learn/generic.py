@@ -470,9 +470,14 @@ class TorchRollout:
         # the sampling counter lives on the device (RolloutState.counters[0]);
         # the torch path reads it once per rollout
         base = int(rollout_state.counters[0].item())
-        ps.begin_rollout()
         N = m.N
         rec = ps.recurrent
+        if m.P > 1:
+            # a population (self-play split, pbt.py:130-133): policy p acts for
+            # env columns [p B, (p + 1) B) (init_training excluded recurrent
+            # and stateful-preprocess populations on this path)
+            return self._collect_population(rollout_state, gamma, key, base)
+        ps.begin_rollout()
         if rec:
             # the live carry in sim order (rollouts.py:898-901, 941-942) and
             # the carry entering every BPTT chunk (rnn_start_states,
@@ -526,6 +531,58 @@ class TorchRollout:
             rnn_in = rollout_state.rnn_states if rec else ps.rnn0
             out, _ = ps.actor_critic.critic_only(rnn_in, ps.preprocess(rollout_state.cur_obs))
         s.bootstrap.copy_(_critic_value(out["critic"]))
+
+    def _step_sim(self, rollout_state, t, gamma):
+        m = self.mgr
+        s = m.store
+        N = m.N
+        step_input = {
+            "state": rollout_state.sim_state,
+            "actions": m._sim_actions(t),
+            "resets": m._resets,
+            "sim_ctrl": rollout_state.sim_ctrl,
+            "pbt": {"policy_assignments": rollout_state.policy_assignments},
+        }
+        so = rollout_state.step_fn(step_input)
+        rew = so["rewards"].reshape(-1)
+        rew = (rew if rew.dtype == torch.float32 else rew.float()).contiguous()
+        dn = so["dones"].reshape(-1)
+        dn = (dn.view(torch.uint8) if dn.dtype == torch.bool else (dn != 0).view(torch.uint8)) \
+            .contiguous()
+        nat.check(nat.lib().mlearn_rollout_post_step(
+            nat.ptr(rew), nat.ptr(dn), N, nat.ptr(s.rewards[t]), nat.ptr(s.dones[t]),
+            nat.ptr(rollout_state.env_returns), nat.ptr(s.env_returns_trace[t]), gamma,
+            nat.stream_handle()), "rollout_post_step")
+        rollout_state.sim_state = so["state"]
+        rollout_state.cur_obs = so["obs"]
+
+    def _collect_population(self, rollout_state, gamma, key, base):
+        """rollout_loop for P torch-path policies: per step every policy's
+        ActorCritic.rollout on its own env columns (its sampling counters are
+        those of its env ids, as in the fused population launch), the store
+        columns written, then one sim step and post-step for all envs."""
+        m = self.mgr
+        s = m.store
+        B = m.B
+        for t in range(m.T):
+            obs = rollout_state.cur_obs
+            for p, ps in enumerate(m.policies):
+                c = slice(p * B, (p + 1) * B)
+                pre = ps.preprocess(_slice_obs(obs, p * B, (p + 1) * B))
+                with torch.no_grad():
+                    out, _ = ps.actor_critic.rollout(
+                        PhiloxKey(key[0], key[1], base + t, m.env_offset + p * B), ps.rnn0, pre)
+                ps.codec.encode(pre, s.obs[t, c])
+                s.actions[t, c].copy_(out["actions"].reshape(B, -1))
+                s.log_probs[t, c].copy_(out["log_probs"].reshape(B, -1))
+                s.values[t, c].copy_(_critic_value(out["critic"]))
+            self._step_sim(rollout_state, t, gamma)
+        obs = rollout_state.cur_obs
+        for p, ps in enumerate(m.policies):
+            with torch.no_grad():
+                out, _ = ps.actor_critic.critic_only(
+                    ps.rnn0, ps.preprocess(_slice_obs(obs, p * B, (p + 1) * B)))
+            s.bootstrap[p * B:(p + 1) * B].copy_(_critic_value(out["critic"]))
 
 
 class TorchPPO:
@@ -614,13 +671,19 @@ class TorchPPO:
         bptt steps, time-major [bptt, mb, ...]; store row of (t, seq) =
         (c * bptt + t) * N + b with c, b = divmod(seq, N)."""
         s = self.store
-        N, bp = s.N, self.bptt
+        # this policy's env columns [col0, col0 + view.N) of the [T][N] store
+        # (a population's policy p: col0 = p B)
+        N, bp = int(self.view.N), self.bptt
+        col0 = int(getattr(self, "col0", 0))
         seq = seqs.long()
         c, b = seq // N, seq % N
         t = torch.arange(bp, device=seq.device)[:, None]
-        rows = (c[None, :] * bp + t) * N + b[None, :]          # [bptt, mb]
-        flat = lambda x: x.reshape(s.T * N, *x.shape[2:])     # noqa: E731
-        adv_src = s.advantages if self.view.advantages == s.advantages.data_ptr() else s.returns
+        rows = (c[None, :] * bp + t) * s.N + col0 + b[None, :]  # [bptt, mb]
+        flat = lambda x: x.reshape(s.T * s.N, *x.shape[2:])   # noqa: E731
+        # the view's advantage column (the returns column with
+        # compute_advantages=False, RolloutManager.view), at this policy's col0
+        adv_src = s.advantages if self.view.advantages == s.advantages.data_ptr() + 4 * col0 \
+            else s.returns
         out = {"obs": flat(s.obs)[rows], "actions": flat(s.actions)[rows],
                "log_probs": flat(s.log_probs)[rows], "values": flat(s.values)[rows],
                "returns": flat(s.returns)[rows], "advantages": flat(adv_src)[rows],

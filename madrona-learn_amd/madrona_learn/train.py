@@ -288,7 +288,7 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         # autograd over the user's modules, HIP kernels around them (generic.py)
         return _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
                                     num_policies, sim_batch, sim_fns, restore_ckpt, profile_port,
-                                    generic_why)
+                                    generic_why, policy_ids=list(policy_ids))
     prefix = policy.actor_critic.backbone.prefix
     from .rollouts import obs_to_matrix
     obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
@@ -415,39 +415,76 @@ def _fused_tree_problem(policy, rollout_state, sim_batch, cfg):
 
 
 def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
-                         num_policies, sim_batch, sim_fns, restore_ckpt, profile_port, why):
+                         num_policies, sim_batch, sim_fns, restore_ckpt, profile_port, why,
+                         policy_ids=(0,)):
     """init_training for a tree outside the fused kernels (generic.py): the
     user's torch modules train under autograd, eagerly (no HIP graph), with
     sampling, post-step, GAE, advantage statistics, action_stats and the
-    optimizer on the HIP kernels."""
+    optimizer on the HIP kernels.  A population (cfg.pbt, self-play split)
+    gets one copy of the tree per train policy this rank holds, each with its
+    own initialisation, optimizer state and update RNG (_make_policies,
+    train_state.py:439-488; the reference vmaps algo.update over the policy
+    axis, train.py:165-174), trained one after the other."""
+    import copy
     import sys
-    from .generic import TorchPolicyState, TorchPPO, TorchTrainState
+    from .generic import TorchPolicyState, TorchPPO, TorchTrainState, _has_state
     from .models import action_groups
-    if num_policies != 1:
-        raise NotImplementedError(f"populations need a fused policy tree ({why})")
+    P = len(policy_ids)
+    if num_policies > 1:
+        if _has_state(policy.obs_preprocess):
+            raise NotImplementedError(
+                "a population on the torch path with a stateful ObservationsPreprocess (its "
+                "per-policy state is not part of the PBT policy copies here)")
+        if any(True for _ in _leaves(policy.actor_critic.init_recurrent_state(1))):
+            raise NotImplementedError("a recurrent population on the torch path")
     print(f"[madrona_learn] policy tree outside the fused kernels ({why}): training it with "
           "torch autograd (HIP sampling / GAE / statistics / optimizer)", file=sys.stderr)
     buckets = [b for _, g in action_groups(cfg.actions) for b in g]
-    ps = TorchPolicyState(policy.actor_critic, policy.obs_preprocess, device,
-                          rollout_state.cur_obs, cfg.compute_dtype, buckets, cfg.seed)
-    if bool(cfg.dreamer_v3_critic) != (ps.critic_bins > 1):
-        raise ValueError(f"TrainConfig.dreamer_v3_critic={cfg.dreamer_v3_critic} does not match "
-                         f"the policy's critic ({ps.critic_bins} output bins)")
-    dp.broadcast_(ps.params)
-    algo = TorchPPO(cfg.algo.setup())
-    ts = TorchTrainState(cfg, algo.init_hyperparams(cfg), ps, _split_seed(cfg.seed, 2))
-    ts.policy_id = 0
+    pss, tss, algos = [], [], []
+    # policy 0 keeps the user's modules (and cfg.seed: single-policy runs are
+    # unchanged); the others train copies taken before any of them creates
+    # its (lazily initialised) parameters, each then initialised with its own
+    # seed like the reference's per-policy init keys (train_state.py:439-488)
+    acs = [policy.actor_critic] + [copy.deepcopy(policy.actor_critic) for _ in policy_ids[1:]]
+    for i, pid in enumerate(policy_ids):
+        ac = acs[i]
+        seed = cfg.seed if num_policies == 1 else \
+            int(np.random.SeedSequence([int(cfg.seed), int(pid)]).generate_state(1)[0] & 0x7FFFFFFF)
+        obs_p = rollout_state.cur_obs if P == 1 else _obs_cols(rollout_state.cur_obs, P, i)
+        ps = TorchPolicyState(ac, policy.obs_preprocess, device, obs_p, cfg.compute_dtype,
+                              buckets, seed)
+        if bool(cfg.dreamer_v3_critic) != (ps.critic_bins > 1):
+            raise ValueError(f"TrainConfig.dreamer_v3_critic={cfg.dreamer_v3_critic} does not "
+                             f"match the policy's critic ({ps.critic_bins} output bins)")
+        dp.broadcast_(ps.params)
+        algo = TorchPPO(cfg.algo.setup())
+        ts = TorchTrainState(cfg, algo.init_hyperparams(cfg), ps,
+                             _split_seed(cfg.seed, 2 + 16 * pid))
+        ts.policy_id = pid
+        pss.append(ps)
+        tss.append(ts)
+        algos.append(algo)
     value_norm = None
     if cfg.normalize_values:
         # EMANormalizer.init_estimates (moving_avg.py:56-76), the fused path's
         # record layout: mu 0, inv_sigma 1, sigma 1, biased sums 0, N 0
-        value_norm = torch.zeros((1, 8), dtype=torch.float32, device=device)
+        value_norm = torch.zeros((P, 8), dtype=torch.float32, device=device)
         value_norm[:, 1] = 1.0
         value_norm[:, 2] = 1.0
-        ts.value_norm_est = value_norm[0]
-        ts.value_norm_count = torch.zeros(1, dtype=torch.int32, device=device)
-    tsm = TrainStateManager(policy_states=ps, train_states=ts, pbt_rng=None,
+        vcount = torch.zeros(P, dtype=torch.int32, device=device)
+        for i, ts in enumerate(tss):
+            ts.value_norm_est, ts.value_norm_count = value_norm[i], vcount[i:i + 1]
+    tsm = TrainStateManager(policy_states=pss[0] if P == 1 else pss,
+                            train_states=tss[0] if P == 1 else tss, pbt_rng=None,
                             user_state=user_hooks.init_user_state(), value_norm=value_norm)
+    if cfg.pbt is not None:
+        # the population key and the initial hyperparameter draw (train.py:320-351)
+        from .pbt import new_pbt_rng, sample_initial_hyperparams
+        tsm.pbt_rng = new_pbt_rng(cfg.seed)
+        sample_initial_hyperparams(cfg, tsm)
+        if cfg.pbt.num_past_policies > 0:
+            from .pbt import init_past_policies
+            init_past_policies(cfg, tsm)
     start = 0
     if restore_ckpt is not None:
         path = _ckpt_file(restore_ckpt, rank, W)
@@ -455,20 +492,41 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
         ckpt_rollout = torch.load(path, map_location="cpu", weights_only=True).get("rollout")
         if ckpt_rollout is not None:
             rollout_state.counters[1].copy_(ckpt_rollout["counters"][1])
-    rollout_mgr = RolloutManager(cfg, rollout_state, [ps], env_offset=rank * sim_batch)
+    rollout_mgr = RolloutManager(cfg, rollout_state, pss, env_offset=rank * sim_batch)
     rollout_mgr.get_episode_scores = policy.get_episode_scores
-    names = algo.add_metrics(cfg, [])
+    names = algos[0].add_metrics(cfg, [])
     names = rollout_mgr.add_metrics(cfg, names)
     names = user_hooks.add_metrics(names)
-    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device, num_policies=1)
-    algo.prepare(cfg, ps, ts, rollout_mgr.view(0), dp, policy_idx=0)
-    algo.store = rollout_mgr.store
+    metrics = TrainingMetrics(names, cfg.metrics_buffer_size, device, num_policies=P)
+    for i, (ps, ts, algo) in enumerate(zip(pss, tss, algos)):
+        algo.prepare(cfg, ps, ts, rollout_mgr.view(i), dp, policy_idx=i)
+        algo.store = rollout_mgr.store
+        algo.col0 = i * rollout_mgr.B
     print(cfg)
-    mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, [algo], user_hooks, dp,
+    mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                           update_idx=start, use_graph=False, profile_port=profile_port)
     mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
     mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
     return mgr
+
+
+def _leaves(x):
+    if isinstance(x, torch.Tensor):
+        yield x
+    elif isinstance(x, dict):
+        for v in x.values():
+            yield from _leaves(v)
+    elif isinstance(x, (list, tuple)):
+        for v in x:
+            yield from _leaves(v)
+
+
+def _obs_cols(obs, P, i):
+    """Policy i's env columns of the observations (sample for its init)."""
+    n = (next(iter(obs.values())) if isinstance(obs, dict) else obs).shape[0] // P
+    if isinstance(obs, dict):
+        return {k: v[i * n:(i + 1) * n] for k, v in obs.items()}
+    return obs[i * n:(i + 1) * n]
 
 
 def stop_training(training_mgr: TrainingManager):  # train.py:148-153

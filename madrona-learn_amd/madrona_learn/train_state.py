@@ -403,6 +403,11 @@ class PolicyState:
 class PolicyTrainState:
     """Optimizer + per-policy training state (train_state.py:85-136)."""
 
+    # mlearn_optim_state.launch_form of the optimizer step: 0 the library's
+    # choice (the fused one-launch chain where it applies), 1 the split
+    # launches, 2 the fused launch (A/B runs; bit-identical results)
+    optim_launch_form = 0
+
     def __init__(self, cfg: TrainConfig, hyper_params, policy_state: PolicyState, key):
         self.hyper_params = hyper_params
         dev = policy_state.device
@@ -435,6 +440,7 @@ class PolicyTrainState:
         o.max_grad_norm = float(hyper_params.max_grad_norm)
         o.normalize_params = 1
         o.normalize_layernorms = 1
+        o.launch_form = int(self.optim_launch_form)
         self.optim_desc = o
 
     def optimizer_step(self, policy_state: PolicyState):

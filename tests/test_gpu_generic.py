@@ -457,3 +457,83 @@ def test_wide_head_routes_to_torch_path(gpu):
     torch.cuda.synchronize()
     assert torch.isfinite(ps.params).all() and not torch.equal(ps.params, p0)
     assert np.isfinite(mgr.metrics.last()["Loss"].mean)
+
+
+def test_population_of_separate_backbones_matches_oracle(gpu):
+    """A population (cfg.pbt, self-play split) of a tree outside the fused
+    kernels: 2 train policies of BackboneSeparate on the torch path, each its
+    own copy of the modules, init, optimizer and update RNG (the reference
+    vmaps algo.update over the policy axis, train.py:165-174).  Policy p acts
+    for env columns [p B, (p + 1) B); each policy's stored values / log-probs
+    against the oracle forward with ITS parameters, GAE bit-exact, and each
+    policy's whole update (2 epochs x 4 minibatches of its own columns)
+    against oracle/separate_ref.py (test_backbone_separate_update_matches_oracle's
+    tolerances)."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    P, B, H, L, mb, T = 2, 64, 64, 2, 16, 32
+    N = P * B
+    dt = torch.float32
+    env = DummyVecEnv(N, 64, 6, seed=8, device=gpu)
+    ac = ml.ActorCritic(
+        backbone=ml.BackboneSeparate(actor_encoder=ml.BackboneEncoder(net=MLP(H, L, dt)),
+                                     critic_encoder=ml.BackboneEncoder(net=MLP(H, L, dt))),
+        actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+        critic=DenseLayerCritic(dt))
+    pbt = ml.PBTConfig(num_teams=1, team_size=1, num_train_policies=P, num_past_policies=0,
+                       self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0)
+    cfg = dataclasses.replace(_cfg(N, mb), pbt=pbt)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac))
+    pss, tss = mgr.state.policy_list, mgr.state.train_list
+    assert len(pss) == P and all(getattr(ps, "generic", False) for ps in pss)
+    assert pss[0].actor_critic is not pss[1].actor_critic
+    p0s = [_named(ps) for ps in pss]
+    order = [n for n, _, _ in pss[0].layout["params"]]
+    assert any(not np.array_equal(p0s[0][k], p0s[1][k]) for k in order)  # own inits
+    oenv = onat.Env(N, 64, env.k0, env.k1, 0)
+    oenv.reset()
+    mgr.update_iter()
+    torch.cuda.synchronize()
+    s = mgr.rollout_mgr.store
+    acts = s.actions.cpu().numpy()
+    obs = s.obs.float().cpu().numpy()
+    for t in range(T):
+        assert np.array_equal(obs[t], oenv.obs), t
+        o, r, d = oenv.step(acts[t])
+        assert np.array_equal(s.rewards[t].cpu().numpy(), r)
+        assert np.array_equal(s.dones[t].cpu().numpy(), d)
+    full = {k: v.float().cpu().numpy() if v.dtype == torch.bfloat16 else v.cpu().numpy()
+            for k, v in s.as_dict().items()}
+    hp = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
+          "normalize_advantages": True}
+    for p in range(P):
+        c = slice(p * B, (p + 1) * B)
+        p0 = p0s[p]
+        logits, V, _ = sref.forward(p0, obs[:, c].reshape(T * B, 64), L, "f32")
+        lp, _ = ref.action_stats(logits, BUCKETS, acts[:, c].reshape(T * B, 6))
+        np.testing.assert_allclose(s.values[:, c].cpu().numpy().reshape(-1), V, rtol=1e-4,
+                                   atol=1e-4)
+        np.testing.assert_allclose(s.log_probs[:, c].cpu().numpy().reshape(-1, 6), lp,
+                                   rtol=1e-4, atol=1e-4)
+        store = {k: (v[:, c] if v.ndim >= 2 else v[c]) for k, v in full.items()}
+        adv, _ = ref.gae_f32(store["rewards"], store["values"], store["dones"],
+                             s.bootstrap[c].cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+        assert np.array_equal(store["advantages"], adv)
+        init_norms = {k: float(np.sqrt((v * v).sum())) for k, v in p0.items()
+                      if k.endswith("kernel") and k.startswith("backbone.")}
+        want, _ = sref.ppo_update(dict(p0), order, store, hp, BUCKETS, L, init_norms,
+                                  num_epochs=2, minibatch_size=mb, bptt=T,
+                                  key=tss[p].update_prng_key, epoch_base=0, mode="f32", lr=3e-4,
+                                  max_grad_norm=0.5)
+        got = _named(pss[p])
+        g = np.concatenate([got[k].reshape(-1) for k in order])
+        w = np.concatenate([want[k].reshape(-1) for k in order])
+        z = np.concatenate([p0[k].reshape(-1) for k in order])
+        np.testing.assert_allclose(g, w, rtol=0, atol=1e-4, err_msg=f"policy {p}")
+        close = np.abs(g - w) <= 2e-5 + 1e-4 * np.abs(w)
+        assert close.mean() >= 0.999, (p, close.mean())
+        dg, dw = g - z, w - z
+        assert dg @ dw / (np.linalg.norm(dg) * np.linalg.norm(dw)) > 0.999
+        assert int(tss[p].step.item()) == 2 * (B // mb)

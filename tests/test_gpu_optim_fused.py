@@ -9,7 +9,8 @@ several steps (one with a clipped norm), with the norm partials taken from
 the gradient reduction (world 1) or formed in the launch (the all-reduced
 gradient, world > 1), on MLP and LSTM layouts.  The oracle comparisons of
 the optimizer (tests/test_gpu_policy.py, tests/test_gpu_lstm.py) and of
-every full update run on the fused launch, the library's default."""
+every full update run on the split launches, the library's default (the
+fused launch measured no faster)."""
 
 import numpy as np
 import pytest
