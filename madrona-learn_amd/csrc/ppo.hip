@@ -870,7 +870,12 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
             for (int e = 0; e < 16; ++e) {
                 const int i = i0 + iw + 32 * a + acc_row(e, lane);
                 const int j = j0 + jw + 32 * b + (lane & 31);
-                if (i < J.I && j < J.J) out[(int64_t)i * J.J + j] = acc[a][b][e];
+                // nontemporal: the slabs are read once, by the next launch
+                // (reduce_grads), so they need not sit dirty in L2 at the
+                // kernel boundary (headline 9.08 / 9.11 -> 8.97 / 9.00 ms per
+                // update, profiles/r06_wgrad_variants_ab.txt)
+                if (i < J.I && j < J.J)
+                    __builtin_nontemporal_store(acc[a][b][e], out + (int64_t)i * J.J + j);
             }
 }
 

@@ -15,7 +15,9 @@ fi
 IFS=';' read -ra RUNS <<< "${ARGS:-}"
 for run in "${RUNS[@]}"; do
   name=${run%%=*}; a=${run#*=}
-  timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline $a > $O/$name.json 2> $O/$name.err
+  # name@variant: bench with madrona-learn_amd/variants/libmlearn_<variant>.so
+  lib=""; if [[ "$name" == *@* ]]; then lib=$PWD/madrona-learn_amd/variants/libmlearn_${name#*@}.so; fi
+  MADRONA_LEARN_LIB=${lib:-$PWD/madrona-learn_amd/madrona_learn/_lib/libmlearn.so} timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline $a > $O/$name.json 2> $O/$name.err
   rc=$?; if [ $rc -ne 0 ]; then echo "$name rc=$rc"; tail -5 $O/$name.err; exit $rc; fi
   python -c "import json; d=json.load(open('$O/$name.json')); k=d.get('kernels',{}); print('$name', round(d['ms_per_step'],4), 'ms', 'mb', {x: round(y,2) if isinstance(y,float) else y for x,y in k.get('minibatch',{}).items()})"
 done
