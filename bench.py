@@ -419,6 +419,8 @@ def main():
     ap.add_argument("--optim-launch", type=int, choices=[0, 1, 2], default=0,
                     help="PolicyTrainState.optim_launch_form: 0 the library's choice, 1 the "
                          "split optimizer launches, 2 the fused one (A/B runs)")
+    ap.add_argument("--no-fused-gae", action="store_true",
+                    help="RolloutManager.fused_gae = False: GAE as its own launch (A/B runs)")
     args = ap.parse_args()
     from madrona_learn.train_state import PolicyTrainState
     PolicyTrainState.optim_launch_form = args.optim_launch
@@ -426,6 +428,7 @@ def main():
     if args.per_policy_rollouts:
         RolloutManager.population_launch = False
     RolloutManager.rollout_kernel = args.rollout_kernel
+    RolloutManager.fused_gae = not args.no_fused_gae
     if args.emulate_world > 1:
         return emulate_world(args)
 

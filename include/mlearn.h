@@ -682,6 +682,18 @@ typedef struct mlearn_rollout_out {
                                    does not apply).  The row split accumulates the trunk and
                                    heads in another order: logits within a bf16 ulp of the
                                    feature split's */
+    float* advantages;          /* [T][ld] or NULL (ABI 21): when set, the call also runs GAE
+                                   (compute_advantages, algo_common.py:84-130) over the rollout
+                                   it just stored -- rewards, values, dones, bootstrap -- writing
+                                   the advantages only (returns = advantages + values derived by
+                                   their consumers, mlearn_gae_f32 with returns = NULL), with
+                                   gae_gamma and the caller's single-rounded gae_gamma_lambda:
+                                   fused into the row-split kernel's tile epilogue (T <= 32,
+                                   each wave reads back the 16 envs' rows it just wrote), else
+                                   a trailing mlearn_gae_f32 launch.  Needs ld == N.  Same bits
+                                   as mlearn_gae_f32.  No value normaliser applies here (the
+                                   caller inverts normalised values with mlearn_gae_vnorm_f32) */
+    float gae_gamma, gae_gamma_lambda;
 } mlearn_rollout_out;
 int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                               const mlearn_lstm_carry* carry, const float* obs, int64_t N,

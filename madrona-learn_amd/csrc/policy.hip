@@ -614,6 +614,8 @@ struct RollK {
     int64_t ld;
     float gamma;
     int max_wg;          // mlearn_rollout_out.max_workgroups
+    float* adv;          // [T][ld] GAE advantages fused into the row-split epilogue, or null
+    float gae_gamma, gae_gl;
 };
 
 #include "rollout_rows16.h"
@@ -1062,7 +1064,8 @@ static int rollout_env_args(const mlearn_mlp_policy* policy, const mlearn_lstm* 
     }
     e->rk = RollK{out->obs, out->actions, out->log_probs, out->values, out->rewards, out->dones,
                   out->env_returns_trace, out->bootstrap, out->env_returns, out->start_h,
-                  out->start_c, out->T, out->bptt_len, out->ld, out->gamma, out->max_workgroups};
+                  out->start_c, out->T, out->bptt_len, out->ld, out->gamma, out->max_workgroups,
+                  nullptr, out->gae_gamma, out->gae_gamma_lambda};
     e->env = EnvK{(int4*)denv->state, denv->obs, denv->rewards, denv->dones, denv->k0, denv->k1,
                   denv->env_offset};
     e->P = make_policy_k(*policy);
@@ -1070,6 +1073,12 @@ static int rollout_env_args(const mlearn_mlp_policy* policy, const mlearn_lstm* 
     e->eoff = env_offset;
     return MLEARN_OK;
 }
+
+static int feature_split_rollout(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                 const PolicyK& P, const LstmK& R, const CarryK& cy,
+                                 const float* obs, int64_t N, const RollK& rk, uint32_t k0,
+                                 uint32_t k1, const uint64_t* step_ctr, uint32_t env_offset,
+                                 const EnvK& ek, hipStream_t s);
 
 extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
                                          const mlearn_lstm_carry* carry, const float* obs,
@@ -1095,8 +1104,37 @@ extern "C" int mlearn_policy_rollout_env(const mlearn_mlp_policy* policy, const 
                "policy_rollout_env: policy_kernel 2 (row split) needs the row-split step's policy "
                "shape, <= 8 action groups, no observation normaliser, max_workgroups 0 and N of "
                "32768 or a multiple of 256 from 65536");
-    if (r16 && out->policy_kernel != 1)
-        return launch_rollout16(P, obs, N, rk, k0, k1, step_ctr, env_offset, ek, s);
+    ML_REQUIRE(!out->advantages || out->ld == N,
+               "policy_rollout_env: advantages need ld == N (ld %lld, N %lld)",
+               (long long)out->ld, (long long)N);
+    if (r16 && out->policy_kernel != 1) {
+        RollK rk2 = rk;
+        if (out->advantages && out->T <= 32) rk2.adv = out->advantages;  // fused GAE
+        const int rc2 = launch_rollout16(P, obs, N, rk2, k0, k1, step_ctr, env_offset, ek, s);
+        if (rc2 || !out->advantages || rk2.adv) return rc2;
+        return mlearn_gae_f32(out->rewards, out->values, out->dones, out->bootstrap,
+                              out->advantages, nullptr, out->T, N, out->gae_gamma,
+                              out->gae_gamma_lambda, stream);
+    }
+    if (out->advantages) {  // the feature-split rollout, then GAE as its own launch
+        const int rc2 = feature_split_rollout(policy, lstm, P, R, cy, obs, N, rk, k0, k1, step_ctr,
+                                              env_offset, ek, s);
+        if (rc2) return rc2;
+        return mlearn_gae_f32(out->rewards, out->values, out->dones, out->bootstrap,
+                              out->advantages, nullptr, out->T, N, out->gae_gamma,
+                              out->gae_gamma_lambda, stream);
+    }
+    return feature_split_rollout(policy, lstm, P, R, cy, obs, N, rk, k0, k1, step_ctr, env_offset,
+                                 ek, s);
+}
+
+// The feature-split whole-rollout launch (policy_rollout_kernel) for the
+// policy's dtype / width / head.
+static int feature_split_rollout(const mlearn_mlp_policy* policy, const mlearn_lstm* lstm,
+                                 const PolicyK& P, const LstmK& R, const CarryK& cy,
+                                 const float* obs, int64_t N, const RollK& rk, uint32_t k0,
+                                 uint32_t k1, const uint64_t* step_ctr, uint32_t env_offset,
+                                 const EnvK& ek, hipStream_t s) {
 #define ML_LAUNCH_HC(T, HH, HC)                                                                 \
     (lstm ? launch_policy_rollout<T, HH, true, HC>(P, obs, N, rk, k0, k1, step_ctr, env_offset, R, \
                                                    cy, ek, s)                                     \
@@ -1135,6 +1173,9 @@ extern "C" int mlearn_policy_pop_prepare(const mlearn_mlp_policy* policies,
                                          void* pop, mlearn_stream_t stream) {
     ML_REQUIRE(num_policies >= 1 && policies && obs && outs && env_offsets && envs && pop,
                "policy_pop_prepare: null argument or no policies");
+    for (int p = 0; p < num_policies; ++p)
+        ML_REQUIRE(!outs[p].advantages,
+                   "policy_pop_prepare: advantages (fused GAE) is a single-policy rollout option");
     ML_REQUIRE(N >= 1, "policy_pop_prepare: N < 1");
     std::vector<PopEntry> h((size_t)num_policies);
     for (int p = 0; p < num_policies; ++p) {

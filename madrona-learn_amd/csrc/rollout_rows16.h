@@ -90,6 +90,51 @@ static bool rollout16_pop_eligible(const PolicyK& P0, int64_t N, int npol, int m
            tiles <= 0x7fffffff;
 }
 
+// GAE (algo_common.py:84-130, gae_kernel's arithmetic and order, so the same
+// bits) of the tile's 16 envs at the end of their rollout: lane (r, g) reads
+// back steps 8g .. 8g + 7 of env n that this wave just stored, the four
+// chunks run from the last to the first with the carry (next value, next
+// advantage) handed between the row's lanes, and the advantages are written
+// nontemporal as gae_kernel's (T <= 32).
+__device__ __forceinline__ void r16_gae(const RollK& rk, int64_t n, float boot, int g, int lane) {
+#pragma clang fp contract(off)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's store rows have landed)
+    constexpr int CH = 8;
+    const int T = rk.T, t0 = CH * g;
+    float v[CH], rw[CH], a[CH];
+    uint32_t d[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int64_t q = (int64_t)(t0 + j < T ? t0 + j : 0) * rk.ld + n;
+        v[j] = rk.values[q];
+        rw[j] = rk.rewards[q];
+        d[j] = rk.dones[q];
+    }
+    float nv = boot, na = 0.f;
+#pragma unroll
+    for (int c = 3; c >= 0; --c) {
+        if (g == c) {
+#pragma unroll
+            for (int j = CH - 1; j >= 0; --j) {
+                if (t0 + j >= T) continue;
+                const float nvj = d[j] ? 0.f : nv;
+                const float naj = d[j] ? 0.f : na;
+                const float td = (rw[j] + rk.gae_gamma * nvj) - v[j];
+                a[j] = td + rk.gae_gl * naj;
+                nv = v[j];
+                na = a[j];
+            }
+        }
+        if (c > 0) {  // chunk c's carry to the row's lane of chunk c - 1
+            nv = __shfl(nv, (lane & 15) + 16 * c);
+            na = __shfl(na, (lane & 15) + 16 * c);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+        if (t0 + j < T) __builtin_nontemporal_store(a[j], rk.adv + (int64_t)(t0 + j) * rk.ld + n);
+}
+
 // One 16-env tile's whole rollout on one wave: T policy steps with the sim
 // step and post-step fused, then the bootstrap critic; the policy's W1 /
 // head / LayerNorm images and action-group table already staged in smem.
@@ -127,6 +172,7 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
     float plp[2] = {0.f, 0.f}, pv = 0.f, prew = 0.f, per = 0.f;
     bool pdone = false;
     int64_t prow = 0;
+    float boot = 0.f;  // the bootstrap critic of env n (the fused GAE's first carry)
     auto flush = [&]() {
         if (!pend) return;
 #pragma unroll
@@ -208,6 +254,7 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
         const float value = to_f32(lgs[r * kR16LGS + A]);
         if (!act) {  // the bootstrap critic (rollouts.py:607-635)
             if (g == 0) rk.bootstrap[n] = value;
+            boot = value;
             break;
         }
         // the sim's next observations: drawn from the state before the
@@ -258,6 +305,7 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
         wave_lds_sync();  // the logits scratch is rewritten by the next step
     }
     flush();
+    if (rk.adv) r16_gae(rk, n, boot, g, lane);
     // the env's state after the rollout: observations, state, running return
     {
         float* orow = env.obs + n * D;

@@ -116,7 +116,8 @@ class RolloutOut(Structure):  # mlearn_rollout_out
                 ("env_returns_trace", c_void_p), ("bootstrap", c_void_p),
                 ("env_returns", c_void_p), ("start_h", c_void_p), ("start_c", c_void_p),
                 ("T", c_int32), ("bptt_len", c_int32), ("ld", c_int64), ("gamma", c_float),
-                ("max_workgroups", c_int32), ("policy_kernel", c_int32)]
+                ("max_workgroups", c_int32), ("policy_kernel", c_int32),
+                ("advantages", c_void_p), ("gae_gamma", c_float), ("gae_gamma_lambda", c_float)]
 
 
 _S = c_void_p  # hipStream_t

@@ -255,6 +255,9 @@ class RolloutManager:  # rollouts.py:373-826
     grid, 2 raises where the row split does not apply)."""
 
     whole_rollout = True
+    # GAE inside the single-policy whole-rollout launch where it applies
+    # (mlearn_rollout_out.advantages); False: always its own launch (A/B runs)
+    fused_gae = True
     rollout_workgroups = 0
     rollout_kernel = 0
     population_launch = True
@@ -442,11 +445,25 @@ class RolloutManager:  # rollouts.py:373-826
             # the built-in sim: every step + the bootstrap in one launch per
             # policy, or one launch for the whole population
             if not self._population_rollout(rollout_state, obs0, sim, key, step_ctr, gamma):
+                # one policy: GAE rides the rollout launch (mlearn_rollout_out.advantages:
+                # fused into the row-split kernel's epilogue) where nothing may
+                # change the rollout between the two (no finish_rollouts hook, no
+                # value normaliser, advantages only)
+                fuse = self.P == 1 and self._gae_in_rollout(train_state_mgr, user_hooks)
                 for p, ps in enumerate(self.policies):
                     c = slice(p * B, (p + 1) * B)
-                    ps.rollout_all(obs0[c], self._rollout_out(rollout_state, p, gamma), key,
+                    o = self._rollout_out(rollout_state, p, gamma)
+                    if fuse:
+                        from .algo_common import _gamma_lambda
+                        o.advantages = s.advantages.data_ptr()
+                        o.gae_gamma = float(self.train_cfg.gamma)
+                        o.gae_gamma_lambda = _gamma_lambda(self.train_cfg)
+                    else:
+                        o.advantages = None
+                    ps.rollout_all(obs0[c], o, key,
                                    step_ctr, self.env_offset + p * B, self._env_desc(sim, p),
                                    carry=self._carry(rollout_state, p, 0) if self.R else None)
+                self._gae_done = fuse
             out = sim.native_outputs()
             rollout_state.sim_state = out["state"]
             rollout_state.cur_obs = out["obs"]
@@ -549,6 +566,16 @@ class RolloutManager:  # rollouts.py:373-826
             nat.ptr(step_ctr), cap, nat.stream_handle()), "policy_rollout_env_pop")
         return True
 
+    def _gae_in_rollout(self, train_state_mgr, user_hooks):
+        """Whether the advantages can be computed by the rollout launch itself:
+        the GAE objective with returns derived (no value normaliser) and the
+        default finish_rollouts hook (which would otherwise see, and may
+        rewrite, the rollout before the advantages exist)."""
+        from .train import TrainHooks
+        return bool(self.use_advantages and self.store.derive_returns and
+                    train_state_mgr.value_norm is None and self.fused_gae and
+                    type(user_hooks).finish_rollouts is TrainHooks.finish_rollouts)
+
     def _rollout_out(self, rollout_state, p, gamma):
         """nat.RolloutOut of policy p's store columns (cached)."""
         if not hasattr(self, "_routs"):
@@ -605,7 +632,9 @@ class RolloutManager:  # rollouts.py:373-826
             for k, v in (rollouts or {}).items():
                 if k in before and v is not before[k]:
                     before[k].copy_(v.reshape(before[k].shape))
-        if self.use_advantages:
+        if getattr(self, "_gae_done", False):
+            self._gae_done = False  # (the rollout launch wrote the advantages)
+        elif self.use_advantages:
             compute_advantages(self.train_cfg, s.rewards, s.values, s.dones, s.bootstrap,
                                out_adv=s.advantages,
                                out_ret=False if s.derive_returns else s._returns,
