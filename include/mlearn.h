@@ -358,8 +358,10 @@ typedef struct mlearn_ppo_hparams {
     int32_t step_kernel;                   /* forward / loss / backward kernel of the MLP
                                               step: 0 = the library's choice (the row-split
                                               kernel where it applies: bf16, hidden 256,
-                                              2 layers, scalar critic, head width 32,
-                                              obs_dim 64, at most 7 action groups,
+                                              2 layers, scalar critic (head width 32) or
+                                              a two-hot critic of <= 64 bins (head width
+                                              96, ABI 21), obs_dim 64, at most 7 action
+                                              groups,
                                               padded rows of exactly 32768 (one 16-row tile
                                               per wave) or a multiple of 256 and >= 65536;
                                               else the feature-split kernel), 1 = the feature-split
@@ -673,7 +675,8 @@ typedef struct mlearn_rollout_out {
                                    < 0: T + 1 per-step launches of the same body (same bits
                                    either way) */
     int32_t policy_kernel;      /* 0: the library's choice (the row-split rollout where it
-                                   applies: the row-split step's policy shape, <= 8 action
+                                   applies: the row-split step's policy shape (incl. the
+                                   two-hot critic at head width 96, ABI 21), <= 8 action
                                    groups, no observation normaliser, max_workgroups 0,
                                    N of exactly 32768 or a multiple of 256 and >= 65536;
                                    else the feature-split

@@ -199,7 +199,7 @@ __device__ inline void r16_ln_bwd(f32x4 (&acc)[kR16NB], uint32_t (&zw)[kR16NB][2
 
 // NW waves per workgroup (8: two per SIMD; 4 or 2: one per SIMD), NT 16-row
 // tiles per wave (rows16_cfg).
-template <bool METRICS, int NW, int NT>
+template <bool METRICS, int NW, int NT, int HC>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3) / 4, (NW + 3) / 4))) void ppo_rows16_kernel(
     PolicyK P, RolloutK ro, const int32_t* __restrict__ mb_seq, int mb, int64_t M,
     const float* __restrict__ adv_st, HpK hp, WsK ws, R16Div dv) {
@@ -207,13 +207,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
 #ifdef ML_STAMPS
     const uint64_t r16_t_entry = __builtin_amdgcn_s_memtime();
 #endif
-    char* w1img = smem + kR16OffW1;
-    char* whimg = smem + kR16OffWh;
-    float* gb = (float*)(smem + kR16OffGb);
-    float* hb = (float*)(smem + kR16OffHb);
+    typedef R16Lay<HC> LY;  // (HC = 96: a two-hot critic, the head image from L2)
+    constexpr int LGS = LY::LGS, NHB = HC / 16;
+    char* w1img = smem + LY::OffW1;
+    char* whimg = smem + LY::OffWh;
+    float* gb = (float*)(smem + LY::OffGb);
+    float* hb = (float*)(smem + LY::OffHb);
+    const float* bins = (const float*)(smem + LY::OffBins);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
+    bf16* lgs = (bf16*)(smem + LY::OffLg) + wave * 16 * LGS;
     const int K = P.K;
     constexpr int D = kR16D, DS = D / 32;  // the first layer's k-steps
 
@@ -222,8 +225,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
     // units; LayerNorm scale / bias, head bias, the loss tasks' group tables
     {
         static_assert(NW == kR16Waves, "r16_stage stages with kR16Waves waves");
-        r16_stage(P, smem, tid);
-        int* tab = (int*)(smem + kR16OffTab);
+        r16_stage<HC>(P, smem, tid);
+        int* tab = (int*)(smem + LY::OffTab);
         if (tid <= MLEARN_MAX_GROUPS) {
             tab[tid] = P.off[tid];
             ((float*)tab)[MLEARN_MAX_GROUPS + 1 + tid] = tid < MLEARN_MAX_GROUPS ? hp.ecoef[tid] : 0.f;
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
 #ifdef ML_STAMPS
     const uint64_t r16_t_pro = __builtin_amdgcn_s_memtime();
 #endif
-    const int* t_off = (const int*)(smem + kR16OffTab);
+    const int* t_off = (const int*)(smem + LY::OffTab);
     const float* t_ec = (const float*)t_off + MLEARN_MAX_GROUPS + 1;
     const float* t_ow = t_ec + MLEARN_MAX_GROUPS + 1;
 
@@ -390,14 +393,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
         R16_STAMP(4);
         // ---- heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
-        f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        r16_mm<2, kR16KS, 4>(ha, [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
-                             [&](int s) { return r16_bfrag(aw, s); });
+        f32x4 ha[NHB];
+#pragma unroll
+        for (int j = 0; j < NHB; ++j) ha[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (HC == 32) {
+            r16_mm<NHB, kR16KS, 4>(
+                ha, [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
+                [&](int s) { return r16_bfrag(aw, s); });
+        } else {  // the head image from L2 (R16Lay): a uniform part (j, s) + one lane offset
+            const bf16* ht = (const bf16*)P.head_t;
+            const uint32_t lo = r16_late((uint32_t)((r + 32 * (g & 1)) * 8 + 4 * (g >> 1)));
+            r16_mm<NHB, kR16KS, kR16RingH>(
+                ha,
+                [&](int j, int s) {
+                    const bf16* p = ht + ((j >> 1) * 8192 + s * 1024 + (j & 1) * 128);
+                    const u2r a = *(const u2r*)(p + lo);
+                    const u2r b = *(const u2r*)(p + 512 + lo);
+                    return __builtin_bit_cast(bf16x8, u4r{a[0], a[1], b[0], b[1]});
+                },
+                [&](int s) { return r16_bfrag(aw, s); });
+        }
         r16_store_rows((bf16*)ws.a[1] + r16_late(row) * kR16H, aw, g);  // A_1 rows
         {
-            bf16* lr = lgs + r * kR16LGS;
+            bf16* lr = lgs + r * LGS;
 #pragma unroll
-            for (int cbk = 0; cbk < 2; ++cbk) {
+            for (int cbk = 0; cbk < NHB; ++cbk) {
                 const int c0 = 16 * cbk + 4 * g;
                 float v[4];
 #pragma unroll
@@ -412,12 +432,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         // one task: padding rows get zero d logits
         auto loss_task = [&](int task, int act, float olp, float adv, float ret, float oval) {
             const int rr = task & 15, grp = task >> 4;
-            bf16* lr = lgs + rr * kR16LGS;
+            bf16* lr = lgs + rr * LGS;
             if (row0 + rr >= M) {
                 if (grp < K)
                     for (int j = t_off[grp]; j < t_off[grp + 1]; ++j) lr[j] = (bf16)0.f;
-                else
-                    for (int j = P.A; j < kR16HC; ++j) lr[j] = (bf16)0.f;
+                else if (HC == 32)
+                    for (int j = P.A; j < HC; ++j) lr[j] = (bf16)0.f;
                 return;
             }
             if (grp < K) {
@@ -425,9 +445,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
                 const int o0 = t_off[grp];
                 loss_group(hp, lr + o0, t_off[grp + 1] - o0, act, olp, adv, t_ec[grp], t_ow[grp],
                            m);
-            } else {
-                loss_value(hp, lr, P.A, kR16HC, ret, oval, m, vn);
-            }
+            } else if (HC == 32) {
+                loss_value(hp, lr, P.A, HC, ret, oval, m, vn);
+            }  // (HC = 96: the two-hot value loss runs below, four lanes per row)
         };
         {
             // the tasks' inputs are registers loaded at the tile's start (K + 1 <= 8
@@ -441,20 +461,60 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
                 loss_task(task, (int)a, b, t_adv, __builtin_bit_cast(float, a), b);
             }
         }
+        if constexpr (HC != 32) {
+            // DreamerV3Critic (ppo.py:169-177): two-hot cross entropy of the
+            // return against the bin logits, by the row's four lanes; the return
+            // is the value task's input (task 16 K + r: lane (16 K + r) % 64 of
+            // pass K / 4); padding rows and columns A + CB .. HC - 1 get zero
+            wave_lds_sync();  // (the group tasks' writes precede the rows' reads)
+            const uint32_t rbits = __shfl(K >= 4 ? t_a[1] : t_a[0], (16 * K + r) & 63);
+            bf16* lr = lgs + r * LGS;
+            const int CB = P.CB;
+            if (row0 + r < M) {
+                float mean;
+                const float R = __builtin_bit_cast(float, rbits);
+                const float vl = r16_twohot_ce(lr + P.A, CB, R, bins,
+                                               hp.vcoef * hp.inv_s * hp.loss_scale, g, &mean);
+                if (g == 0) {
+                    const float verr = fabsf(mean - R);
+                    m.svl += vl;
+                    m.qvl += vl * vl;
+                    m.mnvl = fminf(m.mnvl, vl);
+                    m.mxvl = fmaxf(m.mxvl, vl);
+                    m.serr += verr;
+                    m.qerr += verr * verr;
+                    m.mnerr = fminf(m.mnerr, verr);
+                    m.mxerr = fmaxf(m.mxerr, verr);
+                }
+            } else {
+                for (int j = P.A + g; j < P.A + CB; j += 4) lr[j] = (bf16)0.f;
+            }
+            for (int j = P.A + CB + g; j < HC; j += 4) lr[j] = (bf16)0.f;
+        }
         wave_lds_sync();
         R16_STAMP(6);
         // ---- d head: B operand of the head backward (cols 8g .. 8g+7 of row r),
         // row-major store, head-bias column sums
-        const bf16x8 dh = *(const bf16x8*)(lgs + r * kR16LGS + 8 * g);
-        r16_st16((bf16*)ws.dhead + r16_late(row) * kR16HC + 8 * g, __builtin_bit_cast(u4r, dh));
+        // (k-step s of the head backward: columns 32 s + 8 g .. + 7)
+        constexpr int HKS = HC / 32;
+        bf16x8 dh[HKS];
+#pragma unroll
+        for (int s2 = 0; s2 < HKS; ++s2) {
+            dh[s2] = *(const bf16x8*)(lgs + r * LGS + 32 * s2 + 8 * g);
+            r16_st16((bf16*)ws.dhead + r16_late(row) * HC + 32 * s2 + 8 * g,
+                     __builtin_bit_cast(u4r, dh[s2]));
+        }
         // column partials of this 16-row tile (colpart row NT ptile + tt, WsK::ncp):
         // head bias here, LayerNorm bias / scale in the layer backwards
         float* cprow = ws.colpart + ((int64_t)ptile * NT + tt) * ws.CP;
-        if (lane < kR16HC) {
-            float hbs = 0.f;
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) hbs += to_f32(lgs[rr * kR16LGS + lane]);
-            cprow[2 * 2 * kR16H + lane] = hbs;
+        for (int c0 = 0; c0 < HC; c0 += 64) {
+            if (c0 + lane < HC) {
+                float hbs = 0.f;
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) hbs += to_f32(lgs[rr * LGS + c0 + lane]);
+                cprow[2 * 2 * kR16H + c0 + lane] = hbs;
+            }
         }
         // ---- layer 1 backward: dA_1^T = Wh dHead^T (M = hidden unit = image
         // column, K = head column), recomputed per half in the LayerNorm's
@@ -465,9 +525,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
             f32x4 hacc[kR16NB];
 #pragma unroll
             for (int b = 0; b < kR16NB; ++b) hacc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            r16_mm<kR16NB, 1, kR16Ring>(
-                hacc, [&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
-                [&](int) { return dh; });
+            if constexpr (HC == 32) {
+                r16_mm<kR16NB, 1, kR16Ring>(
+                    hacc,
+                    [&](int b, int) { return r16_tr_frag(whimg, 8 * g, 8 * g + 4, b, lane); },
+                    [&](int) { return dh[0]; });
+            } else {
+                // the head image P.head from L2 (fragment order, natural k,
+                // K = HC: img_index<bf16>(n, k, 96, false)): hidden unit n = 16 b + r,
+                // columns 32 s + 8 g .. + 7 are 16 contiguous bytes, a uniform part
+                // (b, s) plus one lane offset
+                const bf16* hd = (const bf16*)P.head;
+                const uint32_t lo = r16_late((uint32_t)((g >> 1) * 512 + (r + 32 * (g & 1)) * 8));
+                r16_mm<kR16NB, HKS, kR16RingH>(
+                    hacc,
+                    [&](int b, int s2) {
+                        const bf16* p = hd + ((b >> 1) * (HC / 16) * 512 + s2 * 1024 + (b & 1) * 128);
+                        return *(const bf16x8*)(p + lo);
+                    },
+                    [&](int s2) { return dh[s2]; });
+            }
             float cb1[4], cg1[4];
             r16_ln_bwd(hacc, zw, mean, rstd, gb + 2 * kR16H, g, lane, live, dzw, cb1, cg1);
             r16_put_cols(cprow + 2 * kR16H, cb1, cg1, lane);
@@ -555,25 +632,29 @@ static R16Cfg rows16_cfg(int64_t Mp) {
     return R16Cfg{0, 0};
 }
 static bool rows16_eligible(const PolicyK& P, int64_t Mp, int HC, int L, int H, bool bf) {
-    return bf && H == kR16H && L == 2 && HC == kR16HC && P.CB == 1 && P.D == kR16D &&
-           P.K + 1 <= 8 && rows16_cfg(Mp).nw > 0;
+    // head: the scalar critic at width 32, or (round 6) a two-hot critic at
+    // width 96 (R16Lay: the head image streamed from L2)
+    const bool head = (HC == 32 && P.CB == 1) || (HC == 96 && P.CB > 1 && P.CB <= 64);
+    return bf && H == kR16H && L == 2 && head && P.D == kR16D && P.K + 1 <= 8 &&
+           rows16_cfg(Mp).nw > 0;
 }
 
-template <int NW, int NT>
+template <int NW, int NT, int HC>
 static void launch_rows16_cfg(const PolicyK& P, const RolloutK& R, const int32_t* mb_seq, int mb,
                               int64_t M, const float* adv_st, const HpK& hp, const WsK& ws,
                               const R16Div& dv, hipStream_t s) {
+    constexpr int lds = (int)R16Lay<HC>::Lds;
     // (once per shape and device, kept out of graph capture)
-    if (set_lds_attr((const void*)ppo_rows16_kernel<true, NW, NT>, (int)kR16Lds, "ppo_rows16") ||
-        set_lds_attr((const void*)ppo_rows16_kernel<false, NW, NT>, (int)kR16Lds, "ppo_rows16"))
+    if (set_lds_attr((const void*)ppo_rows16_kernel<true, NW, NT, HC>, lds, "ppo_rows16") ||
+        set_lds_attr((const void*)ppo_rows16_kernel<false, NW, NT, HC>, lds, "ppo_rows16"))
         return;  // (the caller's check_launch reports a failed launch; the message is set)
     const int grid = (int)(ws.Mp / (16 * NW * NT));
     if (hp.metrics)
-        hipLaunchKernelGGL((ppo_rows16_kernel<true, NW, NT>), dim3(grid), dim3(64 * NW), kR16Lds, s,
-                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
+        hipLaunchKernelGGL((ppo_rows16_kernel<true, NW, NT, HC>), dim3(grid), dim3(64 * NW), lds,
+                           s, P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
     else
-        hipLaunchKernelGGL((ppo_rows16_kernel<false, NW, NT>), dim3(grid), dim3(64 * NW), kR16Lds, s,
-                           P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
+        hipLaunchKernelGGL((ppo_rows16_kernel<false, NW, NT, HC>), dim3(grid), dim3(64 * NW), lds,
+                           s, P, R, mb_seq, mb, M, adv_st, hp, ws, dv);
 }
 
 // (the caller sets ws.ncp / ws.nlp to the row-split partial-row counts)
@@ -584,8 +665,15 @@ static void launch_rows16(const PolicyK& P, const RolloutK& R, const int32_t* mb
     r16_magic((uint32_t)mb, dv.mb_mag, dv.mb_sh);
     r16_magic((uint32_t)R.N, dv.n_mag, dv.n_sh);
     const R16Cfg c = rows16_cfg(ws.Mp);
-    if (c.nt == 2)
-        launch_rows16_cfg<8, 2>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
-    else
-        launch_rows16_cfg<8, 1>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
+    if (P.HC == 32) {
+        if (c.nt == 2)
+            launch_rows16_cfg<8, 2, 32>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
+        else
+            launch_rows16_cfg<8, 1, 32>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
+    } else {
+        if (c.nt == 2)
+            launch_rows16_cfg<8, 2, 96>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
+        else
+            launch_rows16_cfg<8, 1, 96>(P, R, mb_seq, mb, M, adv_st, hp, ws, dv, s);
+    }
 }

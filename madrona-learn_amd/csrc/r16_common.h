@@ -11,6 +11,7 @@
 #pragma once
 
 #include "common.h"
+#include "dists.h"
 #include "rowtile.h"
 
 namespace ml {
@@ -31,6 +32,10 @@ constexpr int kR16LGS = 40;          // logits scratch row stride (bf16; 80-B ro
 #endif
 constexpr int kR16Ring = ML_R16_RING;    // LDS A fragments in flight per product
 constexpr int kR16Ring0 = ML_R16_RING0;  // first-layer (L2) A fragments in flight
+#ifndef ML_R16_RINGH
+#define ML_R16_RINGH 8
+#endif
+constexpr int kR16RingH = ML_R16_RINGH;  // head (L2, HC = 96) A fragments in flight
 // LDS: W1 image [256 rows = out][512 B], head image [32 rows = col][512 B],
 // LayerNorm scale/bias [2][2][256] f32, head bias [32] f32, per-wave logits
 // scratch [8][16][kR16LGS] bf16, the action groups' logit offsets, entropy
@@ -46,6 +51,26 @@ constexpr size_t kR16OffTab = kR16OffLg + (size_t)kR16Waves * 16 * kR16LGS * 2;
 constexpr int kR16TabN = 3 * (MLEARN_MAX_GROUPS + 1);  // group offsets, entropy coefs, obj weights
 constexpr size_t kR16Lds = kR16OffTab + (size_t)kR16TabN * 4;
 static_assert(kR16Lds <= 160 * 1024, "row-split step LDS budget");
+
+// The same layout for head width HC (the kR16Off* constants above are HC =
+// 32).  At HC = 96 (a DreamerV3 two-hot critic: A logits + up to 63 bins,
+// round 6) the 48 KB head image no longer fits beside W1 and a 16-row
+// logits scratch of 96 columns, so the head products stream the head image
+// from L2 (r16_head_l2) and LDS holds the critic's bin values instead.
+template <int HC> struct R16Lay {
+    static_assert(HC == 32 || HC == 96, "head width");
+    static constexpr int LGS = HC == 32 ? kR16LGS : 104;  // logits scratch row stride (bf16)
+    static constexpr size_t OffW1 = 0;
+    static constexpr size_t OffWh = OffW1 + (size_t)kR16H * 512;
+    static constexpr size_t OffGb = OffWh + (HC == 32 ? (size_t)HC * 512 : 0);
+    static constexpr size_t OffHb = OffGb + (size_t)2 * 2 * kR16H * 4;
+    static constexpr size_t OffBins = OffHb + (size_t)HC * 4;
+    static constexpr size_t OffLg = OffBins + (HC == 32 ? 0 : (size_t)64 * 4);
+    static constexpr size_t OffTab = OffLg + (size_t)kR16Waves * 16 * LGS * 2;
+    static constexpr size_t Lds = OffTab + (size_t)kR16TabN * 4;
+    static_assert(Lds <= 160 * 1024, "row-split LDS budget");
+};
+static_assert(R16Lay<32>::Lds == kR16Lds && R16Lay<32>::OffLg == kR16OffLg, "layouts agree");
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef short short4r __attribute__((ext_vector_type(4)));
@@ -314,11 +339,13 @@ __device__ inline uint32_t r16_udiv(uint32_t n, uint32_t mag, int sh) {
 // head images (P.wt[1], P.head_t: fragment order, permuted k, K = 256)
 // re-laid as [out row][512 B] with swizzled 8-byte units, LayerNorm scale /
 // bias of both layers, head bias.
+template <int HC = kR16HC>
 __device__ inline void r16_stage(const PolicyK& P, char* smem, int tid) {
-    char* w1img = smem + kR16OffW1;
-    char* whimg = smem + kR16OffWh;
-    float* gb = (float*)(smem + kR16OffGb);
-    float* hb = (float*)(smem + kR16OffHb);
+    typedef R16Lay<HC> LY;
+    char* w1img = smem + LY::OffW1;
+    char* whimg = smem + LY::OffWh;
+    float* gb = (float*)(smem + LY::OffGb);
+    float* hb = (float*)(smem + LY::OffHb);
     {
         const u4r* src1 = (const u4r*)P.wt[1];
         const u4r* srch = (const u4r*)P.head_t;
@@ -326,15 +353,16 @@ __device__ inline void r16_stage(const PolicyK& P, char* smem, int tid) {
         u4r v1[N1], vh[2];
 #pragma unroll
         for (int i = 0; i < N1; ++i) v1[i] = src1[tid + i * 64 * kR16Waves];
+        if (HC == 32)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) vh[i] = srch[tid + i * 64 * kR16Waves];
+            for (int i = 0; i < 2; ++i) vh[i] = srch[tid + i * 64 * kR16Waves];
         float pv[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int j = tid + i * 64 * kR16Waves, l = j >> 9, c = j & 511;
             pv[i] = c < kR16H ? P.lns[l][c] : P.lnb[l][c - kR16H];
         }
-        const float hbv = tid < kR16HC ? P.head_b[tid] : 0.f;
+        const float hbv = tid < HC ? P.head_b[tid] : 0.f;
         // 16-byte unit U of a (K = 256, perm) image: n = ((U >> 10) << 5) | (U & 31),
         // h = (U >> 5) & 1, s16 = (U >> 6) & 15; its halves hold inputs
         // 16 s16 + 4h .. +3 and 16 s16 + 8 + 4h .. +3 (units 4 s16 + h, 4 s16 + 2 + h)
@@ -345,12 +373,106 @@ __device__ inline void r16_stage(const PolicyK& P, char* smem, int tid) {
         };
 #pragma unroll
         for (int i = 0; i < N1; ++i) put(w1img, tid + i * 64 * kR16Waves, v1[i]);
+        if (HC == 32)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) put(whimg, tid + i * 64 * kR16Waves, vh[i]);
+            for (int i = 0; i < 2; ++i) put(whimg, tid + i * 64 * kR16Waves, vh[i]);
 #pragma unroll
         for (int i = 0; i < 2; ++i) gb[tid + i * 64 * kR16Waves] = pv[i];
-        if (tid < kR16HC) hb[tid] = hbv;
+        if (tid < HC) hb[tid] = hbv;
+        if (HC != 32 && tid < P.CB)  // the two-hot critic's bin values (dists.py:128-141)
+            ((float*)(smem + LY::OffBins))[tid] = twohot_bin(tid, P.CB);
     }
+}
+
+// A fragment of the head's forward product (M = head column n, the k order of
+// r16_row_frag) straight from the head's L2 image P.head_t (fragment order,
+// permuted k, K = 256; img_index<bf16>(n, k, 256, true)): inputs 32s + 4g ..
+// +3 and 32s + 16 + 4g .. +3 of column n are two 8-byte halves 1 KB apart.
+__device__ inline bf16x8 r16_head_l2(const bf16* head_t, int n, int s, int g) {
+    const int64_t base =
+        ((int64_t)(((n >> 5) * 16 + 2 * s) * 64 + (n & 31) + 32 * (g & 1))) * 8 + 4 * (g >> 1);
+    const u2r lo = *(const u2r*)(head_t + base);
+    const u2r hi = *(const u2r*)(head_t + base + 512);
+    const u4r v = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// two_hot_cross_entropy_loss (dists.py:171-208; twohot_ce_g's arithmetic,
+// the reference's bin weights as written) of one row's CB bin logits (bf16,
+// LDS) against the return R, by the row's four lanes r + 16 g (bins g, g + 4,
+// ...): every lane returns the loss and mean(), and writes scale * d loss /
+// d logit of its own bins in place (bf16: every consumer rounds them).
+__device__ inline float r16_twohot_ce(bf16* lr, int CB, float R, const float* bins, float scale,
+                                      int g, float* mean_out) {
+    float cle = 0.f, cgt = 0.f;
+    for (int j = g; j < CB; j += 4) {
+        cle += bins[j] <= R ? 1.f : 0.f;
+        cgt += bins[j] > R ? 1.f : 0.f;
+    }
+    cle += __shfl_xor(cle, 16);
+    cle += __shfl_xor(cle, 32);
+    cgt += __shfl_xor(cgt, 16);
+    cgt += __shfl_xor(cgt, 32);
+    const int lo = min(max((int)cle - 1, 0), CB - 1);
+    const int up = min(max(CB - (int)cgt, 0), CB - 1);
+    const bool same = lo == up;
+    const float dl = same ? 1.f : fabsf(bins[lo] - R);
+    const float du = same ? 1.f : fabsf(bins[up] - R);
+    const float tot = dl + du;
+    const float wl = dl / tot, wu = du / tot;
+    float mx = -3.4e38f;
+    for (int j = g; j < CB; j += 4) mx = fmaxf(mx, to_f32(lr[j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float se = 0.f;
+    for (int j = g; j < CB; j += 4) se += __expf(to_f32(lr[j]) - mx);
+    se += __shfl_xor(se, 16);
+    se += __shfl_xor(se, 32);
+    const int mid = (CB - 1) / 2;
+    float acc = 0.f;
+    for (int i = g; i < mid; i += 4) {
+        const int a = mid - 1 - i, b = mid + 1 + i;
+        acc += (__expf(to_f32(lr[a]) - mx) / se) * bins[a] +
+               (__expf(to_f32(lr[b]) - mx) / se) * bins[b];
+    }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
+    *mean_out = (__expf(to_f32(lr[mid]) - mx) / se) * bins[mid] + acc;
+    const float lse = mx + __logf(se);
+    const float llo = to_f32(lr[lo]), lup = to_f32(lr[up]);  // (read before the row's writes)
+    const float loss = -(wl * (llo - lse) + wu * (lup - lse));
+    const float wsum = wl + wu;
+    for (int j = g; j < CB; j += 4) {
+        const float pj = __expf(to_f32(lr[j]) - mx) / se;
+        const float w = (j == lo ? wl : 0.f) + (j == up ? wu : 0.f);
+        lr[j] = (bf16)((wsum * pj - w) * scale);
+    }
+    return loss;
+}
+
+// SymExpTwoHotDistribution.mean() (dists.py:143-169, twohot_mean_g's sums)
+// of the CB bin logits of one row (bf16 in LDS), by the row's four lanes
+// r, r + 16, r + 32, r + 48 (g = lane >> 4: bins g, g + 4, ...); every lane of
+// the row returns it.
+__device__ inline float r16_twohot_mean(const bf16* lr, int CB, const float* bins, int g) {
+    float mx = -3.4e38f;
+    for (int j = g; j < CB; j += 4) mx = fmaxf(mx, to_f32(lr[j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float se = 0.f;
+    for (int j = g; j < CB; j += 4) se += __expf(to_f32(lr[j]) - mx);
+    se += __shfl_xor(se, 16);
+    se += __shfl_xor(se, 32);
+    const int mid = (CB - 1) / 2;
+    float acc = 0.f;
+    for (int i = g; i < mid; i += 4) {
+        const int a = mid - 1 - i, b = mid + 1 + i;
+        acc += (__expf(to_f32(lr[a]) - mx) / se) * bins[a] +
+               (__expf(to_f32(lr[b]) - mx) / se) * bins[b];
+    }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
+    return (__expf(to_f32(lr[mid]) - mx) / se) * bins[mid] + acc;
 }
 
 // (mulhi(n, mag) + n) >> sh == n / d for n < 2^31: sh = ceil(log2 d),

@@ -72,8 +72,11 @@ static int rollout16_waves(int64_t N) {
 // per lane), no observation normaliser, a whole-rollout launch (max_workgroups
 // 0) and the env counts rollout16_waves takes.
 static bool rollout16_shape(const PolicyK& P, bool bf, bool rnn) {
-    return bf && !rnn && P.H == kR16H && P.L == 2 && P.HC == kR16HC && P.CB == 1 &&
-           P.D == kR16D && P.K <= 8 && !P.obs_mu && !P.obs_stats;
+    // head: the scalar critic at width 32, or (round 6) a two-hot critic at
+    // width 96 (R16Lay: the head image streamed from L2)
+    const bool head = (P.HC == 32 && P.CB == 1) || (P.HC == 96 && P.CB > 1 && P.CB <= 64);
+    return bf && !rnn && P.H == kR16H && P.L == 2 && head && P.D == kR16D && P.K <= 8 &&
+           !P.obs_mu && !P.obs_stats;
 }
 static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf, bool rnn) {
     return rollout16_shape(P, bf, rnn) && max_wg == 0 && rollout16_waves(N) > 0;
@@ -86,8 +89,8 @@ static bool rollout16_eligible(const PolicyK& P, int64_t N, int max_wg, bool bf,
 static bool rollout16_pop_eligible(const PolicyK& P0, int64_t N, int npol, int max_wg, bool bf,
                                    bool rnn) {
     const int64_t tiles = (int64_t)npol * (N / 16);
-    return rollout16_shape(P0, bf, rnn) && max_wg == 0 && N % 128 == 0 && tiles >= 2048 &&
-           tiles <= 0x7fffffff;
+    return rollout16_shape(P0, bf, rnn) && P0.HC == 32 && max_wg == 0 && N % 128 == 0 &&
+           tiles >= 2048 && tiles <= 0x7fffffff;
 }
 
 // GAE (algo_common.py:84-130, gae_kernel's arithmetic and order, so the same
@@ -138,17 +141,21 @@ __device__ __forceinline__ void r16_gae(const RollK& rk, int64_t n, float boot, 
 // One 16-env tile's whole rollout on one wave: T policy steps with the sim
 // step and post-step fused, then the bootstrap critic; the policy's W1 /
 // head / LayerNorm images and action-group table already staged in smem.
+template <int HC = kR16HC>
 __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __restrict__ obs0,
                                               const RollK& rk, uint32_t k0, uint32_t k1,
                                               uint64_t step0, uint32_t eoff, const EnvK& env,
                                               int tile, int tid, char* smem, int prio_t = -1) {
-    const char* w1img = smem + kR16OffW1;
-    const char* whimg = smem + kR16OffWh;
-    const float* gb = (const float*)(smem + kR16OffGb);
-    const float* hb = (const float*)(smem + kR16OffHb);
+    typedef R16Lay<HC> LY;
+    constexpr int LGS = LY::LGS;
+    const char* w1img = smem + LY::OffW1;
+    const char* whimg = smem + LY::OffWh;
+    const float* gb = (const float*)(smem + LY::OffGb);
+    const float* hb = (const float*)(smem + LY::OffHb);
+    const float* bins = (const float*)(smem + LY::OffBins);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    bf16* lgs = (bf16*)(smem + kR16OffLg) + wave * 16 * kR16LGS;
-    const int* t_off = (const int*)(smem + kR16OffTab);
+    bf16* lgs = (bf16*)(smem + LY::OffLg) + wave * 16 * LGS;
+    const int* t_off = (const int*)(smem + LY::OffTab);
     const int K = P.K, A = P.A;
     constexpr int D = kR16D, DS = D / 32;
     // (the lane through an opaque copy per tile: rows16 kernel, ppo_rows16.h)
@@ -234,14 +241,32 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
             [&](int s) { return r16_bfrag(aw, s); }, zw, mean, rstd);
         r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
         // heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))
-        f32x4 ha[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        r16_mm<2, kR16KS, 4>(ha,
-                             [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
-                             [&](int s) { return r16_bfrag(aw, s); });
-        {
-            bf16* lr = lgs + r * kR16LGS;
+        constexpr int NHB = HC / 16;
+        f32x4 ha[NHB];
 #pragma unroll
-            for (int cbk = 0; cbk < 2; ++cbk) {
+        for (int j = 0; j < NHB; ++j) ha[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (HC == 32) {
+            r16_mm<NHB, kR16KS, 4>(ha,
+                                   [&](int j, int s) { return r16_row_frag(whimg, 16 * j + r, s, g); },
+                                   [&](int s) { return r16_bfrag(aw, s); });
+        } else {  // the head image from L2 (R16Lay, r16_head_l2's addressing)
+            const bf16* ht = (const bf16*)P.head_t;
+            // column 16j + r, k-step s: a uniform part (j, s) plus one lane offset
+            const uint32_t lo = r16_late((uint32_t)((r + 32 * (g & 1)) * 8 + 4 * (g >> 1)));
+            r16_mm<NHB, kR16KS, kR16RingH>(
+                ha,
+                [&](int j, int s) {
+                    const bf16* p = ht + ((j >> 1) * 8192 + s * 1024 + (j & 1) * 128);
+                    const u2r a = *(const u2r*)(p + lo);
+                    const u2r b = *(const u2r*)(p + 512 + lo);
+                    return __builtin_bit_cast(bf16x8, u4r{a[0], a[1], b[0], b[1]});
+                },
+                [&](int s) { return r16_bfrag(aw, s); });
+        }
+        {
+            bf16* lr = lgs + r * LGS;
+#pragma unroll
+            for (int cbk = 0; cbk < NHB; ++cbk) {
                 const int c0 = 16 * cbk + 4 * g;
                 float v[4];
 #pragma unroll
@@ -251,7 +276,10 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
             }
         }
         wave_lds_sync();
-        const float value = to_f32(lgs[r * kR16LGS + A]);
+        // the critic (rollouts.py:601-605): the scalar head column, or
+        // SymExpTwoHotDistribution.mean() of the bin columns
+        const float value = HC == 32 ? to_f32(lgs[r * LGS + A])
+                                     : r16_twohot_mean(lgs + r * LGS + A, P.CB, bins, g);
         if (!act) {  // the bootstrap critic (rollouts.py:607-635)
             if (g == 0) rk.bootstrap[n] = value;
             boot = value;
@@ -279,7 +307,7 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
             plp[u] = 0.f;
             if (grp < K) {
                 const int o0 = t_off[grp];
-                r16_pick(lgs + r * kR16LGS, o0, t_off[grp + 1] - o0, ge, step, k0, k1, pa[u],
+                r16_pick(lgs + r * LGS, o0, t_off[grp + 1] - o0, ge, step, k0, k1, pa[u],
                          plp[u]);
             }
             if (u == 0) a0 = pa[0];  // lanes 0..15: group 0 of row r
@@ -328,16 +356,16 @@ __device__ __forceinline__ void r16_roll_tile(const PolicyK& P, const float* __r
 #define ML_ROLL_PRIO_NUM 6  // eighths of T: the step the second wave takes priority
 #endif
 
-template <int NW>
+template <int NW, int HC>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3) / 4, (NW + 3) / 4))) void rollout16_kernel(
     PolicyK P, const float* __restrict__ obs0, int64_t N, RollK rk, uint32_t k0, uint32_t k1,
     const uint64_t* step_ctr, uint32_t eoff, EnvK env) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int* tab = (int*)(smem + kR16OffTab);
+    int* tab = (int*)(smem + R16Lay<HC>::OffTab);
     static_assert(NW == kR16Waves, "r16_stage stages with kR16Waves waves");
-    r16_stage(P, smem, tid);
+    r16_stage<HC>(P, smem, tid);
     if (tid <= MLEARN_MAX_GROUPS) tab[tid] = P.off[tid];
     __syncthreads();
     const uint64_t step0 = step_ctr ? *step_ctr : 0ull;
@@ -353,27 +381,34 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         if (NW > 4 && wave >= NW / 2 && tile + TW >= ntile) __builtin_amdgcn_s_setprio(1);
         const int pt = (NW > 4 && wave >= NW / 2 && tile + 2 * TW >= ntile)
                            ? rk.T * ML_ROLL_PRIO_NUM / 8 : -1;
-        r16_roll_tile(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem, pt);
+        r16_roll_tile<HC>(P, obs0, rk, k0, k1, step0, eoff, env, tile, tid, smem, pt);
     }
 }
 
-template <int NW>
+template <int NW, int HC>
 static void launch_rollout16_nw(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
                                 uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
                                 const EnvK& env, int cus, hipStream_t s) {
-    // (once per shape and device, kept out of graph capture)
-    if (set_lds_attr((const void*)rollout16_kernel<NW>, (int)kR16Lds, "rollout16")) return;
+    constexpr int lds = (int)R16Lay<HC>::Lds;
     const int64_t waves = N / 16;
     int64_t grid = cus > 0 ? cus : 256;
     if (grid * NW > waves) grid = waves / NW;
-    hipLaunchKernelGGL((rollout16_kernel<NW>), dim3((unsigned)grid), dim3(64 * NW), kR16Lds, s, P,
+    hipLaunchKernelGGL((rollout16_kernel<NW, HC>), dim3((unsigned)grid), dim3(64 * NW), lds, s, P,
                        obs, N, rk, k0, k1, step_ctr, eoff, env);
 }
 
 static int launch_rollout16(const PolicyK& P, const float* obs, int64_t N, const RollK& rk,
                             uint32_t k0, uint32_t k1, const uint64_t* step_ctr, uint32_t eoff,
                             const EnvK& env, hipStream_t s) {
-    if (set_lds_attr((const void*)rollout16_kernel<8>, (int)kR16Lds, "rollout16")) return MLEARN_EHIP;
-    launch_rollout16_nw<8>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, device_cus(), s);
+    // (the LDS attribute once per shape and device, kept out of graph capture)
+    if (P.HC == 32) {
+        if (set_lds_attr((const void*)rollout16_kernel<8, 32>, (int)R16Lay<32>::Lds, "rollout16"))
+            return MLEARN_EHIP;
+        launch_rollout16_nw<8, 32>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, device_cus(), s);
+    } else {
+        if (set_lds_attr((const void*)rollout16_kernel<8, 96>, (int)R16Lay<96>::Lds, "rollout16"))
+            return MLEARN_EHIP;
+        launch_rollout16_nw<8, 96>(P, obs, N, rk, k0, k1, step_ctr, eoff, env, device_cus(), s);
+    }
     return check_launch("policy_rollout_env (row split)");
 }

@@ -86,7 +86,8 @@ def test_param_count_matches_oracle_layout():
 
 def test_step_kernel_selection():
     """mlearn_ppo_step_kernel: the row-split step kernel exactly where it
-    applies (bf16, H 256, 2 layers, scalar critic, obs 64, <= 7 action
+    applies (bf16, H 256, 2 layers, scalar critic or a two-hot critic of <= 63
+    bins (head width 96), obs 64, <= 7 action
     groups, padded rows of 32,768 or a multiple of 256 from 65,536: one
     8-wave workgroup per CU), the feature-split kernel elsewhere; an explicit
     row-split request elsewhere is -1 (EINVAL)."""
@@ -115,8 +116,12 @@ def test_step_kernel_selection():
         assert sel(d, rows) == 1 and sel(d, rows, 2) == -1
     assert sel(d, 65536 + 64) == 1                           # not a multiple of 256
     for other in (desc(dtype=nat.DTYPE_F32), desc(H=128), desc(layers=3),
-                  desc(buckets=(2,) * 8), desc(bins=9)):
+                  desc(buckets=(2,) * 8), desc(bins=65)):
         assert sel(other, 65536) == 1 and sel(other, 65536, 2) == -1
+    # a two-hot critic (head width 96, round 6): the row split too
+    for bins in (9, 63):
+        assert sel(desc(bins=bins), 65536) == 2 and sel(desc(bins=bins), 32768) == 2
+        assert sel(desc(bins=bins), 65536, 1) == 1
     assert sel(d, 65536, 3) == -1 and sel(d, 0) == -1
     # the population launch (mlearn_policy_rollout_pop_kernel): the row split
     # uncapped over >= 2048 16-env tiles of policies with N a multiple of 128

@@ -52,14 +52,25 @@ def _cfg(N, mb, epochs=1, pbt_policies=0, seed=5):
         dreamer_v3_critic=False, compute_dtype=torch.bfloat16, pbt=pbt)
 
 
-def _check_store(s, ro, cols=slice(None)):
+def _check_store(s, ro, cols=slice(None), vscale=None):
+    """vscale (two-hot critics): per-value scale E_p|bin| of the oracle's bin
+    distribution ([T + 1, n], bootstrap last): a bf16 ulp of one bin logit
+    moves mean() by ~ulp * p_j |b_j| with |b_j| up to symexp(14) = 1.2e6, so
+    the value tolerance is relative to that scale, not to the value."""
     assert np.array_equal(s.obs[:, cols].float().cpu().numpy(), ro["obs"])
     assert np.array_equal(s.rewards[:, cols].cpu().numpy(), ro["rewards"])
     assert np.array_equal(s.dones[:, cols].cpu().numpy(), ro["dones"])
     tol = 3e-2
-    np.testing.assert_allclose(s.values[:, cols].cpu().numpy(), ro["values"], rtol=tol, atol=tol)
-    np.testing.assert_allclose(s.bootstrap[cols].cpu().numpy(), ro["bootstrap"], rtol=tol,
-                               atol=tol)
+    if vscale is None:
+        np.testing.assert_allclose(s.values[:, cols].cpu().numpy(), ro["values"], rtol=tol,
+                                   atol=tol)
+        np.testing.assert_allclose(s.bootstrap[cols].cpu().numpy(), ro["bootstrap"], rtol=tol,
+                                   atol=tol)
+    else:
+        got = np.concatenate([s.values[:, cols].cpu().numpy(), s.bootstrap[cols].cpu().numpy()[None]])
+        want = np.concatenate([ro["values"], np.asarray(ro["bootstrap"])[None]])
+        bad = np.abs(got - want) > tol * vscale + tol
+        assert not bad.any(), (np.argwhere(bad)[:5], got[bad][:5], want[bad][:5], vscale[bad][:5])
     np.testing.assert_allclose(s.log_probs[:, cols].cpu().numpy(), ro["log_probs"], rtol=tol,
                                atol=tol)
     adv, _ = ref.gae_f32(s.rewards[:, cols].cpu().numpy(), s.values[:, cols].cpu().numpy(),
@@ -383,14 +394,14 @@ def test_row_split_rollout_rank_sizes(gpu, N):
     _replay_windows(mgr, env, cfg, [0, N // 2 + 32 * 5, N - 32])
 
 
-def _replay_windows(mgr, env, cfg, windows):
+def _replay_windows(mgr, env, cfg, windows, critic_bins=1):
     ps = mgr.state.policy_states
     rm = mgr.rollout_mgr
     p0 = ps.params.cpu().numpy().astype(np.float64)
     mgr.update_iter()
     torch.cuda.synchronize()
     s = rm.store
-    lay = ref.param_layout(D, H, 2, 26)
+    lay = ref.param_layout(D, H, 2, 26, critic_bins)
     for e0 in windows:
         c = slice(e0, e0 + 32)
         oenv = onat.Env(32, D, env.k0, env.k1, e0)
@@ -398,7 +409,16 @@ def _replay_windows(mgr, env, cfg, windows):
         acts = s.actions[:, c].cpu().numpy()
         ro, _ = ref.rollout(p0, lay, oenv, T, BUCKETS, mgr.rollout.prng_key, 0, mode="bf16",
                             gamma=cfg.gamma, actions_override=acts)
-        _check_store(s, ro, c)
+        vscale = None
+        if critic_bins > 1:  # E_p|bin| of the oracle's bin distributions, every step + bootstrap
+            P0 = ref.unflatten(p0, lay)
+            x = np.concatenate([ro["obs"], env.obs[c].cpu().numpy()[None]]).reshape(-1, D)
+            _, _, cache = ref.forward(P0, ref.rnd(x, "bf16"), "bf16")
+            crit = np.asarray(cache["crit"], np.float64)
+            pr = np.exp(crit - crit.max(-1, keepdims=True))
+            pr /= pr.sum(-1, keepdims=True)
+            vscale = (pr * np.abs(ref.twohot_bins(critic_bins))).sum(-1).reshape(T + 1, 32)
+        _check_store(s, ro, c, vscale)
         gum = np.stack([onat.gumbel_table(*mgr.rollout.prng_key, t, e0, 32, 26)
                         for t in range(T)])
         noisy = ro["logits"] + gum
@@ -415,3 +435,31 @@ def _replay_windows(mgr, env, cfg, windows):
         assert np.array_equal(env.rewards[c].cpu().numpy().reshape(-1), oenv.rew), e0
         assert np.array_equal(env.dones[c].cpu().numpy().reshape(-1).astype(np.uint8),
                               oenv.done), e0
+
+
+def test_twohot_rollout_row_split(gpu):
+    """The row-split rollout with the reference's default critic, a DreamerV3
+    two-hot critic of 63 bins (round 6: head width 96, the head image streamed
+    from L2, SymExpTwoHotDistribution.mean() by each row's four lanes), at the
+    headline's 65,536 envs: oracle windows in several tile rounds (obs /
+    rewards / dones / GAE bit-exact, values and log-probs within the bf16
+    tolerance, sampled actions where the Gumbel margin is clear) with
+    perturbed, non-trivial bin weights (the critic is zero-initialised)."""
+    import dataclasses
+    from madrona_learn import _native as nat
+    from madrona_learn.envs import DummyVecEnv
+    import madrona_learn as ml
+    from tests.test_gpu_policy import perturb
+    from tests.test_gpu_train import make_policy
+    N, mb = 65536, 2048
+    env = DummyVecEnv(N, D, 6, seed=8, device=gpu)
+    cfg = dataclasses.replace(_cfg(N, mb, seed=19), dreamer_v3_critic=True)
+    mgr = ml.init_training(gpu, cfg, env.sim_fns(),
+                           make_policy(torch.bfloat16, H, critic_bins=63), use_graph=False)
+    ps = mgr.state.policy_states
+    assert ps.arch.critic_bins == 63
+    perturb(ps, 11)
+    L_ = nat.lib()
+    assert L_.mlearn_policy_rollout_kernel(ps.desc, None, N, 0, 0) == 2  # auto: row split
+    waves = torch.cuda.get_device_properties(gpu).multi_processor_count * 8
+    _replay_windows(mgr, env, cfg, [(16 * (waves + 7)) // 32 * 32, N - 32, 0], critic_bins=63)

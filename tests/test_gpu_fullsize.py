@@ -241,6 +241,39 @@ def test_row_split_step_kernel(gpu, mb, bptt):
     _check("bf16", g2, o2, loss, ref.flatten(G, oracle_layout(ps)), met, mb * bptt)
 
 
+@pytest.mark.parametrize("mb,bptt", [(2048, 32), (1023, 32)])
+def test_row_split_step_kernel_twohot(gpu, mb, bptt):
+    """The row-split step kernel with the reference's default critic, a
+    DreamerV3 two-hot critic of 63 bins (round 6: head width 96, both head
+    products streaming the head image from L2, the two-hot cross entropy by
+    each row's four lanes) against the oracle and the feature-split kernel on
+    the same minibatch (65,536 rows: 8 waves x 2 tiles; 32,736 rows: 8 x 1
+    with padding rows)."""
+    T, N, D, H, L = 32, 8192, 64, 256, 2
+    ps = make_policy_state(gpu, D, H, L, torch.bfloat16, seed=61, critic_bins=63)
+    perturb(ps, 62, scale=0.2)
+    rng = np.random.default_rng(63)
+    nseq = (T // bptt) * N
+    seqs = rng.permutation(nseq)[:mb].astype(np.int32)
+    st, rows = _minibatch_store(rng, ps, T, N, D, "bf16", seqs, bptt)
+    s = _device_store(gpu, st, torch.bfloat16)
+    batch = ref.gather_minibatch(st, rows)
+    adv = batch["advantages"].astype(np.float64)
+    stats = (adv.mean(), adv.var())
+    g2, o2 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, step_kernel=2)
+    g1, o1 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, step_kernel=1)
+    g0, o0 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
+    assert np.array_equal(g0, g2) and np.array_equal(o0, o2), "auto must pick the row split"
+    scale = np.abs(g1).max()
+    assert np.abs(g2 - g1).max() / scale < 1e-2
+    assert g2 @ g1 / (np.linalg.norm(g2) * np.linalg.norm(g1)) > 0.9999
+    np.testing.assert_allclose(o2[[0, 10, 15, 20]], o1[[0, 10, 15, 20]], rtol=2e-3)
+    assert o2[14] == mb * bptt and o2[24] == mb * bptt * 6
+    P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
+    loss, G, met, _ = ref.ppo_loss_grads(P, batch, HP, BUCKETS, "bf16", adv_stats=stats)
+    _check("bf16", g2, o2, loss, ref.flatten(G, oracle_layout(ps)), met, mb * bptt)
+
+
 def test_row_split_rejects_ineligible(gpu):
     """step_kernel 2 on a minibatch the row split cannot take is EINVAL."""
     from madrona_learn import _native as nat
