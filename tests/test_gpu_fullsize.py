@@ -89,7 +89,7 @@ def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats, step_kernel=0):
     return grad.cpu().numpy(), out.cpu().numpy()
 
 
-def _check(mode, g, o, loss, gflat, met, M, full_size=False):
+def _check(mode, g, o, loss, gflat, met, M, full_size=False, verr_atol=0.0):
     scale = np.abs(gflat).max()
     if mode == "f32" and full_size:
         # 65,536 rows x 512 ReLUs: tens of pre-activations sit within an f32
@@ -117,9 +117,20 @@ def _check(mode, g, o, loss, gflat, met, M, full_size=False):
         assert cos > 0.999, cos
         mtol = 2e-2
     np.testing.assert_allclose(o[10], met["Value Loss"].mean(), rtol=mtol)
-    np.testing.assert_allclose(o[15], np.abs(met["Value Errors"]).mean(), rtol=mtol)
+    np.testing.assert_allclose(o[15], np.abs(met["Value Errors"]).mean(), rtol=mtol,
+                               atol=verr_atol)
     np.testing.assert_allclose(o[20], met["Entropy"].mean(), rtol=mtol)
     assert o[14] == M and o[24] == M * 6
+
+
+def _twohot_value_scale(P, obs):
+    """Mean over rows of E_p|b| of the oracle's two-hot bin distributions: the
+    scale of mean() (as vscale in test_gpu_configs._check_store)."""
+    _, _, cache = ref.forward(P, obs, "bf16")
+    lg = np.asarray(cache["crit"], np.float64)
+    p = np.exp(lg - lg.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    return float((p * np.abs(ref.twohot_bins(lg.shape[-1]))).sum(-1).mean())
 
 
 HP = {"clip_coef": 0.2, "value_loss_coef": 0.5, "entropy_coef": 0.01,
@@ -268,15 +279,22 @@ def test_row_split_step_kernel_twohot(gpu, mb, bptt):
     assert np.abs(g2 - g1).max() / scale < 1e-2
     assert g2 @ g1 / (np.linalg.norm(g2) * np.linalg.norm(g1)) > 0.9999
     np.testing.assert_allclose(o2[[0, 10, 20]], o1[[0, 10, 20]], rtol=2e-3)
-    # 'Value Errors' = mean |mean() - R|: mean() weighs the bins' symexp values
-    # (up to 1.2e6) by the bin probabilities, so a bf16 ulp of a bin logit
-    # (the two kernels accumulate the head in different orders) moves it far
-    # more than the loss; it is held to the oracle in _check
-    np.testing.assert_allclose(o2[15], o1[15], rtol=5e-2)
     assert o2[14] == mb * bptt and o2[24] == mb * bptt * 6
     P = ref.unflatten(ps.params.cpu().numpy(), oracle_layout(ps))
     loss, G, met, _ = ref.ppo_loss_grads(P, batch, HP, BUCKETS, "bf16", adv_stats=stats)
-    _check("bf16", g2, o2, loss, ref.flatten(G, oracle_layout(ps)), met, mb * bptt)
+    # 'Value Errors' = mean |mean() - R|: mean() weighs the bins' symexp values
+    # (up to 1.2e6) by the bin probabilities, so one bf16 ulp of a bin logit
+    # (the kernels and the oracle accumulate the head in different orders)
+    # moves a row's mean by p_j |b_j - mean| ulp(l_j), far more than it moves
+    # the loss; and the store's returns are the oracle's own means + N(0, 1),
+    # so the oracle's metric is E|N(0,1)| = 0.8 while a kernel's adds its ulp
+    # noise.  With these perturbed bin weights mean() is ~1.2e5 (E_p|b| ~1.5e5)
+    # and the kernels' metric sits ~1.7 (1e-5 of that scale) off the oracle's:
+    # both comparisons are held to 1e-4 of the value scale
+    verr_atol = 1e-4 * _twohot_value_scale(P, batch["obs"])
+    assert abs(o2[15] - o1[15]) <= 2 * verr_atol, (o2[15], o1[15], verr_atol)
+    _check("bf16", g2, o2, loss, ref.flatten(G, oracle_layout(ps)), met, mb * bptt,
+           verr_atol=verr_atol)
 
 
 def test_row_split_rejects_ineligible(gpu):
