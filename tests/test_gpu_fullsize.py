@@ -125,7 +125,7 @@ def _check(mode, g, o, loss, gflat, met, M, full_size=False, verr_atol=0.0):
 
 def _twohot_value_scale(P, obs):
     """Mean over rows of E_p|b| of the oracle's two-hot bin distributions: the
-    scale of mean() (as vscale in test_gpu_configs._check_store)."""
+    scale of mean()."""
     _, _, cache = ref.forward(P, obs, "bf16")
     lg = np.asarray(cache["crit"], np.float64)
     p = np.exp(lg - lg.max(-1, keepdims=True))
