@@ -416,6 +416,9 @@ def main():
     ap.add_argument("--rollout-kernel", type=int, choices=[0, 1, 2], default=0,
                     help="RolloutManager.rollout_kernel: 0 the library's choice, 1 the "
                          "feature-split rollout kernels, 2 the row-split ones (A/B runs)")
+    ap.add_argument("--step-kernel", type=int, choices=[0, 1, 2], default=0,
+                    help="PPO.step_kernel: 0 the library's choice, 1 the feature-split "
+                         "minibatch kernel, 2 the row-split one (A/B runs)")
     ap.add_argument("--optim-launch", type=int, choices=[0, 1, 2], default=0,
                     help="PolicyTrainState.optim_launch_form: 0 the library's choice, 1 the "
                          "split optimizer launches, 2 the fused one (A/B runs)")
@@ -424,6 +427,8 @@ def main():
     args = ap.parse_args()
     from madrona_learn.train_state import PolicyTrainState
     PolicyTrainState.optim_launch_form = args.optim_launch
+    from madrona_learn.ppo import PPO
+    PPO.step_kernel = args.step_kernel
     from madrona_learn.rollouts import RolloutManager
     if args.per_policy_rollouts:
         RolloutManager.population_launch = False

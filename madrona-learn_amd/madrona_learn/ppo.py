@@ -55,6 +55,11 @@ def _base(x):
 
 
 class PPO(AlgoBase):  # ppo.py:49-106
+    # mlearn_ppo_hparams.step_kernel of every minibatch launch: 0 the library's
+    # choice (mlearn_ppo_step_kernel), 1 the feature split, 2 the row split
+    # (A/B runs; 2 raises where the row split does not apply)
+    step_kernel = 0
+
     def init_hyperparams(self, cfg):
         if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
             assert not cfg.algo.clip_value_loss
@@ -163,6 +168,7 @@ class PPO(AlgoBase):  # ppo.py:49-106
         hp.clip_value_loss = 1 if algo.clip_value_loss else 0
         hp.huber_value_loss = 1 if algo.huber_value_loss else 0
         hp.loss_scale = 1.0 / dp.world_size
+        hp.step_kernel = int(self.step_kernel)
         # single-rank training: the gradient reduction also emits the partial
         # sums of squares clip_by_global_norm needs, so the optimizer step skips
         # its own pass over the gradient (under DP the norm is of the
