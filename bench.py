@@ -419,6 +419,9 @@ def main():
     ap.add_argument("--step-kernel", type=int, choices=[0, 1, 2], default=0,
                     help="PPO.step_kernel: 0 the library's choice, 1 the feature-split "
                          "minibatch kernel, 2 the row-split one (A/B runs)")
+    ap.add_argument("--wgrad-form", type=int, choices=[0, 1, 2], default=0,
+                    help="PPO.wgrad_form: 0 the library's choice, 1 the register-staged "
+                         "weight-gradient launch, 2 the LDS-DMA pipeline (A/B runs)")
     ap.add_argument("--optim-launch", type=int, choices=[0, 1, 2], default=0,
                     help="PolicyTrainState.optim_launch_form: 0 the library's choice, 1 the "
                          "split optimizer launches, 2 the fused one (A/B runs)")
@@ -429,6 +432,7 @@ def main():
     PolicyTrainState.optim_launch_form = args.optim_launch
     from madrona_learn.ppo import PPO
     PPO.step_kernel = args.step_kernel
+    PPO.wgrad_form = args.wgrad_form
     from madrona_learn.rollouts import RolloutManager
     if args.per_policy_rollouts:
         RolloutManager.population_launch = False

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MLEARN_ABI_VERSION 21
+#define MLEARN_ABI_VERSION 22
 
 #define MLEARN_OK 0
 #define MLEARN_EINVAL (-1)
@@ -369,7 +369,13 @@ typedef struct mlearn_ppo_hparams {
                                               where it does not apply).  Same inputs and
                                               outputs; results within the compute dtype's
                                               rounding of each other (summation orders) */
-    int32_t pad;
+    int32_t wgrad_form;                    /* operand staging of the bf16 weight-gradient
+                                              launch (ABI 22): 0 = the library's choice
+                                              (2), 1 = register-staged (round 5: two
+                                              chunks in flight through registers),
+                                              2 = LDS-DMA pipeline (global_load_lds,
+                                              ML_WG_STAGES stages).  Same fragments in
+                                              the same order: bit-identical gradients */
 } mlearn_ppo_hparams;
 
 /* Number of partials mlearn_ppo_hparams.grad_sumsq_out receives: one per 64

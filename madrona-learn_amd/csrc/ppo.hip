@@ -725,7 +725,11 @@ struct WgJobs {
 template <typename T> struct WgCfg {
     static constexpr int LD = sizeof(T) == 2 ? 160 : 132;  // LDS row (elements)
     static constexpr size_t buf = (size_t)wg_chunk<T>() * LD * sizeof(T);  // one operand, one stage
-    static constexpr size_t lds = 4 * buf;
+    // register-staged form: 2 stages x 2 operands; LDS-DMA form (bf16): ML_WG_STAGES stages of
+    // two 32-row x 256-B operand images
+    static constexpr size_t glds = (size_t)ML_WG_STAGES * 2 * ML_WG_GCH * 256;
+    static constexpr size_t lds =
+        (sizeof(T) == 2 && ML_WG_GLDS && glds > 4 * buf) ? glds : 4 * buf;
 };
 
 typedef short short4v __attribute__((ext_vector_type(4)));
@@ -879,6 +883,180 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
             }
 }
 
+// ---------------------------------------------------------------------------
+// The bf16 weight-gradient tile with its operand chunks staged by LDS-DMA
+// (global_load_lds_dwordx4: no staging registers, no LDS write pass), S
+// stages deep: chunk c + S - 1 is issued right after the barrier that opens
+// chunk c, so each chunk's loads have S - 1 chunk times to land (the
+// register-staged form above gives them about one: its time per chunk was
+// the load latency -- a second back-to-back launch on cache-hot operands ran
+// 28.9 vs 29.4 us, and a 32 768-row minibatch at one workgroup per CU 24 us
+// for half the bytes, profiles/r06_spill_probes.txt).  Same MFMA fragments
+// in the same order as wgrad_tile<bf16>, so the slabs are bit-identical.
+//
+// LDS image of one operand chunk: 32 rows of P bytes (P = 256 for a 128-
+// column tile, 128 for a tile of <= 64 columns), no padding; one DMA
+// instruction writes 1 KB lane-linearly (lane l -> bytes 16 l), so the XOR
+// swizzle that keeps the transposed fragment reads conflict-free is applied
+// to each lane's SOURCE address: 16-byte unit u of row r sits at unit
+// u ^ swz(r), swz = 4 (r & 3) at P = 256, 4 ((r >> 1) & 1) at P = 128 (the
+// four rows of a half-wave's ds_read_b64_tr_b16 land on four 64-byte bank
+// groups).  Columns past the operand's width load unit 0 of the tile again:
+// they meet only output rows / columns that are never stored.
+// ---------------------------------------------------------------------------
+template <int P> __device__ inline int wg_swz(int row) {
+    return P == 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+}
+
+// one 16-byte-per-lane LDS-DMA piece: LDS bytes [lds_dst + 16 lane, +16) <- gsrc
+// (M0 written and restored in the same statement; hipcc does not count these
+// loads, the caller's s_waitcnt vmcnt does)
+__device__ inline void wg_glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+template <int N> __device__ inline void wg_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int PX, int PY, int CH>
+__device__ inline void wgrad_tile_glds(const WgJobs& jobs, const WgJob& J, int local, char* smem) {
+    constexpr int S = ML_WG_STAGES;
+    static_assert(S >= 2, "at least two stages");
+    constexpr int XB = CH * PX, YB = CH * PY, SB = XB + YB;  // bytes per operand / stage
+    constexpr int NXW = XB / 1024 / 4, NYW = YB / 1024 / 4;  // DMA pieces per wave
+    constexpr int G = NXW + NYW;
+    const int nt = J.ti * J.tj;
+    int split, t;
+    if ((J.splits & 7) == 0 && (J.wg0 & 7) == 0) {  // XCD-aware, as wgrad_tile
+        const int x = local & 7, q = local >> 3;
+        t = q % nt;
+        split = (q / nt) * 8 + x;
+    } else {
+        split = local / nt;
+        t = local - split * nt;
+    }
+    const int i0 = (t % J.ti) * kWgTile, j0 = (t / J.ti) * kWgTile;
+    const int64_t m0 = split * J.rps;
+    const int64_t m1 = m0 + J.rps < jobs.Mp ? m0 + J.rps : jobs.Mp;
+    const int nchunks = (int)((m1 - m0) / CH);
+    const bf16* X = (const bf16*)J.X;
+    const bf16* Y = (const bf16*)J.Y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int iw = (w & 1) * 64, jw = (w >> 1) * 64;
+    const bool wi_on = i0 + iw < J.I, wj_on = j0 + jw < J.J;
+
+    // per-lane source offsets (elements, relative to the chunk's first row)
+    int ox[NXW], oy[NYW];
+#pragma unroll
+    for (int k = 0; k < NXW; ++k) {
+        const int b = (w * NXW + k) * 1024 + lane * 16, r = b / PX;
+        const int u = ((b % PX) >> 4) ^ wg_swz<PX>(r);
+        const int col = i0 + 8 * u < J.I ? i0 + 8 * u : i0;
+        ox[k] = r * J.I + col;
+    }
+#pragma unroll
+    for (int k = 0; k < NYW; ++k) {
+        const int b = (w * NYW + k) * 1024 + lane * 16, r = b / PY;
+        const int u = ((b % PY) >> 4) ^ wg_swz<PY>(r);
+        const int col = j0 + 8 * u < J.J ? j0 + 8 * u : j0;
+        oy[k] = r * J.J + col;
+    }
+    const uint32_t lbase =
+        (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)smem;
+    auto issue = [&](int c, int st) {
+        const bf16* xb = X + (m0 + CH * (int64_t)c) * J.I;
+        const bf16* yb = Y + (m0 + CH * (int64_t)c) * J.J;
+        const uint32_t sb = lbase + (uint32_t)(st * SB);
+#pragma unroll
+        for (int k = 0; k < NXW; ++k)
+            wg_glds16(xb + ox[k], __builtin_amdgcn_readfirstlane(sb + (uint32_t)((w * NXW + k) * 1024)));
+#pragma unroll
+        for (int k = 0; k < NYW; ++k)
+            wg_glds16(yb + oy[k],
+                      __builtin_amdgcn_readfirstlane(sb + (uint32_t)(XB + (w * NYW + k) * 1024)));
+    };
+
+    // fragment reads: lane (g = lane >> 4: hh = g >> 1, cc = g & 1; q, p) reads rows
+    // 16 ks + 8 hh + q (+ 4) at columns c0 + 16 cc + 4 p .. + 3 (wgrad_tile's WgFrag)
+    const int g = lane >> 4, hh = g >> 1, cc = g & 1, q = (lane >> 2) & 3, p = lane & 3;
+    auto fofs = [&](int c0, int P, int swz) {
+        const int u = (c0 >> 3) + 2 * cc + (p >> 1);
+        return (8 * hh + q) * P + ((u ^ swz) << 4) + (p & 1) * 8;
+    };
+    int fx[2], fy[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        fx[a] = fofs(iw + 32 * a, PX, wg_swz<PX>(q));
+        fy[a] = fofs(jw + 32 * a, PY, wg_swz<PY>(q));
+    }
+    typedef __attribute__((address_space(3))) short4v* lp;
+    typedef short short8v __attribute__((ext_vector_type(8)));
+    auto frag = [&](const char* base, int ofs, int ks, int P) {
+        const char* a = base + ks * 16 * P + ofs;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(a));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(a + 4 * P));
+        short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) zero_acc<2>(acc[a]);
+    const bool on = wi_on && wj_on;
+
+#pragma unroll
+    for (int k = 0; k < S - 1; ++k)
+        if (k < nchunks) issue(k, k);
+    int st = 0;  // stage of chunk c
+    for (int c = 0; c < nchunks; ++c) {
+        // chunk c's pieces (this wave's) have landed: S - 2 younger chunks may
+        // stay in flight (fewer near the end)
+        if (c + S - 2 < nchunks) wg_vmcnt<G * (S - 2)>();
+        else wg_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's pieces in; stage (c - 1) % S read out
+        __builtin_amdgcn_sched_barrier(0);
+        if (c + S - 1 < nchunks) issue(c + S - 1, st == 0 ? S - 1 : st - 1);
+        if (on) {
+            const char* xs = smem + st * SB;
+            const char* ys = xs + XB;
+#pragma unroll
+            for (int ks = 0; ks < CH / 16; ++ks) {
+                bf16x8 fa[2], fb[2];
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    fa[a] = frag(xs, fx[a], ks, PX);
+                    fb[a] = frag(ys, fy[a], ks, PY);
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) acc[a][b] = MT<bf16>::mma(fa[a], fb[b], acc[a][b]);
+            }
+        }
+        st = st + 1 == S ? 0 : st + 1;
+    }
+    if (!on) return;
+    float* out = J.out + (int64_t)split * J.I * J.J;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int i = i0 + iw + 32 * a + acc_row(e, lane);
+                const int j = j0 + jw + 32 * b + (lane & 31);
+                if (i < J.I && j < J.J)
+                    __builtin_nontemporal_store(acc[a][b][e], out + (int64_t)i * J.J + j);
+            }
+}
+
 // Blocks [0, nwg) compute weight gradients; the next ncol blocks the first
 // level of the column partials; one more (if loss_out) the loss metrics.
 // (The fixed-order reduction into the flat gradient is the next launch,
@@ -897,6 +1075,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES
     int jb = 0;
     while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
     const WgJob& J = jobs.job[jb];
+#if ML_WG_GLDS
+    if constexpr (sizeof(T) == 2) if (hp.wg_form != 1) {
+        static_assert(kWgTile == 128, "LDS-DMA tile shape");
+        const int local = blockIdx.x - J.wg0;
+        // ML_WG_GCH-row chunks where the split's rows divide (Mp is a multiple of 64)
+        constexpr int C2 = ML_WG_GCH;
+        if (C2 != 32 && J.rps % C2 == 0) {
+            if (J.I <= 64) {
+                if (J.J <= 64) wgrad_tile_glds<128, 128, C2>(jobs, J, local, smem);
+                else wgrad_tile_glds<128, 256, C2>(jobs, J, local, smem);
+            } else {
+                if (J.J <= 64) wgrad_tile_glds<256, 128, C2>(jobs, J, local, smem);
+                else wgrad_tile_glds<256, 256, C2>(jobs, J, local, smem);
+            }
+            return;
+        }
+        if (J.I <= 64) {
+            if (J.J <= 64) wgrad_tile_glds<128, 128, 32>(jobs, J, local, smem);
+            else wgrad_tile_glds<128, 256, 32>(jobs, J, local, smem);
+        } else {
+            if (J.J <= 64) wgrad_tile_glds<256, 128, 32>(jobs, J, local, smem);
+            else wgrad_tile_glds<256, 256, 32>(jobs, J, local, smem);
+        }
+        return;
+    }
+#endif
     wgrad_tile<T>(jobs, J, blockIdx.x - J.wg0, smem);
 }
 
@@ -1168,6 +1372,10 @@ static void launch_wgrad(const WgJobs& jobs, const WsK& ws, const HpK& hp, int64
     const int blocks = jobs.nwg + jobs.ncol + (loss_out ? 1 : 0);
     hipLaunchKernelGGL((wgrad_kernel<T>), dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
                        K, loss_out);
+#ifdef ML_PROBE_WG_TWICE  // (timing probe: the same launch again, operands now cache-hot)
+    hipLaunchKernelGGL((wgrad_kernel<T>), dim3(blocks), dim3(256), WgCfg<T>::lds, s, jobs, ws, hp, M,
+                       K, loss_out);
+#endif
     hipLaunchKernelGGL(reduce_grads_kernel, dim3((unsigned)((Lk.total + 63) / 64)), dim3(256), 0, s,
                        Lk, ws, grad, sumsq);
 }
@@ -1199,6 +1407,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.metrics = loss_out != nullptr;
+    hp.wg_form = h.wgrad_form;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
 
@@ -1284,6 +1493,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.metrics = loss_out != nullptr;
+    hp.wg_form = h.wgrad_form;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
     const int L = p.num_layers;

@@ -29,6 +29,7 @@ struct HpK {
     float objw[MLEARN_MAX_GROUPS];  // per sub-action surrogate weight (K / K_key)
     int norm_adv, clip_vl, huber, norm_vals;
     int metrics;  // reduce the loss metrics (only the minibatch whose metrics are recorded)
+    int wg_form;  // mlearn_ppo_hparams.wgrad_form (bf16 weight-gradient staging)
     float loss_scale;
     float inv_sk, inv_s;
 };
@@ -49,6 +50,15 @@ constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number o
 
 #ifndef ML_WG_SETS
 #define ML_WG_SETS 2  // weight-gradient chunks in flight (register sets of staged rows)
+#endif
+#ifndef ML_WG_GLDS
+#define ML_WG_GLDS 1  // bf16 weight-gradient tiles staged by LDS-DMA (global_load_lds) pipelines
+#endif
+#ifndef ML_WG_STAGES
+#define ML_WG_STAGES 2  // LDS stages of the LDS-DMA pipeline (S - 1 chunks in flight)
+#endif
+#ifndef ML_WG_GCH
+#define ML_WG_GCH 32  // rows per LDS-DMA chunk (32 or 64; 64 where a split's rows divide)
 #endif
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for

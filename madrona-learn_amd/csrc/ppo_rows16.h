@@ -365,12 +365,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         }
         R16_STAMP(1);
         // X_0 rows for the weight gradient (16 bytes per lane and k-step)
+#ifndef ML_PROBE_NO_X0  // (timing probe only: numerics invalid without the store)
         {
             bf16* xrow = (bf16*)ws.x0 + r16_late(row) * D;
 #pragma unroll
             for (int s = 0; s < DS; ++s)
                 r16_st16(xrow + 32 * s + 8 * g, __builtin_bit_cast(u4r, xf[s]));
         }
+#endif
         // the previous tile's layer-0 dZ rows go out behind this tile's loads
         if (tt > 0) {
             r16_store_rows((bf16*)ws.dz[0] + r16_late(prev_row) * kR16H, dz0w, g);
@@ -389,7 +391,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((NW + 3
         // (update 8.43-8.50 -> 8.36-8.38 ms on one box; from the last tile's
         // start: -1..2 % kernel time; from the kernel's start: slower)
         if (NW > 4 && tt == 0 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#ifndef ML_PROBE_NO_A0  // (timing probe only)
         r16_store_rows((bf16*)ws.a[0] + r16_late(row) * kR16H, aw, g);  // A_0 rows
+#endif
         r16_ln_apply(zw, mean, rstd, gb + 2 * kR16H, g, aw);
         R16_STAMP(4);
         // ---- heads (models.py:122-154): logits / value = rnd(rnd(A_1 Wh) + rnd(b))

@@ -17,7 +17,7 @@ import torch
 LIB_PATH = os.environ.get(
     "MADRONA_LEARN_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmlearn.so"))
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
@@ -67,7 +67,7 @@ class PPOHparams(Structure):
                 ("clip_value_loss", c_int32), ("huber_value_loss", c_int32),
                 ("loss_scale", c_float), ("normalize_values", c_int32),
                 ("obj_weight", c_float * MAX_GROUPS),
-                ("grad_sumsq_out", c_void_p), ("step_kernel", c_int32), ("pad", c_int32)]
+                ("grad_sumsq_out", c_void_p), ("step_kernel", c_int32), ("wgrad_form", c_int32)]
 
 
 class FlatGroup(Structure):  # mlearn_flat_group

@@ -59,6 +59,9 @@ class PPO(AlgoBase):  # ppo.py:49-106
     # choice (mlearn_ppo_step_kernel), 1 the feature split, 2 the row split
     # (A/B runs; 2 raises where the row split does not apply)
     step_kernel = 0
+    # mlearn_ppo_hparams.wgrad_form (ABI 22): 0 the library's choice (the
+    # LDS-DMA pipeline), 1 register-staged, 2 LDS-DMA; bit-identical (A/B runs)
+    wgrad_form = 0
 
     def init_hyperparams(self, cfg):
         if cfg.dreamer_v3_critic or cfg.hlgauss_critic:
@@ -169,6 +172,7 @@ class PPO(AlgoBase):  # ppo.py:49-106
         hp.huber_value_loss = 1 if algo.huber_value_loss else 0
         hp.loss_scale = 1.0 / dp.world_size
         hp.step_kernel = int(self.step_kernel)
+        hp.wgrad_form = int(self.wgrad_form)
         # single-rank training: the gradient reduction also emits the partial
         # sums of squares clip_by_global_norm needs, so the optimizer step skips
         # its own pass over the gradient (under DP the norm is of the

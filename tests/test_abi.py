@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from madrona_learn import _native as nat
-    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 21
+    assert nat.lib().mlearn_abi_version() == nat.ABI_VERSION == 22
     hdr = open(HEADER).read()
     assert f"#define MLEARN_ABI_VERSION {nat.ABI_VERSION}" in hdr
 

@@ -64,10 +64,11 @@ def _device_store(gpu, st, dtype):
     return s
 
 
-def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats, step_kernel=0):
+def _run_grad(gpu, ps, s, seqs, mb, bptt, hpd, stats, step_kernel=0, wgrad_form=0):
     from madrona_learn import _native as nat
     hp = nat.PPOHparams()
     hp.step_kernel = step_kernel
+    hp.wgrad_form = wgrad_form
     hp.clip_coef, hp.value_loss_coef = hpd["clip_coef"], hpd["value_loss_coef"]
     for k in range(6):
         hp.entropy_coef[k] = hpd["entropy_coef"]
@@ -308,3 +309,33 @@ def test_row_split_rejects_ineligible(gpu):
     s = _device_store(gpu, st, torch.bfloat16)
     with pytest.raises(RuntimeError, match="step_kernel"):
         _run_grad(gpu, ps, s, seqs, mb, bptt, HP, (0.0, 1.0), step_kernel=2)
+
+
+@pytest.mark.parametrize("D,H,L,CB,mb,bptt", [
+    (64, 256, 2, 1, 2048, 32),   # the headline minibatch (row-split step, 65,536 rows)
+    (64, 256, 2, 63, 1023, 32),  # two-hot critic: head width 96, padding rows
+    (64, 128, 3, 1, 200, 16),    # feature-split step, 128-column tiles
+    (32, 64, 1, 1, 77, 16),      # obs 32 / hidden 64: 64-byte and 128-byte operand rows
+])
+def test_wgrad_staging_forms_bit_identical(gpu, D, H, L, CB, mb, bptt):
+    """mlearn_ppo_hparams.wgrad_form (ABI 22): the LDS-DMA weight-gradient
+    pipeline (2, the default) and the register-staged form (1) feed the same
+    fragments to the same MFMAs in the same order -- the flat gradient and
+    the loss metrics must be bit-identical, and the default must be form 2's."""
+    T, N = 32, 8192 if mb >= 1023 else 256
+    ps = make_policy_state(gpu, D, H, L, torch.bfloat16, seed=51, critic_bins=CB)
+    perturb(ps, 52, scale=0.2)
+    rng = np.random.default_rng(53)
+    nseq = (T // bptt) * N
+    seqs = rng.permutation(nseq)[:mb].astype(np.int32)
+    st, rows = _minibatch_store(rng, ps, T, N, D, "bf16", seqs, bptt)
+    s = _device_store(gpu, st, torch.bfloat16)
+    adv = ref.gather_minibatch(st, rows)["advantages"].astype(np.float64)
+    stats = (adv.mean(), adv.var())
+    g1, o1 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, wgrad_form=1)
+    g2, o2 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, wgrad_form=2)
+    g0, o0 = _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats)
+    assert np.all(np.isfinite(g2)) and np.abs(g2).max() > 0
+    assert np.array_equal(g1, g2), np.abs(g1 - g2).max()
+    assert np.array_equal(o1, o2)
+    assert np.array_equal(g0, g2) and np.array_equal(o0, o2)
