@@ -838,6 +838,7 @@ def _record_metrics(metrics, policy_idx, met):
         x = met[k].double().reshape(-1)
         n = float(x.numel())
         mean = x.mean()
+        # (the count by a fill, not a host copy: this runs inside HIP-graph capture)
         rows.append(torch.stack([mean, ((x - mean) ** 2).sum(), x.min(), x.max(),
-                                 torch.tensor(n, dtype=torch.float64, device=x.device)]))
+                                 torch.full((), n, dtype=torch.float64, device=x.device)]))
     out.copy_(torch.stack(rows).reshape(out.shape).to(out.dtype))

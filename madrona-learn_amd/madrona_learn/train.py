@@ -73,27 +73,40 @@ class TrainingManager:  # train.py:35-64
         self.profile_port = profile_port
         self._segments = None
         self._eager_iters = 0
+        # "all": the whole update is captured (the fused kernels); "learn":
+        # the torch path (generic.py) -- its rollout runs eagerly (it reads the
+        # device sampling counter on the host once per rollout) and the PPO
+        # update (autograd through the user's modules, HIP action_stats and
+        # flat optimizer) is captured; a tree whose modules cannot be captured
+        # falls back to eager updates
+        self.graph_scope = "all"
+        self._side = None  # the torch path's learn stream (warm-up and capture)
 
     # -- one update as a generator over collectives --------------------------
+    def _collect(self):
+        with profile("Collect Rollouts"):
+            (self.state, self.rollout, self._rollout_data, _obs_stats,
+             self.metrics) = self.rollout_mgr.collect(self.state, self.rollout, self.metrics,
+                                                      self.user_hooks)
+
+    def _learn(self):
+        with profile("Learn"):
+            # algo_wrapper = vmap over the train policies (train.py:165-174,
+            # 206-210): each local policy updates on its own env columns
+            epoch_ctr = self.rollout.counters[1:2]
+            for ps, ts, algo in zip(self.state.policy_list, self.state.train_list, self.algos):
+                self.metrics = yield from algo.update_program(
+                    self.cfg, ps, ts, self._rollout_data, self.user_hooks.optimize_metrics,
+                    self.metrics, epoch_ctr)
+            self.algos[0].advance_epochs(epoch_ctr)
+
     def _program(self):
         with profile("Update Iter"):
-            with profile("Collect Rollouts"):
-                (self.state, self.rollout, rollout_data, _obs_stats,
-                 self.metrics) = self.rollout_mgr.collect(self.state, self.rollout, self.metrics,
-                                                          self.user_hooks)
-            with profile("Learn"):
-                # algo_wrapper = vmap over the train policies (train.py:165-174,
-                # 206-210): each local policy updates on its own env columns
-                epoch_ctr = self.rollout.counters[1:2]
-                for ps, ts, algo in zip(self.state.policy_list, self.state.train_list,
-                                        self.algos):
-                    self.metrics = yield from algo.update_program(
-                        self.cfg, ps, ts, rollout_data, self.user_hooks.optimize_metrics,
-                        self.metrics, epoch_ctr)
-                self.algos[0].advance_epochs(epoch_ctr)
+            self._collect()
+            yield from self._learn()
 
-    def _run_eager(self):
-        gen = self._program()
+    def _run_eager(self, gen=None):
+        gen = self._program() if gen is None else gen
         try:
             while True:
                 op, t = next(gen)
@@ -102,12 +115,13 @@ class TrainingManager:  # train.py:35-64
         except StopIteration:
             pass
 
-    def _capture(self):
-        """Capture the update into HIP graphs split at the collectives."""
-        gen = self._program()
+    def _capture(self, gen=None, s=None):
+        """Capture the update (or the generator gen) into HIP graphs split at
+        the collectives."""
+        gen = self._program() if gen is None else gen
         segments = []
         done = False
-        s = torch.cuda.Stream()
+        s = torch.cuda.Stream() if s is None else s
         s.wait_stream(torch.cuda.current_stream())
         while not done:
             g = torch.cuda.CUDAGraph()
@@ -128,9 +142,43 @@ class TrainingManager:  # train.py:35-64
             if coll is not None:
                 self.dp.all_reduce_sum_(coll)
 
+    def _update_learn_graph(self):
+        """graph_scope "learn": eager rollout, then the update from HIP graphs
+        (one eager update first, on the stream the capture uses, so that the
+        lazily created library handles and autograd's stream state exist
+        before capture)."""
+        import sys
+        self._collect()
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        cur = torch.cuda.current_stream()
+        if self._segments is None and self._eager_iters >= 1:
+            try:
+                self._segments = self._capture(self._learn(), self._side)
+            except Exception as e:  # modules with host reads / syncs: stay eager
+                cur.wait_stream(self._side)
+                torch.cuda.synchronize()
+                print(f"[madrona_learn] torch-path update not capturable ({type(e).__name__}: "
+                      f"{e}); updating eagerly", file=sys.stderr)
+                self._segments = None
+                self.use_graph = False
+                self._run_eager(self._learn())
+                return
+            self._replay()  # the capture recorded the update without running it
+        elif self._segments is not None:
+            self._replay()
+        else:
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                self._run_eager(self._learn())
+            cur.wait_stream(self._side)
+            self._eager_iters += 1
+
     def update_iter(self):
         """One PPO iteration; returns self (the reference returns a new pytree)."""
-        if self.use_graph and self._segments is None and self._eager_iters >= 1:
+        if self.use_graph and self.graph_scope == "learn":
+            self._update_learn_graph()
+        elif self.use_graph and self._segments is None and self._eager_iters >= 1:
             # capture runs the program once: it performs this iteration's work
             self._segments = self._capture()
             self._replay_collectives_of_capture()
@@ -288,7 +336,8 @@ def init_training(dev, cfg: TrainConfig, sim_fns: Dict[str, Callable], policy: P
         # autograd over the user's modules, HIP kernels around them (generic.py)
         return _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
                                     num_policies, sim_batch, sim_fns, restore_ckpt, profile_port,
-                                    generic_why, policy_ids=list(policy_ids))
+                                    generic_why, policy_ids=list(policy_ids),
+                                    use_graph=use_graph)
     prefix = policy.actor_critic.backbone.prefix
     from .rollouts import obs_to_matrix
     obs0 = obs_to_matrix(prefix(rollout_state.cur_obs, train=False), sim_batch)
@@ -416,9 +465,10 @@ def _fused_tree_problem(policy, rollout_state, sim_batch, cfg):
 
 def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, rank, W,
                          num_policies, sim_batch, sim_fns, restore_ckpt, profile_port, why,
-                         policy_ids=(0,)):
+                         policy_ids=(0,), use_graph=True):
     """init_training for a tree outside the fused kernels (generic.py): the
-    user's torch modules train under autograd, eagerly (no HIP graph), with
+    user's torch modules train under autograd (the update captured in HIP
+    graphs after one eager update, TrainingManager.graph_scope "learn"), with
     sampling, post-step, GAE, advantage statistics, action_stats and the
     optimizer on the HIP kernels.  A population (cfg.pbt, self-play split)
     gets one copy of the tree per train policy this rank holds, each with its
@@ -503,8 +553,13 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
         algo.store = rollout_mgr.store
         algo.col0 = i * rollout_mgr.B
     print(cfg)
+    # HIP graphs over the update only (TrainingManager.graph_scope "learn");
+    # fp16 (DynamicScale reads the gradient norm on the host) stays eager
     mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
-                          update_idx=start, use_graph=False, profile_port=profile_port)
+                          update_idx=start,
+                          use_graph=use_graph and all(ts.scaler is None for ts in tss),
+                          profile_port=profile_port)
+    mgr.graph_scope = "learn"
     mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
     mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
     return mgr

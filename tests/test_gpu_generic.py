@@ -59,7 +59,8 @@ def test_backbone_separate_update_matches_oracle(gpu):
     cfg = _cfg(N, mb)
     mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac), use_graph=True)
     ps, ts = mgr.state.policy_states, mgr.state.train_states
-    assert getattr(ps, "generic", False) and not mgr.use_graph
+    # (the torch path captures its update in HIP graphs from update 2 on)
+    assert getattr(ps, "generic", False) and mgr.use_graph and mgr.graph_scope == "learn"
     order = [n for n, _, _ in ps.layout["params"]]
     p0 = _named(ps)
     init_norms = {k: float(np.sqrt((v * v).sum())) for k, v in p0.items() if k.endswith("kernel")
@@ -537,3 +538,67 @@ def test_population_of_separate_backbones_matches_oracle(gpu):
         dg, dw = g - z, w - z
         assert dg @ dw / (np.linalg.norm(dg) * np.linalg.norm(dw)) > 0.999
         assert int(tss[p].step.item()) == 2 * (B // mb)
+
+
+def _torch_tree(kind, dt):
+    import madrona_learn as ml
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+    from madrona_learn.rnn import LSTM
+    if kind == "lstm2":
+        bb = ml.BackboneShared(encoder=ml.RecurrentBackboneEncoder(net=MLP(64, 1, dt),
+                                                                   rnn=LSTM(64, 2, dt)))
+    else:
+        bb = ml.BackboneSeparate(actor_encoder=ml.BackboneEncoder(net=MLP(64, 2, dt)),
+                                 critic_encoder=ml.BackboneEncoder(net=MLP(64, 2, dt)))
+    return ml.ActorCritic(backbone=bb,
+                          actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+                          critic=DenseLayerCritic(dt))
+
+
+@pytest.mark.parametrize("kind", ["separate", "lstm2", "pop2"])
+def test_torch_path_graph_replay_matches_eager(gpu, kind):
+    """The torch path's update captured in HIP graphs (TrainingManager
+    graph_scope "learn": update 1 eager on the capture stream, update 2
+    captured, update 3 replayed) against the same tree trained eagerly
+    (use_graph=False): parameters, Adam state, the rollout store and the loss
+    metrics bit-identical after every update -- BackboneSeparate, a two-layer
+    LSTM (per-chunk start states, C = 2) and a 2-policy population."""
+    import dataclasses
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    dt = torch.float32
+    P = 2 if kind == "pop2" else 1
+    N = 64 * P
+    cfg = _cfg(N, 16)
+    if kind == "lstm2":
+        cfg = dataclasses.replace(cfg, num_bptt_chunks=2)
+    if kind == "pop2":
+        cfg = dataclasses.replace(cfg, pbt=ml.PBTConfig(
+            num_teams=1, team_size=1, num_train_policies=P, num_past_policies=0,
+            self_play_portion=1.0, cross_play_portion=0.0, past_play_portion=0.0))
+    mgrs = []
+    for use_graph in (False, True):
+        env = DummyVecEnv(N, 64, 6, seed=12, device=gpu)
+        mgrs.append(ml.init_training(gpu, cfg, env.sim_fns(),
+                                     ml.Policy(actor_critic=_torch_tree(kind, dt)),
+                                     use_graph=use_graph))
+    eager, graph = mgrs
+    assert not eager.use_graph and graph.use_graph and graph.graph_scope == "learn"
+    for it in range(3):
+        for m in mgrs:
+            m.update_iter()
+        torch.cuda.synchronize()
+        assert graph.use_graph, "the update fell back to eager"
+        assert (graph._segments is not None) == (it >= 1)
+        for pe, pg in zip(eager.state.policy_list, graph.state.policy_list):
+            assert torch.equal(pe.params, pg.params), (it, kind)
+        for te, tg in zip(eager.state.train_list, graph.state.train_list):
+            assert torch.equal(te.adam_m, tg.adam_m) and torch.equal(te.adam_v, tg.adam_v)
+            assert torch.equal(te.step, tg.step)
+        se, sg = eager.rollout_mgr.store, graph.rollout_mgr.store
+        for k, v in se.as_dict().items():
+            assert torch.equal(v, sg.as_dict()[k]), (it, k)
+        le, lg = eager.metrics.last(), graph.metrics.last()
+        for k in ("Loss", "Value Loss", "Entropy"):
+            assert le[k].mean == lg[k].mean, (it, k)
+    assert int(graph.state.train_list[0].step.item()) == 3 * 2 * (cfg.num_bptt_chunks * 64 // 16)
