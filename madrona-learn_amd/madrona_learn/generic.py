@@ -36,8 +36,9 @@ concatenated along the output axis) project per gate, each of the 8 gate
 kernels to its own initial norm, as flax's separate per-gate Dense leaves do
 (rnn.py:30-36; the fused optimizer's per-gate slots).
 Recurrent trees (a user's recurrent backbone, multi-layer LSTMs) train here
-with the rollout carry and per-chunk start states.  This path runs eagerly
-(no HIP-graph capture); the value normaliser and populations raise.
+with the rollout carry and per-chunk start states.  The rollout runs eagerly;
+the update is captured in HIP graphs after one eager update
+(TrainingManager.graph_scope "learn"; fp16 stays eager).
 """
 
 import ctypes
