@@ -1052,8 +1052,13 @@ __device__ inline void wgrad_tile_glds(const WgJobs& jobs, const WgJob& J, int l
             for (int e = 0; e < 16; ++e) {
                 const int i = i0 + iw + 32 * a + acc_row(e, lane);
                 const int j = j0 + jw + 32 * b + (lane & 31);
-                if (i < J.I && j < J.J)
+                if (i < J.I && j < J.J) {
+#if ML_WG_SLAB_NT
                     __builtin_nontemporal_store(acc[a][b][e], out + (int64_t)i * J.J + j);
+#else
+                    out[(int64_t)i * J.J + j] = acc[a][b][e];
+#endif
+                }
             }
 }
 

@@ -57,6 +57,9 @@ constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number o
 #ifndef ML_WG_STAGES
 #define ML_WG_STAGES 2  // LDS stages of the LDS-DMA pipeline (S - 1 chunks in flight)
 #endif
+#ifndef ML_WG_SLAB_NT
+#define ML_WG_SLAB_NT 1  // LDS-DMA tile: split-K slabs stored nontemporal
+#endif
 #ifndef ML_WG_GCH
 #define ML_WG_GCH 32  // rows per LDS-DMA chunk (32 or 64; 64 where a split's rows divide)
 #endif
