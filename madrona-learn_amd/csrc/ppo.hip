@@ -727,7 +727,7 @@ template <typename T> struct WgCfg {
     static constexpr size_t buf = (size_t)wg_chunk<T>() * LD * sizeof(T);  // one operand, one stage
     // register-staged form: 2 stages x 2 operands; LDS-DMA form (bf16): ML_WG_STAGES stages of
     // two 32-row x 256-B operand images
-    static constexpr size_t glds = (size_t)ML_WG_STAGES * 2 * ML_WG_GCH * 256;
+    static constexpr size_t glds = (size_t)ML_WG_STAGES * 2 * 32 * 256;
     static constexpr size_t lds =
         (sizeof(T) == 2 && ML_WG_GLDS && glds > 4 * buf) ? glds : 4 * buf;
 };
@@ -1081,29 +1081,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ML_WG_WAVES
     while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.job[jb + 1].wg0) ++jb;
     const WgJob& J = jobs.job[jb];
 #if ML_WG_GLDS
-    if constexpr (sizeof(T) == 2) if (hp.wg_form != 1) {
+    if constexpr (sizeof(T) == 2) {
         static_assert(kWgTile == 128, "LDS-DMA tile shape");
-        const int local = blockIdx.x - J.wg0;
-        // ML_WG_GCH-row chunks where the split's rows divide (Mp is a multiple of 64)
-        constexpr int C2 = ML_WG_GCH;
-        if (C2 != 32 && J.rps % C2 == 0) {
+        if (hp.wg_form != 1) {  // mlearn_ppo_hparams.wgrad_form: 0 / 2 = LDS-DMA
+            // operand image rows of 128 B (<= 64 columns) or 256 B
+            const int local = blockIdx.x - J.wg0;
             if (J.I <= 64) {
-                if (J.J <= 64) wgrad_tile_glds<128, 128, C2>(jobs, J, local, smem);
-                else wgrad_tile_glds<128, 256, C2>(jobs, J, local, smem);
+                if (J.J <= 64) wgrad_tile_glds<128, 128, 32>(jobs, J, local, smem);
+                else wgrad_tile_glds<128, 256, 32>(jobs, J, local, smem);
             } else {
-                if (J.J <= 64) wgrad_tile_glds<256, 128, C2>(jobs, J, local, smem);
-                else wgrad_tile_glds<256, 256, C2>(jobs, J, local, smem);
+                if (J.J <= 64) wgrad_tile_glds<256, 128, 32>(jobs, J, local, smem);
+                else wgrad_tile_glds<256, 256, 32>(jobs, J, local, smem);
             }
             return;
         }
-        if (J.I <= 64) {
-            if (J.J <= 64) wgrad_tile_glds<128, 128, 32>(jobs, J, local, smem);
-            else wgrad_tile_glds<128, 256, 32>(jobs, J, local, smem);
-        } else {
-            if (J.J <= 64) wgrad_tile_glds<256, 128, 32>(jobs, J, local, smem);
-            else wgrad_tile_glds<256, 256, 32>(jobs, J, local, smem);
-        }
-        return;
     }
 #endif
     wgrad_tile<T>(jobs, J, blockIdx.x - J.wg0, smem);
@@ -1412,6 +1403,7 @@ static int launch_minibatch(const mlearn_mlp_policy& p, const mlearn_rollout_vie
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.metrics = loss_out != nullptr;
+    ML_REQUIRE(h.wgrad_form >= 0 && h.wgrad_form <= 2, "ppo: wgrad_form %d", h.wgrad_form);
     hp.wg_form = h.wgrad_form;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));
@@ -1498,6 +1490,7 @@ static int launch_minibatch_lstm(const mlearn_mlp_policy& p, const mlearn_lstm& 
     hp.huber = h.huber_value_loss;
     hp.loss_scale = h.loss_scale;
     hp.metrics = loss_out != nullptr;
+    ML_REQUIRE(h.wgrad_form >= 0 && h.wgrad_form <= 2, "ppo: wgrad_form %d", h.wgrad_form);
     hp.wg_form = h.wgrad_form;
     hp.inv_s = (float)(1.0 / (double)M);
     hp.inv_sk = (float)(1.0 / ((double)M * p.actions.num_groups));

@@ -60,9 +60,6 @@ constexpr int kRowAlign = 64;  // Mp granularity of the update (an even number o
 #ifndef ML_WG_SLAB_NT
 #define ML_WG_SLAB_NT 1  // LDS-DMA tile: split-K slabs stored nontemporal
 #endif
-#ifndef ML_WG_GCH
-#define ML_WG_GCH 32  // rows per LDS-DMA chunk (32 or 64; 64 where a split's rows divide)
-#endif
 #ifndef ML_WG_WAVES
 #define ML_WG_WAVES 3  // waves per SIMD the weight-gradient kernel is register-budgeted for
 #endif

@@ -339,3 +339,5 @@ def test_wgrad_staging_forms_bit_identical(gpu, D, H, L, CB, mb, bptt):
     assert np.array_equal(g1, g2), np.abs(g1 - g2).max()
     assert np.array_equal(o1, o2)
     assert np.array_equal(g0, g2) and np.array_equal(o0, o2)
+    with pytest.raises(Exception, match="wgrad_form"):
+        _run_grad(gpu, ps, s, seqs, mb, bptt, HP, stats, wgrad_form=3)
