@@ -126,23 +126,29 @@ def flop_per_sample(D=OBS, H=HID, L=LAYERS, A1=sum(BUCKETS) + 1):
     return fwd, bwd_dx, wgrad
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r05.json")
+# newest first: this round's summary of the headline kernels, then round 5's
+# (which also holds the feature-split kernels the other configs run)
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("pmc_r06.json", "pmc_r05.json")]
+PMC_SOURCE = {}
 
 
 def pmc_traffic(kernel_key):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
-    of this round (profiles/pmc_r05.json, tools/pmc_traffic.py): FETCH_SIZE
-    doubled (gfx950 reports half the bytes of 16-B streaming reads,
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC
+    summaries (profiles/pmc_r06.json, then pmc_r05.json; tools/pmc_traffic.py):
+    FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B streaming reads,
     MI355X_MICROARCH.md HBM) + WRITE_SIZE, with the profiled kernel's name.
-    (None, None) when no summary is committed."""
-    if not os.path.exists(PMC_FILE):
-        return None, None
-    with open(PMC_FILE) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel_key)
-    if k is None:
-        return None, None
-    return k.get("hbm_bytes_per_launch"), k.get("kernel_name")
+    The summary's path is kept in PMC_SOURCE[kernel_key].  (None, None) when
+    no summary holds the kernel."""
+    for path in PMC_FILES:
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel_key)
+        if k is not None:
+            PMC_SOURCE[kernel_key] = os.path.relpath(path, ROOT)
+            return k.get("hbm_bytes_per_launch"), k.get("kernel_name")
+    return None, None
 
 
 def cpu_model():
@@ -185,18 +191,19 @@ def kernel_rooflines(mgr, dev, n_local, iters=20):
     if sk == 2:
         kname = "ppo_rows16_kernel<false> (row-split)"
         mangled = ("ppo_rows16_kernel",)
-        traffic, pmc_name = pmc_traffic("ppo_rows16")
+        pmc_key = "ppo_rows16"
     else:
         kname = f"ppo_step_kernel<bf16,{HID},{LAYERS},0,{HC},1> (feature-split)"
         mangled = ("ppo_step_kernel", f"Li{HC}ELi1E")
-        traffic, pmc_name = pmc_traffic("ppo_step")
+        pmc_key = "ppo_step"
+    traffic, pmc_name = pmc_traffic(pmc_key)
     if pmc_name is None or not all(m in pmc_name for m in mangled) or "<true>" in pmc_name or "ILb1" in pmc_name:
         traffic, pmc_name = None, None  # the committed PMC pass profiled another kernel
     roof = {
         "kernel": f"{kname} (mlearn_ppo_minibatch_fwd_bwd)",
         "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
         "frac": achieved / BF16_PEAK_TFS, "traffic": traffic,
-        "traffic_source": (f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc_name})"
+        "traffic_source": (f"{PMC_SOURCE.get(pmc_key)} ({pmc_name})"
                            if traffic is not None else None),
         "avg_launch_us": t_step * 1e6, "algorithmic_flop_per_launch": step_flop,
         # achieved / frac use avg_launch_us: HIP events on the stream the
