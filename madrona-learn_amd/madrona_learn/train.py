@@ -155,7 +155,7 @@ class TrainingManager:  # train.py:35-64
         if self._segments is None and self._eager_iters >= 1:
             try:
                 self._segments = self._capture(self._learn(), self._side)
-            except Exception as e:  # modules with host reads / syncs: stay eager
+            except RuntimeError as e:  # modules with host reads / syncs: stay eager
                 cur.wait_stream(self._side)
                 torch.cuda.synchronize()
                 print(f"[madrona_learn] torch-path update not capturable ({type(e).__name__}: "
