@@ -602,3 +602,42 @@ def test_torch_path_graph_replay_matches_eager(gpu, kind):
         for k in ("Loss", "Value Loss", "Entropy"):
             assert le[k].mean == lg[k].mean, (it, k)
     assert int(graph.state.train_list[0].step.item()) == 3 * 2 * (cfg.num_bptt_chunks * 64 // 16)
+
+
+def test_torch_path_uncapturable_tree_falls_back_to_eager(gpu, capsys):
+    """A user module that reads a device value on the host in its training
+    forward (not capturable in a HIP graph) keeps training: the capture at
+    update 2 fails, the manager says so and runs that update (and every later
+    one) eagerly -- bit-identical to a use_graph=False run."""
+    import madrona_learn as ml
+    from madrona_learn.envs import DummyVecEnv
+    from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
+
+    class SyncingMLP(MLP):
+        def forward(self, inputs, train=False):
+            if train:
+                _ = float(inputs.float().abs().max().item())  # a host read
+            return super().forward(inputs, train)
+
+    dt = torch.float32
+
+    def tree():
+        return ml.ActorCritic(
+            backbone=ml.BackboneSeparate(actor_encoder=ml.BackboneEncoder(net=SyncingMLP(64, 2, dt)),
+                                         critic_encoder=ml.BackboneEncoder(net=MLP(64, 2, dt))),
+            actor=DenseLayerDiscreteActor(ml.DiscreteActionsConfig(BUCKETS), dt),
+            critic=DenseLayerCritic(dt))
+
+    mgrs = []
+    for use_graph in (False, True):
+        env = DummyVecEnv(64, 64, 6, seed=13, device=gpu)
+        mgrs.append(ml.init_training(gpu, _cfg(64, 16), env.sim_fns(),
+                                     ml.Policy(actor_critic=tree()), use_graph=use_graph))
+    eager, graph = mgrs
+    for it in range(3):
+        for m in mgrs:
+            m.update_iter()
+        torch.cuda.synchronize()
+        assert torch.equal(eager.state.policy_states.params, graph.state.policy_states.params), it
+    assert not graph.use_graph and graph._segments is None
+    assert "not capturable" in capsys.readouterr().err
