@@ -12,13 +12,17 @@ from . import _native as nat
 
 
 class PhiloxKey:
-    """Counter-based key replacing jax.random keys: (k0, k1) plus a step."""
+    """Counter-based key replacing jax.random keys: (k0, k1) plus a step.
+    With ctr (a device tensor whose first element is a uint64 counter) the
+    step is ctr[0] + step, read by the sampling kernel itself (no host read:
+    a rollout that samples this way can be captured in a HIP graph)."""
 
-    def __init__(self, k0, k1, step=0, env_offset=0):
+    def __init__(self, k0, k1, step=0, env_offset=0, ctr=None):
         self.k0 = int(k0) & 0xFFFFFFFF
         self.k1 = int(k1) & 0xFFFFFFFF
         self.step = int(step)
         self.env_offset = int(env_offset)
+        self.ctr = ctr
 
 
 class DiscreteActionDistributions:
@@ -42,7 +46,8 @@ class DiscreteActionDistributions:
         logp = torch.empty((N, K), dtype=torch.float32, device=lg.device) if sample else None
         L = nat.lib()
         nat.check(L.mlearn_discrete_sample_f32(
-            nat.ptr(lg), lg.shape[1], self._layout, N, key.k0, key.k1, None, key.step,
+            nat.ptr(lg), lg.shape[1], self._layout, N, key.k0, key.k1,
+            None if key.ctr is None else nat.ptr(key.ctr), key.step,
             key.env_offset, 1 if sample else 0, nat.ptr(actions), nat.ptr(logp),
             nat.stream_handle()), "discrete_sample")
         shape = self.all_logits.shape[:-1] + (K,)

@@ -36,9 +36,11 @@ concatenated along the output axis) project per gate, each of the 8 gate
 kernels to its own initial norm, as flax's separate per-gate Dense leaves do
 (rnn.py:30-36; the fused optimizer's per-gate slots).
 Recurrent trees (a user's recurrent backbone, multi-layer LSTMs) train here
-with the rollout carry and per-chunk start states.  The rollout runs eagerly;
-the update is captured in HIP graphs after one eager update
-(TrainingManager.graph_scope "learn"; fp16 stays eager).
+with the rollout carry and per-chunk start states.  After one eager update
+the whole update (rollout included: the sampling kernel reads the device
+step counter itself) is captured in HIP graphs; where the user's sim or
+modules cannot be captured, the PPO update alone, else nothing
+(TrainingManager._update_torch; fp16 stays eager).
 """
 
 import ctypes
@@ -274,7 +276,8 @@ class TorchPolicyState:
     def update_obs_norm(self):
         pre = self.obs_preprocess
         if _has_state(pre) and getattr(self, "obs_stats", None) is not None:
-            self.obs_pre_state = pre.update_state(self.obs_pre_state, self.obs_stats, False)
+            self.obs_pre_state = _carry_back(
+                self.obs_pre_state, pre.update_state(self.obs_pre_state, self.obs_stats, False))
 
     def sync_weights(self):
         pass  # the modules read the arena directly
@@ -329,6 +332,38 @@ def _zip_leaves(fn, a, b):
     elif isinstance(a, (list, tuple)):
         for x, y in zip(a, b):
             _zip_leaves(fn, x, y)
+
+
+def _leaf_pairs(a, b, out):
+    if isinstance(a, torch.Tensor):
+        out.append((a, b))
+        return isinstance(b, torch.Tensor)
+    if isinstance(a, dict):
+        return isinstance(b, dict) and a.keys() == b.keys() and \
+            all(_leaf_pairs(a[k], b[k], out) for k in a)
+    if isinstance(a, (list, tuple)):
+        return isinstance(b, (list, tuple)) and len(a) == len(b) and \
+            all(_leaf_pairs(x, y, out) for x, y in zip(a, b))
+    return a is b or (isinstance(a, (int, float, bool, str, type(None))) and type(a) is type(b)
+                      and a == b)
+
+
+def _carry_back(start, cur):
+    """State carried from one update to the next (the sim state, the current
+    observations, the recurrent carry, a preprocess's estimates) kept at the
+    addresses it had when the update began: cur's tensors are copied into
+    start's, which is returned.  A captured update (HIP graph) reads these
+    tensors at its start and must find the previous replay's values there.
+    cur is returned as is where the structures, shapes or dtypes differ."""
+    pairs = []
+    if start is cur or not _leaf_pairs(start, cur, pairs):
+        return cur
+    if any(a.shape != b.shape or a.dtype != b.dtype or a.device != b.device for a, b in pairs):
+        return cur
+    for a, b in pairs:
+        if a is not b:
+            a.copy_(b)
+    return start
 
 
 def _nonempty(x):
@@ -469,15 +504,17 @@ class TorchRollout:
         strm = nat.stream_handle()
         key = rollout_state.prng_key
         # the sampling counter lives on the device (RolloutState.counters[0]);
-        # the torch path reads it once per rollout
-        base = int(rollout_state.counters[0].item())
+        # the sampling kernel adds it to the step itself (no host read, so the
+        # rollout can be captured in a HIP graph)
+        ctr = rollout_state.counters[0:1]
         N = m.N
         rec = ps.recurrent
         if m.P > 1:
             # a population (self-play split, pbt.py:130-133): policy p acts for
             # env columns [p B, (p + 1) B) (init_training excluded recurrent
             # and stateful-preprocess populations on this path)
-            return self._collect_population(rollout_state, gamma, key, base)
+            return self._collect_population(rollout_state, gamma, key, ctr)
+        start_state, start_obs = rollout_state.sim_state, rollout_state.cur_obs
         ps.begin_rollout()
         if rec:
             # the live carry in sim order (rollouts.py:898-901, 941-942) and
@@ -489,6 +526,7 @@ class TorchRollout:
                 s.torch_start = _map_leaves(
                     lambda x: torch.zeros((C, *x.shape), dtype=x.dtype, device=x.device),
                     rollout_state.rnn_states)
+            start_rnn = rollout_state.rnn_states
         for t in range(m.T):
             obs = rollout_state.cur_obs
             pre = ps.preprocess(obs)
@@ -501,7 +539,7 @@ class TorchRollout:
                 rnn_in = rollout_state.rnn_states
             with torch.no_grad():
                 out, rnn_out = ps.actor_critic.rollout(
-                    PhiloxKey(key[0], key[1], base + t, m.env_offset), rnn_in, pre)
+                    PhiloxKey(key[0], key[1], t, m.env_offset, ctr=ctr), rnn_in, pre)
             ps.codec.encode(pre, s.obs[t])
             s.actions[t].copy_(out["actions"].reshape(N, -1))
             s.log_probs[t].copy_(out["log_probs"].reshape(N, -1))
@@ -532,6 +570,10 @@ class TorchRollout:
             rnn_in = rollout_state.rnn_states if rec else ps.rnn0
             out, _ = ps.actor_critic.critic_only(rnn_in, ps.preprocess(rollout_state.cur_obs))
         s.bootstrap.copy_(_critic_value(out["critic"]))
+        rollout_state.sim_state = _carry_back(start_state, rollout_state.sim_state)
+        rollout_state.cur_obs = _carry_back(start_obs, rollout_state.cur_obs)
+        if rec:
+            rollout_state.rnn_states = _carry_back(start_rnn, rollout_state.rnn_states)
 
     def _step_sim(self, rollout_state, t, gamma):
         m = self.mgr
@@ -557,7 +599,7 @@ class TorchRollout:
         rollout_state.sim_state = so["state"]
         rollout_state.cur_obs = so["obs"]
 
-    def _collect_population(self, rollout_state, gamma, key, base):
+    def _collect_population(self, rollout_state, gamma, key, ctr):
         """rollout_loop for P torch-path policies: per step every policy's
         ActorCritic.rollout on its own env columns (its sampling counters are
         those of its env ids, as in the fused population launch), the store
@@ -565,6 +607,7 @@ class TorchRollout:
         m = self.mgr
         s = m.store
         B = m.B
+        start_state, start_obs = rollout_state.sim_state, rollout_state.cur_obs
         for t in range(m.T):
             obs = rollout_state.cur_obs
             for p, ps in enumerate(m.policies):
@@ -572,7 +615,8 @@ class TorchRollout:
                 pre = ps.preprocess(_slice_obs(obs, p * B, (p + 1) * B))
                 with torch.no_grad():
                     out, _ = ps.actor_critic.rollout(
-                        PhiloxKey(key[0], key[1], base + t, m.env_offset + p * B), ps.rnn0, pre)
+                        PhiloxKey(key[0], key[1], t, m.env_offset + p * B, ctr=ctr), ps.rnn0,
+                        pre)
                 ps.codec.encode(pre, s.obs[t, c])
                 s.actions[t, c].copy_(out["actions"].reshape(B, -1))
                 s.log_probs[t, c].copy_(out["log_probs"].reshape(B, -1))
@@ -584,6 +628,8 @@ class TorchRollout:
                 out, _ = ps.actor_critic.critic_only(
                     ps.rnn0, ps.preprocess(_slice_obs(obs, p * B, (p + 1) * B)))
             s.bootstrap[p * B:(p + 1) * B].copy_(_critic_value(out["critic"]))
+        rollout_state.sim_state = _carry_back(start_state, rollout_state.sim_state)
+        rollout_state.cur_obs = _carry_back(start_obs, rollout_state.cur_obs)
 
 
 class TorchPPO:

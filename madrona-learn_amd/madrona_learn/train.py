@@ -80,7 +80,8 @@ class TrainingManager:  # train.py:35-64
         # flat optimizer) is captured; a tree whose modules cannot be captured
         # falls back to eager updates
         self.graph_scope = "all"
-        self._side = None  # the torch path's learn stream (warm-up and capture)
+        self._side = None  # the torch path's stream (its warm-up and capture)
+        self._torch_path = False  # set by _init_training_torch (see _update_torch)
 
     # -- one update as a generator over collectives --------------------------
     def _collect(self):
@@ -174,9 +175,59 @@ class TrainingManager:  # train.py:35-64
             cur.wait_stream(self._side)
             self._eager_iters += 1
 
+    def _host_refs(self):
+        # the Python references a (failed) capture may have moved to tensors
+        # of its never-executed graph (sim state, observations, carries, ...)
+        objs = [self, self.state, self.rollout, self.rollout_mgr, self.rollout_mgr.store]
+        objs += list(self.state.policy_list) + list(self.state.train_list)
+        return [(o, dict(vars(o))) for o in objs]
+
+    @staticmethod
+    def _restore_host_refs(saved):
+        for o, d in saved:
+            vars(o).clear()
+            vars(o).update(d)
+
+    def _update_torch(self):
+        """The torch path (generic.py) under use_graph: update 1 runs eagerly
+        on the capture stream; update 2 captures the whole program (rollout +
+        update, split at the collectives) and replays it from then on.  If the
+        user's sim or modules cannot be captured, the host references the
+        failed capture moved are restored and only the PPO update is captured
+        (graph_scope "learn"; if that fails too, updates run eagerly)."""
+        import sys
+        if self.graph_scope == "learn":
+            return self._update_learn_graph()
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        cur = torch.cuda.current_stream()
+        if self._segments is not None:
+            self._replay()
+        elif self._eager_iters < 1:
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                self._run_eager()
+            cur.wait_stream(self._side)
+            self._eager_iters += 1
+        else:
+            saved = self._host_refs()
+            try:
+                self._segments = self._capture(self._program(), self._side)
+            except RuntimeError as e:
+                cur.wait_stream(self._side)
+                torch.cuda.synchronize()
+                self._restore_host_refs(saved)
+                print(f"[madrona_learn] torch-path rollout not capturable ({type(e).__name__}: "
+                      f"{e}); capturing the PPO update only", file=sys.stderr)
+                self.graph_scope = "learn"
+                return self._update_learn_graph()
+            self._replay()  # the capture recorded the update without running it
+
     def update_iter(self):
         """One PPO iteration; returns self (the reference returns a new pytree)."""
-        if self.use_graph and self.graph_scope == "learn":
+        if self.use_graph and self._torch_path:
+            self._update_torch()
+        elif self.use_graph and self.graph_scope == "learn":
             self._update_learn_graph()
         elif self.use_graph and self._segments is None and self._eager_iters >= 1:
             # capture runs the program once: it performs this iteration's work
@@ -467,8 +518,8 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
                          num_policies, sim_batch, sim_fns, restore_ckpt, profile_port, why,
                          policy_ids=(0,), use_graph=True):
     """init_training for a tree outside the fused kernels (generic.py): the
-    user's torch modules train under autograd (the update captured in HIP
-    graphs after one eager update, TrainingManager.graph_scope "learn"), with
+    user's torch modules train under autograd (captured in HIP graphs after
+    one eager update, TrainingManager._update_torch), with
     sampling, post-step, GAE, advantage statistics, action_stats and the
     optimizer on the HIP kernels.  A population (cfg.pbt, self-play split)
     gets one copy of the tree per train policy this rank holds, each with its
@@ -553,13 +604,14 @@ def _init_training_torch(device, cfg, policy, rollout_state, user_hooks, dp, ran
         algo.store = rollout_mgr.store
         algo.col0 = i * rollout_mgr.B
     print(cfg)
-    # HIP graphs over the update only (TrainingManager.graph_scope "learn");
-    # fp16 (DynamicScale reads the gradient norm on the host) stays eager
+    # HIP graphs (TrainingManager._update_torch: the whole update, else the
+    # PPO update only); fp16 (DynamicScale reads the gradient norm on the
+    # host) stays eager
     mgr = TrainingManager(tsm, rollout_state, metrics, cfg, rollout_mgr, algos, user_hooks, dp,
                           update_idx=start,
                           use_graph=use_graph and all(ts.scaler is None for ts in tss),
                           profile_port=profile_port)
-    mgr.graph_scope = "learn"
+    mgr._torch_path = True  # whole-update capture, falling back to the update only
     mgr._sim_get_ckpts = sim_fns.get("get_ckpts")
     mgr._sim_load_ckpts = sim_fns.get("load_ckpts")
     return mgr

@@ -59,8 +59,8 @@ def test_backbone_separate_update_matches_oracle(gpu):
     cfg = _cfg(N, mb)
     mgr = ml.init_training(gpu, cfg, env.sim_fns(), ml.Policy(actor_critic=ac), use_graph=True)
     ps, ts = mgr.state.policy_states, mgr.state.train_states
-    # (the torch path captures its update in HIP graphs from update 2 on)
-    assert getattr(ps, "generic", False) and mgr.use_graph and mgr.graph_scope == "learn"
+    # (the torch path captures its updates in HIP graphs from update 2 on)
+    assert getattr(ps, "generic", False) and mgr.use_graph and mgr._torch_path
     order = [n for n, _, _ in ps.layout["params"]]
     p0 = _named(ps)
     init_norms = {k: float(np.sqrt((v * v).sum())) for k, v in p0.items() if k.endswith("kernel")
@@ -557,12 +557,13 @@ def _torch_tree(kind, dt):
 
 @pytest.mark.parametrize("kind", ["separate", "lstm2", "pop2"])
 def test_torch_path_graph_replay_matches_eager(gpu, kind):
-    """The torch path's update captured in HIP graphs (TrainingManager
-    graph_scope "learn": update 1 eager on the capture stream, update 2
-    captured, update 3 replayed) against the same tree trained eagerly
-    (use_graph=False): parameters, Adam state, the rollout store and the loss
-    metrics bit-identical after every update -- BackboneSeparate, a two-layer
-    LSTM (per-chunk start states, C = 2) and a 2-policy population."""
+    """The torch path's whole update (rollout with the user's modules and
+    the sim, GAE, the PPO update under autograd) captured in HIP graphs
+    (TrainingManager._update_torch: update 1 eager on the capture stream,
+    update 2 captured, update 3 replayed) against the same tree trained
+    eagerly (use_graph=False): parameters, Adam state, the rollout store and
+    the loss metrics bit-identical after every update -- BackboneSeparate, a
+    two-layer LSTM (per-chunk start states, C = 2) and a 2-policy population."""
     import dataclasses
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
@@ -583,7 +584,7 @@ def test_torch_path_graph_replay_matches_eager(gpu, kind):
                                      ml.Policy(actor_critic=_torch_tree(kind, dt)),
                                      use_graph=use_graph))
     eager, graph = mgrs
-    assert not eager.use_graph and graph.use_graph and graph.graph_scope == "learn"
+    assert not eager.use_graph and graph.use_graph and graph._torch_path
     for it in range(3):
         for m in mgrs:
             m.update_iter()
@@ -601,21 +602,25 @@ def test_torch_path_graph_replay_matches_eager(gpu, kind):
         le, lg = eager.metrics.last(), graph.metrics.last()
         for k in ("Loss", "Value Loss", "Entropy"):
             assert le[k].mean == lg[k].mean, (it, k)
+    assert graph.graph_scope == "all"  # the rollout was captured too
     assert int(graph.state.train_list[0].step.item()) == 3 * 2 * (cfg.num_bptt_chunks * 64 // 16)
 
 
-def test_torch_path_uncapturable_tree_falls_back_to_eager(gpu, capsys):
-    """A user module that reads a device value on the host in its training
-    forward (not capturable in a HIP graph) keeps training: the capture at
-    update 2 fails, the manager says so and runs that update (and every later
-    one) eagerly -- bit-identical to a use_graph=False run."""
+@pytest.mark.parametrize("where", ["rollout", "update"])
+def test_torch_path_uncapturable_tree_falls_back(gpu, capsys, where):
+    """A user module that reads a device value on the host (not capturable in
+    a HIP graph) keeps training.  In its rollout forward: the whole-update
+    capture at update 2 fails, the host references it moved are restored and
+    only the PPO update is captured (graph_scope "learn").  In its training
+    forward: that capture fails too and updates run eagerly.  Either way
+    bit-identical to a use_graph=False run."""
     import madrona_learn as ml
     from madrona_learn.envs import DummyVecEnv
     from madrona_learn.models import MLP, DenseLayerCritic, DenseLayerDiscreteActor
 
     class SyncingMLP(MLP):
         def forward(self, inputs, train=False):
-            if train:
+            if train == (where == "update"):
                 _ = float(inputs.float().abs().max().item())  # a host read
             return super().forward(inputs, train)
 
@@ -639,5 +644,8 @@ def test_torch_path_uncapturable_tree_falls_back_to_eager(gpu, capsys):
             m.update_iter()
         torch.cuda.synchronize()
         assert torch.equal(eager.state.policy_states.params, graph.state.policy_states.params), it
-    assert not graph.use_graph and graph._segments is None
+    if where == "update":
+        assert not graph.use_graph and graph._segments is None
+    else:
+        assert graph.use_graph and graph.graph_scope == "learn" and graph._segments is not None
     assert "not capturable" in capsys.readouterr().err

@@ -1,5 +1,5 @@
 """Torch-path (generic.py) update timing, eager vs HIP-graph-replayed update
-(TrainingManager.graph_scope "learn"): BackboneSeparate MLP[256,256] x 2
+(TrainingManager._update_torch: the whole update, else the PPO update only): BackboneSeparate MLP[256,256] x 2
 encoders, f32, N envs, T = 32, 2 epochs x 4 minibatches, synthetic env.
 usage: python tools/torch_path_bench.py [N] [updates]"""
 import os
@@ -47,4 +47,4 @@ for use_graph in (False, True):
     out["graph" if use_graph else "eager"] = ts[len(ts) // 2] * 1e3
     print(f"{'graph' if use_graph else 'eager'}: {ts[len(ts) // 2] * 1e3:.2f} ms per update "
           f"(median of {U}), use_graph={mgr.use_graph}", flush=True)
-print(f"N={N}: eager {out['eager']:.2f} ms, learn graphs {out['graph']:.2f} ms per update")
+print(f"N={N}: eager {out['eager']:.2f} ms, graphs {out['graph']:.2f} ms per update")
