@@ -887,12 +887,12 @@ __device__ inline void wgrad_tile(const WgJobs& jobs, const WgJob& J, int local,
 // The bf16 weight-gradient tile with its operand chunks staged by LDS-DMA
 // (global_load_lds_dwordx4: no staging registers, no LDS write pass), S
 // stages deep: chunk c + S - 1 is issued right after the barrier that opens
-// chunk c, so each chunk's loads have S - 1 chunk times to land (the
-// register-staged form above gives them about one: its time per chunk was
-// the load latency -- a second back-to-back launch on cache-hot operands ran
-// 28.9 vs 29.4 us, and a 32 768-row minibatch at one workgroup per CU 24 us
-// for half the bytes, profiles/r06_spill_probes.txt).  Same MFMA fragments
-// in the same order as wgrad_tile<bf16>, so the slabs are bit-identical.
+// chunk c.  The launch is not bound by where its operands live (a second
+// back-to-back launch on cache-hot operands: 28.9 vs 29.4 us) but by its
+// chunk loop; 2 stages measured best (27.6 vs 29.0 us register-staged; 3 / 4
+// stages 29.8 / 31.6 us: more bytes in flight only congest,
+// profiles/r06_spill_probes.txt).  Same MFMA fragments in the same order as
+// wgrad_tile<bf16>, so the slabs are bit-identical.
 //
 // LDS image of one operand chunk: 32 rows of P bytes (P = 256 for a 128-
 // column tile, 128 for a tile of <= 64 columns), no padding; one DMA
