@@ -64,3 +64,25 @@ def test_fused_admission_routes_other_shapes():
         except NotImplementedError:
             continue
         raise AssertionError("expected the torch path")
+
+
+def test_carry_back_keeps_addresses():
+    """generic._carry_back: state carried between updates (sim state, current
+    observations, recurrent carry, preprocess estimates) returns to the
+    tensors it started in -- what a HIP-graph replay of the whole torch-path
+    update reads at its start -- and is left as is where the structure,
+    shapes or dtypes changed."""
+    from madrona_learn.generic import _carry_back
+    start = {"obs": torch.zeros(4, 3), "state": [torch.zeros(4, dtype=torch.int32), 7]}
+    cur = {"obs": torch.ones(4, 3), "state": [torch.full((4,), 5, dtype=torch.int32), 7]}
+    out = _carry_back(start, cur)
+    assert out is start and out["obs"] is start["obs"]
+    assert torch.equal(start["obs"], torch.ones(4, 3))
+    assert torch.equal(start["state"][0], torch.full((4,), 5, dtype=torch.int32))
+    same = torch.arange(3.0)
+    assert _carry_back(same, same) is same  # an in-place sim: nothing to copy
+    wide = {"obs": torch.ones(4, 5), "state": [torch.zeros(4, dtype=torch.int32), 7]}
+    assert _carry_back(start, wide) is wide  # a shape changed
+    other = {"obs": torch.ones(4, 3), "state": [torch.zeros(4, dtype=torch.int32), 8]}
+    assert _carry_back(start, other) is other  # a non-tensor leaf changed
+    assert _carry_back(start, {"obs": torch.ones(4, 3)}) is not start  # keys changed
