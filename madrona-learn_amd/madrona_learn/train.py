@@ -269,6 +269,11 @@ class TrainingManager:  # train.py:35-64
         if "rollout" in sd:
             self._load_rollout_state(sd["rollout"])
         torch.cuda.synchronize()
+        # captured graphs hold launch arguments taken from the host state they
+        # were captured with (the update RNG key, a torch-path preprocess's
+        # estimate tensors): the next updates run eagerly once, then capture again
+        self._segments = None
+        self._eager_iters = 0
         return self
 
     def _rollout_state_dict(self):
